@@ -1,0 +1,122 @@
+/* n2v2r.h -- C-ABI of the MI355X-native node2vec2rank fit-and-rank engine (libn2v2r_hip.so).
+ *
+ * Plain C types only (no torch, no HIP types).  Host pointers unless a name says "_dev".
+ * One handle drives one GPU; it owns every device buffer; it is NOT thread-safe.
+ * Every function returns an n2v2r_status; on failure n2v2r_last_error() has the message.
+ *
+ * Reference seams these entry points replace (file:line in /root/reference):
+ *   - n2v2r_set_layer_csr + n2v2r_uase + n2v2r_get_embedding
+ *       replace  se.UASE(csc_layers, max_embed_dim)           node2vec2rank/model.py:51-55
+ *       (third-party spectral_embedding.UASE -> scipy.sparse.linalg.svds / ARPACK)
+ *   - n2v2r_rank (+ n2v2r_get_distances)
+ *       replaces N2V2R.__rank                                 node2vec2rank/model.py:57-96
+ *       and compute_pairwise_distances                        node2vec2rank/model_utils.py:39-67
+ *   - n2v2r_rank (+ n2v2r_get_borda)
+ *       replaces the per-column sort of aggregate_transform   node2vec2rank/model.py:167-185
+ *       and borda_aggregate_parallel / _get_ranking           node2vec2rank/model_utils.py:22-36
+ *   - n2v2r_pairwise_distances: host-array form of            node2vec2rank/model_utils.py:39
+ *   - n2v2r_borda_columns:      host-array form of            node2vec2rank/model_utils.py:28
+ *   - n2v2r_column_sums:        float32 column sums for       node2vec2rank/model.py:282-311
+ */
+#ifndef N2V2R_H
+#define N2V2R_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  N2V2R_OK = 0,
+  N2V2R_ERR_BAD_ARG = 1,            /* -> ValueError */
+  N2V2R_ERR_UNSUPPORTED_METRIC = 2, /* -> NotImplementedError, model_utils.py:64-65 */
+  N2V2R_ERR_NO_CONVERGENCE = 3,     /* -> ArpackNoConvergence analogue */
+  N2V2R_ERR_HIP = 4,                /* -> RuntimeError */
+  N2V2R_ERR_OUT_OF_MEMORY = 5,      /* -> MemoryError */
+  N2V2R_ERR_NOT_READY = 6,          /* -> ValueError("No n2v2r embeddings found"), model.py:199 */
+  N2V2R_ERR_UNSUPPORTED_AGG = 7     /* -> NotImplementedError, model.py:182-183 */
+} n2v2r_status;
+
+/* comp_strategy (model.py:59-84) */
+enum { N2V2R_SEQUENTIAL = 0, N2V2R_ONE_VS_BEFORE = 1, N2V2R_ONE_VS_REST = 2 };
+/* distance metrics (model_utils.py:55-63) */
+enum { N2V2R_COSINE = 0, N2V2R_EUCLIDEAN = 1, N2V2R_CORRELATION = 2 };
+/* symmetric hint for n2v2r_set_layer_csr */
+enum { N2V2R_SYM_DETECT = -1, N2V2R_SYM_NO = 0, N2V2R_SYM_YES = 1 };
+
+typedef struct n2v2r_handle n2v2r_handle;
+
+typedef struct {
+  int block;          /* Krylov block width b: 32 or 64 (0 = auto) */
+  int max_basis;      /* max basis columns before a thick restart (0 = auto) */
+  int keep;           /* Ritz vectors kept at a restart (0 = auto) */
+  int max_restarts;   /* (0 = auto: 2000) */
+  double tol;         /* stop when ||M x_j - theta_j x_j|| <= tol * theta_1 for j < d (<=0: 1e-6) */
+  uint64_t seed;      /* start block seed */
+} n2v2r_eig_opts;
+
+typedef struct {
+  int restarts;              /* Rayleigh-Ritz cycles run */
+  int block_applications;    /* applications of M = sum_k A_k A_k^T to a b-wide block */
+  int converged;             /* Ritz pairs (of d) that met tol */
+  int basis;                 /* max basis columns used */
+  double max_residual;       /* max_j<d ||M x_j - theta_j x_j|| / theta_1 */
+  double ms_total, ms_spmm, ms_ortho, ms_rr_host; /* wall-clock split */
+  int64_t spmm_launches;     /* SpMM kernel launches (for roofline accounting) */
+  double spmm_algo_bytes;    /* sum over launches of the SURVEY 8(d) algorithmic bytes */
+  int stagnated;             /* 1: stopped at the fp32 residual floor (within 100x tol) */
+} n2v2r_eig_stats;
+
+/* lifecycle */
+int n2v2r_create(int device, n2v2r_handle** out);
+void n2v2r_destroy(n2v2r_handle* h);
+int n2v2r_last_error(const n2v2r_handle* h, char* buf, size_t len);
+const char* n2v2r_version(void);
+
+/* graph layers: K layers over the same N nodes.  CSR is copied to HBM (int64 row pointers are
+ * accepted; int32 column indices; fp32 values).  symmetric: N2V2R_SYM_* (DETECT compares the
+ * pattern and values with the transpose on the host).  Non-symmetric layers also keep A^T. */
+int n2v2r_set_num_layers(n2v2r_handle* h, int num_layers, int64_t n);
+int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const int64_t* indptr,
+                        const int32_t* indices, const float* data, int symmetric);
+
+/* UASE: top-d truncated SVD of the unfolded [A_1 | ... | A_K]; embeddings stay in HBM. */
+int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_stats* stats);
+int n2v2r_get_embedding(n2v2r_handle* h, float* Y /* K*N*d, row-major [k][n][j] */);
+int n2v2r_get_left_embedding(n2v2r_handle* h, float* X /* N*d */);
+int n2v2r_get_singular_values(n2v2r_handle* h, double* s /* d, descending */);
+int n2v2r_set_embedding(n2v2r_handle* h, int num_layers, int64_t n, int d, const float* Y);
+
+/* fit-and-rank tail: distances for every (comparison, dim, metric) column and their Borda
+ * aggregate, all device-resident.  Columns: dims outer, metrics inner, cosine skipped at dim 1.
+ * method: 0 = Borda (only one supported, model.py:179-183). */
+int n2v2r_rank(n2v2r_handle* h, int strategy, const int* dims, int n_dims, const int* metrics,
+               int n_metrics, int method, int* n_comparisons, int* n_cols);
+int n2v2r_get_distances(n2v2r_handle* h, int comparison, double* D /* C*N, column-major */);
+int n2v2r_get_borda(n2v2r_handle* h, int comparison, int64_t* borda /* N, node order */);
+int n2v2r_rank_timing(n2v2r_handle* h, double* ms_distances, double* ms_borda);
+
+/* host-array seams */
+int n2v2r_pairwise_distances(n2v2r_handle* h, const double* m1, const double* m2, int64_t n,
+                             int dim, int metric, double* out);
+int n2v2r_borda_columns(n2v2r_handle* h, const double* D /* C*N column-major */, int64_t n,
+                        int n_cols, int64_t* borda);
+int n2v2r_column_sums(n2v2r_handle* h, int k, float* out /* N */);
+
+/* device sync */
+int n2v2r_synchronize(n2v2r_handle* h);
+
+/* SpMM kernel alone (tests + roofline): Y = A_k X (transpose = 0) or A_k^T X (1) for a host
+ * N x b panel X (b = 32 or 64), timed with HIP events on the engine stream over `reps`
+ * launches after one warm-up.  avg_ms = mean launch duration; algo_bytes = SURVEY 8(d) bytes
+ * per launch (8 nnz + 4 (N+1) + 8 N b).  Y may be NULL. */
+int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, const float* X,
+                     float* Y, double* avg_ms, double* algo_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* N2V2R_H */

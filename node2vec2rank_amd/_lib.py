@@ -1,0 +1,317 @@
+"""ctypes binding of libn2v2r_hip.so (the C-ABI in include/n2v2r.h).
+
+There is no CPU fallback: if the library is missing, or no GPU is visible, every entry point
+raises.  Status codes map onto the exception types the reference raises for the same
+conditions (model_utils.py:64-65, model.py:182-183, model.py:199).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("N2V2R_LIB", os.path.join(_HERE, "lib", "libn2v2r_hip.so"))
+
+OK = 0
+ERR_BAD_ARG = 1
+ERR_UNSUPPORTED_METRIC = 2
+ERR_NO_CONVERGENCE = 3
+ERR_HIP = 4
+ERR_OUT_OF_MEMORY = 5
+ERR_NOT_READY = 6
+ERR_UNSUPPORTED_AGG = 7
+
+STRATEGY = {"sequential": 0, "one_vs_before": 1, "one_vs_rest": 2}
+METRIC = {"cosine": 0, "euclidean": 1, "correlation": 2}
+SYM_DETECT, SYM_NO, SYM_YES = -1, 0, 1
+
+# every symbol include/n2v2r.h declares (checked by tests/test_capi.py)
+EXPORTED = [
+    "n2v2r_create", "n2v2r_destroy", "n2v2r_last_error", "n2v2r_version",
+    "n2v2r_set_num_layers", "n2v2r_set_layer_csr", "n2v2r_uase", "n2v2r_get_embedding",
+    "n2v2r_get_left_embedding", "n2v2r_get_singular_values", "n2v2r_set_embedding",
+    "n2v2r_rank", "n2v2r_get_distances", "n2v2r_get_borda", "n2v2r_rank_timing",
+    "n2v2r_pairwise_distances", "n2v2r_borda_columns", "n2v2r_column_sums",
+    "n2v2r_synchronize", "n2v2r_bench_spmm",
+]
+
+
+class ArpackNoConvergence(RuntimeError):
+    """UASE eigensolver did not reach the residual tolerance (scipy raises
+    ``ArpackNoConvergence`` in the reference's svds path)."""
+
+
+class EigOpts(ctypes.Structure):
+    _fields_ = [("block", ctypes.c_int), ("max_basis", ctypes.c_int), ("keep", ctypes.c_int),
+                ("max_restarts", ctypes.c_int), ("tol", ctypes.c_double),
+                ("seed", ctypes.c_uint64)]
+
+
+class EigStats(ctypes.Structure):
+    _fields_ = [("restarts", ctypes.c_int), ("block_applications", ctypes.c_int),
+                ("converged", ctypes.c_int), ("basis", ctypes.c_int),
+                ("max_residual", ctypes.c_double), ("ms_total", ctypes.c_double),
+                ("ms_spmm", ctypes.c_double), ("ms_ortho", ctypes.c_double),
+                ("ms_rr_host", ctypes.c_double), ("spmm_launches", ctypes.c_int64),
+                ("spmm_algo_bytes", ctypes.c_double), ("stagnated", ctypes.c_int)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+_lock = threading.Lock()
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_i64 = ctypes.c_int64
+
+
+def _p(dtype):
+    return np.ctypeslib.ndpointer(dtype=dtype, flags="C_CONTIGUOUS")
+
+
+def load(path: str | None = None):
+    """Load (once) and return the ctypes library.  Raises if the .so is absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise RuntimeError(
+                f"n2v2r HIP library not found at {p}; build it with "
+                "`python -m node2vec2rank_amd.build` (there is no CPU fallback)")
+        lib = ctypes.CDLL(p)
+        sig = {
+            "n2v2r_create": (_i, [_i, ctypes.POINTER(_vp)]),
+            "n2v2r_destroy": (None, [_vp]),
+            "n2v2r_last_error": (_i, [_vp, ctypes.c_char_p, ctypes.c_size_t]),
+            "n2v2r_version": (ctypes.c_char_p, []),
+            "n2v2r_set_num_layers": (_i, [_vp, _i, _i64]),
+            "n2v2r_set_layer_csr": (_i, [_vp, _i, _i64, _i64, _p(np.int64), _p(np.int32),
+                                         _p(np.float32), _i]),
+            "n2v2r_uase": (_i, [_vp, _i, ctypes.POINTER(EigOpts), ctypes.POINTER(EigStats)]),
+            "n2v2r_get_embedding": (_i, [_vp, _p(np.float32)]),
+            "n2v2r_get_left_embedding": (_i, [_vp, _p(np.float32)]),
+            "n2v2r_get_singular_values": (_i, [_vp, _p(np.float64)]),
+            "n2v2r_set_embedding": (_i, [_vp, _i, _i64, _i, _p(np.float32)]),
+            "n2v2r_rank": (_i, [_vp, _i, _p(np.int32), _i, _p(np.int32), _i, _i,
+                                ctypes.POINTER(_i), ctypes.POINTER(_i)]),
+            "n2v2r_get_distances": (_i, [_vp, _i, _p(np.float64)]),
+            "n2v2r_get_borda": (_i, [_vp, _i, _p(np.int64)]),
+            "n2v2r_rank_timing": (_i, [_vp, ctypes.POINTER(ctypes.c_double),
+                                       ctypes.POINTER(ctypes.c_double)]),
+            "n2v2r_pairwise_distances": (_i, [_vp, _p(np.float64), _p(np.float64), _i64, _i, _i,
+                                              _p(np.float64)]),
+            "n2v2r_borda_columns": (_i, [_vp, _p(np.float64), _i64, _i, _p(np.int64)]),
+            "n2v2r_column_sums": (_i, [_vp, _i, _p(np.float32)]),
+            "n2v2r_synchronize": (_i, [_vp]),
+            "n2v2r_bench_spmm": (_i, [_vp, _i, _i, _i, _i, _p(np.float32), _vp,
+                                      ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(ctypes.c_double)]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(lib, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = lib
+        return lib
+
+
+class Engine:
+    """One GPU, one handle.  Thin, typed wrapper over the C-ABI."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        h = _vp()
+        st = self.lib.n2v2r_create(int(device), ctypes.byref(h))
+        if st != OK:
+            raise RuntimeError(
+                f"n2v2r_create(device={device}) failed with status {st}: no usable HIP GPU "
+                "(the engine has no CPU fallback)")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.n2v2r_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- errors --------------------------------------------------------------------------
+    def _err(self) -> str:
+        buf = ctypes.create_string_buffer(1024)
+        self.lib.n2v2r_last_error(self.h, buf, len(buf))
+        return buf.value.decode(errors="replace")
+
+    def _check(self, st: int, what: str):
+        if st == OK:
+            return
+        msg = f"{what}: {self._err()}"
+        if st == ERR_UNSUPPORTED_METRIC:
+            raise NotImplementedError("Unsupported metric")
+        if st == ERR_UNSUPPORTED_AGG:
+            raise NotImplementedError("Aggregation method not found. Available methods: Borda")
+        if st == ERR_NOT_READY:
+            raise ValueError("No n2v2r embeddings found")
+        if st == ERR_NO_CONVERGENCE:
+            raise ArpackNoConvergence(msg)
+        if st == ERR_OUT_OF_MEMORY:
+            raise MemoryError(msg)
+        if st == ERR_BAD_ARG:
+            raise ValueError(msg)
+        raise RuntimeError(msg)
+
+    # -- layers ----------------------------------------------------------------------------
+    def set_layers(self, layers, symmetric=SYM_DETECT):
+        """layers: list of scipy.sparse matrices (any format) or dense arrays, N x N."""
+        import scipy.sparse as sp
+        mats = [sp.csr_matrix(a, dtype=np.float32) for a in layers]
+        n = mats[0].shape[0]
+        for m in mats:
+            if m.shape != (n, n):
+                raise ValueError("all layers must be square and share the node set")
+        self._check(self.lib.n2v2r_set_num_layers(self.h, len(mats), n), "set_num_layers")
+        for k, m in enumerate(mats):
+            m.sum_duplicates()
+            m.sort_indices()
+            indptr = np.ascontiguousarray(m.indptr, dtype=np.int64)
+            indices = np.ascontiguousarray(m.indices, dtype=np.int32)
+            data = np.ascontiguousarray(m.data, dtype=np.float32)
+            self._check(self.lib.n2v2r_set_layer_csr(self.h, k, n, int(m.nnz), indptr, indices,
+                                                     data, int(symmetric)), f"layer {k}")
+        self.n = n
+        self.num_layers = len(mats)
+
+    # -- UASE ------------------------------------------------------------------------------
+    def uase(self, d: int, block=0, max_basis=0, keep=0, max_restarts=0, tol=0.0, seed=0,
+             raise_on_no_convergence=True):
+        o = EigOpts(int(block), int(max_basis), int(keep), int(max_restarts), float(tol),
+                    int(seed) & 0xFFFFFFFFFFFFFFFF)
+        s = EigStats()
+        st = self.lib.n2v2r_uase(self.h, int(d), ctypes.byref(o), ctypes.byref(s))
+        if st == ERR_NO_CONVERGENCE and not raise_on_no_convergence:
+            pass
+        else:
+            self._check(st, "uase")
+        self.d = int(d)
+        return s.as_dict()
+
+    def embedding(self):
+        Y = np.empty((self.num_layers, self.n, self.d), dtype=np.float32)
+        self._check(self.lib.n2v2r_get_embedding(self.h, Y), "get_embedding")
+        return Y
+
+    def left_embedding(self):
+        X = np.empty((self.n, self.d), dtype=np.float32)
+        self._check(self.lib.n2v2r_get_left_embedding(self.h, X), "get_left_embedding")
+        return X
+
+    def singular_values(self):
+        s = np.empty(self.d, dtype=np.float64)
+        self._check(self.lib.n2v2r_get_singular_values(self.h, s), "get_singular_values")
+        return s
+
+    def set_embedding(self, Y):
+        Y = np.ascontiguousarray(Y, dtype=np.float32)
+        K, n, d = Y.shape
+        self._check(self.lib.n2v2r_set_embedding(self.h, K, n, d, Y), "set_embedding")
+        self.num_layers, self.n, self.d = K, n, d
+
+    # -- rank --------------------------------------------------------------------------------
+    def rank(self, strategy: str, dims, metrics, method: int = 0):
+        if strategy not in STRATEGY:
+            raise ValueError(f"unknown comp_strategy {strategy!r}")
+        mids = []
+        for m in metrics:
+            if m not in METRIC:
+                raise NotImplementedError("Unsupported metric")
+            mids.append(METRIC[m])
+        dims_a = np.ascontiguousarray(dims, dtype=np.int32)
+        met_a = np.ascontiguousarray(mids, dtype=np.int32)
+        ncmp = ctypes.c_int()
+        ncol = ctypes.c_int()
+        self._check(self.lib.n2v2r_rank(self.h, STRATEGY[strategy], dims_a, len(dims_a), met_a,
+                                        len(met_a), int(method), ctypes.byref(ncmp),
+                                        ctypes.byref(ncol)), "rank")
+        self.ncmp, self.ncols = ncmp.value, ncol.value
+        return self.ncmp, self.ncols
+
+    def distances(self, comparison: int):
+        D = np.empty((self.ncols, self.n), dtype=np.float64)
+        self._check(self.lib.n2v2r_get_distances(self.h, int(comparison), D), "get_distances")
+        return D.T  # N x C view (column-major on device)
+
+    def borda(self, comparison: int):
+        b = np.empty(self.n, dtype=np.int64)
+        self._check(self.lib.n2v2r_get_borda(self.h, int(comparison), b), "get_borda")
+        return b
+
+    def rank_timing(self):
+        a, b = ctypes.c_double(), ctypes.c_double()
+        self.lib.n2v2r_rank_timing(self.h, ctypes.byref(a), ctypes.byref(b))
+        return a.value, b.value
+
+    # -- seams ------------------------------------------------------------------------------
+    def pairwise_distances(self, m1, m2, metric: str):
+        if metric not in METRIC:
+            raise NotImplementedError("Unsupported metric")
+        a = np.ascontiguousarray(m1, dtype=np.float64)
+        b = np.ascontiguousarray(m2, dtype=np.float64)
+        if a.ndim == 1:
+            a = a[:, None]
+            b = b[:, None]
+        n, dim = a.shape
+        out = np.empty(n, dtype=np.float64)
+        self._check(self.lib.n2v2r_pairwise_distances(self.h, a, b, n, dim, METRIC[metric], out),
+                    "pairwise_distances")
+        return out
+
+    def borda_columns(self, D):
+        """D: N x C float64 (one ranking column per column) -> int64 Borda in row order."""
+        Dc = np.ascontiguousarray(np.asarray(D, dtype=np.float64).T)
+        c, n = Dc.shape
+        out = np.empty(n, dtype=np.int64)
+        self._check(self.lib.n2v2r_borda_columns(self.h, Dc, n, c, out), "borda_columns")
+        return out
+
+    def column_sums(self, k: int):
+        out = np.empty(self.n, dtype=np.float32)
+        self._check(self.lib.n2v2r_column_sums(self.h, int(k), out), "column_sums")
+        return out
+
+    def bench_spmm(self, k: int, X, transpose: bool = False, reps: int = 20, want_y=True):
+        """Time the SpMM kernel alone (HIP events on the engine stream)."""
+        X = np.ascontiguousarray(X, dtype=np.float32)
+        n, b = X.shape
+        Y = np.empty_like(X) if want_y else None
+        ms, by = ctypes.c_double(), ctypes.c_double()
+        yp = Y.ctypes.data_as(ctypes.c_void_p) if want_y else None
+        self._check(self.lib.n2v2r_bench_spmm(self.h, int(k), int(bool(transpose)), int(b),
+                                              int(reps), X, yp, ctypes.byref(ms),
+                                              ctypes.byref(by)), "bench_spmm")
+        return Y, ms.value, by.value
+
+    def synchronize(self):
+        self._check(self.lib.n2v2r_synchronize(self.h), "synchronize")
+
+
+_default = {}
+
+
+def default_engine(device: int = 0) -> Engine:
+    """Process-wide engine per device (the handle is not thread-safe)."""
+    e = _default.get(device)
+    if e is None or e.h is None:
+        e = Engine(device)
+        _default[device] = e
+    return e

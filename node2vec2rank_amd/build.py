@@ -1,0 +1,67 @@
+"""Build libn2v2r_hip.so in-tree with hipcc for gfx950 (no JIT cache: the .so travels with the
+repository snapshot to the GPU box).
+
+    python -m node2vec2rank_amd.build [--force]
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT_DIR = os.path.join(HERE, "lib")
+LIB = os.path.join(OUT_DIR, "libn2v2r_hip.so")
+OBJ_DIR = os.path.join(OUT_DIR, "obj")
+
+HIP_SOURCES = ["spmm.hip", "dense.hip", "rank.hip", "engine.cpp"]
+HOST_SOURCES = ["eig_host.cpp"]
+HEADERS = ["common.h", os.path.join("..", "..", "include", "n2v2r.h")]
+ARCH = os.environ.get("N2V2R_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.isabs(c) and os.path.exists(c) or not os.path.isabs(c)):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    hipcc = _hipcc()
+    headers = [os.path.join(CSRC, h) for h in HEADERS]
+    objs = []
+    for src in HIP_SOURCES + HOST_SOURCES:
+        path = os.path.join(CSRC, src)
+        obj = os.path.join(OBJ_DIR, src + ".o")
+        objs.append(obj)
+        if not force and not _newer(obj, [path, __file__] + headers):
+            continue
+        if src in HIP_SOURCES:
+            lang = ["-x", "hip"]
+            cmd = [hipcc, *lang, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+                   "-munsafe-fp-atomics", "-c", path, "-o", obj]
+        else:
+            cmd = ["g++", "-O3", "-march=x86-64-v3", "-std=c++17", "-fPIC", "-c", path, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    if force or _newer(LIB, objs):
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,58 @@
+// Shared device helpers for the n2v2r HIP kernels (gfx950 / CDNA4, wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#define N2V2R_WAVE 64
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// A b-wide row-major panel: row r starts at ptr + r * ld.
+struct Panel {
+  float* ptr;
+  int64_t ld;
+};
+
+// One CSR matrix resident in HBM (fp32 values, int32 column indices, int64 row pointers).
+struct CsrDev {
+  const int64_t* indptr;
+  const int32_t* indices;
+  const float* data;
+  int64_t n_rows;
+  int64_t nnz;
+};
+
+// Up to this many basis blocks are addressed through a by-value pointer table.
+#define N2V2R_MAX_BLOCKS 40
+
+struct BlockList {
+  const float* blk[N2V2R_MAX_BLOCKS];
+  int count;   // number of blocks
+  int width;   // columns per block (32 or 64)
+};
+
+struct OutBlockList {
+  float* blk[N2V2R_MAX_BLOCKS];
+  int count;
+  int width;
+};
+
+__device__ __forceinline__ float wave_shfl_xor(float v, int mask) {
+  return __shfl_xor(v, mask, N2V2R_WAVE);
+}
+
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, N2V2R_WAVE);
+  return v;
+}
+
+// splitmix64 -> counter-based normal deviates for the Krylov start block.
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}

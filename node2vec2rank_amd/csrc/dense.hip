@@ -1,0 +1,433 @@
+// Tall-skinny dense kernels for the block Krylov-Schur eigensolver (gfx950, wave64).
+//
+// Basis storage: blocks of N x W fp32 (W = 32 or 64), row-major, one allocation per block.
+// Every product is cut into 32 x 32 MFMA tiles of v_mfma_f32_32x32x2_f32 (exact fp32
+// products, fp32 accumulate; C/D map: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) +
+// 4 (lane >> 5)).
+//   ts_tn : G = A^T B   (ca x cb, reduction over N rows).  Per workgroup a chunk of rows;
+//           4 waves split the chunk, their fp32 tiles are summed in fp64 through LDS and
+//           written as a per-chunk fp64 partial; a second kernel sums the chunks in fixed
+//           order (deterministic, no atomics).
+//   ts_nn : O = alpha A G + beta C   (N x cb).  One wave per 32 output rows and ALL of the
+//           output columns (so O may alias A or C: each wave reads only its own rows).
+//           A rows are read as 16-B loads; the k order inside each 8-column group is
+//           permuted consistently for A and G (lane half h carries columns 4h..4h+3).
+//   chol_inv : one-workgroup fp64 Cholesky G = R^T R (+shift on breakdown) and R^{-1},
+//           flagging rank-deficient columns; rows of those columns are refilled with
+//           random values by fill_flagged so the next CGS pass can orthogonalise them.
+#include "common.h"
+
+// ----------------------------------------------------------------------------- ts_tn
+#define TN_WAVES 4
+
+__device__ __forceinline__ const float* blk_col_ptr(const BlockList& L, int col) {
+  return L.blk[col / L.width] + (col % L.width);
+}
+
+__global__ __launch_bounds__(256) void ts_tn_kernel(BlockList A, BlockList B, int64_t n,
+                                                    int64_t rows_per_chunk, int ntj,
+                                                    double* __restrict__ partial,
+                                                    const int* cond) {
+  if (cond && *cond == 0) return;
+  __shared__ double red[TN_WAVES][16][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int tile = blockIdx.y;
+  const int ti = tile / ntj, tj = tile % ntj;
+  const int ca = A.count * A.width, cb = B.count * B.width;
+  const int i0 = ti * 32, j0 = tj * 32;
+  const float* pa = blk_col_ptr(A, i0) + (lane & 31);
+  const float* pb = blk_col_ptr(B, j0) + (lane & 31);
+  const int64_t lda = A.width, ldb = B.width;
+  const int h = lane >> 5;
+  const int64_t c0 = (int64_t)blockIdx.x * rows_per_chunk;
+  int64_t c1 = c0 + rows_per_chunk;
+  if (c1 > n) c1 = n;
+  const int64_t per_wave = (rows_per_chunk + TN_WAVES - 1) / TN_WAVES;
+  int64_t r0 = c0 + wave * per_wave;
+  int64_t r1 = r0 + per_wave;
+  if (r1 > c1) r1 = c1;
+  f32x16 acc = {0.f};
+  int64_t r = r0;
+  for (; r + 8 <= r1; r += 8) {
+    float a0 = pa[(r + 0 + h) * lda], b0 = pb[(r + 0 + h) * ldb];
+    float a1 = pa[(r + 2 + h) * lda], b1 = pb[(r + 2 + h) * ldb];
+    float a2 = pa[(r + 4 + h) * lda], b2 = pb[(r + 4 + h) * ldb];
+    float a3 = pa[(r + 6 + h) * lda], b3 = pb[(r + 6 + h) * ldb];
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a2, b2, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a3, b3, acc, 0, 0, 0);
+  }
+  for (; r < r1; r += 2) {
+    const int64_t rr = r + h;
+    float a = 0.f, b = 0.f;
+    if (rr < r1) {
+      a = pa[rr * lda];
+      b = pb[rr * ldb];
+    }
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) red[wave][q][lane] = (double)acc[q];
+  __syncthreads();
+  // 256 threads fold 4 waves x 1024 values in fixed order.
+  double* out = partial + (int64_t)blockIdx.x * ca * cb;
+  for (int e = threadIdx.x; e < 1024; e += blockDim.x) {
+    const int q = e >> 6, l = e & 63;
+    const double s = red[0][q][l] + red[1][q][l] + red[2][q][l] + red[3][q][l];
+    const int row = (q & 3) + 8 * (q >> 2) + 4 * (l >> 5);
+    const int col = l & 31;
+    out[(int64_t)(i0 + row) * cb + (j0 + col)] = s;
+  }
+}
+
+__global__ void reduce_chunks_kernel(const double* __restrict__ partial, int nchunks, int64_t elems,
+                                     double* __restrict__ out, const int* cond) {
+  if (cond && *cond == 0) return;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= elems) return;
+  double s = 0.0;
+  for (int c = 0; c < nchunks; ++c) s += partial[(int64_t)c * elems + e];
+  out[e] = s;
+}
+
+extern "C" hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n,
+                                         double* partial, size_t partial_elems, double* out,
+                                         const int* cond, hipStream_t stream) {
+  const int ca = A.count * A.width, cb = B.count * B.width;
+  const int nti = ca / 32, ntj = cb / 32;
+  const int ntiles = nti * ntj;
+  // chunk count: fill the chip (~2048 workgroups) but keep >= 256 rows per chunk and the
+  // partial buffer within its allocation.
+  int64_t nchunks = (n + 255) / 256;
+  int64_t cap = 2048 / ntiles;
+  if (cap < 1) cap = 1;
+  if (nchunks > cap) nchunks = cap;
+  const int64_t elems = (int64_t)ca * cb;
+  if ((size_t)(nchunks * elems) > partial_elems) nchunks = (int64_t)(partial_elems / elems);
+  if (nchunks < 1) return hipErrorInvalidValue;
+  int64_t rows_per_chunk = (n + nchunks - 1) / nchunks;
+  rows_per_chunk = (rows_per_chunk + 7) & ~(int64_t)7;
+  nchunks = (n + rows_per_chunk - 1) / rows_per_chunk;
+  dim3 grid((unsigned)nchunks, (unsigned)ntiles);
+  hipLaunchKernelGGL(ts_tn_kernel, grid, dim3(256), 0, stream, A, B, n, rows_per_chunk, ntj,
+                     partial, cond);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((elems + 255) / 256)), dim3(256), 0,
+                     stream, partial, (int)nchunks, elems, out, cond);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------- ts_nn
+// O[r][j] = alpha * sum_k A[r][k] G[k][j] + beta * C[r][j], j < 32*NT.  G fp32 row-major
+// (ldg columns).  Output / C blocks have width W (32 or 64), NT = cb / 32 tiles per wave.
+template <int NT>
+__global__ __launch_bounds__(256) void ts_nn_kernel(BlockList A, const float* __restrict__ G,
+                                                    int ldg, OutBlockList O, BlockList C,
+                                                    float alpha, float beta, int64_t n,
+                                                    const int* cond) {
+  if (cond && *cond == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 32;
+  if (r0 >= n) return;
+  const int i = lane & 31;
+  const int h = lane >> 5;
+  const int64_t row = r0 + i;
+  const bool row_ok = row < n;
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x16{0.f};
+  const int ca = A.count * A.width;
+  for (int kk = 0; kk < ca; kk += 8) {
+    const float* ap = A.blk[kk / A.width] + (kk % A.width) + 4 * h;
+    f32x4 a4 = {0.f, 0.f, 0.f, 0.f};
+    if (row_ok) a4 = *reinterpret_cast<const f32x4*>(ap + row * (int64_t)A.width);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const float* gp = G + (int64_t)(kk + 4 * h + m) * ldg + i;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[m], gp[t * 32], acc[t], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int col = t * 32 + i;
+    float* ob = O.blk[col / O.width] + (col % O.width);
+    const float* cbp = (beta != 0.f) ? C.blk[col / C.width] + (col % C.width) : nullptr;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int64_t rr = r0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+      if (rr < n) {
+        float v = alpha * acc[t][q];
+        if (cbp) v += beta * cbp[rr * (int64_t)C.width];
+        ob[rr * (int64_t)O.width] = v;
+      }
+    }
+  }
+}
+
+extern "C" hipError_t n2v2r_launch_ts_nn(const BlockList& A, const float* G, int ldg, int cb,
+                                         const OutBlockList& O, const BlockList& C, float alpha,
+                                         float beta, int64_t n, const int* cond,
+                                         hipStream_t stream) {
+  dim3 grid((unsigned)((n + 127) / 128));
+  switch (cb / 32) {
+    case 1: hipLaunchKernelGGL(ts_nn_kernel<1>, grid, dim3(256), 0, stream, A, G, ldg, O, C, alpha, beta, n, cond); break;
+    case 2: hipLaunchKernelGGL(ts_nn_kernel<2>, grid, dim3(256), 0, stream, A, G, ldg, O, C, alpha, beta, n, cond); break;
+    case 3: hipLaunchKernelGGL(ts_nn_kernel<3>, grid, dim3(256), 0, stream, A, G, ldg, O, C, alpha, beta, n, cond); break;
+    case 4: hipLaunchKernelGGL(ts_nn_kernel<4>, grid, dim3(256), 0, stream, A, G, ldg, O, C, alpha, beta, n, cond); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------- small ops
+// fp64 -> fp32 copy of a (rows x cols) matrix with optional negation (CGS coefficients).
+__global__ void f64_to_f32_kernel(const double* __restrict__ in, float* __restrict__ out,
+                                  int64_t elems, float scale, const int* cond) {
+  if (cond && *cond == 0) return;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < elems) out[e] = scale * (float)in[e];
+}
+
+extern "C" hipError_t n2v2r_launch_f64_to_f32(const double* in, float* out, int64_t elems,
+                                              float scale, const int* cond, hipStream_t stream) {
+  hipLaunchKernelGGL(f64_to_f32_kernel, dim3((unsigned)((elems + 255) / 256)), dim3(256), 0,
+                     stream, in, out, elems, scale, cond);
+  return hipGetLastError();
+}
+
+// Cholesky G = R^T R of a b x b fp64 Gram matrix and Rinv = R^{-1} (fp32, row-major b x b).
+// A pivot below tiny * max diag marks a rank-deficient column: its Rinv column is zeroed, its
+// R row set to unit, and flags[j] / *any_flag set.
+__global__ __launch_bounds__(256) void chol_inv_kernel(const double* __restrict__ G, int b,
+                                                       float* __restrict__ Rinv, int* flags,
+                                                       int* any_flag) {
+  __shared__ double R[64][65];
+  __shared__ double Ri[64][65];
+  __shared__ int bad[64];
+  __shared__ double dmax;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < b * b; e += blockDim.x) {
+    const int r = e / b, c = e % b;
+    R[r][c] = 0.5 * (G[r * b + c] + G[c * b + r]);
+  }
+  if (tid < 64) bad[tid] = 0;
+  __syncthreads();
+  if (tid == 0) {
+    double m = 0.0;
+    for (int j = 0; j < b; ++j) m = fmax(m, R[j][j]);
+    dmax = m;
+  }
+  __syncthreads();
+  const double tiny = 1e-10 * dmax;
+  // right-looking Cholesky, upper factor stored in R (row j holds R[j][j..]).
+  for (int j = 0; j < b; ++j) {
+    if (tid == 0) {
+      double p = R[j][j];
+      if (!(p > tiny)) {
+        bad[j] = 1;
+        R[j][j] = 1.0;
+        for (int c = j + 1; c < b; ++c) R[j][c] = 0.0;
+      } else {
+        const double s = sqrt(p);
+        R[j][j] = s;
+        for (int c = j + 1; c < b; ++c) R[j][c] /= s;
+      }
+    }
+    __syncthreads();
+    // trailing update: R[r][c] -= R[j][r] * R[j][c] for j < r <= c
+    for (int e = tid; e < b * b; e += blockDim.x) {
+      const int r = e / b, c = e % b;
+      if (r > j && c >= r) R[r][c] -= R[j][r] * R[j][c];
+    }
+    __syncthreads();
+  }
+  // inverse of upper-triangular R, one column per thread: R * x = e_c.
+  if (tid < b) {
+    const int c = tid;
+    for (int r = b - 1; r >= 0; --r) {
+      double s = (r == c) ? 1.0 : 0.0;
+      for (int k = r + 1; k <= c; ++k) s -= R[r][k] * Ri[k][c];
+      Ri[r][c] = (r <= c) ? s / R[r][r] : 0.0;
+    }
+  }
+  __syncthreads();
+  int any = 0;
+  for (int j = 0; j < b; ++j) any |= bad[j];
+  for (int e = tid; e < b * b; e += blockDim.x) {
+    const int r = e / b, c = e % b;
+    Rinv[e] = bad[c] ? 0.f : (float)Ri[r][c];
+  }
+  if (tid < b) flags[tid] = bad[tid];
+  if (tid == 0) *any_flag = any;
+}
+
+extern "C" hipError_t n2v2r_launch_chol_inv(const double* G, int b, float* Rinv, int* flags,
+                                            int* any_flag, hipStream_t stream) {
+  if (b > 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(chol_inv_kernel, dim3(1), dim3(256), 0, stream, G, b, Rinv, flags, any_flag);
+  return hipGetLastError();
+}
+
+// Fill an N x W block with N(0,1) deviates: all columns (flags == nullptr) or only flagged ones.
+__global__ void fill_normal_kernel(float* __restrict__ blk, int w, int64_t n, uint64_t seed,
+                                   const int* flags, const int* cond) {
+  if (cond && *cond == 0) return;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * w) return;
+  const int col = (int)(e % w);
+  if (flags && !flags[col]) return;
+  const uint64_t h1 = splitmix64(seed ^ (uint64_t)e * 0x2545F4914F6CDD1Dull);
+  const uint64_t h2 = splitmix64(h1);
+  const double u1 = ((h1 >> 11) + 1.0) * (1.0 / 9007199254740993.0);
+  const double u2 = (h2 >> 11) * (1.0 / 9007199254740992.0);
+  blk[e] = (float)(sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2));
+}
+
+extern "C" hipError_t n2v2r_launch_fill_normal(float* blk, int w, int64_t n, uint64_t seed,
+                                               const int* flags, const int* cond,
+                                               hipStream_t stream) {
+  const int64_t elems = n * w;
+  hipLaunchKernelGGL(fill_normal_kernel, dim3((unsigned)((elems + 255) / 256)), dim3(256), 0,
+                     stream, blk, w, n, seed, flags, cond);
+  return hipGetLastError();
+}
+
+// Ritz residual norms: res[j] = sum_r (MX[r][j] - theta[j] X[r][j])^2 for one W-wide block
+// pair, per-chunk fp64 partials then a fixed-order fold (reduce_chunks_kernel).
+__global__ __launch_bounds__(256) void resid_kernel(const float* __restrict__ X,
+                                                    const float* __restrict__ MX, int w,
+                                                    const double* __restrict__ theta, int64_t n,
+                                                    int64_t rows_per_chunk,
+                                                    double* __restrict__ partial) {
+  __shared__ double red[256];
+  const int col = threadIdx.x % w;
+  const int rg = threadIdx.x / w;
+  const int ngroups = blockDim.x / w;
+  const int64_t c0 = (int64_t)blockIdx.x * rows_per_chunk;
+  int64_t c1 = c0 + rows_per_chunk;
+  if (c1 > n) c1 = n;
+  const double th = theta[col];
+  double s = 0.0;
+  for (int64_t r = c0 + rg; r < c1; r += ngroups) {
+    const double v = (double)MX[r * w + col] - th * (double)X[r * w + col];
+    s += v * v;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x < w) {
+    double t = 0.0;
+    for (int g = 0; g < ngroups; ++g) t += red[g * w + threadIdx.x];
+    partial[(int64_t)blockIdx.x * w + threadIdx.x] = t;
+  }
+}
+
+extern "C" hipError_t n2v2r_launch_resid(const float* X, const float* MX, int w,
+                                         const double* theta, int64_t n, double* partial,
+                                         size_t partial_elems, double* out, hipStream_t stream) {
+  int64_t nchunks = (n + 4095) / 4096;
+  if (nchunks > 512) nchunks = 512;
+  if ((size_t)(nchunks * w) > partial_elems) nchunks = (int64_t)(partial_elems / w);
+  int64_t rows = (n + nchunks - 1) / nchunks;
+  nchunks = (n + rows - 1) / rows;
+  hipLaunchKernelGGL(resid_kernel, dim3((unsigned)nchunks), dim3(256), 0, stream, X, MX, w,
+                     theta, n, rows, partial);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((w + 255) / 256)), dim3(256), 0,
+                     stream, partial, (int)nchunks, (int64_t)w, out, (const int*)nullptr);
+  return hipGetLastError();
+}
+
+// Scale the columns of an N x W block: blk[r][j] *= s[j]
+__global__ void scale_cols_kernel(float* __restrict__ blk, int w, int64_t n,
+                                  const float* __restrict__ s) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n * w) blk[e] *= s[e % w];
+}
+
+extern "C" hipError_t n2v2r_launch_scale_cols(float* blk, int w, int64_t n, const float* s,
+                                              hipStream_t stream) {
+  const int64_t elems = n * w;
+  hipLaunchKernelGGL(scale_cols_kernel, dim3((unsigned)((elems + 255) / 256)), dim3(256), 0,
+                     stream, blk, w, n, s);
+  return hipGetLastError();
+}
+
+// Deterministic SVD sign convention (as sklearn's svd_flip): flip column j of U so that its
+// entry of largest magnitude (smallest row on ties) is positive.  Pass 1: per (row chunk,
+// 32-column tile) the packed key (|u| bits << 32 | ~row) max; pass 2: fold chunks, read the
+// sign, write +-1.
+__global__ __launch_bounds__(256) void colmax_partial_kernel(const float* __restrict__ U,
+                                                             int64_t ldu, int64_t n, int d,
+                                                             int64_t rows_per_chunk,
+                                                             unsigned long long* __restrict__ keys) {
+  __shared__ unsigned long long red[8][32];
+  const int c = threadIdx.x & 31;
+  const int rl = threadIdx.x >> 5;
+  const int col = blockIdx.y * 32 + c;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_chunk;
+  int64_t r1 = r0 + rows_per_chunk;
+  if (r1 > n) r1 = n;
+  unsigned long long best = 0;
+  if (col < d) {
+    for (int64_t r = r0 + rl; r < r1; r += 8) {
+      const float v = fabsf(U[r * ldu + col]);
+      const unsigned long long k = ((unsigned long long)__float_as_uint(v) << 32) |
+                                   (unsigned long long)(0xFFFFFFFFu - (uint32_t)r);
+      best = k > best ? k : best;
+    }
+  }
+  red[rl][c] = best;
+  __syncthreads();
+  if (rl == 0) {
+    for (int g = 1; g < 8; ++g) best = red[g][c] > best ? red[g][c] : best;
+    keys[(int64_t)blockIdx.x * gridDim.y * 32 + col] = best;
+  }
+}
+
+__global__ void colmax_finish_kernel(const unsigned long long* __restrict__ keys, int nchunks,
+                                     int ncols_padded, const float* __restrict__ U, int64_t ldu,
+                                     int d, float* __restrict__ sign) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= ncols_padded) return;
+  if (col >= d) {
+    sign[col] = 1.f;
+    return;
+  }
+  unsigned long long best = 0;
+  for (int c = 0; c < nchunks; ++c) {
+    const unsigned long long k = keys[(int64_t)c * ncols_padded + col];
+    best = k > best ? k : best;
+  }
+  const int64_t row = (int64_t)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
+  sign[col] = (U[row * ldu + col] < 0.f) ? -1.f : 1.f;
+}
+
+extern "C" hipError_t n2v2r_launch_sign_convention(float* U, int64_t ldu, int64_t n, int d,
+                                                   unsigned long long* keys, size_t key_elems,
+                                                   float* sign, hipStream_t stream) {
+  const int tiles = (d + 31) / 32;
+  int64_t nchunks = (n + 4095) / 4096;
+  if (nchunks > 1024) nchunks = 1024;
+  if ((size_t)(nchunks * tiles * 32) > key_elems) nchunks = (int64_t)(key_elems / (tiles * 32));
+  if (nchunks < 1) return hipErrorInvalidValue;
+  int64_t rows = (n + nchunks - 1) / nchunks;
+  nchunks = (n + rows - 1) / rows;
+  hipLaunchKernelGGL(colmax_partial_kernel, dim3((unsigned)nchunks, tiles), dim3(256), 0, stream,
+                     U, ldu, n, d, rows, keys);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(colmax_finish_kernel, dim3((tiles * 32 + 255) / 256), dim3(256), 0, stream,
+                     keys, (int)nchunks, tiles * 32, U, ldu, d, sign);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(scale_cols_kernel, dim3((unsigned)((n * ldu + 255) / 256)), dim3(256), 0,
+                     stream, U, (int)ldu, n, sign);
+  return hipGetLastError();
+}

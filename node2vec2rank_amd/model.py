@@ -1,0 +1,233 @@
+"""Drop-in ``N2V2R`` for the fit-and-rank path, backed by the MI355X engine.
+
+Mirrors ``node2vec2rank/model.py:17-311`` of the reference: same constructor, config keys,
+return types, column names, dict keys, index order, printed stage lines, output files and
+exceptions.  The arithmetic runs in libn2v2r_hip.so (HIP on gfx950); nothing here computes
+embeddings, distances or Borda scores on the host.
+
+Differences a user can observe (documented in DESIGN.md):
+  * embeddings come from a block Krylov-Schur solver instead of ARPACK, so they match the
+    reference within the tolerance stated in tests (per-column signs are arbitrary there too);
+  * Borda ties (exactly equal distances) are broken by ascending node index (a stable sort);
+    the reference's order for ties depends on numpy's unstable quicksort.
+"""
+from __future__ import annotations
+
+import json
+import os
+import random
+import time
+from datetime import datetime
+
+import numpy as np
+import pandas as pd
+import scipy.sparse as sp
+
+from . import _lib
+
+
+def _as_layer(g):
+    if isinstance(g, pd.DataFrame):
+        g = g.values
+    if sp.issparse(g):
+        return sp.csr_matrix(g, dtype=np.float32)
+    return sp.csr_matrix(np.asarray(g, dtype=np.float32))
+
+
+class N2V2R:
+    """``N2V2R(graphs, nodes, config)`` (reference ``model.py:18``)."""
+
+    def __init__(self, graphs: list, nodes: list, config: dict, device: int = 0,
+                 eig_options: dict | None = None):
+        self.config = config
+        self.node_names = nodes
+        self.graphs = graphs
+        self.num_graphs = len(graphs)
+        self.embed_dimensions = self.config['embed_dimensions']
+        self.max_embed_dim = max(self.embed_dimensions)
+        self.distance_metrics = self.config['distance_metrics']
+        self.save_dir = None
+        self.comp_strategy = self.config['comp_strategy']
+
+        self._node_embeddings = None
+        self.pairwise_ranks = None
+        self.pairwise_signed_ranks = None
+        self.pairwise_aggregate_ranks = None
+        self.pairwise_signed_aggregate_ranks = None
+        self.prior_singed_ranks = None
+        self.eig_stats = None
+        self.stage_seconds = {}
+
+        # model.py:36-38: a falsy seed means "unseeded"
+        self._seed = None
+        if self.config["seed"]:
+            random.seed(self.config["seed"])
+            np.random.seed(self.config["seed"])
+            self._seed = int(self.config["seed"])
+
+        now = datetime.now().strftime(r"%m_%d_%Y_%H_%M_%S")
+        if self.config.get("save_dir"):
+            self.save_dir = os.path.join(self.config["save_dir"], now)
+            print(self.save_dir)
+            os.makedirs(self.save_dir)
+            with open(os.path.join(self.save_dir, "config.json"), 'w', encoding="utf-8") as f:
+                json.dump(self.config, f)
+
+        self._engine = _lib.Engine(device)  # one handle per model: it owns the layers in HBM
+        self._eig_options = dict(eig_options or {})
+        self._layers_loaded = False
+        self._keys = None
+        self._cols = None
+
+    # ------------------------------------------------------------------------------------
+    def _load_layers(self):
+        if not self._layers_loaded:
+            self._engine.set_layers([_as_layer(g) for g in self.graphs])
+            self._layers_loaded = True
+
+    def __fit(self):
+        """UASE on the GPU (replaces ``se.UASE``, model.py:51-55)."""
+        self._load_layers()
+        seed = self._seed if self._seed is not None else int(np.random.randint(1, 2**31 - 1))
+        opts = dict(seed=seed)
+        opts.update(self._eig_options)
+        self.eig_stats = self._engine.uase(self.max_embed_dim, **opts)
+
+    def __rank(self):
+        """Distances + Borda for every comparison on the GPU (model.py:57-96,149-201)."""
+        ncmp, ncols = self._engine.rank(self.comp_strategy, self.embed_dimensions,
+                                        self.distance_metrics)
+        if self.comp_strategy != 'one_vs_rest':
+            keys = [str(i) for i in range(1, self.num_graphs)]
+        else:
+            keys = [str(i + 1) for i in range(self.num_graphs)]
+        cols = []
+        for dim in self.embed_dimensions:
+            for m in self.distance_metrics:
+                if m == 'cosine' and dim == 1:
+                    continue
+                cols.append(f"dim-{dim}_distance-{m}")
+        assert len(keys) == ncmp and len(cols) == ncols
+        self._keys, self._cols = keys, cols
+        out = {}
+        for c, key in enumerate(keys):
+            D = self._engine.distances(c)
+            out[key] = pd.DataFrame(D, index=self.node_names, columns=cols)
+        return out
+
+    def fit_transform_rank(self):
+        """Computes the differential ranks of nodes for a given sequence of graphs
+        (reference ``model.py:98-147``).  Returns ``dict[str, DataFrame(N x C)]``."""
+        if self.config["verbose"] >= 0:
+            print(f"\nRunning n2v2r with dimensions {self.embed_dimensions} and distance "
+                  f"metrics {self.distance_metrics} ...")
+        tic = time.time()
+        tic_uase = time.time()
+        self.__fit()
+        toc_uase = time.time()
+        if self.config["verbose"] == 1:
+            print(f"\tMulti-layer embedding in {round(toc_uase - tic_uase, 2)} seconds")
+        self._node_embeddings = None  # fetched lazily from HBM on first access
+        self.pairwise_ranks = self.__rank()
+        num_rankings = sum(len(df.columns) for df in self.pairwise_ranks.values())
+        toc = time.time()
+        self.stage_seconds.update(uase=toc_uase - tic_uase, rank=toc - toc_uase)
+        if self.config["verbose"] >= 0:
+            print(f"n2v2r computed {num_rankings} rankings for {len(self.pairwise_ranks)} "
+                  f"comparison(s) in {round(toc - tic, 2)} seconds")
+        if self.save_dir:
+            for key, rank in self.pairwise_ranks.items():
+                rank.to_csv(os.path.join(self.save_dir, key + ".tsv"), sep='\t', index=True)
+        return self.pairwise_ranks
+
+    @property
+    def node_embeddings(self):
+        """(K, N, d_max) float64 embeddings, as ``node_embeddings`` in the reference
+        (fetched from HBM on first access after ``fit_transform_rank``)."""
+        if self._node_embeddings is None and self.eig_stats is not None:
+            self._node_embeddings = self._engine.embedding().astype(np.float64)
+        return self._node_embeddings
+
+    @node_embeddings.setter
+    def node_embeddings(self, value):
+        self._node_embeddings = value
+
+    def aggregate_transform(self, method='Borda'):
+        """Borda aggregation (reference ``model.py:149-201``); the scores were computed on the
+        GPU together with the distances.  Returns ``dict[str, DataFrame['borda_ranks']]``."""
+        if self.pairwise_ranks:
+            start = time.time()
+            if self.config["verbose"] >= 0:
+                print("\nRank aggregation with Borda ...")
+            if method.casefold() != 'borda':
+                raise NotImplementedError('Aggregation method not found. Available methods: Borda')
+            out = {}
+            for c, key in enumerate(self._keys):
+                b = self._engine.borda(c)
+                out[key] = pd.DataFrame(b, index=self.node_names, columns=['borda_ranks'])
+            self.pairwise_aggregate_ranks = out
+            if self.config["verbose"] == 1:
+                print(f"\tFinished aggregation in {round(time.time() - start, 2)} seconds")
+            if self.save_dir:
+                for k, rank in self.pairwise_aggregate_ranks.items():
+                    rank.to_csv(os.path.join(self.save_dir, k + "_agg.tsv"), sep='\t', index=True)
+        else:
+            raise ValueError("No n2v2r embeddings found")
+        return self.pairwise_aggregate_ranks
+
+    def degree_difference_ranking(self):
+        """DeDi (reference ``model.py:282-311``): float32 column sums on the GPU."""
+        self._load_layers()
+        sums = [self._engine.column_sums(k) for k in range(self.num_graphs)]
+        out = {}
+        for i in range(1, self.num_graphs):
+            dedi = sums[i - 1] - sums[i]
+            ranking = pd.DataFrame({"DeDi": dedi, "absDeDi": np.abs(dedi)})
+            ranking.index = self.node_names
+            out[str(i)] = ranking
+        self.prior_singed_ranks = [v.iloc[:, 0] for v in out.values()]
+        if self.save_dir:
+            for k, rank in out.items():
+                rank.to_csv(os.path.join(self.save_dir, k + "_degDif.tsv"), sep='\t', index=True)
+        return out
+
+    def signed_ranks_transform(self, prior_signed_ranks=None):
+        """Sign each ranking by a prior (reference ``model.py:203-280`` +
+        ``model_utils.py:7-19``): rank kept where prior > 0, negated otherwise, restricted to
+        nodes present in the prior."""
+        if prior_signed_ranks is None:
+            if self.prior_singed_ranks:
+                prior_signed_ranks = self.prior_singed_ranks
+            else:
+                raise ValueError("Prior signed ranks needed, run degree_difference_ranking "
+                                 "beforehand or provide them in arguments.")
+        if not self.pairwise_ranks:
+            raise ValueError("No n2v2r embeddings found")
+        print("\nSigned ranks transformation ...")
+        start = time.time()
+        signed, signed_agg = {}, {}
+        for index, key in enumerate(self.pairwise_ranks):
+            prior = prior_signed_ranks[index]
+            df = self.pairwise_ranks[key]
+            keep = df.index.isin(prior.index)
+            sub = df.loc[keep]
+            sign = np.where(prior.reindex(sub.index).to_numpy() > 0, 1.0, -1.0)
+            signed[key] = pd.DataFrame(sub.to_numpy() * sign[:, None], index=sub.index,
+                                       columns=df.columns)
+            if self.pairwise_aggregate_ranks:
+                agg = self.pairwise_aggregate_ranks[key].iloc[:, 0].loc[keep]
+                signed_agg[key] = pd.DataFrame(agg.to_numpy() * sign.astype(np.int64),
+                                               index=agg.index, columns=["signed_agg_ranks"])
+        self.pairwise_signed_ranks = signed
+        if self.pairwise_aggregate_ranks:
+            self.pairwise_signed_aggregate_ranks = signed_agg
+        if self.config["verbose"] == 1:
+            print(f"\tFinished signed transformation in {round(time.time() - start, 2)} seconds")
+        if self.save_dir:
+            for k, v in self.pairwise_signed_ranks.items():
+                v.to_csv(os.path.join(self.save_dir, k + "_signed.tsv"), sep='\t', index=True)
+            if self.pairwise_aggregate_ranks:
+                for k, v in self.pairwise_signed_aggregate_ranks.items():
+                    v.to_csv(os.path.join(self.save_dir, str(k) + "_agg_signed.tsv"), sep='\t',
+                             index=True)
+        return self.pairwise_signed_ranks

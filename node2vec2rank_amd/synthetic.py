@@ -1,0 +1,65 @@
+"""Synthetic multilayer graphs for tests and the bench (host-side numpy, not on the hot path).
+
+Layer recipe follows SURVEY.md 8(d): symmetric Erdos-Renyi, no self loops, binary weights
+1.0f, one ``numpy.random.default_rng(seed_base + k)`` stream per layer, so layers are
+independent and distances have no exact ties.  Edges are drawn as ``N*avg_deg/2`` random
+(i, j) pairs; duplicates and self loops are dropped, so the realised mean degree is a hair
+under ``avg_deg``.
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.sparse as sp
+
+
+def er_layer(n: int, avg_deg: float, seed: int, dtype=np.float32) -> sp.csr_matrix:
+    rng = np.random.default_rng(seed)
+    m = int(round(n * avg_deg / 2.0))
+    i = rng.integers(0, n, size=m, dtype=np.int64)
+    j = rng.integers(0, n, size=m, dtype=np.int64)
+    keep = i != j
+    i, j = i[keep], j[keep]
+    lo = np.minimum(i, j)
+    hi = np.maximum(i, j)
+    key = np.unique(lo * n + hi)
+    lo = key // n
+    hi = key % n
+    rows = np.concatenate([lo, hi])
+    cols = np.concatenate([hi, lo])
+    data = np.ones(rows.shape[0], dtype=dtype)
+    a = sp.csr_matrix((data, (rows, cols)), shape=(n, n))
+    a.sum_duplicates()
+    a.sort_indices()
+    return a
+
+
+def er_layers(n: int, avg_deg: float, num_layers: int = 2, seed_base: int = 1000):
+    return [er_layer(n, avg_deg, seed_base + k) for k in range(num_layers)]
+
+
+def er_layer_p(n: int, p: float, seed: int) -> sp.csr_matrix:
+    """ER with edge probability p (BASELINE cfg1: N=1000, p=0.01)."""
+    return er_layer(n, p * (n - 1), seed)
+
+
+def sbm_layers(n: int, num_layers: int, k_comm: int = 5, p_in: float = 0.2,
+               p_out: float = 0.02, rewire_frac: float = 0.15, seed: int = 0):
+    """Planted-partition layers whose first community's links are rewired layer by layer
+    (a small stand-in for the reference's demo graphs, data/networks/demo)."""
+    rng = np.random.default_rng(seed)
+    comm = rng.integers(0, k_comm, size=n)
+    layers = []
+    for k in range(num_layers):
+        p = np.where(comm[:, None] == comm[None, :], p_in, p_out)
+        if k > 0:
+            changed = comm == 0
+            shuffle = rng.permutation(k_comm)
+            ck = np.where(changed, shuffle[comm], comm)
+            flip = changed & (rng.random(n) < max(rewire_frac * k, 1.0))
+            ck = np.where(flip, ck, comm)
+            p = np.where(ck[:, None] == ck[None, :], p_in, p_out)
+        u = rng.random((n, n)) < p
+        u = np.triu(u, 1)
+        a = (u | u.T).astype(np.float32)
+        layers.append(sp.csr_matrix(a))
+    return layers, comm

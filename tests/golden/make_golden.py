@@ -1,0 +1,175 @@
+"""Generate the golden vectors in tests/golden/*.npz by running the REFERENCE itself.
+
+Run in the survey container only (needs /root/reference; never runs on the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 PYTHONHASHSEED=0 python tests/golden/make_golden.py
+
+The reference's ``node2vec2rank/model.py`` is imported unchanged.  Its UASE dependency
+(``spectral_embedding``, un-vendored and unavailable offline, ``environment.yaml:19``) is
+provided as an in-memory module restating ``UASE`` per SURVEY.md Appendix A
+(hstack -> ``svds`` -> descending reorder -> sqrt scaling -> split into (K, N, d)).
+``DataLoader`` is bypassed (its ``match_networks`` set-intersection makes node order depend on
+PYTHONHASHSEED, ``preprocessing_utils.py:300-304``): graphs go to ``N2V2R`` directly, in file
+order, after the reference's own ``network_transform`` with the demo config's defaults.
+
+Each fixture holds the inputs (CSR per layer) and the reference's outputs: embeddings Y
+(K, N, d_max), singular values, per comparison key the N x C float64 distance matrix with its
+column names and the int64 Borda scores, and the DeDi ranking.  The script also checks that
+``oracle/n2v2r_oracle.py`` (faithful mode) reproduces every output bit-exactly before writing.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+import numpy as np
+import pandas as pd
+import scipy.sparse as sp
+from scipy.sparse.linalg import svds
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+
+
+def _uase_shim(As, d, **_kw):
+    A = sp.hstack(As)
+    u, s, vT = svds(A, d)
+    o = np.argsort(s[::-1])
+    S = np.sqrt(s[o])
+    XA = u[:, o] @ np.diag(S)
+    XB = vT.T[:, o] @ np.diag(S)
+    K = len(As)
+    n = As[0].shape[0]
+    YA = np.zeros((K, n, d))
+    for t in range(K):
+        YA[t] = XB[n * t:n * (t + 1)]
+    return XA, YA
+
+
+def _import_reference():
+    mod = types.ModuleType("spectral_embedding")
+    mod.UASE = _uase_shim
+    sys.modules["spectral_embedding"] = mod
+    sys.path.insert(0, REF)
+    from node2vec2rank.model import N2V2R  # noqa: E402
+    from node2vec2rank.preprocessing_utils import network_transform  # noqa: E402
+    return N2V2R, network_transform
+
+
+def _run_reference(N2V2R, graphs, nodes, dims, metrics, strategy, seed):
+    config = dict(embed_dimensions=list(dims), distance_metrics=list(metrics), seed=seed,
+                  comp_strategy=strategy, verbose=-1, save_dir=None)
+    model = N2V2R(graphs=graphs, nodes=nodes, config=config)
+    ranks = model.fit_transform_rank()
+    agg = model.aggregate_transform()
+    dedi = model.degree_difference_ranking() if strategy == "sequential" else {}
+    return model, ranks, agg, dedi
+
+
+def _pack_case(name, layers, nodes, dims, metrics, strategies, seed, N2V2R):
+    from oracle import n2v2r_oracle as orc
+    out = {}
+    for li, a in enumerate(layers):
+        a = sp.csr_matrix(a, dtype=np.float32)
+        a.sort_indices()
+        out[f"layer{li}_indptr"] = a.indptr.astype(np.int64)
+        out[f"layer{li}_indices"] = a.indices.astype(np.int32)
+        out[f"layer{li}_data"] = a.data.astype(np.float32)
+    out["num_layers"] = np.int64(len(layers))
+    out["n"] = np.int64(layers[0].shape[0])
+    out["nodes"] = np.asarray([str(x) for x in nodes])
+    out["dims"] = np.asarray(dims, dtype=np.int64)
+    out["metrics"] = np.asarray(metrics)
+    out["strategies"] = np.asarray(strategies)
+    out["seed"] = np.int64(seed)
+    dense = [np.asarray(sp.csr_matrix(a).todense(), dtype=np.float32) for a in layers]
+    for strategy in strategies:
+        model, ranks, agg, dedi = _run_reference(N2V2R, dense, list(nodes), dims, metrics,
+                                                 strategy, seed)
+        if "Y" not in out:
+            out["Y"] = np.asarray(model.node_embeddings, dtype=np.float64)
+        # oracle (faithful) must match bit-exactly
+        Yo, so, _ = orc.uase([sp.csc_matrix(g) for g in dense], max(dims), seed=seed)
+        assert np.array_equal(Yo, out["Y"]), f"{name}: oracle UASE differs from reference"
+        out["sigma"] = so
+        od = orc.rank_distances(Yo, dims, metrics, strategy, faithful=True)
+        for key, df in ranks.items():
+            cols = list(df.columns)
+            D = df.to_numpy(dtype=np.float64)
+            ocols, oD = od[key]
+            assert cols == ocols, (cols, ocols)
+            assert np.array_equal(np.isnan(D), np.isnan(oD))
+            assert np.array_equal(np.nan_to_num(D, nan=-1), np.nan_to_num(oD, nan=-1)), name
+            b = agg[key]["borda_ranks"].to_numpy(dtype=np.int64)
+            ob = orc.borda(D, faithful=True)
+            assert np.array_equal(b, ob), f"{name}/{strategy}/{key}: oracle Borda differs"
+            out[f"{strategy}/{key}/D"] = D
+            out[f"{strategy}/{key}/cols"] = np.asarray(cols)
+            out[f"{strategy}/{key}/borda"] = b
+            out[f"{strategy}/{key}/borda_stable"] = orc.borda(D, faithful=False)
+        out[f"{strategy}/keys"] = np.asarray(list(ranks.keys()))
+        for key, df in dedi.items():
+            out[f"dedi/{key}"] = df["DeDi"].to_numpy(dtype=np.float32)
+            od_ = orc.degree_difference(dense)[key][0]
+            assert np.array_equal(od_, out[f"dedi/{key}"])
+    path = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(path, **out)
+    print(f"wrote {path} ({os.path.getsize(path) / 1024:.0f} KB)")
+
+
+def main():
+    N2V2R, network_transform = _import_reference()
+    from node2vec2rank_amd import synthetic
+
+    # 1. the reference's demo graphs (data/networks/demo, configs/config_demo_adj.json)
+    demo_dir = os.path.join(REF, "data", "networks", "demo")
+    g = [pd.read_csv(os.path.join(demo_dir, f), index_col=0, header=0, sep=",")
+         for f in ("adj_matrix_1.csv", "adj_matrix_2.csv")]
+    nodes = list(g[0].columns)
+    g = [network_transform(x, threshold=None, top_percent_keep=100, binarize=False,
+                           absolute=False, project_unipartite_on=None) for x in g]
+    comm = pd.read_csv(os.path.join(demo_dir, "comm_asiggnments.csv"), index_col=0, header=0)
+    _pack_case("demo", [sp.csr_matrix(x) for x in g], nodes, list(range(4, 25, 2)),
+               ["euclidean", "cosine"], ["sequential"], 42, N2V2R)
+    np.save(os.path.join(HERE, "demo_communities.npy"), comm["0"].to_numpy(dtype=np.int64))
+
+    # 2. BASELINE cfg1: 2-layer ER N=1000, p=0.01, d=8
+    layers = [synthetic.er_layer_p(1000, 0.01, 1000 + k) for k in range(2)]
+    _pack_case("er_cfg1", layers, list(range(1000)), [8], ["cosine", "euclidean"],
+               ["sequential"], 42, N2V2R)
+
+    # 3. K=4, all three strategies, dim 1 (cosine skipped) and correlation
+    layers, _ = synthetic.sbm_layers(400, 4, seed=3)
+    _pack_case("k4_strategies", layers, list(range(400)), [1, 2, 4, 6],
+               ["cosine", "euclidean", "correlation"],
+               ["sequential", "one_vs_before", "one_vs_rest"], 7, N2V2R)
+
+    # 4. ties (planted unchanged nodes) + NaN cosine (a node isolated in layer 2)
+    rng = np.random.default_rng(11)
+    a1 = synthetic.er_layer(300, 12, 21).toarray()
+    a2 = synthetic.er_layer(300, 12, 22).toarray()
+    same = rng.choice(300, size=20, replace=False)
+    a2[same, :] = a1[same, :]
+    a2[:, same] = a1[:, same]
+    a2[5, :] = 0
+    a2[:, 5] = 0
+    _pack_case("ties_nan", [sp.csr_matrix(a1), sp.csr_matrix(a2)], list(range(300)),
+               [2, 4, 8], ["cosine", "euclidean"], ["sequential"], 42, N2V2R)
+
+    # 5. directed, weighted layers (exercises A_k^T and non-binary values)
+    rng = np.random.default_rng(5)
+    lay = []
+    for k in range(3):
+        m = (rng.random((250, 250)) < 0.05).astype(np.float32)
+        np.fill_diagonal(m, 0)
+        m *= rng.random((250, 250)).astype(np.float32) + 0.5
+        lay.append(sp.csr_matrix(m))
+    _pack_case("directed_weighted", lay, list(range(250)), [3, 5, 10],
+               ["cosine", "euclidean"], ["sequential", "one_vs_rest"], 123, N2V2R)
+
+
+if __name__ == "__main__":
+    main()
