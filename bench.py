@@ -1,0 +1,227 @@
+"""Benchmark: nodes ranked/s of the fit-and-rank path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg1|cfg4]
+
+One step = ``fit_transform_rank()`` + ``aggregate_transform()`` of the engine on one synthetic
+2-layer graph whose CSR layers are already resident in HBM: UASE (block Krylov-Schur on the
+GPU), distances for every (dim, metric) column, Borda, and the copy of the distance table and
+Borda scores back to the host (what the reference API returns).  Default workload is
+BASELINE.json configs[1] (cfg2: 2-layer ER N=100k, avg-deg 20, d=64).
+
+Multi-GPU (torchrun, one process per GPU): every rank ranks its own independent graph
+(different generator seeds): no data-path collective ("scaling": "weak", replicas).  A gloo
+group provides the barrier and the max-over-ranks of the timed region.
+
+Extra JSON fields: ``roofline`` (SpMM kernel, HIP-event timed on the engine stream at the
+Krylov panel width) and ``cpu_baseline`` (the reference algorithm restated in oracle/, on a
+bounded sample, rank 0 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+CONFIGS = {
+    "cfg1": dict(n=1000, avg_deg=9.99, dims=[8], d=8,
+                 desc="cfg1: 2-layer ER N=1000 p=0.01, d=8, cosine+euclidean, sequential"),
+    "cfg2": dict(n=100_000, avg_deg=20.0, dims=[64], d=64,
+                 desc="cfg2: 2-layer ER N=100k avg-deg 20, d=64, cosine+euclidean, sequential"),
+    "cfg4": dict(n=1_000_000, avg_deg=50.0, dims=[8, 16, 32, 64, 128], d=128,
+                 desc="cfg4: 2-layer ER N=1M avg-deg 50, dims {8,16,32,64,128} x "
+                      "{cosine,euclidean}, sequential"),
+}
+METRICS = ["cosine", "euclidean"]
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def _dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return world, rank, local
+
+
+class _Group:
+    """Control-plane barrier / max over ranks (gloo; the data path has no collective)."""
+
+    def __init__(self, world):
+        self.world = world
+        self.dist = None
+        if world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x: float) -> float:
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def _torch_sync():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+    except Exception:
+        pass
+
+
+def run_step(eng, cfg, seed):
+    st = eng.uase(cfg["d"], seed=seed)
+    ncmp, _ = eng.rank("sequential", cfg["dims"], METRICS)
+    out = []
+    for c in range(ncmp):
+        out.append((eng.distances(c), eng.borda(c)))
+    return st, out
+
+
+def cpu_baseline(sample_n=20_000, avg_deg=20.0, d=64, dims=(64,)):
+    """Reference algorithm (oracle/, faithful mode) on a bounded sample, 1 thread:
+    ARPACK svds + per-row scipy distances + the O(C N^2) list.index Borda."""
+    from threadpoolctl import threadpool_limits
+
+    from node2vec2rank_amd import synthetic
+    from oracle import n2v2r_oracle as orc
+    layers = synthetic.er_layers(sample_n, avg_deg, 2, seed_base=7000)
+    with threadpool_limits(1):
+        t0 = time.time()
+        Y, _, _ = orc.uase(layers, d, seed=42)
+        t1 = time.time()
+        ranks = orc.rank_distances(Y, list(dims), METRICS, "sequential", faithful=True)
+        t2 = time.time()
+        for _, (_, D) in ranks.items():
+            orc.borda_reference_loop(D)
+        t3 = time.time()
+    total = t3 - t0
+    return {
+        "value": sample_n / total, "unit": "nodes/s", "cores": 1, "kind": "port",
+        "sample": (f"2-layer ER N={sample_n} avg-deg {avg_deg:g}, d={d}, cosine+euclidean "
+                   f"(the bench workload at 1/{100_000 // sample_n} of its nodes; the Borda "
+                   f"stage is O(C N^2) so the full-size rate is lower), oracle faithful mode, "
+                   f"1 thread"),
+        "stages_s": {"svds": round(t1 - t0, 3), "distances": round(t2 - t1, 3),
+                     "borda": round(t3 - t2, 3)},
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=20_000)
+    args = ap.parse_args()
+
+    world, rank, local = _dist_env()
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    group = _Group(world)
+    cfg = CONFIGS[args.config]
+
+    from node2vec2rank_amd import _lib, synthetic
+    eng = _lib.Engine(local)
+    layers = synthetic.er_layers(cfg["n"], cfg["avg_deg"], 2, seed_base=1000 + 17 * rank)
+    nnz = [int(a.nnz) for a in layers]
+    eng.set_layers(layers)  # CSR -> HBM, untimed (inputs resident when timing starts)
+    seed = 42 + rank
+
+    for _ in range(args.warmup):
+        run_step(eng, cfg, seed)
+    eng.synchronize()
+    _torch_sync()
+    group.barrier()
+    t0 = time.perf_counter()
+    stats = None
+    for _ in range(args.steps):
+        stats, _ = run_step(eng, cfg, seed)
+    eng.synchronize()
+    _torch_sync()
+    group.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed_max = group.max(elapsed)
+    ncmp = 1
+    nodes_total = group.sum(float(cfg["n"] * ncmp * args.steps))
+    value = nodes_total / elapsed_max
+
+    # dominant kernel: the CSR x panel SpMM at the Krylov panel width, HIP events on the
+    # engine stream (same launch configuration as inside UASE)
+    b = 32
+    X = np.random.default_rng(0).standard_normal((cfg["n"], b)).astype(np.float32)
+    _, spmm_ms, spmm_bytes = eng.bench_spmm(0, X, reps=50, want_y=False)
+    achieved = spmm_bytes / (spmm_ms * 1e-3) / 1e9
+    ms_dist, ms_borda = eng.rank_timing()
+
+    traffic = None
+    tpath = os.path.join(REPO, "profiles", "spmm_traffic.json")
+    if os.path.exists(tpath):
+        try:
+            t = json.load(open(tpath))
+            if t.get("config") == args.config:
+                traffic = t.get("bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    result = {
+        "metric": "nodes ranked/sec (fit_transform_rank + aggregate_transform)",
+        "value": round(value, 1),
+        "unit": "nodes/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic",
+        "config": {"workload": cfg["desc"], "nodes": cfg["n"], "layers": 2,
+                   "avg_degree": cfg["avg_deg"], "nnz_per_layer": nnz, "embed_dim": cfg["d"],
+                   "columns": len(cfg["dims"]) * len(METRICS), "comparisons": ncmp,
+                   "parallelism": f"replicas x{world}" if world > 1 else "single"},
+        "roofline": {"bound": "hbm", "kernel": "spmm_csr_panel_kernel<32>",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                     "algo_bytes_per_launch": spmm_bytes, "avg_launch_ms": round(spmm_ms, 5)},
+        "eig": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in stats.items()},
+        "rank_ms": {"distances": round(ms_dist, 3), "borda": round(ms_borda, 3)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(sample_n=args.cpu_sample)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    group.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -82,14 +82,20 @@ __global__ __launch_bounds__(256) void ts_tn_kernel(BlockList A, BlockList B, in
   }
 }
 
-__global__ void reduce_chunks_kernel(const double* __restrict__ partial, int nchunks, int64_t elems,
-                                     double* __restrict__ out, const int* cond) {
+// out[e] = sum_c partial[c][e]: one wave per element, lanes stride the chunks, fixed-order
+// xor-tree fold (deterministic).
+__global__ __launch_bounds__(256) void reduce_chunks_kernel(const double* __restrict__ partial,
+                                                            int nchunks, int64_t elems,
+                                                            double* __restrict__ out,
+                                                            const int* cond) {
   if (cond && *cond == 0) return;
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (e >= elems) return;
   double s = 0.0;
-  for (int c = 0; c < nchunks; ++c) s += partial[(int64_t)c * elems + e];
-  out[e] = s;
+  for (int c = lane; c < nchunks; c += 64) s += partial[(int64_t)c * elems + e];
+  s = wave_sum_f64(s);
+  if (lane == 0) out[e] = s;
 }
 
 extern "C" hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n,
@@ -98,10 +104,9 @@ extern "C" hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B,
   const int ca = A.count * A.width, cb = B.count * B.width;
   const int nti = ca / 32, ntj = cb / 32;
   const int ntiles = nti * ntj;
-  // chunk count: fill the chip (~2048 workgroups) but keep >= 256 rows per chunk and the
-  // partial buffer within its allocation.
-  int64_t nchunks = (n + 255) / 256;
-  int64_t cap = 2048 / ntiles;
+  // chunk count: ~1024 workgroups with >= 512 rows per chunk, partials within the buffer
+  int64_t nchunks = (n + 511) / 512;
+  int64_t cap = 1024 / ntiles;
   if (cap < 1) cap = 1;
   if (nchunks > cap) nchunks = cap;
   const int64_t elems = (int64_t)ca * cb;
@@ -115,7 +120,7 @@ extern "C" hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B,
                      partial, cond);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((elems + 255) / 256)), dim3(256), 0,
+  hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((elems + 3) / 4)), dim3(256), 0,
                      stream, partial, (int)nchunks, elems, out, cond);
   return hipGetLastError();
 }
@@ -201,67 +206,75 @@ extern "C" hipError_t n2v2r_launch_f64_to_f32(const double* in, float* out, int6
   return hipGetLastError();
 }
 
-// Cholesky G = R^T R of a b x b fp64 Gram matrix and Rinv = R^{-1} (fp32, row-major b x b).
-// A pivot below tiny * max diag marks a rank-deficient column: its Rinv column is zeroed, its
-// R row set to unit, and flags[j] / *any_flag set.
-__global__ __launch_bounds__(256) void chol_inv_kernel(const double* __restrict__ G, int b,
-                                                       float* __restrict__ Rinv, int* flags,
-                                                       int* any_flag) {
+// Cholesky G = R^T R of a b x b fp64 Gram matrix and Rinv = R^{-1} (fp32, row-major b x b),
+// one 1024-thread workgroup, every step parallel over the trailing b x b entries.
+// A pivot below 1e-10 * max diag marks a rank-deficient column: its R row becomes the unit row,
+// its Rinv column is zeroed and flags[j] / *any_flag are set.
+__global__ __launch_bounds__(1024) void chol_inv_kernel(const double* __restrict__ G, int b,
+                                                        float* __restrict__ Rinv, int* flags,
+                                                        int* any_flag) {
   __shared__ double R[64][65];
-  __shared__ double Ri[64][65];
+  __shared__ double X[64][65];
+  __shared__ double piv[64];
   __shared__ int bad[64];
   __shared__ double dmax;
   const int tid = threadIdx.x;
-  for (int e = tid; e < b * b; e += blockDim.x) {
+  const int nt = blockDim.x;
+  for (int e = tid; e < b * b; e += nt) {
     const int r = e / b, c = e % b;
     R[r][c] = 0.5 * (G[r * b + c] + G[c * b + r]);
+    X[r][c] = (r == c) ? 1.0 : 0.0;
   }
   if (tid < 64) bad[tid] = 0;
   __syncthreads();
-  if (tid == 0) {
-    double m = 0.0;
-    for (int j = 0; j < b; ++j) m = fmax(m, R[j][j]);
-    dmax = m;
+  if (tid < 64) {
+    double m = (tid < b) ? R[tid][tid] : 0.0;
+    for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    if (tid == 0) dmax = m;
   }
   __syncthreads();
   const double tiny = 1e-10 * dmax;
-  // right-looking Cholesky, upper factor stored in R (row j holds R[j][j..]).
+  // right-looking: row j of R = (row j of the Schur complement) / sqrt(pivot)
   for (int j = 0; j < b; ++j) {
     if (tid == 0) {
-      double p = R[j][j];
+      const double p = R[j][j];
       if (!(p > tiny)) {
         bad[j] = 1;
-        R[j][j] = 1.0;
-        for (int c = j + 1; c < b; ++c) R[j][c] = 0.0;
+        piv[j] = 0.0;
       } else {
-        const double s = sqrt(p);
-        R[j][j] = s;
-        for (int c = j + 1; c < b; ++c) R[j][c] /= s;
+        piv[j] = sqrt(p);
       }
     }
     __syncthreads();
-    // trailing update: R[r][c] -= R[j][r] * R[j][c] for j < r <= c
-    for (int e = tid; e < b * b; e += blockDim.x) {
-      const int r = e / b, c = e % b;
-      if (r > j && c >= r) R[r][c] -= R[j][r] * R[j][c];
+    const double pj = piv[j];
+    const int isbad = bad[j];
+    // scale row j (c >= j)
+    for (int c = j + tid; c < b; c += nt) R[j][c] = isbad ? (c == j ? 1.0 : 0.0) : (c == j ? pj : R[j][c] / pj);
+    __syncthreads();
+    // trailing update R[r][c] -= R[j][r] R[j][c], j < r <= c
+    const int m = b - j - 1;
+    for (int e = tid; e < m * m; e += nt) {
+      const int r = j + 1 + e / m, c = j + 1 + e % m;
+      if (c >= r) R[r][c] -= R[j][r] * R[j][c];
     }
     __syncthreads();
   }
-  // inverse of upper-triangular R, one column per thread: R * x = e_c.
-  if (tid < b) {
-    const int c = tid;
-    for (int r = b - 1; r >= 0; --r) {
-      double s = (r == c) ? 1.0 : 0.0;
-      for (int k = r + 1; k <= c; ++k) s -= R[r][k] * Ri[k][c];
-      Ri[r][c] = (r <= c) ? s / R[r][r] : 0.0;
+  // Gauss-Jordan on [R | I] from the last row up: X <- R^{-1}
+  for (int j = b - 1; j >= 0; --j) {
+    const double inv = 1.0 / R[j][j];
+    for (int c = tid; c < b; c += nt) X[j][c] *= inv;
+    __syncthreads();
+    for (int e = tid; e < j * b; e += nt) {
+      const int r = e / b, c = e % b;
+      X[r][c] -= R[r][j] * X[j][c];
     }
+    __syncthreads();
   }
-  __syncthreads();
   int any = 0;
   for (int j = 0; j < b; ++j) any |= bad[j];
-  for (int e = tid; e < b * b; e += blockDim.x) {
+  for (int e = tid; e < b * b; e += nt) {
     const int r = e / b, c = e % b;
-    Rinv[e] = bad[c] ? 0.f : (float)Ri[r][c];
+    Rinv[e] = bad[c] ? 0.f : (float)X[r][c];
   }
   if (tid < b) flags[tid] = bad[tid];
   if (tid == 0) *any_flag = any;
@@ -270,7 +283,7 @@ __global__ __launch_bounds__(256) void chol_inv_kernel(const double* __restrict_
 extern "C" hipError_t n2v2r_launch_chol_inv(const double* G, int b, float* Rinv, int* flags,
                                             int* any_flag, hipStream_t stream) {
   if (b > 64) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(chol_inv_kernel, dim3(1), dim3(256), 0, stream, G, b, Rinv, flags, any_flag);
+  hipLaunchKernelGGL(chol_inv_kernel, dim3(1), dim3(1024), 0, stream, G, b, Rinv, flags, any_flag);
   return hipGetLastError();
 }
 
@@ -298,24 +311,27 @@ extern "C" hipError_t n2v2r_launch_fill_normal(float* blk, int w, int64_t n, uin
   return hipGetLastError();
 }
 
-// Ritz residual norms: res[j] = sum_r (MX[r][j] - theta[j] X[r][j])^2 for one W-wide block
-// pair, per-chunk fp64 partials then a fixed-order fold (reduce_chunks_kernel).
-__global__ __launch_bounds__(256) void resid_kernel(const float* __restrict__ X,
-                                                    const float* __restrict__ MX, int w,
+// Ritz residual norms: res[j] = sum_r (MX[r][j] - theta[j] X[r][j])^2 over all blocks of X/MX
+// (grid.y = block), per-chunk fp64 partials then the fixed-order wave fold.
+__global__ __launch_bounds__(256) void resid_kernel(BlockList X, BlockList MX,
                                                     const double* __restrict__ theta, int64_t n,
                                                     int64_t rows_per_chunk,
                                                     double* __restrict__ partial) {
   __shared__ double red[256];
+  const int w = X.width;
+  const int q = blockIdx.y;
+  const float* xb = X.blk[q];
+  const float* mb = MX.blk[q];
   const int col = threadIdx.x % w;
   const int rg = threadIdx.x / w;
   const int ngroups = blockDim.x / w;
   const int64_t c0 = (int64_t)blockIdx.x * rows_per_chunk;
   int64_t c1 = c0 + rows_per_chunk;
   if (c1 > n) c1 = n;
-  const double th = theta[col];
+  const double th = theta[q * w + col];
   double s = 0.0;
   for (int64_t r = c0 + rg; r < c1; r += ngroups) {
-    const double v = (double)MX[r * w + col] - th * (double)X[r * w + col];
+    const double v = (double)mb[r * w + col] - th * (double)xb[r * w + col];
     s += v * v;
   }
   red[threadIdx.x] = s;
@@ -323,24 +339,26 @@ __global__ __launch_bounds__(256) void resid_kernel(const float* __restrict__ X,
   if (threadIdx.x < w) {
     double t = 0.0;
     for (int g = 0; g < ngroups; ++g) t += red[g * w + threadIdx.x];
-    partial[(int64_t)blockIdx.x * w + threadIdx.x] = t;
+    const int64_t ncols = (int64_t)X.count * w;
+    partial[(int64_t)blockIdx.x * ncols + q * w + threadIdx.x] = t;
   }
 }
 
-extern "C" hipError_t n2v2r_launch_resid(const float* X, const float* MX, int w,
+extern "C" hipError_t n2v2r_launch_resid(const BlockList& X, const BlockList& MX,
                                          const double* theta, int64_t n, double* partial,
                                          size_t partial_elems, double* out, hipStream_t stream) {
-  int64_t nchunks = (n + 4095) / 4096;
-  if (nchunks > 512) nchunks = 512;
-  if ((size_t)(nchunks * w) > partial_elems) nchunks = (int64_t)(partial_elems / w);
+  const int64_t ncols = (int64_t)X.count * X.width;
+  int64_t nchunks = (n + 1023) / 1024;
+  if (nchunks > 256) nchunks = 256;
+  if ((size_t)(nchunks * ncols) > partial_elems) nchunks = (int64_t)(partial_elems / ncols);
   int64_t rows = (n + nchunks - 1) / nchunks;
   nchunks = (n + rows - 1) / rows;
-  hipLaunchKernelGGL(resid_kernel, dim3((unsigned)nchunks), dim3(256), 0, stream, X, MX, w,
+  hipLaunchKernelGGL(resid_kernel, dim3((unsigned)nchunks, X.count), dim3(256), 0, stream, X, MX,
                      theta, n, rows, partial);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((w + 255) / 256)), dim3(256), 0,
-                     stream, partial, (int)nchunks, (int64_t)w, out, (const int*)nullptr);
+  hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((ncols + 3) / 4)), dim3(256), 0, stream,
+                     partial, (int)nchunks, ncols, out, (const int*)nullptr);
   return hipGetLastError();
 }
 

@@ -63,7 +63,7 @@ hipError_t n2v2r_launch_chol_inv(const double* G, int b, float* Rinv, int* flags
                                  hipStream_t stream);
 hipError_t n2v2r_launch_fill_normal(float* blk, int w, int64_t n, uint64_t seed, const int* flags,
                                     const int* cond, hipStream_t stream);
-hipError_t n2v2r_launch_resid(const float* X, const float* MX, int w, const double* theta,
+hipError_t n2v2r_launch_resid(const BlockList& X, const BlockList& MX, const double* theta,
                               int64_t n, double* partial, size_t partial_elems, double* out,
                               hipStream_t stream);
 hipError_t n2v2r_launch_scale_cols(float* blk, int w, int64_t n, const float* s,
@@ -524,10 +524,9 @@ struct Eig {
           }
         }
       }
-      for (int q = 0; q < pb; ++q)
-        HIPCHK(n2v2r_launch_resid(X[q], MX[q], b, h->theta.as<double>() + q * b, n,
-                                  h->partial.as<double>(), h->partial_elems,
-                                  h->resid.as<double>() + q * b, st));
+      HIPCHK(n2v2r_launch_resid(blocks(X, 0, pb), blocks(MX, 0, pb), h->theta.as<double>(), n,
+                                h->partial.as<double>(), h->partial_elems, h->resid.as<double>(),
+                                st));
       HIPCHK(hipMemcpyAsync(res2.data(), h->resid.as<double>(), sizeof(double) * keep,
                             hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
