@@ -55,6 +55,10 @@ typedef struct {
   int max_restarts;   /* (0 = auto: 2000) */
   double tol;         /* stop when ||M x_j - theta_j x_j|| <= tol * theta_1 for j < d (<=0: 1e-6) */
   uint64_t seed;      /* start block seed */
+  int overlap;        /* EXPERIMENTAL: blocks expanded on the GPU (against the un-restarted basis)
+                         while the host solves the projected problem; 0 = off (default),
+                         k > 0 = fixed, -2 = adaptive.  Breaks the Krylov-Schur structure:
+                         residuals stall near 1e-4, so it is off unless asked for. */
 } n2v2r_eig_opts;
 
 typedef struct {

@@ -25,7 +25,7 @@ struct CsrDev {
 };
 
 // Up to this many basis blocks are addressed through a by-value pointer table.
-#define N2V2R_MAX_BLOCKS 40
+#define N2V2R_MAX_BLOCKS 96
 
 struct BlockList {
   const float* blk[N2V2R_MAX_BLOCKS];

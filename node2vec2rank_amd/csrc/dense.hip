@@ -20,7 +20,10 @@
 // ----------------------------------------------------------------------------- ts_tn
 #define TN_WAVES 4
 
+// Column `col` of a block list (nullptr past the last column): per lane, so a 32-wide tile may
+// span several 8/16-wide blocks.
 __device__ __forceinline__ const float* blk_col_ptr(const BlockList& L, int col) {
+  if (col >= L.count * L.width) return nullptr;
   return L.blk[col / L.width] + (col % L.width);
 }
 
@@ -36,8 +39,12 @@ __global__ __launch_bounds__(256) void ts_tn_kernel(BlockList A, BlockList B, in
   const int ti = tile / ntj, tj = tile % ntj;
   const int ca = A.count * A.width, cb = B.count * B.width;
   const int i0 = ti * 32, j0 = tj * 32;
-  const float* pa = blk_col_ptr(A, i0) + (lane & 31);
-  const float* pb = blk_col_ptr(B, j0) + (lane & 31);
+  const float* pa = blk_col_ptr(A, i0 + (lane & 31));
+  const float* pb = blk_col_ptr(B, j0 + (lane & 31));
+  // lanes past the last column read a valid row of column 0 and multiply by zero
+  const float ma = pa ? 1.f : 0.f, mb = pb ? 1.f : 0.f;
+  if (!pa) pa = A.blk[0];
+  if (!pb) pb = B.blk[0];
   const int64_t lda = A.width, ldb = B.width;
   const int h = lane >> 5;
   const int64_t c0 = (int64_t)blockIdx.x * rows_per_chunk;
@@ -50,10 +57,10 @@ __global__ __launch_bounds__(256) void ts_tn_kernel(BlockList A, BlockList B, in
   f32x16 acc = {0.f};
   int64_t r = r0;
   for (; r + 8 <= r1; r += 8) {
-    float a0 = pa[(r + 0 + h) * lda], b0 = pb[(r + 0 + h) * ldb];
-    float a1 = pa[(r + 2 + h) * lda], b1 = pb[(r + 2 + h) * ldb];
-    float a2 = pa[(r + 4 + h) * lda], b2 = pb[(r + 4 + h) * ldb];
-    float a3 = pa[(r + 6 + h) * lda], b3 = pb[(r + 6 + h) * ldb];
+    float a0 = ma * pa[(r + 0 + h) * lda], b0 = mb * pb[(r + 0 + h) * ldb];
+    float a1 = ma * pa[(r + 2 + h) * lda], b1 = mb * pb[(r + 2 + h) * ldb];
+    float a2 = ma * pa[(r + 4 + h) * lda], b2 = mb * pb[(r + 4 + h) * ldb];
+    float a3 = ma * pa[(r + 6 + h) * lda], b3 = mb * pb[(r + 6 + h) * ldb];
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a2, b2, acc, 0, 0, 0);
@@ -63,8 +70,8 @@ __global__ __launch_bounds__(256) void ts_tn_kernel(BlockList A, BlockList B, in
     const int64_t rr = r + h;
     float a = 0.f, b = 0.f;
     if (rr < r1) {
-      a = pa[rr * lda];
-      b = pb[rr * ldb];
+      a = ma * pa[rr * lda];
+      b = mb * pb[rr * ldb];
     }
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
   }
@@ -76,9 +83,9 @@ __global__ __launch_bounds__(256) void ts_tn_kernel(BlockList A, BlockList B, in
   for (int e = threadIdx.x; e < 1024; e += blockDim.x) {
     const int q = e >> 6, l = e & 63;
     const double s = red[0][q][l] + red[1][q][l] + red[2][q][l] + red[3][q][l];
-    const int row = (q & 3) + 8 * (q >> 2) + 4 * (l >> 5);
-    const int col = l & 31;
-    out[(int64_t)(i0 + row) * cb + (j0 + col)] = s;
+    const int row = i0 + (q & 3) + 8 * (q >> 2) + 4 * (l >> 5);
+    const int col = j0 + (l & 31);
+    if (row < ca && col < cb) out[(int64_t)row * cb + col] = s;
   }
 }
 
@@ -102,7 +109,7 @@ extern "C" hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B,
                                          double* partial, size_t partial_elems, double* out,
                                          const int* cond, hipStream_t stream) {
   const int ca = A.count * A.width, cb = B.count * B.width;
-  const int nti = ca / 32, ntj = cb / 32;
+  const int nti = (ca + 31) / 32, ntj = (cb + 31) / 32;
   const int ntiles = nti * ntj;
   // chunk count: ~1024 workgroups with >= 512 rows per chunk, partials within the buffer
   int64_t nchunks = (n + 511) / 512;
@@ -130,7 +137,7 @@ extern "C" hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B,
 // (ldg columns).  Output / C blocks have width W (32 or 64), NT = cb / 32 tiles per wave.
 template <int NT>
 __global__ __launch_bounds__(256) void ts_nn_kernel(BlockList A, const float* __restrict__ G,
-                                                    int ldg, OutBlockList O, BlockList C,
+                                                    int ldg, int cb, OutBlockList O, BlockList C,
                                                     float alpha, float beta, int64_t n,
                                                     const int* cond) {
   if (cond && *cond == 0) return;
@@ -154,13 +161,16 @@ __global__ __launch_bounds__(256) void ts_nn_kernel(BlockList A, const float* __
     for (int m = 0; m < 4; ++m) {
       const float* gp = G + (int64_t)(kk + 4 * h + m) * ldg + i;
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[m], gp[t * 32], acc[t], 0, 0, 0);
+      for (int t = 0; t < NT; ++t) {
+        const float g = (t * 32 + i < cb) ? gp[t * 32] : 0.f;
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[m], g, acc[t], 0, 0, 0);
+      }
     }
   }
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int col = t * 32 + i;
+    if (col >= cb) continue;
     float* ob = O.blk[col / O.width] + (col % O.width);
     const float* cbp = (beta != 0.f) ? C.blk[col / C.width] + (col % C.width) : nullptr;
 #pragma unroll
@@ -175,16 +185,71 @@ __global__ __launch_bounds__(256) void ts_nn_kernel(BlockList A, const float* __
   }
 }
 
+// Narrow outputs (cb <= 16, the Krylov block at b = 8/16): one thread per row, coefficients
+// staged in LDS and read as broadcasts, A rows read as 16-B loads (consecutive lanes read
+// consecutive rows of a block: coalesced).  VALU FMAs; the pass is HBM-bound on A.
+template <int CB>
+__global__ __launch_bounds__(256) void ts_nn_rows_kernel(BlockList A, const float* __restrict__ G,
+                                                         int ldg, int cb, OutBlockList O,
+                                                         BlockList C, float alpha, float beta,
+                                                         int64_t n, const int* cond) {
+  if (cond && *cond == 0) return;
+  extern __shared__ __attribute__((aligned(16))) float gs[];
+  const int ca = A.count * A.width;
+  for (int e = threadIdx.x; e < ca * CB; e += blockDim.x) {
+    const int k = e / CB, j = e % CB;
+    gs[e] = (j < cb) ? G[(int64_t)k * ldg + j] : 0.f;
+  }
+  __syncthreads();
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= n) return;
+  float acc[CB];
+#pragma unroll
+  for (int j = 0; j < CB; ++j) acc[j] = 0.f;
+  const int w = A.width;
+  for (int q = 0; q < A.count; ++q) {
+    const float* ap = A.blk[q] + row * (int64_t)w;
+    for (int kk = 0; kk < w; kk += 4) {
+      const f32x4 a4 = *reinterpret_cast<const f32x4*>(ap + kk);
+      const float* g = gs + (q * w + kk) * CB;
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int j = 0; j < CB; ++j) acc[j] += a4[m] * g[m * CB + j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < CB; ++j) {
+    if (j >= cb) break;
+    float v = alpha * acc[j];
+    if (beta != 0.f) v += beta * C.blk[j / C.width][row * (int64_t)C.width + (j % C.width)];
+    O.blk[j / O.width][row * (int64_t)O.width + (j % O.width)] = v;
+  }
+}
+
 extern "C" hipError_t n2v2r_launch_ts_nn(const BlockList& A, const float* G, int ldg, int cb,
                                          const OutBlockList& O, const BlockList& C, float alpha,
                                          float beta, int64_t n, const int* cond,
                                          hipStream_t stream) {
+  if ((A.count * A.width) % 8 != 0 || A.width % 8 != 0) return hipErrorInvalidValue;
+  const size_t lds8 = sizeof(float) * (size_t)A.count * A.width * 8;
+  const size_t lds16 = 2 * lds8;
+  if (cb <= 8 && lds8 <= 64 * 1024) {
+    hipLaunchKernelGGL(ts_nn_rows_kernel<8>, dim3((unsigned)((n + 255) / 256)), dim3(256), lds8,
+                       stream, A, G, ldg, cb, O, C, alpha, beta, n, cond);
+    return hipGetLastError();
+  }
+  if (cb <= 16 && lds16 <= 64 * 1024) {
+    hipLaunchKernelGGL(ts_nn_rows_kernel<16>, dim3((unsigned)((n + 255) / 256)), dim3(256), lds16,
+                       stream, A, G, ldg, cb, O, C, alpha, beta, n, cond);
+    return hipGetLastError();
+  }
   dim3 grid((unsigned)((n + 127) / 128));
-  switch (cb / 32) {
-    case 1: hipLaunchKernelGGL(ts_nn_kernel<1>, grid, dim3(256), 0, stream, A, G, ldg, O, C, alpha, beta, n, cond); break;
-    case 2: hipLaunchKernelGGL(ts_nn_kernel<2>, grid, dim3(256), 0, stream, A, G, ldg, O, C, alpha, beta, n, cond); break;
-    case 3: hipLaunchKernelGGL(ts_nn_kernel<3>, grid, dim3(256), 0, stream, A, G, ldg, O, C, alpha, beta, n, cond); break;
-    case 4: hipLaunchKernelGGL(ts_nn_kernel<4>, grid, dim3(256), 0, stream, A, G, ldg, O, C, alpha, beta, n, cond); break;
+  switch ((cb + 31) / 32) {
+    case 1: hipLaunchKernelGGL(ts_nn_kernel<1>, grid, dim3(256), 0, stream, A, G, ldg, cb, O, C, alpha, beta, n, cond); break;
+    case 2: hipLaunchKernelGGL(ts_nn_kernel<2>, grid, dim3(256), 0, stream, A, G, ldg, cb, O, C, alpha, beta, n, cond); break;
+    case 3: hipLaunchKernelGGL(ts_nn_kernel<3>, grid, dim3(256), 0, stream, A, G, ldg, cb, O, C, alpha, beta, n, cond); break;
+    case 4: hipLaunchKernelGGL(ts_nn_kernel<4>, grid, dim3(256), 0, stream, A, G, ldg, cb, O, C, alpha, beta, n, cond); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -280,6 +345,125 @@ __global__ __launch_bounds__(1024) void chol_inv_kernel(const double* __restrict
   if (tid == 0) *any_flag = any;
 }
 
+// Fused block classical Gram-Schmidt + Cholesky QR ("Pythagorean" form): given
+// G = [Q Z]^T Z ((c + b) x b, fp64) with C = Q^T Z (first c rows) and Z^T Z (last b rows),
+// P = Z^T Z - C^T C is the Gram matrix of Z - Q C; P = R^T R and the NN coefficients
+// F = [-C R^{-1}; R^{-1}] ((c + b) x b, fp32) give Z <- (Z - Q C) R^{-1} in ONE pass over
+// [Q Z].  Rank-deficient columns (pivot below 1e-10 max diag) get a zero F column and a flag.
+__global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict__ G, int c, int b,
+                                                        float* __restrict__ F, int* flags,
+                                                        int* any_flag, const int* cond) {
+  if (cond && *cond == 0) {
+    if (threadIdx.x < b) flags[threadIdx.x] = 0;
+    if (threadIdx.x == 0) *any_flag = 0;
+    return;
+  }
+  __shared__ double R[64][65];
+  __shared__ double X[64][65];
+  __shared__ double piv[64];
+  __shared__ int bad[64];
+  __shared__ double dmax;
+  const int tid = threadIdx.x;
+  const int nt = blockDim.x;
+  // P = Gzz - C^T C (symmetrised); the c-long sums are split over k-slices of the 1024
+  // threads and folded through LDS in fixed order
+  __shared__ double part[16][64];
+  const int bb = b * b;
+  if (bb <= 64) {
+    const int e = tid % 64, slice = tid / 64;  // 16 slices of 64 threads
+    double acc = 0.0;
+    if (e < bb) {
+      const int i = e / b, j = e % b;
+      for (int k = slice; k < c; k += 16) acc += G[(int64_t)k * b + i] * G[(int64_t)k * b + j];
+    }
+    part[slice][e] = acc;
+    __syncthreads();
+    if (tid < bb) {
+      const int i = tid / b, j = tid % b;
+      double s = 0.5 * (G[(int64_t)(c + i) * b + j] + G[(int64_t)(c + j) * b + i]);
+      for (int sl = 0; sl < 16; ++sl) s -= part[sl][tid];
+      R[i][j] = s;
+    }
+  } else {
+    for (int e = tid; e < bb; e += nt) {
+      const int i = e / b, j = e % b;
+      double s = 0.5 * (G[(int64_t)(c + i) * b + j] + G[(int64_t)(c + j) * b + i]);
+      for (int k = 0; k < c; ++k) s -= G[(int64_t)k * b + i] * G[(int64_t)k * b + j];
+      R[i][j] = s;
+    }
+  }
+  for (int e = tid; e < bb; e += nt) X[e / b][e % b] = (e / b == e % b) ? 1.0 : 0.0;
+  if (tid < 64) bad[tid] = 0;
+  __syncthreads();
+  if (tid < 64) {
+    double m = (tid < b) ? R[tid][tid] : 0.0;
+    for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    if (tid == 0) dmax = m;
+  }
+  __syncthreads();
+  const double tiny = 1e-10 * dmax;
+  for (int j = 0; j < b; ++j) {
+    if (tid == 0) {
+      const double p = R[j][j];
+      if (!(p > tiny)) {
+        bad[j] = 1;
+        piv[j] = 0.0;
+      } else {
+        piv[j] = sqrt(p);
+      }
+    }
+    __syncthreads();
+    const double pj = piv[j];
+    const int isbad = bad[j];
+    for (int cc = j + tid; cc < b; cc += nt)
+      R[j][cc] = isbad ? (cc == j ? 1.0 : 0.0) : (cc == j ? pj : R[j][cc] / pj);
+    __syncthreads();
+    const int m = b - j - 1;
+    for (int e = tid; e < m * m; e += nt) {
+      const int r = j + 1 + e / m, cc = j + 1 + e % m;
+      if (cc >= r) R[r][cc] -= R[j][r] * R[j][cc];
+    }
+    __syncthreads();
+  }
+  for (int j = b - 1; j >= 0; --j) {
+    const double inv = 1.0 / R[j][j];
+    for (int cc = tid; cc < b; cc += nt) X[j][cc] *= inv;
+    __syncthreads();
+    for (int e = tid; e < j * b; e += nt) {
+      const int r = e / b, cc = e % b;
+      X[r][cc] -= R[r][j] * X[j][cc];
+    }
+    __syncthreads();
+  }
+  // F = [-C X; X], flagged columns zeroed
+  for (int e = tid; e < (c + b) * b; e += nt) {
+    const int r = e / b, j = e % b;
+    double v = 0.0;
+    if (!bad[j]) {
+      if (r < c) {
+        for (int k = 0; k <= j; ++k) v -= G[(int64_t)r * b + k] * X[k][j];
+      } else {
+        v = X[r - c][j];
+      }
+    }
+    F[e] = (float)v;
+  }
+  if (tid < b) flags[tid] = bad[tid];
+  if (tid == 0) {
+    int any = 0;
+    for (int j = 0; j < b; ++j) any |= bad[j];
+    *any_flag = any;
+  }
+}
+
+extern "C" hipError_t n2v2r_launch_pip_chol(const double* G, int c, int b, float* F, int* flags,
+                                            int* any_flag, const int* cond, hipStream_t stream) {
+  if (b > 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pip_chol_kernel, dim3(1), dim3(1024), 0, stream, G, c, b, F, flags, any_flag,
+                     cond);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t n2v2r_launch_chol_inv(const double* G, int b, float* Rinv, int* flags,
                                             int* any_flag, hipStream_t stream) {
   if (b > 64) return hipErrorInvalidValue;
@@ -291,23 +475,26 @@ extern "C" hipError_t n2v2r_launch_chol_inv(const double* G, int b, float* Rinv,
 __global__ void fill_normal_kernel(float* __restrict__ blk, int w, int64_t n, uint64_t seed,
                                    const int* flags, const int* cond) {
   if (cond && *cond == 0) return;
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n * w) return;
-  const int col = (int)(e % w);
-  if (flags && !flags[col]) return;
-  const uint64_t h1 = splitmix64(seed ^ (uint64_t)e * 0x2545F4914F6CDD1Dull);
-  const uint64_t h2 = splitmix64(h1);
-  const double u1 = ((h1 >> 11) + 1.0) * (1.0 / 9007199254740993.0);
-  const double u2 = (h2 >> 11) * (1.0 / 9007199254740992.0);
-  blk[e] = (float)(sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2));
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * w;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int col = (int)(e % w);
+    if (flags && !flags[col]) continue;
+    const uint64_t h1 = splitmix64(seed ^ (uint64_t)e * 0x2545F4914F6CDD1Dull);
+    const uint64_t h2 = splitmix64(h1);
+    const double u1 = ((h1 >> 11) + 1.0) * (1.0 / 9007199254740993.0);
+    const double u2 = (h2 >> 11) * (1.0 / 9007199254740992.0);
+    blk[e] = (float)(sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2));
+  }
 }
 
 extern "C" hipError_t n2v2r_launch_fill_normal(float* blk, int w, int64_t n, uint64_t seed,
                                                const int* flags, const int* cond,
                                                hipStream_t stream) {
   const int64_t elems = n * w;
-  hipLaunchKernelGGL(fill_normal_kernel, dim3((unsigned)((elems + 255) / 256)), dim3(256), 0,
-                     stream, blk, w, n, seed, flags, cond);
+  int64_t nb = (elems + 255) / 256;
+  if (nb > 2048) nb = 2048;
+  hipLaunchKernelGGL(fill_normal_kernel, dim3((unsigned)nb), dim3(256), 0, stream, blk, w, n, seed,
+                     flags, cond);
   return hipGetLastError();
 }
 

@@ -23,6 +23,7 @@
 #include <memory>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/n2v2r.h"
@@ -61,6 +62,8 @@ hipError_t n2v2r_launch_f64_to_f32(const double* in, float* out, int64_t elems, 
                                    const int* cond, hipStream_t stream);
 hipError_t n2v2r_launch_chol_inv(const double* G, int b, float* Rinv, int* flags, int* any_flag,
                                  hipStream_t stream);
+hipError_t n2v2r_launch_pip_chol(const double* G, int c, int b, float* F, int* flags,
+                                 int* any_flag, const int* cond, hipStream_t stream);
 hipError_t n2v2r_launch_fill_normal(float* blk, int w, int64_t n, uint64_t seed, const int* flags,
                                     const int* cond, hipStream_t stream);
 hipError_t n2v2r_launch_resid(const BlockList& X, const BlockList& MX, const double* theta,
@@ -357,40 +360,44 @@ struct Eig {
     t_spmm += now_ms() - t0;
   }
 
-  // Z -= Q (Q^T Z), Q = nq blocks
-  void cgs(float* Z, int nq, const int* cond) {
-    const int c = nq * b;
-    HIPCHK(n2v2r_launch_ts_tn(blocks(Q, 0, nq), one(Z), n, h->partial.as<double>(),
-                              h->partial_elems, gsmall.as<double>(), cond, st));
-    HIPCHK(n2v2r_launch_f64_to_f32(gsmall.as<double>(), csmall.as<float>(), (int64_t)c * b, -1.f,
-                                   cond, st));
-    HIPCHK(n2v2r_launch_ts_nn(blocks(Q, 0, nq), csmall.as<float>(), b, b, out_one(Z), one(Z),
-                              1.f, 1.f, n, cond, st));
+  // One fused BCGS + CholQR pass: G = [Q Z]^T Z -> F -> Z <- [Q Z] F, refill deficient columns.
+  // `cond` (device int, nullptr = always) skips the whole pass when zero.
+  void pip_pass(float* Z, const std::vector<float*>& basis, const int* cond, int* flags_out,
+                int* any_out) {
+    const int nq = (int)basis.size();
+    std::vector<float*> qz(basis);
+    qz.push_back(Z);
+    const BlockList L = blocks(qz, 0, nq + 1);
+    HIPCHK(n2v2r_launch_ts_tn(L, one(Z), n, h->partial.as<double>(), h->partial_elems,
+                              gsmall.as<double>(), cond, st));
+    HIPCHK(n2v2r_launch_pip_chol(gsmall.as<double>(), nq * b, b, csmall.as<float>(), flags_out,
+                                 any_out, cond, st));
+    HIPCHK(n2v2r_launch_ts_nn(L, csmall.as<float>(), b, b, out_one(Z), one(nullptr), 1.f, 0.f, n,
+                              cond, st));
+    HIPCHK(n2v2r_launch_fill_normal(Z, b, n, seed ^ (0xABCDull + ++fill_counter), flags_out,
+                                    any_out, st));
   }
 
-  void cholqr(float* Z, bool refill) {
-    HIPCHK(n2v2r_launch_ts_tn(one(Z), one(Z), n, h->partial.as<double>(), h->partial_elems,
-                              gsmall.as<double>(), nullptr, st));
-    HIPCHK(n2v2r_launch_chol_inv(gsmall.as<double>(), b, rinv.as<float>(), flg.as<int>(),
-                                 anyflag.as<int>(), st));
-    HIPCHK(n2v2r_launch_ts_nn(one(Z), rinv.as<float>(), b, b, out_one(Z), one(Z), 1.f, 0.f, n,
-                              nullptr, st));
-    if (refill)
-      HIPCHK(n2v2r_launch_fill_normal(Z, b, n, seed ^ (0xABCDull + ++fill_counter), flg.as<int>(),
-                                      anyflag.as<int>(), st));
-  }
-
-  // orthonormalise Z against Q[0..nq) and within itself
-  void orthonormalize(float* Z, int nq) {
+  // orthonormalise Z against Q[0..nq) and within itself: two fused passes (BCGS-PIP2), a third
+  // only when the second one had to refill a rank-deficient column.
+  void orthonormalize(float* Z, const std::vector<float*>& basis) {
     const double t0 = now_ms();
-    if (nq > 0) {
-      cgs(Z, nq, nullptr);
-      cgs(Z, nq, nullptr);
-    }
-    cholqr(Z, true);
-    if (nq > 0) cgs(Z, nq, anyflag.as<int>());
-    cholqr(Z, false);
+    pip_pass(Z, basis, nullptr, flg.as<int>(), anyflag.as<int>());
+    pip_pass(Z, basis, nullptr, flg.as<int>() + 64, anyflag.as<int>() + 1);
+    pip_pass(Z, basis, anyflag.as<int>() + 1, flg.as<int>() + 128, anyflag.as<int>() + 2);
     t_ortho += now_ms() - t0;
+  }
+
+  // z = orth(W_from) against `basis`, w = M z; appended to (qs, ws)
+  void expand_one(const float* w_from, const std::vector<float*>& basis, std::vector<float*>& qs,
+                  std::vector<float*>& ws) {
+    float* z = take();
+    HIPCHK(hipMemcpyAsync(z, w_from, sizeof(float) * n * b, hipMemcpyDeviceToDevice, st));
+    orthonormalize(z, basis);
+    float* w = take();
+    apply_M(z, w);
+    qs.push_back(z);
+    ws.push_back(w);
   }
 
   int run(int d_, const n2v2r_eig_opts& o, std::vector<double>& theta_out, float* Uout,
@@ -399,19 +406,25 @@ struct Eig {
     seed = o.seed ? o.seed : 0x5EEDull;
     const double tol = o.tol > 0 ? o.tol : 1e-6;
     const int max_restarts = o.max_restarts > 0 ? o.max_restarts : 2000;
-    b = o.block ? o.block : 32;
-    if (b != 32 && b != 64) throw StatusFail{N2V2R_ERR_BAD_ARG, "block must be 32 or 64"};
-    int keep = o.keep ? o.keep : std::max(d + 16, (d * 5) / 4);
-    keep = ((keep + b - 1) / b) * b;
+    b = o.block ? o.block : 8;
+    if (b != 8 && b != 16 && b != 32 && b != 64)
+      throw StatusFail{N2V2R_ERR_BAD_ARG, "block must be 8, 16, 32 or 64"};
+    // small graphs: shrink the block until the Krylov space fits well inside R^n
+    int keep = 0, maxc = 0;
+    for (;; b /= 2) {
+      keep = o.keep ? o.keep : std::max(d + 16, (d * 5) / 4);
+      keep = ((keep + b - 1) / b) * b;
+      maxc = o.max_basis ? o.max_basis : std::max(keep + 3 * b, (16 * keep) / 5);
+      maxc = ((maxc + b - 1) / b) * b;
+      const int cap =
+          (int)std::min<int64_t>((n / 2) / b * b, (int64_t)(N2V2R_MAX_BLOCKS - 1) * b);
+      if (maxc > cap) maxc = cap;
+      if (maxc >= keep + b) break;
+      if (b == 8)
+        throw StatusFail{N2V2R_ERR_BAD_ARG,
+                         "graph too small for the requested dimension: need n >= 2*(keep+8)"};
+    }
     pb = keep / b;
-    int maxc = o.max_basis ? o.max_basis : std::max(keep + 3 * b, 3 * keep);
-    maxc = ((maxc + b - 1) / b) * b;
-    // the Krylov space must stay well inside R^n
-    const int cap = (int)std::min<int64_t>((n / 2) / b * b, (int64_t)(N2V2R_MAX_BLOCKS - 1) * b);
-    if (maxc > cap) maxc = cap;
-    if (maxc < keep + b)
-      throw StatusFail{N2V2R_ERR_BAD_ARG,
-                       "graph too small for the requested dimension: need n >= 2*(keep+block)"};
     nb_max = maxc / b;
     const int c_max = maxc;
     // scratch
@@ -425,20 +438,19 @@ struct Eig {
     gsmall.ensure(sizeof(double) * (size_t)c_max * c_max);
     csmall.ensure(sizeof(float) * (size_t)c_max * c_max);
     rinv.ensure(sizeof(float) * 64 * 64);
-    flg.ensure(sizeof(int) * 64);
+    flg.ensure(sizeof(int) * 256);
     anyflag.ensure(sizeof(int) * 4);
     h->theta.ensure(sizeof(double) * c_max);
     h->resid.ensure(sizeof(double) * c_max);
 
-    std::vector<double> Hh((size_t)c_max * c_max), Sh((size_t)c_max * keep), wh(keep);
-    std::vector<float> Sf((size_t)c_max * keep);
+    std::vector<double> Sh((size_t)c_max * keep), wh(keep);
     std::vector<double> res2(keep);
 
     // start block
     float* q0 = take();
     HIPCHK(n2v2r_launch_fill_normal(q0, b, n, seed, nullptr, nullptr, st));
     Q.assign(1, q0);
-    orthonormalize(q0, 0);
+    orthonormalize(q0, {});
     W.assign(1, take());
     apply_M(Q[0], W[0]);
     int apps = 1;
@@ -450,41 +462,86 @@ struct Eig {
     int stagnated = 0;
     const double t_start = now_ms();
     double t_rr = 0;
+    // pinned host staging for the projected matrix and the Ritz coefficients
+    double* Hh = nullptr;
+    float* Sf = nullptr;
+    HIPCHK(hipHostMalloc((void**)&Hh, sizeof(double) * (size_t)c_max * c_max, 0));
+    HIPCHK(hipHostMalloc((void**)&Sf, sizeof(float) * (size_t)c_max * keep, 0));
+    struct PinnedFree {
+      double* h;
+      float* s;
+      ~PinnedFree() {
+        if (h) (void)hipHostFree(h);
+        if (s) (void)hipHostFree(s);
+      }
+    } pinned_guard{Hh, Sf};
+    hipEvent_t ev_h, ev_e0, ev_e1;
+    HIPCHK(hipEventCreateWithFlags(&ev_h, hipEventDisableTiming));
+    HIPCHK(hipEventCreate(&ev_e0));
+    HIPCHK(hipEventCreate(&ev_e1));
+    struct EvFree {
+      hipEvent_t a, b, c;
+      ~EvFree() {
+        (void)hipEventDestroy(a);
+        (void)hipEventDestroy(b);
+        (void)hipEventDestroy(c);
+      }
+    } ev_guard{ev_h, ev_e0, ev_e1};
+    // extra blocks expanded (against the old basis) while the host solves the projected
+    // problem; adapted so that their GPU time covers the host Rayleigh-Ritz time
+    int extras = 0;
+    if (o.overlap == -2) extras = std::max(1, std::min(nb_max - pb - 1, (nb_max - pb) / 2));
+    if (o.overlap > 0) extras = std::min(o.overlap, nb_max - pb - 1);
+    const bool adaptive = o.overlap == -2;
+    double t_blk_est = 0.0;
     for (;; ++cycle) {
+      const double tcy0 = now_ms();
+      int nexp = 0;
       while ((int)Q.size() < nb_max) {
-        float* z = take();
-        HIPCHK(hipMemcpyAsync(z, W.back(), sizeof(float) * n * b, hipMemcpyDeviceToDevice, st));
-        orthonormalize(z, (int)Q.size());
-        Q.push_back(z);
-        float* w = take();
-        apply_M(z, w);
-        W.push_back(w);
+        expand_one(W.back(), Q, Q, W);
         ++apps;
+        ++nexp;
       }
       const int nq = (int)Q.size();
       const int c = nq * b;
-      // H = Q^T W
-      {
-        const double t0 = now_ms();
-        HIPCHK(n2v2r_launch_ts_tn(blocks(Q, 0, nq), blocks(W, 0, nq), n, h->partial.as<double>(),
-                                  h->partial_elems, gsmall.as<double>(), nullptr, st));
-        t_ortho += now_ms() - t0;
-      }
-      HIPCHK(hipMemcpyAsync(Hh.data(), gsmall.as<double>(), sizeof(double) * c * c,
+      // H = Q^T W -> pinned host, then the host solves it on a worker thread
+      HIPCHK(n2v2r_launch_ts_tn(blocks(Q, 0, nq), blocks(W, 0, nq), n, h->partial.as<double>(),
+                                h->partial_elems, gsmall.as<double>(), nullptr, st));
+      HIPCHK(hipMemcpyAsync(Hh, gsmall.as<double>(), sizeof(double) * c * c,
                             hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
-      const double tr0 = now_ms();
-      for (int i = 0; i < c; ++i)
-        for (int j = 0; j < i; ++j) {
-          const double s = 0.5 * (Hh[(size_t)i * c + j] + Hh[(size_t)j * c + i]);
-          Hh[(size_t)i * c + j] = s;
-          Hh[(size_t)j * c + i] = s;
+      HIPCHK(hipEventRecord(ev_h, st));
+      double rr_ms = 0.0;
+      int rr_status = 0;
+      std::thread rr([&]() {
+        if (hipEventSynchronize(ev_h) != hipSuccess) {
+          rr_status = -1;
+          return;
         }
-      if (n2v2r_host_sym_eig_top(c, Hh.data(), keep, wh.data(), Sh.data()) != 0)
+        const double tr0 = now_ms();
+        for (int i = 0; i < c; ++i)
+          for (int j = 0; j < i; ++j) {
+            const double sv = 0.5 * (Hh[(size_t)i * c + j] + Hh[(size_t)j * c + i]);
+            Hh[(size_t)i * c + j] = sv;
+            Hh[(size_t)j * c + i] = sv;
+          }
+        rr_status = n2v2r_host_sym_eig_top(c, Hh, keep, wh.data(), Sh.data());
+        for (size_t i = 0; i < (size_t)c * keep; ++i) Sf[i] = (float)Sh[i];
+        rr_ms = now_ms() - tr0;
+      });
+      // meanwhile: continue the Krylov sequence against the un-restarted basis
+      std::vector<float*> E, EW, basis_e(Q);
+      HIPCHK(hipEventRecord(ev_e0, st));
+      for (int i = 0; i < extras; ++i) {
+        expand_one(i == 0 ? W.back() : EW.back(), basis_e, E, EW);
+        basis_e.push_back(E.back());
+        ++apps;
+      }
+      HIPCHK(hipEventRecord(ev_e1, st));
+      rr.join();
+      if (rr_status != 0)
         throw StatusFail{N2V2R_ERR_NO_CONVERGENCE, "Rayleigh-Ritz eigensolve failed"};
-      t_rr += now_ms() - tr0;
-      for (size_t i = 0; i < (size_t)c * keep; ++i) Sf[i] = (float)Sh[i];
-      HIPCHK(hipMemcpyAsync(csmall.as<float>(), Sf.data(), sizeof(float) * c * keep,
+      t_rr += rr_ms;
+      HIPCHK(hipMemcpyAsync(csmall.as<float>(), Sf, sizeof(float) * c * keep,
                             hipMemcpyHostToDevice, st));
       HIPCHK(hipMemcpyAsync(h->theta.as<double>(), wh.data(), sizeof(double) * keep,
                             hipMemcpyHostToDevice, st));
@@ -494,35 +551,22 @@ struct Eig {
         MX[q] = take();
       }
       const double to0 = now_ms();
-      for (int q0b = 0; q0b < pb; q0b += 4) {
-        const int nt = std::min(4, pb - q0b);  // output blocks in this launch (<= 128 cols)
+      const int per_launch = std::max(1, 128 / b);  // output blocks per ts_nn launch (<= 128 cols)
+      for (int q0b = 0; q0b < pb; q0b += per_launch) {
+        const int nt = std::min(per_launch, pb - q0b);
         OutBlockList ox{}, omx{};
         ox.width = omx.width = b;
-        // output blocks are b wide; ts_nn tiles are 32 wide -> cols = nt * b
-        const int cols = nt * b;
-        if (cols > 128) {
-          // b = 64: split into launches of 2 blocks
-        }
         ox.count = omx.count = nt;
         for (int t = 0; t < nt; ++t) {
           ox.blk[t] = X[q0b + t];
           omx.blk[t] = MX[q0b + t];
         }
-        // G slice: columns [q0b*b, q0b*b + cols) of S (ld = keep)
+        // G slice: columns [q0b*b, q0b*b + nt*b) of S (ld = keep)
         const float* g = csmall.as<float>() + q0b * b;
-        if (cols <= 128) {
-          HIPCHK(n2v2r_launch_ts_nn(blocks(Q, 0, nq), g, keep, cols, ox, one(nullptr), 1.f, 0.f, n,
-                                    nullptr, st));
-          HIPCHK(n2v2r_launch_ts_nn(blocks(W, 0, nq), g, keep, cols, omx, one(nullptr), 1.f, 0.f,
-                                    n, nullptr, st));
-        } else {
-          for (int t = 0; t < nt; ++t) {
-            HIPCHK(n2v2r_launch_ts_nn(blocks(Q, 0, nq), g + t * b, keep, b, out_one(X[q0b + t]),
-                                      one(nullptr), 1.f, 0.f, n, nullptr, st));
-            HIPCHK(n2v2r_launch_ts_nn(blocks(W, 0, nq), g + t * b, keep, b, out_one(MX[q0b + t]),
-                                      one(nullptr), 1.f, 0.f, n, nullptr, st));
-          }
-        }
+        HIPCHK(n2v2r_launch_ts_nn(blocks(Q, 0, nq), g, keep, nt * b, ox, one(nullptr), 1.f, 0.f, n,
+                                  nullptr, st));
+        HIPCHK(n2v2r_launch_ts_nn(blocks(W, 0, nq), g, keep, nt * b, omx, one(nullptr), 1.f, 0.f,
+                                  n, nullptr, st));
       }
       HIPCHK(n2v2r_launch_resid(blocks(X, 0, pb), blocks(MX, 0, pb), h->theta.as<double>(), n,
                                 h->partial.as<double>(), h->partial_elems, h->resid.as<double>(),
@@ -531,6 +575,17 @@ struct Eig {
                             hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
       t_ortho += now_ms() - to0;
+      // adapt the overlap: enough extra blocks that their GPU time covers the host solve
+      if (extras > 0 && adaptive) {
+        float ems = 0.f;
+        HIPCHK(hipEventElapsedTime(&ems, ev_e0, ev_e1));
+        const double per_blk = std::max(1e-3, (double)ems / extras);
+        t_blk_est = t_blk_est > 0 ? 0.5 * (t_blk_est + per_blk) : per_blk;
+        const int want = (int)std::ceil(1.1 * rr_ms / t_blk_est);
+        extras = std::max(1, std::min(nb_max - pb - 1, want));
+      }
+      (void)tcy0;
+      (void)nexp;
       maxres = 0;
       conv = 0;
       const double th1 = std::max(wh[0], 1e-300);
@@ -539,30 +594,37 @@ struct Eig {
         maxres = std::max(maxres, r);
         if (r <= tol) ++conv;
       }
-      if (conv == d || cycle + 1 >= max_restarts) break;
-      // fp32 noise floor: the true residual of W = M Q cannot fall below ~eps32 * sqrt(nnz/row)
-      // * theta_1.  Stop when the worst residual has stalled for 4 cycles within 100x of tol.
-      hist_res.push_back(maxres);
-      if (hist_res.size() >= 5) {
-        const double prev = *std::min_element(hist_res.end() - 5, hist_res.end() - 1);
-        if (maxres > 0.95 * prev && maxres <= 100.0 * tol) {
-          stagnated = 1;
-          break;
+      bool done = (conv == d || cycle + 1 >= max_restarts);
+      if (!done) {
+        // fp32 noise floor: the true residual of W = M Q cannot fall below ~eps32 *
+        // sqrt(nnz/row) * theta_1.  Stop when the worst residual has stalled for 4 cycles
+        // within 100x of tol.
+        hist_res.push_back(maxres);
+        if (hist_res.size() >= 5) {
+          const double prev = *std::min_element(hist_res.end() - 5, hist_res.end() - 1);
+          if (maxres > 0.95 * prev && maxres <= 100.0 * tol) {
+            stagnated = 1;
+            done = true;
+          }
         }
       }
-      // restart: next block from the old basis, then [X | next]
-      float* z = take();
-      HIPCHK(hipMemcpyAsync(z, W.back(), sizeof(float) * n * b, hipMemcpyDeviceToDevice, st));
-      orthonormalize(z, nq);
+      if (done) {
+        for (float* p : E) give(p);
+        for (float* p : EW) give(p);
+        break;
+      }
+      // restart: [X | extras]; the extras are orthogonal to the old basis, hence to X.
+      // Without overlap, the classic Krylov-Schur next block (W_last against the old basis).
+      if (E.empty()) {
+        expand_one(W.back(), Q, E, EW);
+        ++apps;
+      }
       for (float* p : Q) give(p);
       for (float* p : W) give(p);
       Q.assign(X.begin(), X.end());
       W.assign(MX.begin(), MX.end());
-      Q.push_back(z);
-      float* w = take();
-      apply_M(z, w);
-      W.push_back(w);
-      ++apps;
+      Q.insert(Q.end(), E.begin(), E.end());
+      W.insert(W.end(), EW.begin(), EW.end());
     }
     // U = first d columns of X (row stride ldu); theta
     theta_out.assign(wh.begin(), wh.begin() + d);
@@ -746,12 +808,12 @@ int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_sta
     eig.n = h->n;
     eig.K = h->K;
     eig.stats = stats;
-    const int b = o.block ? o.block : 32;
-    const int ldu = ((d + b - 1) / b) * b;
+    const int ldu = ((d + 63) / 64) * 64;  // a multiple of every block width
     h->U.ensure(sizeof(float) * h->n * ldu);
     HIPCHK(hipMemsetAsync(h->U.p, 0, sizeof(float) * h->n * ldu, h->stream));
     std::vector<double> theta;
     const int st = eig.run(d, o, theta, h->U.as<float>(), ldu);
+    const int b = eig.b;
     // deterministic signs: largest-magnitude entry of every column of U positive
     h->partial.ensure(sizeof(double) * 1024 * (size_t)ldu);
     h->colscale.ensure(sizeof(float) * ldu);
@@ -1053,7 +1115,8 @@ int n2v2r_column_sums(n2v2r_handle* h, int k, float* out) {
 int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, const float* X,
                      float* Y, double* avg_ms, double* algo_bytes) {
   return guarded(h, [&]() -> int {
-    if (k < 0 || k >= h->K || !h->layers[k]->loaded || (b != 32 && b != 64) || reps < 1 || !X)
+    if (k < 0 || k >= h->K || !h->layers[k]->loaded || (b != 8 && b != 16 && b != 32 && b != 64) ||
+        reps < 1 || !X)
       return N2V2R_ERR_BAD_ARG;
     const LayerDev& L = *h->layers[k];
     DevBuf xd, yd;

@@ -1,12 +1,13 @@
 // CSR x dense-panel SpMM for the Gram operator M = sum_k A_k A_k^T (gfx950, wave64).
 //
 // Layout: CSR per layer (int64 row pointers, int32 columns, fp32 values) resident in HBM;
-// dense panels row-major N x B fp32 (B = 32 or 64: one 128-B / 256-B line per row).
-// One wave owns one output row.  The row's column indices and values are loaded once,
-// coalesced, 64 at a time, and broadcast with __shfl; the wave then gathers NPS = 64 / (B/4)
-// panel rows per step, each by B/4 lanes with one 16-B load per lane, so a panel row is one
-// coalesced 128/256-B segment.  Partial sums of the NPS lane groups are folded with xor
-// shuffles and the B/4 lanes of group 0 store the output row with 16-B stores.
+// dense panels row-major N x B fp32 (B = 8, 16, 32 or 64: a 32..256-B segment per row).
+// A wave owns RPW output rows (a group of 64/RPW lanes per row, RPW picked from the mean row
+// length).  A row's column indices and values are loaded once, coalesced, one group-width at a
+// time, and broadcast with __shfl; the group then gathers panel rows, each by B/4 lanes with
+// one 16-B load per lane, so a panel row is one coalesced 32..256-B segment.  Partial sums are
+// folded with xor shuffles inside the group and its first B/4 lanes store the output row with
+// 16-B stores.
 // There is no LDS staging: an ER/co-expression row's columns are uniformly random, so a
 // workgroup has no panel reuse to stage; reuse comes from L2 / Infinity Cache.
 //
@@ -26,93 +27,137 @@ struct SpmmArgs {
   const float* colscale; // optional per-column scale of the output (nullptr = none)
 };
 
-template <int B>
+// RPW rows per wave: each row owns a group of L = 64 / RPW lanes; inside the group LPN = B / 4
+// lanes gather one panel row (one 16-B load each) and NPS = L / LPN panel rows are gathered
+// per step.  Short rows (ER / k-NN graphs: tens of nnz) then keep several rows' gathers in
+// flight per wave instead of leaving most lanes idle.
+template <int B, int RPW>
 __device__ __forceinline__ void spmm_row_accumulate(const CsrDev& A, const float* __restrict__ X,
-                                                    int64_t ldx, int64_t row, int lane,
-                                                    f32x4& acc) {
-  constexpr int LPN = B / 4;      // lanes per gathered panel row
-  constexpr int NPS = 64 / LPN;   // panel rows gathered per step
-  const int grp = lane / LPN;
-  const int sub = lane % LPN;
-  const int64_t beg = A.indptr[row];
-  const int64_t end = A.indptr[row + 1];
-  for (int64_t base = beg; base < end; base += 64) {
-    const int nn = (int)((end - base) < 64 ? (end - base) : 64);
+                                                    int64_t ldx, int64_t row, bool row_ok,
+                                                    int lane, f32x4& acc) {
+  constexpr int L = 64 / RPW;
+  constexpr int LPN = B / 4;
+  constexpr int NPS = L / LPN;
+  static_assert(NPS >= 1, "row group narrower than one panel row");
+  const int g = lane / L;
+  const int li = lane % L;
+  const int sub = li % LPN;
+  const int srcbase = g * L + li / LPN;
+  int64_t beg = 0, end = 0;
+  if (row_ok) {
+    beg = A.indptr[row];
+    end = A.indptr[row + 1];
+  }
+  // the wave loops until its longest row is done
+  int64_t len = end - beg;
+  int64_t maxlen = len;
+#pragma unroll
+  for (int m = L; m < 64; m <<= 1) {
+    const int64_t o = __shfl_xor(maxlen, m, 64);
+    maxlen = o > maxlen ? o : maxlen;
+  }
+  for (int64_t off = 0; off < maxlen; off += L) {
     int colv = 0;
     float valv = 0.f;
-    if (lane < nn) {
-      colv = A.indices[base + lane];
-      valv = A.data[base + lane];
+    if (off + li < len) {
+      colv = A.indices[beg + off + li];
+      valv = A.data[beg + off + li];
     }
+    int64_t rem = maxlen - off;
+    const int nn = (int)(rem < L ? rem : L);
     const int steps = (nn + NPS - 1) / NPS;
     int s = 0;
-    for (; s + 4 <= steps; s += 4) {
-      int c0 = __shfl(colv, (s + 0) * NPS + grp, 64);
-      int c1 = __shfl(colv, (s + 1) * NPS + grp, 64);
-      int c2 = __shfl(colv, (s + 2) * NPS + grp, 64);
-      int c3 = __shfl(colv, (s + 3) * NPS + grp, 64);
-      float v0 = __shfl(valv, (s + 0) * NPS + grp, 64);
-      float v1 = __shfl(valv, (s + 1) * NPS + grp, 64);
-      float v2 = __shfl(valv, (s + 2) * NPS + grp, 64);
-      float v3 = __shfl(valv, (s + 3) * NPS + grp, 64);
-      f32x4 x0 = *reinterpret_cast<const f32x4*>(X + (int64_t)c0 * ldx + sub * 4);
-      f32x4 x1 = *reinterpret_cast<const f32x4*>(X + (int64_t)c1 * ldx + sub * 4);
-      f32x4 x2 = *reinterpret_cast<const f32x4*>(X + (int64_t)c2 * ldx + sub * 4);
-      f32x4 x3 = *reinterpret_cast<const f32x4*>(X + (int64_t)c3 * ldx + sub * 4);
+    for (; s + 2 <= steps; s += 2) {
+      const int c0 = __shfl(colv, srcbase + (s + 0) * NPS, 64);
+      const int c1 = __shfl(colv, srcbase + (s + 1) * NPS, 64);
+      const float v0 = __shfl(valv, srcbase + (s + 0) * NPS, 64);
+      const float v1 = __shfl(valv, srcbase + (s + 1) * NPS, 64);
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(X + (int64_t)c0 * ldx + sub * 4);
+      const f32x4 x1 = *reinterpret_cast<const f32x4*>(X + (int64_t)c1 * ldx + sub * 4);
       acc += v0 * x0;
       acc += v1 * x1;
-      acc += v2 * x2;
-      acc += v3 * x3;
     }
-    for (; s < steps; ++s) {
-      int c0 = __shfl(colv, s * NPS + grp, 64);
-      float v0 = __shfl(valv, s * NPS + grp, 64);
-      f32x4 x0 = *reinterpret_cast<const f32x4*>(X + (int64_t)c0 * ldx + sub * 4);
+    if (s < steps) {
+      const int c0 = __shfl(colv, srcbase + s * NPS, 64);
+      const float v0 = __shfl(valv, srcbase + s * NPS, 64);
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(X + (int64_t)c0 * ldx + sub * 4);
       acc += v0 * x0;
     }
   }
 }
 
-template <int B>
+template <int B, int RPW>
 __global__ __launch_bounds__(256) void spmm_csr_panel_kernel(SpmmArgs args) {
+  constexpr int L = 64 / RPW;
   constexpr int LPN = B / 4;
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   const int k0 = args.sum ? 0 : (int)blockIdx.y;
   const int64_t n = args.A[k0].n_rows;
-  if (row >= n) return;
+  const int64_t wave_row0 = ((int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * RPW;
+  if (wave_row0 >= n) return;
+  const int64_t row = wave_row0 + lane / L;
+  const bool row_ok = row < n;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   if (args.sum) {
     for (int k = 0; k < args.K; ++k)
-      spmm_row_accumulate<B>(args.A[k], args.X[k], args.ldx, row, lane, acc);
+      spmm_row_accumulate<B, RPW>(args.A[k], args.X[k], args.ldx, row, row_ok, lane, acc);
   } else {
-    spmm_row_accumulate<B>(args.A[k0], args.X[k0], args.ldx, row, lane, acc);
+    spmm_row_accumulate<B, RPW>(args.A[k0], args.X[k0], args.ldx, row, row_ok, lane, acc);
   }
 #pragma unroll
-  for (int m = LPN; m < 64; m <<= 1) {
+  for (int m = LPN; m < L; m <<= 1) {
     acc.x += __shfl_xor(acc.x, m, 64);
     acc.y += __shfl_xor(acc.y, m, 64);
     acc.z += __shfl_xor(acc.z, m, 64);
     acc.w += __shfl_xor(acc.w, m, 64);
   }
-  if (lane < LPN) {
+  const int li = lane % L;
+  if (row_ok && li < LPN) {
     if (args.colscale) {
-      f32x4 sc = *reinterpret_cast<const f32x4*>(args.colscale + lane * 4);
+      f32x4 sc = *reinterpret_cast<const f32x4*>(args.colscale + li * 4);
       acc *= sc;
     }
-    *reinterpret_cast<f32x4*>(args.Y[k0] + row * args.ldy + lane * 4) = acc;
+    *reinterpret_cast<f32x4*>(args.Y[k0] + row * args.ldy + li * 4) = acc;
+  }
+}
+
+template <int B, int RPW>
+static void launch_spmm_t(const SpmmArgs& args, hipStream_t stream) {
+  const int64_t n = args.A[0].n_rows;
+  const int64_t waves = (n + RPW - 1) / RPW;
+  dim3 grid((unsigned)((waves + 3) / 4), args.sum ? 1 : args.K);
+  hipLaunchKernelGGL((spmm_csr_panel_kernel<B, RPW>), grid, dim3(256), 0, stream, args);
+}
+
+// rows per wave from the mean row length: a row group of L lanes gathers L / (B/4) panel rows
+// per step; aim for ~3-4 steps per row.
+template <int B>
+static void launch_spmm_b(const SpmmArgs& args, hipStream_t stream) {
+  double avg = 0.0;
+  int kk = args.sum ? args.K : args.K;
+  for (int k = 0; k < kk; ++k) avg += (double)args.A[k].nnz / (double)(args.A[k].n_rows > 0 ? args.A[k].n_rows : 1);
+  avg /= (kk > 0 ? kk : 1);
+  constexpr int LPN = B / 4;
+  const double want_l = LPN * avg / 3.5;
+  int rpw = 1;
+  while (rpw < 8 && 64 / (rpw * 2) >= LPN && 64.0 / (rpw * 2) >= want_l) rpw *= 2;
+  switch (rpw) {
+    case 8: if constexpr (64 / 8 >= LPN) { launch_spmm_t<B, 8>(args, stream); break; } [[fallthrough]];
+    case 4: if constexpr (64 / 4 >= LPN) { launch_spmm_t<B, 4>(args, stream); break; } [[fallthrough]];
+    case 2: launch_spmm_t<B, 2>(args, stream); break;
+    default: launch_spmm_t<B, 1>(args, stream); break;
   }
 }
 
 extern "C" hipError_t n2v2r_launch_spmm(const SpmmArgs& args, int B, hipStream_t stream) {
-  const int64_t n = args.A[0].n_rows;
-  const int waves_per_block = 4;
-  dim3 grid((unsigned)((n + waves_per_block - 1) / waves_per_block), args.sum ? 1 : args.K);
-  dim3 block(64 * waves_per_block);
-  if (B == 32)
-    hipLaunchKernelGGL(spmm_csr_panel_kernel<32>, grid, block, 0, stream, args);
+  if (B == 8)
+    launch_spmm_b<8>(args, stream);
+  else if (B == 16)
+    launch_spmm_b<16>(args, stream);
+  else if (B == 32)
+    launch_spmm_b<32>(args, stream);
   else if (B == 64)
-    hipLaunchKernelGGL(spmm_csr_panel_kernel<64>, grid, block, 0, stream, args);
+    launch_spmm_b<64>(args, stream);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

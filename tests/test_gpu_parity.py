@@ -261,3 +261,19 @@ def test_uase_residuals_er_20k(engine):
     np.testing.assert_allclose(X.T @ X, np.eye(d), atol=1e-5)
     _, s_ref, _ = orc.uase(layers, d, seed=42)
     np.testing.assert_allclose(s, s_ref, rtol=1e-5)
+
+
+@pytest.mark.parametrize("block", [8, 16, 64])
+@pytest.mark.parametrize("name", ["er_cfg1", "directed_weighted", "demo"])
+def test_uase_block_widths(engine, name, block):
+    """Every supported Krylov block width reproduces the reference embedding."""
+    fx = load_fixture(name)
+    layers = fixture_layers(fx)
+    d = int(fx["dims"].max())
+    engine.set_layers(layers)
+    engine.uase(d, seed=int(fx["seed"]), block=block)
+    np.testing.assert_allclose(engine.singular_values(), fx["sigma"], rtol=2e-5)
+    Ya = orc.align_signs(engine.embedding().astype(np.float64), fx["Y"])
+    env, _ = _envelope(layers, d, int(fx["seed"]))
+    err = np.abs(Ya - fx["Y"]).max() / np.abs(fx["Y"]).max()
+    assert err <= max(5e-4, 3 * env), (name, block, err, env)
