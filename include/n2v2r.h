@@ -70,7 +70,7 @@ typedef struct {
   double ms_total, ms_spmm, ms_ortho, ms_rr_host; /* wall-clock split */
   int64_t spmm_launches;     /* SpMM kernel launches (for roofline accounting) */
   double spmm_algo_bytes;    /* sum over launches of the SURVEY 8(d) algorithmic bytes */
-  int stagnated;             /* 1: stopped at the fp32 residual floor (within 100x tol) */
+  int stagnated;             /* 1: stopped at the fp32 residual floor (flat 8 cycles, <= 100x tol) */
 } n2v2r_eig_stats;
 
 /* lifecycle */

@@ -597,12 +597,12 @@ struct Eig {
       bool done = (conv == d || cycle + 1 >= max_restarts);
       if (!done) {
         // fp32 noise floor: the true residual of W = M Q cannot fall below ~eps32 *
-        // sqrt(nnz/row) * theta_1.  Stop when the worst residual has stalled for 4 cycles
-        // within 100x of tol.
+        // sqrt(nnz/row) * theta_1.  Stop when the worst residual has not improved by 2% over
+        // 8 cycles and is within 100x of tol.
         hist_res.push_back(maxres);
-        if (hist_res.size() >= 5) {
-          const double prev = *std::min_element(hist_res.end() - 5, hist_res.end() - 1);
-          if (maxres > 0.95 * prev && maxres <= 100.0 * tol) {
+        if (hist_res.size() >= 9) {
+          const double prev = *std::min_element(hist_res.end() - 9, hist_res.end() - 1);
+          if (maxres > 0.98 * prev && maxres <= 100.0 * tol) {
             stagnated = 1;
             done = true;
           }
