@@ -213,7 +213,7 @@ def main():
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "algo_bytes_per_launch": spmm_bytes, "avg_launch_ms": round(spmm_ms, 5)},
-        "eig": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in stats.items()},
+        "eig": {k: (float(f"{v:.4g}") if isinstance(v, float) else v) for k, v in stats.items()},
         "rank_ms": {"distances": round(ms_dist, 3), "borda": round(ms_borda, 3)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -47,9 +47,10 @@ enum { N2V2R_COSINE = 0, N2V2R_EUCLIDEAN = 1, N2V2R_CORRELATION = 2 };
 enum { N2V2R_SYM_DETECT = -1, N2V2R_SYM_NO = 0, N2V2R_SYM_YES = 1 };
 
 typedef struct n2v2r_handle n2v2r_handle;
+typedef struct n2v2r_simgroup n2v2r_simgroup;
 
 typedef struct {
-  int block;          /* Krylov block width b: 32 or 64 (0 = auto) */
+  int block;          /* Krylov block width b: 8, 16, 32 or 64 (0 = auto: 8) */
   int max_basis;      /* max basis columns before a thick restart (0 = auto) */
   int keep;           /* Ritz vectors kept at a restart (0 = auto) */
   int max_restarts;   /* (0 = auto: 2000) */
@@ -79,12 +80,37 @@ void n2v2r_destroy(n2v2r_handle* h);
 int n2v2r_last_error(const n2v2r_handle* h, char* buf, size_t len);
 const char* n2v2r_version(void);
 
+/* Row-partitioned multi-GPU (no reference counterpart: the reference is
+ * single-process).  Rank g of W owns rows [g*R, min(N,(g+1)*R)), R = ceil(N/W), of every layer,
+ * of every Krylov block and of the embedding; panels are all-gathered per SpMM stage and the
+ * small Gram / projection / residual reductions all-reduced.  Every rank calls every function
+ * in the same order (collective semantics).  Results: n2v2r_get_embedding /
+ * n2v2r_get_left_embedding return the LOCAL rows (n_local x d); distances, Borda, singular
+ * values and column sums are global on every rank.
+ *   RCCL, one process per GPU: rank 0 calls n2v2r_comm_unique_id, broadcasts the bytes
+ *   (N2V2R_UNIQUE_ID_BYTES) over its own control plane, every rank calls n2v2r_create_rccl.
+ *   Thread group, W ranks on ONE device in one process (tests): n2v2r_simgroup_create, then one
+ *   thread per rank calls n2v2r_create_sim and drives its handle. */
+#define N2V2R_UNIQUE_ID_BYTES 128
+int n2v2r_comm_unique_id(char* out, size_t len);
+int n2v2r_create_rccl(int device, int rank, int world, const char* unique_id, n2v2r_handle** out);
+int n2v2r_simgroup_create(int world, n2v2r_simgroup** out);
+void n2v2r_simgroup_destroy(n2v2r_simgroup* g);
+int n2v2r_create_sim(int device, n2v2r_simgroup* g, int rank, n2v2r_handle** out);
+int n2v2r_dist_info(const n2v2r_handle* h, int* rank, int* world, int64_t* row0, int64_t* n_local);
+
 /* graph layers: K layers over the same N nodes.  CSR is copied to HBM (int64 row pointers are
  * accepted; int32 column indices; fp32 values).  symmetric: N2V2R_SYM_* (DETECT compares the
  * pattern and values with the transpose on the host).  Non-symmetric layers also keep A^T. */
 int n2v2r_set_num_layers(n2v2r_handle* h, int num_layers, int64_t n);
 int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const int64_t* indptr,
                         const int32_t* indices, const float* data, int symmetric);
+/* distributed ingest without the global CSR on every rank: the caller's own rows
+ * [row0, row0 + n_rows) (must equal n2v2r_dist_info's) of a SYMMETRIC layer, indptr local
+ * (starting at 0), column indices global. */
+int n2v2r_set_layer_csr_rows(n2v2r_handle* h, int k, int64_t n, int64_t row0, int64_t n_rows,
+                             int64_t nnz, const int64_t* indptr, const int32_t* indices,
+                             const float* data);
 
 /* UASE: top-d truncated SVD of the unfolded [A_1 | ... | A_K]; embeddings stay in HBM. */
 int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_stats* stats);
@@ -113,8 +139,8 @@ int n2v2r_column_sums(n2v2r_handle* h, int k, float* out /* N */);
 int n2v2r_synchronize(n2v2r_handle* h);
 
 /* SpMM kernel alone (tests + roofline): Y = A_k X (transpose = 0) or A_k^T X (1) for a host
- * N x b panel X (b = 32 or 64), timed with HIP events on the engine stream over `reps`
- * launches after one warm-up.  avg_ms = mean launch duration; algo_bytes = SURVEY 8(d) bytes
+ * N x b panel X (b = 8, 16, 32 or 64), timed with HIP events on the engine stream over `reps`
+ * launches after one warm-up (single-GPU handles only).  avg_ms = mean launch duration; algo_bytes = SURVEY 8(d) bytes
  * per launch (8 nnz + 4 (N+1) + 8 N b).  Y may be NULL. */
 int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, const float* X,
                      float* Y, double* avg_ms, double* algo_bytes);

@@ -36,7 +36,10 @@ EXPORTED = [
     "n2v2r_rank", "n2v2r_get_distances", "n2v2r_get_borda", "n2v2r_rank_timing",
     "n2v2r_pairwise_distances", "n2v2r_borda_columns", "n2v2r_column_sums",
     "n2v2r_synchronize", "n2v2r_bench_spmm",
+    "n2v2r_comm_unique_id", "n2v2r_create_rccl", "n2v2r_simgroup_create",
+    "n2v2r_simgroup_destroy", "n2v2r_create_sim", "n2v2r_dist_info", "n2v2r_set_layer_csr_rows",
 ]
+UNIQUE_ID_BYTES = 128
 
 
 class ArpackNoConvergence(RuntimeError):
@@ -113,6 +116,15 @@ def load(path: str | None = None):
             "n2v2r_bench_spmm": (_i, [_vp, _i, _i, _i, _i, _p(np.float32), _vp,
                                       ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_double)]),
+            "n2v2r_comm_unique_id": (_i, [ctypes.c_char_p, ctypes.c_size_t]),
+            "n2v2r_create_rccl": (_i, [_i, _i, _i, ctypes.c_char_p, ctypes.POINTER(_vp)]),
+            "n2v2r_simgroup_create": (_i, [_i, ctypes.POINTER(_vp)]),
+            "n2v2r_simgroup_destroy": (None, [_vp]),
+            "n2v2r_create_sim": (_i, [_i, _vp, _i, ctypes.POINTER(_vp)]),
+            "n2v2r_dist_info": (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i),
+                                     ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
+            "n2v2r_set_layer_csr_rows": (_i, [_vp, _i, _i64, _i64, _i64, _i64, _p(np.int64),
+                                              _p(np.int32), _p(np.float32)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
@@ -122,19 +134,81 @@ def load(path: str | None = None):
         return lib
 
 
-class Engine:
-    """One GPU, one handle.  Thin, typed wrapper over the C-ABI."""
+def comm_unique_id() -> bytes:
+    """RCCL unique id (rank 0 creates it and broadcasts the bytes over its control plane)."""
+    lib = load()
+    buf = ctypes.create_string_buffer(UNIQUE_ID_BYTES)
+    st = lib.n2v2r_comm_unique_id(buf, UNIQUE_ID_BYTES)
+    if st != OK:
+        raise RuntimeError(f"n2v2r_comm_unique_id failed with status {st}")
+    return buf.raw
 
-    def __init__(self, device: int = 0):
+
+class SimGroup:
+    """W ranks as threads of one process on one GPU (the row-partitioned algorithm without W
+    devices).  Create one, then one thread per rank builds ``Engine.sim(device, group, r)``."""
+
+    def __init__(self, world: int):
         self.lib = load()
-        h = _vp()
-        st = self.lib.n2v2r_create(int(device), ctypes.byref(h))
+        g = _vp()
+        st = self.lib.n2v2r_simgroup_create(int(world), ctypes.byref(g))
         if st != OK:
-            raise RuntimeError(
-                f"n2v2r_create(device={device}) failed with status {st}: no usable HIP GPU "
-                "(the engine has no CPU fallback)")
+            raise RuntimeError(f"n2v2r_simgroup_create failed with status {st}")
+        self.g = g
+        self.world = int(world)
+
+    def close(self):
+        if getattr(self, "g", None):
+            self.lib.n2v2r_simgroup_destroy(self.g)
+            self.g = None
+
+
+class Engine:
+    """One GPU, one handle.  Thin, typed wrapper over the C-ABI.
+
+    Distributed handles (``Engine.rccl`` / ``Engine.sim``) own rows [row0, row0 + n_local) of
+    the node set: ``embedding()`` / ``left_embedding()`` return those rows; distances, Borda,
+    singular values and column sums are global on every rank."""
+
+    def __init__(self, device: int = 0, _handle=None):
+        self.lib = load()
+        if _handle is None:
+            h = _vp()
+            st = self.lib.n2v2r_create(int(device), ctypes.byref(h))
+            if st != OK:
+                raise RuntimeError(
+                    f"n2v2r_create(device={device}) failed with status {st}: no usable HIP GPU "
+                    "(the engine has no CPU fallback)")
+        else:
+            h = _handle
         self.h = h
         self.device = device
+
+    @classmethod
+    def rccl(cls, device: int, rank: int, world: int, unique_id: bytes) -> "Engine":
+        lib = load()
+        h = _vp()
+        st = lib.n2v2r_create_rccl(int(device), int(rank), int(world), bytes(unique_id),
+                                   ctypes.byref(h))
+        if st != OK:
+            raise RuntimeError(f"n2v2r_create_rccl(rank={rank}, world={world}) failed: {st}")
+        return cls(device, _handle=h)
+
+    @classmethod
+    def sim(cls, device: int, group: SimGroup, rank: int) -> "Engine":
+        lib = load()
+        h = _vp()
+        st = lib.n2v2r_create_sim(int(device), group.g, int(rank), ctypes.byref(h))
+        if st != OK:
+            raise RuntimeError(f"n2v2r_create_sim(rank={rank}) failed with status {st}")
+        return cls(device, _handle=h)
+
+    def dist_info(self):
+        """(rank, world, row0, n_local) of this handle's row block."""
+        r, w, r0, nl = _i(), _i(), _i64(), _i64()
+        self._check(self.lib.n2v2r_dist_info(self.h, ctypes.byref(r), ctypes.byref(w),
+                                             ctypes.byref(r0), ctypes.byref(nl)), "dist_info")
+        return r.value, w.value, r0.value, nl.value
 
     def close(self):
         if getattr(self, "h", None):
@@ -192,6 +266,27 @@ class Engine:
         self.n = n
         self.num_layers = len(mats)
 
+    def set_layer_rows(self, n: int, num_layers: int, local_layers):
+        """Distributed ingest of symmetric layers from this rank's own rows only:
+        ``local_layers[k]`` is the (n_local x n) CSR block of rows [row0, row0 + n_local)."""
+        import scipy.sparse as sp
+        self._check(self.lib.n2v2r_set_num_layers(self.h, int(num_layers), int(n)),
+                    "set_num_layers")
+        _, _, row0, nl = self.dist_info()
+        for k, blk in enumerate(local_layers):
+            m = sp.csr_matrix(blk, dtype=np.float32)
+            m.sum_duplicates()
+            m.sort_indices()
+            if m.shape != (nl, n):
+                raise ValueError(f"layer {k}: local block must be {nl} x {n}, got {m.shape}")
+            self._check(self.lib.n2v2r_set_layer_csr_rows(
+                self.h, k, int(n), int(row0), int(nl), int(m.nnz),
+                np.ascontiguousarray(m.indptr, dtype=np.int64),
+                np.ascontiguousarray(m.indices, dtype=np.int32),
+                np.ascontiguousarray(m.data, dtype=np.float32)), f"layer {k} rows")
+        self.n = int(n)
+        self.num_layers = int(num_layers)
+
     # -- UASE ------------------------------------------------------------------------------
     def uase(self, d: int, block=0, max_basis=0, keep=0, max_restarts=0, tol=0.0, seed=0,
              overlap=0, raise_on_no_convergence=True):
@@ -206,13 +301,16 @@ class Engine:
         self.d = int(d)
         return s.as_dict()
 
+    def _n_local(self):
+        return self.dist_info()[3]
+
     def embedding(self):
-        Y = np.empty((self.num_layers, self.n, self.d), dtype=np.float32)
+        Y = np.empty((self.num_layers, self._n_local(), self.d), dtype=np.float32)
         self._check(self.lib.n2v2r_get_embedding(self.h, Y), "get_embedding")
         return Y
 
     def left_embedding(self):
-        X = np.empty((self.n, self.d), dtype=np.float32)
+        X = np.empty((self._n_local(), self.d), dtype=np.float32)
         self._check(self.lib.n2v2r_get_left_embedding(self.h, X), "get_left_embedding")
         return X
 

@@ -17,6 +17,16 @@
 //           random values by fill_flagged so the next CGS pass can orthogonalise them.
 #include "common.h"
 
+// ----------------------------------------------------------------------------- helpers
+// N(0,1) deviate from a counter (Box-Muller on two splitmix64 draws)
+__device__ __forceinline__ float counter_normal(uint64_t seed, uint64_t ctr) {
+  const uint64_t h1 = splitmix64(seed ^ ctr * 0x2545F4914F6CDD1Dull);
+  const uint64_t h2 = splitmix64(h1);
+  const double u1 = ((h1 >> 11) + 1.0) * (1.0 / 9007199254740993.0);
+  const double u2 = (h2 >> 11) * (1.0 / 9007199254740992.0);
+  return (float)(sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2));
+}
+
 // ----------------------------------------------------------------------------- ts_tn
 #define TN_WAVES 4
 
@@ -133,18 +143,42 @@ extern "C" hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B,
 }
 
 // ----------------------------------------------------------------------------- ts_nn
-// O[r][j] = alpha * sum_k A[r][k] G[k][j] + beta * C[r][j], j < 32*NT.  G fp32 row-major
-// (ldg columns).  Output / C blocks have width W (32 or 64), NT = cb / 32 tiles per wave.
+// O[r][j] = alpha * sum_k A[r][k] F[k][j] + beta * C[r][j] (j < cb), with the coefficient
+// matrix F either a plain fp32 matrix (G, ld ldg) or, in "PIP" mode, built on the fly from the
+// fused Gram-Schmidt/Cholesky factors: F = [-C R^{-1}; R^{-1}] with C = pip_g[0:c] (fp64,
+// row-major (c+b) x b) and R^{-1} = pip_x (fp64 b x b, flagged columns already zero).
+struct Coef {
+  const float* G;
+  int ldg;
+  const double* pip_g;
+  const double* pip_x;
+  int pip_c;
+};
+
+__device__ __forceinline__ float coef_at(const Coef& F, int k, int j, int cb) {
+  if (F.G) return F.G[(int64_t)k * F.ldg + j];
+  if (k >= F.pip_c) return (float)F.pip_x[(k - F.pip_c) * cb + j];
+  double v = 0.0;
+  const double* crow = F.pip_g + (int64_t)k * cb;
+  for (int m = 0; m <= j; ++m) v -= crow[m] * F.pip_x[m * cb + j];
+  return (float)v;
+}
+
+// MFMA form for cb >= 32 (Ritz vectors X = Q S, and b = 32/64 blocks): one wave per 32 output
+// rows and all output columns (NT 32-wide tiles), so O may alias A or C.  A rows are read as
+// 16-B loads; the k order inside each 8-column group is permuted consistently for A and F
+// (lane half h carries columns 4h..4h+3).  F is staged through LDS 64 rows at a time.
+#define NN_KCH 64
 template <int NT>
-__global__ __launch_bounds__(256) void ts_nn_kernel(BlockList A, const float* __restrict__ G,
-                                                    int ldg, int cb, OutBlockList O, BlockList C,
-                                                    float alpha, float beta, int64_t n,
-                                                    const int* cond) {
+__global__ __launch_bounds__(256) void ts_nn_kernel(BlockList A, Coef F, int cb, OutBlockList O,
+                                                    BlockList C, float alpha, float beta,
+                                                    int64_t n, const int* cond, const int* flags,
+                                                    uint64_t seed, int64_t row0) {
   if (cond && *cond == 0) return;
+  __shared__ float fs[NN_KCH][NT * 32];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 32;
-  if (r0 >= n) return;
   const int i = lane & 31;
   const int h = lane >> 5;
   const int64_t row = r0 + i;
@@ -153,52 +187,66 @@ __global__ __launch_bounds__(256) void ts_nn_kernel(BlockList A, const float* __
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f32x16{0.f};
   const int ca = A.count * A.width;
-  for (int kk = 0; kk < ca; kk += 8) {
-    const float* ap = A.blk[kk / A.width] + (kk % A.width) + 4 * h;
-    f32x4 a4 = {0.f, 0.f, 0.f, 0.f};
-    if (row_ok) a4 = *reinterpret_cast<const f32x4*>(ap + row * (int64_t)A.width);
+  for (int k0 = 0; k0 < ca; k0 += NN_KCH) {
+    const int kn = (ca - k0) < NN_KCH ? (ca - k0) : NN_KCH;
+    __syncthreads();
+    for (int e = threadIdx.x; e < NN_KCH * NT * 32; e += blockDim.x) {
+      const int k = e / (NT * 32), j = e % (NT * 32);
+      fs[k][j] = (k < kn && j < cb) ? coef_at(F, k0 + k, j, cb) : 0.f;
+    }
+    __syncthreads();
+    if (r0 < n) {
+      for (int kk = 0; kk < kn; kk += 8) {
+        const int kg = k0 + kk;
+        const float* ap = A.blk[kg / A.width] + (kg % A.width) + 4 * h;
+        f32x4 a4 = {0.f, 0.f, 0.f, 0.f};
+        if (row_ok) a4 = *reinterpret_cast<const f32x4*>(ap + row * (int64_t)A.width);
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const float* gp = G + (int64_t)(kk + 4 * h + m) * ldg + i;
+        for (int m = 0; m < 4; ++m) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const float g = (t * 32 + i < cb) ? gp[t * 32] : 0.f;
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[m], g, acc[t], 0, 0, 0);
+          for (int t = 0; t < NT; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[m], fs[kk + 4 * h + m][t * 32 + i],
+                                                           acc[t], 0, 0, 0);
+        }
       }
     }
   }
+  if (r0 >= n) return;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int col = t * 32 + i;
-    if (col >= cb) continue;
-    float* ob = O.blk[col / O.width] + (col % O.width);
-    const float* cbp = (beta != 0.f) ? C.blk[col / C.width] + (col % C.width) : nullptr;
+    const bool colok = col < cb;
+    float* ob = colok ? O.blk[col / O.width] + (col % O.width) : nullptr;
+    const float* cbp = (colok && beta != 0.f) ? C.blk[col / C.width] + (col % C.width) : nullptr;
+    const bool refill = colok && flags && flags[col];
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int64_t rr = r0 + (q & 3) + 8 * (q >> 2) + 4 * h;
-      if (rr < n) {
+      if (colok && rr < n) {
         float v = alpha * acc[t][q];
         if (cbp) v += beta * cbp[rr * (int64_t)C.width];
+        if (refill) v = counter_normal(seed, (uint64_t)(row0 + rr) * 64 + col);
         ob[rr * (int64_t)O.width] = v;
       }
     }
   }
 }
 
-// Narrow outputs (cb <= 16, the Krylov block at b = 8/16): one thread per row, coefficients
-// staged in LDS and read as broadcasts, A rows read as 16-B loads (consecutive lanes read
-// consecutive rows of a block: coalesced).  VALU FMAs; the pass is HBM-bound on A.
+// Narrow outputs (cb <= 16, the Krylov block at b = 8/16): one thread per row, F staged in LDS
+// and read as broadcasts, A rows read as 16-B loads (consecutive lanes read consecutive rows of
+// a block: coalesced).  VALU FMAs; the pass is HBM-bound on A.
 template <int CB>
-__global__ __launch_bounds__(256) void ts_nn_rows_kernel(BlockList A, const float* __restrict__ G,
-                                                         int ldg, int cb, OutBlockList O,
-                                                         BlockList C, float alpha, float beta,
-                                                         int64_t n, const int* cond) {
+__global__ __launch_bounds__(256) void ts_nn_rows_kernel(BlockList A, Coef F, int cb,
+                                                         OutBlockList O, BlockList C, float alpha,
+                                                         float beta, int64_t n, const int* cond,
+                                                         const int* flags, uint64_t seed,
+                                                         int64_t row0) {
   if (cond && *cond == 0) return;
   extern __shared__ __attribute__((aligned(16))) float gs[];
   const int ca = A.count * A.width;
   for (int e = threadIdx.x; e < ca * CB; e += blockDim.x) {
     const int k = e / CB, j = e % CB;
-    gs[e] = (j < cb) ? G[(int64_t)k * ldg + j] : 0.f;
+    gs[e] = (j < cb) ? coef_at(F, k, j, cb) : 0.f;
   }
   __syncthreads();
   const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -223,36 +271,58 @@ __global__ __launch_bounds__(256) void ts_nn_rows_kernel(BlockList A, const floa
     if (j >= cb) break;
     float v = alpha * acc[j];
     if (beta != 0.f) v += beta * C.blk[j / C.width][row * (int64_t)C.width + (j % C.width)];
+    if (flags && flags[j]) v = counter_normal(seed, (uint64_t)(row0 + row) * 64 + j);
     O.blk[j / O.width][row * (int64_t)O.width + (j % O.width)] = v;
   }
 }
 
-extern "C" hipError_t n2v2r_launch_ts_nn(const BlockList& A, const float* G, int ldg, int cb,
-                                         const OutBlockList& O, const BlockList& C, float alpha,
-                                         float beta, int64_t n, const int* cond,
-                                         hipStream_t stream) {
+static hipError_t launch_nn(const BlockList& A, const Coef& F, int cb, const OutBlockList& O,
+                            const BlockList& C, float alpha, float beta, int64_t n,
+                            const int* cond, const int* flags, uint64_t seed, int64_t row0,
+                            hipStream_t stream) {
   if ((A.count * A.width) % 8 != 0 || A.width % 8 != 0) return hipErrorInvalidValue;
   const size_t lds8 = sizeof(float) * (size_t)A.count * A.width * 8;
   const size_t lds16 = 2 * lds8;
   if (cb <= 8 && lds8 <= 64 * 1024) {
     hipLaunchKernelGGL(ts_nn_rows_kernel<8>, dim3((unsigned)((n + 255) / 256)), dim3(256), lds8,
-                       stream, A, G, ldg, cb, O, C, alpha, beta, n, cond);
+                       stream, A, F, cb, O, C, alpha, beta, n, cond, flags, seed, row0);
     return hipGetLastError();
   }
   if (cb <= 16 && lds16 <= 64 * 1024) {
     hipLaunchKernelGGL(ts_nn_rows_kernel<16>, dim3((unsigned)((n + 255) / 256)), dim3(256), lds16,
-                       stream, A, G, ldg, cb, O, C, alpha, beta, n, cond);
+                       stream, A, F, cb, O, C, alpha, beta, n, cond, flags, seed, row0);
     return hipGetLastError();
   }
   dim3 grid((unsigned)((n + 127) / 128));
   switch ((cb + 31) / 32) {
-    case 1: hipLaunchKernelGGL(ts_nn_kernel<1>, grid, dim3(256), 0, stream, A, G, ldg, cb, O, C, alpha, beta, n, cond); break;
-    case 2: hipLaunchKernelGGL(ts_nn_kernel<2>, grid, dim3(256), 0, stream, A, G, ldg, cb, O, C, alpha, beta, n, cond); break;
-    case 3: hipLaunchKernelGGL(ts_nn_kernel<3>, grid, dim3(256), 0, stream, A, G, ldg, cb, O, C, alpha, beta, n, cond); break;
-    case 4: hipLaunchKernelGGL(ts_nn_kernel<4>, grid, dim3(256), 0, stream, A, G, ldg, cb, O, C, alpha, beta, n, cond); break;
+    case 1: hipLaunchKernelGGL(ts_nn_kernel<1>, grid, dim3(256), 0, stream, A, F, cb, O, C, alpha, beta, n, cond, flags, seed, row0); break;
+    case 2: hipLaunchKernelGGL(ts_nn_kernel<2>, grid, dim3(256), 0, stream, A, F, cb, O, C, alpha, beta, n, cond, flags, seed, row0); break;
+    case 3: hipLaunchKernelGGL(ts_nn_kernel<3>, grid, dim3(256), 0, stream, A, F, cb, O, C, alpha, beta, n, cond, flags, seed, row0); break;
+    case 4: hipLaunchKernelGGL(ts_nn_kernel<4>, grid, dim3(256), 0, stream, A, F, cb, O, C, alpha, beta, n, cond, flags, seed, row0); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+// flags (nullptr = none): output columns j with flags[j] != 0 are written with N(0,1) deviates
+// (counter-based, seed) instead of the product: the refill of rank-deficient Krylov columns.
+extern "C" hipError_t n2v2r_launch_ts_nn(const BlockList& A, const float* G, int ldg, int cb,
+                                         const OutBlockList& O, const BlockList& C, float alpha,
+                                         float beta, int64_t n, const int* cond,
+                                         const int* flags, uint64_t seed, hipStream_t stream) {
+  const Coef F{G, ldg, nullptr, nullptr, 0};
+  return launch_nn(A, F, cb, O, C, alpha, beta, n, cond, flags, seed, 0, stream);
+}
+
+// Z <- [Q Z] [-C R^{-1}; R^{-1}] (fused BCGS + CholQR apply), C = G[0:c], R^{-1} = xinv.
+extern "C" hipError_t n2v2r_launch_pip_apply(const BlockList& QZ, const double* G,
+                                             const double* xinv, int c, int b,
+                                             const OutBlockList& Z, int64_t n, const int* cond,
+                                             const int* flags, uint64_t seed, int64_t row0,
+                                             hipStream_t stream) {
+  const Coef F{nullptr, 0, G, xinv, c};
+  BlockList none{};
+  return launch_nn(QZ, F, b, Z, none, 1.f, 0.f, n, cond, flags, seed, row0, stream);
 }
 
 // ----------------------------------------------------------------------------- small ops
@@ -347,11 +417,13 @@ __global__ __launch_bounds__(1024) void chol_inv_kernel(const double* __restrict
 
 // Fused block classical Gram-Schmidt + Cholesky QR ("Pythagorean" form): given
 // G = [Q Z]^T Z ((c + b) x b, fp64) with C = Q^T Z (first c rows) and Z^T Z (last b rows),
-// P = Z^T Z - C^T C is the Gram matrix of Z - Q C; P = R^T R and the NN coefficients
-// F = [-C R^{-1}; R^{-1}] ((c + b) x b, fp32) give Z <- (Z - Q C) R^{-1} in ONE pass over
-// [Q Z].  Rank-deficient columns (pivot below 1e-10 max diag) get a zero F column and a flag.
+// P = Z^T Z - C^T C is the Gram matrix of Z - Q C.  This kernel forms P (1024 threads, the
+// c-long sums split over 16 k-slices and folded in fixed order), then one wave does the
+// Cholesky P = R^T R and R^{-1} (xinv, fp64 b x b).  The apply pass builds
+// F = [-C R^{-1}; R^{-1}] in LDS and writes Z <- (Z - Q C) R^{-1} in ONE pass over [Q Z].
+// Rank-deficient columns (pivot below 1e-10 max diag) get a zero xinv column and a flag.
 __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict__ G, int c, int b,
-                                                        float* __restrict__ F, int* flags,
+                                                        double* __restrict__ xinv, int* flags,
                                                         int* any_flag, const int* cond) {
   if (cond && *cond == 0) {
     if (threadIdx.x < b) flags[threadIdx.x] = 0;
@@ -360,17 +432,15 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
   }
   __shared__ double R[64][65];
   __shared__ double X[64][65];
+  __shared__ double part[16][64];
   __shared__ double piv[64];
   __shared__ int bad[64];
   __shared__ double dmax;
   const int tid = threadIdx.x;
   const int nt = blockDim.x;
-  // P = Gzz - C^T C (symmetrised); the c-long sums are split over k-slices of the 1024
-  // threads and folded through LDS in fixed order
-  __shared__ double part[16][64];
   const int bb = b * b;
   if (bb <= 64) {
-    const int e = tid % 64, slice = tid / 64;  // 16 slices of 64 threads
+    const int e = tid % 64, slice = tid / 64;
     double acc = 0.0;
     if (e < bb) {
       const int i = e / b, j = e % b;
@@ -393,9 +463,12 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
     }
   }
   for (int e = tid; e < bb; e += nt) X[e / b][e % b] = (e / b == e % b) ? 1.0 : 0.0;
-  if (tid < 64) bad[tid] = 0;
   __syncthreads();
-  if (tid < 64) {
+  if (tid >= 64) return;  // O(b^3), b <= 64: one wave from here on
+  const int nw = 64;
+  bad[tid] = 0;
+  __syncthreads();
+  {
     double m = (tid < b) ? R[tid][tid] : 0.0;
     for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
     if (tid == 0) dmax = m;
@@ -415,11 +488,11 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
     __syncthreads();
     const double pj = piv[j];
     const int isbad = bad[j];
-    for (int cc = j + tid; cc < b; cc += nt)
+    for (int cc = j + tid; cc < b; cc += nw)
       R[j][cc] = isbad ? (cc == j ? 1.0 : 0.0) : (cc == j ? pj : R[j][cc] / pj);
     __syncthreads();
     const int m = b - j - 1;
-    for (int e = tid; e < m * m; e += nt) {
+    for (int e = tid; e < m * m; e += nw) {
       const int r = j + 1 + e / m, cc = j + 1 + e % m;
       if (cc >= r) R[r][cc] -= R[j][r] * R[j][cc];
     }
@@ -427,26 +500,17 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
   }
   for (int j = b - 1; j >= 0; --j) {
     const double inv = 1.0 / R[j][j];
-    for (int cc = tid; cc < b; cc += nt) X[j][cc] *= inv;
+    for (int cc = tid; cc < b; cc += nw) X[j][cc] *= inv;
     __syncthreads();
-    for (int e = tid; e < j * b; e += nt) {
+    for (int e = tid; e < j * b; e += nw) {
       const int r = e / b, cc = e % b;
       X[r][cc] -= R[r][j] * X[j][cc];
     }
     __syncthreads();
   }
-  // F = [-C X; X], flagged columns zeroed
-  for (int e = tid; e < (c + b) * b; e += nt) {
-    const int r = e / b, j = e % b;
-    double v = 0.0;
-    if (!bad[j]) {
-      if (r < c) {
-        for (int k = 0; k <= j; ++k) v -= G[(int64_t)r * b + k] * X[k][j];
-      } else {
-        v = X[r - c][j];
-      }
-    }
-    F[e] = (float)v;
+  for (int e = tid; e < bb; e += nw) {
+    const int r = e / b, cc = e % b;
+    xinv[e] = bad[cc] ? 0.0 : X[r][cc];
   }
   if (tid < b) flags[tid] = bad[tid];
   if (tid == 0) {
@@ -456,11 +520,12 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
   }
 }
 
-extern "C" hipError_t n2v2r_launch_pip_chol(const double* G, int c, int b, float* F, int* flags,
-                                            int* any_flag, const int* cond, hipStream_t stream) {
+extern "C" hipError_t n2v2r_launch_pip_chol(const double* G, int c, int b, double* xinv,
+                                            int* flags, int* any_flag, const int* cond,
+                                            hipStream_t stream) {
   if (b > 64) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pip_chol_kernel, dim3(1), dim3(1024), 0, stream, G, c, b, F, flags, any_flag,
-                     cond);
+  hipLaunchKernelGGL(pip_chol_kernel, dim3(1), dim3(1024), 0, stream, G, c, b, xinv, flags,
+                     any_flag, cond);
   return hipGetLastError();
 }
 
@@ -473,28 +538,25 @@ extern "C" hipError_t n2v2r_launch_chol_inv(const double* G, int b, float* Rinv,
 
 // Fill an N x W block with N(0,1) deviates: all columns (flags == nullptr) or only flagged ones.
 __global__ void fill_normal_kernel(float* __restrict__ blk, int w, int64_t n, uint64_t seed,
-                                   const int* flags, const int* cond) {
+                                   const int* flags, const int* cond, uint64_t ctr0) {
   if (cond && *cond == 0) return;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * w;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int col = (int)(e % w);
     if (flags && !flags[col]) continue;
-    const uint64_t h1 = splitmix64(seed ^ (uint64_t)e * 0x2545F4914F6CDD1Dull);
-    const uint64_t h2 = splitmix64(h1);
-    const double u1 = ((h1 >> 11) + 1.0) * (1.0 / 9007199254740993.0);
-    const double u2 = (h2 >> 11) * (1.0 / 9007199254740992.0);
-    blk[e] = (float)(sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2));
+    blk[e] = counter_normal(seed, ctr0 + (uint64_t)e);
   }
 }
 
+// ctr0: counter offset (global first row x w), so a row-partitioned run draws the same values
 extern "C" hipError_t n2v2r_launch_fill_normal(float* blk, int w, int64_t n, uint64_t seed,
-                                               const int* flags, const int* cond,
+                                               const int* flags, const int* cond, uint64_t ctr0,
                                                hipStream_t stream) {
   const int64_t elems = n * w;
   int64_t nb = (elems + 255) / 256;
   if (nb > 2048) nb = 2048;
   hipLaunchKernelGGL(fill_normal_kernel, dim3((unsigned)nb), dim3(256), 0, stream, blk, w, n, seed,
-                     flags, cond);
+                     flags, cond, ctr0);
   return hipGetLastError();
 }
 
@@ -570,7 +632,7 @@ extern "C" hipError_t n2v2r_launch_scale_cols(float* blk, int w, int64_t n, cons
 // sign, write +-1.
 __global__ __launch_bounds__(256) void colmax_partial_kernel(const float* __restrict__ U,
                                                              int64_t ldu, int64_t n, int d,
-                                                             int64_t rows_per_chunk,
+                                                             int64_t rows_per_chunk, int64_t row0,
                                                              unsigned long long* __restrict__ keys) {
   __shared__ unsigned long long red[8][32];
   const int c = threadIdx.x & 31;
@@ -584,7 +646,7 @@ __global__ __launch_bounds__(256) void colmax_partial_kernel(const float* __rest
     for (int64_t r = r0 + rl; r < r1; r += 8) {
       const float v = fabsf(U[r * ldu + col]);
       const unsigned long long k = ((unsigned long long)__float_as_uint(v) << 32) |
-                                   (unsigned long long)(0xFFFFFFFFu - (uint32_t)r);
+                                   (unsigned long long)(0xFFFFFFFFu - (uint32_t)(row0 + r));
       best = k > best ? k : best;
     }
   }
@@ -596,43 +658,63 @@ __global__ __launch_bounds__(256) void colmax_partial_kernel(const float* __rest
   }
 }
 
-__global__ void colmax_finish_kernel(const unsigned long long* __restrict__ keys, int nchunks,
-                                     int ncols_padded, const float* __restrict__ U, int64_t ldu,
-                                     int d, float* __restrict__ sign) {
+// fold chunk keys -> best[col] (packed |u| bits and ~global row)
+__global__ void colmax_fold_kernel(const unsigned long long* __restrict__ keys, int nchunks,
+                                   int ncols_padded, unsigned long long* __restrict__ best_out) {
   const int col = blockIdx.x * blockDim.x + threadIdx.x;
   if (col >= ncols_padded) return;
-  if (col >= d) {
-    sign[col] = 1.f;
-    return;
-  }
   unsigned long long best = 0;
   for (int c = 0; c < nchunks; ++c) {
     const unsigned long long k = keys[(int64_t)c * ncols_padded + col];
     best = k > best ? k : best;
   }
-  const int64_t row = (int64_t)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
-  sign[col] = (U[row * ldu + col] < 0.f) ? -1.f : 1.f;
+  best_out[col] = best;
 }
 
-extern "C" hipError_t n2v2r_launch_sign_convention(float* U, int64_t ldu, int64_t n, int d,
-                                                   unsigned long long* keys, size_t key_elems,
-                                                   float* sign, hipStream_t stream) {
+// sign[col] = sign of U at the winning row if this rank owns it, else 0 (summed over ranks)
+__global__ void colmax_sign_kernel(const unsigned long long* __restrict__ best, int ncols_padded,
+                                   const float* __restrict__ U, int64_t ldu, int d, int64_t row0,
+                                   int64_t n, float* __restrict__ sign) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= ncols_padded) return;
+  if (col >= d) {
+    sign[col] = row0 == 0 ? 1.f : 0.f;
+    return;
+  }
+  const int64_t grow = (int64_t)(0xFFFFFFFFu - (uint32_t)(best[col] & 0xFFFFFFFFull));
+  const int64_t r = grow - row0;
+  float sgn = 0.f;
+  if (r >= 0 && r < n) sgn = (U[r * ldu + col] < 0.f) ? -1.f : 1.f;
+  sign[col] = sgn;
+}
+
+extern "C" hipError_t n2v2r_launch_colmax_keys(const float* U, int64_t ldu, int64_t n, int d,
+                                               int64_t row0, unsigned long long* keys,
+                                               size_t key_elems, unsigned long long* best,
+                                               hipStream_t stream) {
   const int tiles = (d + 31) / 32;
   int64_t nchunks = (n + 4095) / 4096;
   if (nchunks > 1024) nchunks = 1024;
+  if (nchunks < 1) nchunks = 1;
   if ((size_t)(nchunks * tiles * 32) > key_elems) nchunks = (int64_t)(key_elems / (tiles * 32));
   if (nchunks < 1) return hipErrorInvalidValue;
   int64_t rows = (n + nchunks - 1) / nchunks;
+  if (rows < 1) rows = 1;
   nchunks = (n + rows - 1) / rows;
+  if (nchunks < 1) nchunks = 1;
   hipLaunchKernelGGL(colmax_partial_kernel, dim3((unsigned)nchunks, tiles), dim3(256), 0, stream,
-                     U, ldu, n, d, rows, keys);
+                     U, ldu, n, d, rows, row0, keys);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(colmax_finish_kernel, dim3((tiles * 32 + 255) / 256), dim3(256), 0, stream,
-                     keys, (int)nchunks, tiles * 32, U, ldu, d, sign);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(scale_cols_kernel, dim3((unsigned)((n * ldu + 255) / 256)), dim3(256), 0,
-                     stream, U, (int)ldu, n, sign);
+  hipLaunchKernelGGL(colmax_fold_kernel, dim3((tiles * 32 + 255) / 256), dim3(256), 0, stream,
+                     keys, (int)nchunks, tiles * 32, best);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t n2v2r_launch_colmax_sign(const unsigned long long* best, int ncols_padded,
+                                               const float* U, int64_t ldu, int d, int64_t row0,
+                                               int64_t n, float* sign, hipStream_t stream) {
+  hipLaunchKernelGGL(colmax_sign_kernel, dim3((ncols_padded + 255) / 256), dim3(256), 0, stream,
+                     best, ncols_padded, U, ldu, d, row0, n, sign);
   return hipGetLastError();
 }

@@ -1,26 +1,39 @@
-// n2v2r engine: handle, CSR ingest, block Krylov-Schur UASE driver, ranking orchestration
-// and the extern "C" boundary declared in include/n2v2r.h.
+// n2v2r engine: handle, CSR ingest, block Krylov-Schur UASE driver, ranking orchestration,
+// row-partitioned multi-GPU execution and the extern "C" boundary declared in include/n2v2r.h.
 //
 // UASE (replaces se.UASE -> scipy svds/ARPACK, model.py:51-55): top-d eigenpairs of
 // M = sum_k A_k A_k^T (N x N, = A A^T for the unfolded A = [A_1 | ... | A_K]) by a block
 // Krylov-Schur iteration with explicit Rayleigh-Ritz:
 //   basis Q = [Q_0 .. Q_{m-1}] (b-wide fp32 blocks in HBM), W_j = M Q_j kept beside it;
-//   expand: Z = W_last, CGS2 against Q, CholeskyQR2 (+random refill of deficient columns),
-//           Q_m = Z, W_m = M Q_m (2 SpMM launches: Z_k = A_k^T Q ; W = sum_k A_k Z_k);
+//   expand: Z = W_last, two fused BCGS + CholeskyQR passes (+random refill of deficient
+//           columns, third pass only then), Q_m = Z, W_m = M Q_m
+//           (2 SpMM launches: Z_k = A_k^T Q ; W = sum_k A_k Z_k);
 //   cycle:  H = Q^T W (fp64) -> host top-p eigenpairs -> Ritz X = Q S, MX = W S,
 //           residuals ||MX_j - theta_j X_j||; converged when all d <= tol * theta_1;
 //   restart: next block = orth(W_last) against the old Q, keep [X_p | next] (thick restart).
 // Embedding: Y_k = A_k^T U diag(sigma)^(-1/2) (= V diag(sigma)^(1/2) split per layer),
 // sigma = sqrt(theta), columns in descending sigma order.
+//
+// Multi-GPU: rank g of W owns rows [g R, min(N, (g+1) R)), R = ceil(N / W), of
+// every layer (and of A_k^T), of every basis block and of the embedding.  Column indices stay
+// global: a panel gathered from all ranks (W x R rows, rank-major) is indexed by them directly.
+// Per application of M: all-gather X, local SpMM, all-gather each Z_k, local SpMM.  Every
+// reduction over rows (Gram blocks, H, residuals, sign keys) is a local fixed-order partial
+// + an all-reduce, so every rank holds identical small matrices and runs the identical host
+// Rayleigh-Ritz.  Communicators: RCCL (one process per GPU) or an in-process thread group
+// (W ranks on one GPU, for testing the partitioned algorithm without W devices).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <numeric>
 #include <string>
 #include <thread>
@@ -57,26 +70,30 @@ hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n,
                               hipStream_t stream);
 hipError_t n2v2r_launch_ts_nn(const BlockList& A, const float* G, int ldg, int cb,
                               const OutBlockList& O, const BlockList& C, float alpha, float beta,
-                              int64_t n, const int* cond, hipStream_t stream);
-hipError_t n2v2r_launch_f64_to_f32(const double* in, float* out, int64_t elems, float scale,
-                                   const int* cond, hipStream_t stream);
-hipError_t n2v2r_launch_chol_inv(const double* G, int b, float* Rinv, int* flags, int* any_flag,
-                                 hipStream_t stream);
-hipError_t n2v2r_launch_pip_chol(const double* G, int c, int b, float* F, int* flags,
+                              int64_t n, const int* cond, const int* flags, uint64_t seed,
+                              hipStream_t stream);
+hipError_t n2v2r_launch_pip_chol(const double* G, int c, int b, double* xinv, int* flags,
                                  int* any_flag, const int* cond, hipStream_t stream);
+hipError_t n2v2r_launch_pip_apply(const BlockList& QZ, const double* G, const double* xinv,
+                                  int c, int b, const OutBlockList& Z, int64_t n, const int* cond,
+                                  const int* flags, uint64_t seed, int64_t row0,
+                                  hipStream_t stream);
 hipError_t n2v2r_launch_fill_normal(float* blk, int w, int64_t n, uint64_t seed, const int* flags,
-                                    const int* cond, hipStream_t stream);
+                                    const int* cond, uint64_t ctr0, hipStream_t stream);
 hipError_t n2v2r_launch_resid(const BlockList& X, const BlockList& MX, const double* theta,
                               int64_t n, double* partial, size_t partial_elems, double* out,
                               hipStream_t stream);
 hipError_t n2v2r_launch_scale_cols(float* blk, int w, int64_t n, const float* s,
                                    hipStream_t stream);
-hipError_t n2v2r_launch_sign_convention(float* U, int64_t ldu, int64_t n, int d,
-                                        unsigned long long* keys, size_t key_elems, float* sign,
-                                        hipStream_t stream);
-hipError_t n2v2r_launch_distances(const float* Y, int K, int64_t n, int64_t ldy, int strategy,
-                                  int layer_i, const DistPlan& plan, double* out,
-                                  hipStream_t stream);
+hipError_t n2v2r_launch_colmax_keys(const float* U, int64_t ldu, int64_t n, int d, int64_t row0,
+                                    unsigned long long* keys, size_t key_elems,
+                                    unsigned long long* best, hipStream_t stream);
+hipError_t n2v2r_launch_colmax_sign(const unsigned long long* best, int ncols_padded,
+                                    const float* U, int64_t ldu, int d, int64_t row0, int64_t n,
+                                    float* sign, hipStream_t stream);
+hipError_t n2v2r_launch_distances(const float* Y, int K, int64_t n, int64_t ldy, int64_t lrows,
+                                  int strategy, int layer_i, const DistPlan& plan, double* out,
+                                  int64_t ldo, hipStream_t stream);
 hipError_t n2v2r_launch_pairwise(const double* a, const double* b, int64_t n, int dim, int metric,
                                  double* out, hipStream_t stream);
 hipError_t n2v2r_launch_borda_init(const double* vals, int64_t n, int nseg, uint64_t* keys,
@@ -113,7 +130,7 @@ double now_ms() {
   return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
 }
 
-// Device allocation owned by the handle.
+// Device allocation owned by the handle (zero-filled on allocation: padded rows stay zero).
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
@@ -126,7 +143,9 @@ struct DevBuf {
     p = nullptr;
     bytes = 0;
   }
-  void ensure(size_t b) {
+  // The zero fill is ordered on `st` (the engine stream, non-blocking w.r.t. the null stream);
+  // with st == nullptr it completes before ensure() returns.
+  void ensure(size_t b, hipStream_t st = nullptr) {
     if (bytes >= b && p) return;
     release();
     if (b == 0) b = 16;
@@ -136,6 +155,13 @@ struct DevBuf {
       throw StatusFail{N2V2R_ERR_OUT_OF_MEMORY,
                        "hipMalloc of " + std::to_string(b) + " bytes failed"};
     }
+    if (st) {
+      e = hipMemsetAsync(p, 0, b, st);
+    } else {
+      e = hipMemset(p, 0, b);
+      if (e == hipSuccess) e = hipDeviceSynchronize();
+    }
+    if (e != hipSuccess) throw HipFail{e, "hipMemset"};
     bytes = b;
   }
   template <class T>
@@ -145,9 +171,10 @@ struct DevBuf {
 };
 
 struct LayerDev {
-  DevBuf indptr, indices, data;        // A (CSR)
-  DevBuf t_indptr, t_indices, t_data;  // A^T (CSR) when not symmetric
-  int64_t nnz = 0;
+  DevBuf indptr, indices, data;        // local rows of A (CSR, global column indices)
+  DevBuf t_indptr, t_indices, t_data;  // local rows of A^T when A is not symmetric
+  int64_t nnz = 0, t_nnz = 0;
+  int64_t n_rows = 0;                  // local rows
   bool symmetric = true;
   bool loaded = false;
   CsrDev csr() const {
@@ -156,9 +183,119 @@ struct LayerDev {
   CsrDev csr_t() const {
     if (symmetric) return csr();
     return CsrDev{t_indptr.as<int64_t>(), t_indices.as<int32_t>(), t_data.as<float>(), n_rows,
-                  nnz};
+                  t_nnz};
   }
-  int64_t n_rows = 0;
+};
+
+// ---- communicators ----------------------------------------------------------------------
+struct Comm {
+  int rank = 0, world = 1;
+  virtual ~Comm() = default;
+  // recv = world x bytes, rank-major (rank r's bytes at r * bytes)
+  virtual void allgather(const void* send, void* recv, size_t bytes, hipStream_t st) = 0;
+  virtual void allreduce_sum_f64(double* buf, size_t count, hipStream_t st) = 0;
+  virtual void allreduce_max_u64(unsigned long long* buf, size_t count, hipStream_t st) = 0;
+  virtual void allreduce_sum_f32(float* buf, size_t count, hipStream_t st) = 0;
+  virtual const char* kind() const = 0;
+};
+
+struct NcclFail {
+  ncclResult_t r;
+  std::string where;
+};
+#define NCCLCHK(expr)                                   \
+  do {                                                  \
+    ncclResult_t _r = (expr);                           \
+    if (_r != ncclSuccess) throw NcclFail{_r, #expr};   \
+  } while (0)
+
+struct RcclComm : Comm {
+  ncclComm_t c = nullptr;
+  ~RcclComm() override {
+    if (c) (void)ncclCommDestroy(c);
+  }
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t st) override {
+    NCCLCHK(ncclAllGather(send, recv, bytes, ncclChar, c, st));
+  }
+  void allreduce_sum_f64(double* buf, size_t count, hipStream_t st) override {
+    NCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c, st));
+  }
+  void allreduce_max_u64(unsigned long long* buf, size_t count, hipStream_t st) override {
+    NCCLCHK(ncclAllReduce(buf, buf, count, ncclUint64, ncclMax, c, st));
+  }
+  void allreduce_sum_f32(float* buf, size_t count, hipStream_t st) override {
+    NCCLCHK(ncclAllReduce(buf, buf, count, ncclFloat, ncclSum, c, st));
+  }
+  const char* kind() const override { return "rccl"; }
+};
+
+}  // namespace
+
+// W ranks of one process on one device (threads): the partitioned algorithm, testable on one
+// GPU.  Collectives: stream sync, publish a pointer, barrier, copy / fixed-order host sum.
+struct n2v2r_simgroup {
+  int world = 1;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t generation = 0;
+  std::vector<const void*> ptrs;
+  std::vector<std::vector<unsigned char>> host;
+  void barrier() {
+    std::unique_lock<std::mutex> lk(m);
+    const uint64_t gen = generation;
+    if (++arrived == world) {
+      arrived = 0;
+      ++generation;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return generation != gen; });
+    }
+  }
+};
+
+namespace {
+
+struct ThreadComm : Comm {
+  n2v2r_simgroup* g = nullptr;
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t st) override {
+    HIPCHK(hipStreamSynchronize(st));
+    g->ptrs[rank] = send;
+    g->barrier();
+    for (int r = 0; r < world; ++r)
+      HIPCHK(hipMemcpyAsync(static_cast<char*>(recv) + (size_t)r * bytes, g->ptrs[r], bytes,
+                            hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+    g->barrier();
+  }
+  template <class T, class Op>
+  void allreduce(T* buf, size_t count, hipStream_t st, Op op) {
+    auto& mine = g->host[rank];
+    mine.resize(sizeof(T) * count);
+    HIPCHK(hipMemcpyAsync(mine.data(), buf, sizeof(T) * count, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    g->barrier();
+    std::vector<T> acc(count);
+    std::memcpy(acc.data(), g->host[0].data(), sizeof(T) * count);
+    for (int r = 1; r < world; ++r) {
+      const T* o = reinterpret_cast<const T*>(g->host[r].data());
+      for (size_t i = 0; i < count; ++i) acc[i] = op(acc[i], o[i]);
+    }
+    g->barrier();
+    HIPCHK(hipMemcpyAsync(buf, acc.data(), sizeof(T) * count, hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  void allreduce_sum_f64(double* buf, size_t count, hipStream_t st) override {
+    allreduce(buf, count, st, [](double a, double b) { return a + b; });
+  }
+  void allreduce_max_u64(unsigned long long* buf, size_t count, hipStream_t st) override {
+    allreduce(buf, count, st,
+              [](unsigned long long a, unsigned long long b) { return a > b ? a : b; });
+  }
+  void allreduce_sum_f32(float* buf, size_t count, hipStream_t st) override {
+    allreduce(buf, count, st, [](float a, float b) { return a + b; });
+  }
+  const char* kind() const override { return "thread"; }
 };
 
 }  // namespace
@@ -168,33 +305,39 @@ struct n2v2r_handle {
   hipStream_t stream = nullptr;
   std::string err;
   int K = 0;
-  int64_t n = 0;
+  int64_t n = 0;        // global nodes
+  // row partition (single GPU: rank 0 of 1, row0 = 0, nloc = npad = n)
+  std::unique_ptr<Comm> comm;
+  int rank = 0, world = 1;
+  int64_t row0 = 0, nloc = 0, npad = 0;
   std::vector<std::unique_ptr<LayerDev>> layers;
 
   // UASE results
   int d = 0;
   int ldy = 0;              // row stride of the per-layer embedding
-  DevBuf Y;                 // [K][n][ldy] fp32
-  DevBuf U;                 // [n][ldu] fp32 left singular vectors (ldu = ldy)
+  DevBuf Y;                 // [K][npad][ldy] fp32 (local rows)
+  DevBuf U;                 // [npad][ldy] fp32 left singular vectors (local rows)
   std::vector<double> sigma;
   bool have_embedding = false;
 
-  // rank results
+  // rank results (global after the gather)
   int ncmp = 0, ncols = 0;
   DevBuf D;                 // [ncmp][ncols][n] fp64
+  DevBuf Dloc;              // [ncmp][ncols][npad] fp64 (distributed)
+  DevBuf Dgat;              // [world][npad] staging of one gathered column
   DevBuf borda;             // [ncmp][n] int64
   double ms_dist = 0, ms_borda = 0;
 
   // scratch
   DevBuf partial;           // chunk partials of the tall-skinny reductions
   size_t partial_elems = 0;
-  DevBuf small64;           // c x c fp64 (H, G, ...)
-  DevBuf small32;           // c x c fp32 (coefficients)
-  DevBuf flags;             // int flags
   DevBuf theta;             // fp64 Ritz values
   DevBuf resid;             // fp64 residuals
   DevBuf colscale;          // fp32
+  DevBuf keys, best;        // sign convention
+  DevBuf gath;              // gathered panels
   DevBuf rs_keys[2], rs_idx[2], rs_pos, rs_hist, rs_or, rs_and;
+
 
   void set_err(const char* fmt, ...) {
     char buf[1024];
@@ -203,6 +346,32 @@ struct n2v2r_handle {
     vsnprintf(buf, sizeof(buf), fmt, ap);
     va_end(ap);
     err = buf;
+  }
+
+  void set_partition(int64_t n_global) {
+    n = n_global;
+    if (world <= 1) {
+      row0 = 0;
+      nloc = npad = n;
+      return;
+    }
+    npad = (n + world - 1) / world;
+    row0 = std::min<int64_t>(n, (int64_t)rank * npad);
+    nloc = std::max<int64_t>(0, std::min<int64_t>(n, row0 + npad) - row0);
+  }
+
+  // gather a local [npad][w] panel of every rank into the global [world*npad][w] panel
+  void gather_panel(const float* local, float* global, int w) {
+    if (!comm) {
+      if (local != global)
+        HIPCHK(hipMemcpyAsync(global, local, sizeof(float) * npad * w, hipMemcpyDeviceToDevice,
+                              stream));
+      return;
+    }
+    comm->allgather(local, global, sizeof(float) * npad * w, stream);
+  }
+  void allreduce_f64(double* buf, size_t count) {
+    if (comm) comm->allreduce_sum_f64(buf, count, stream);
   }
 };
 
@@ -217,6 +386,9 @@ int guarded(n2v2r_handle* h, F&& f) {
     return f();
   } catch (const HipFail& hf) {
     h->set_err("HIP error %d (%s) at %s", (int)hf.e, hipGetErrorString(hf.e), hf.where.c_str());
+    return N2V2R_ERR_HIP;
+  } catch (const NcclFail& nf) {
+    h->set_err("RCCL error %d (%s) at %s", (int)nf.r, ncclGetErrorString(nf.r), nf.where.c_str());
     return N2V2R_ERR_HIP;
   } catch (const StatusFail& sf) {
     h->err = sf.msg;
@@ -244,9 +416,9 @@ void host_transpose(int64_t n, int64_t nnz, const int64_t* ip, const int32_t* ix
     }
 }
 
-bool host_is_symmetric(int64_t n, int64_t nnz, const int64_t* ip, const int32_t* ix,
-                       const float* dv, const std::vector<int64_t>& tp,
-                       const std::vector<int32_t>& tx, const std::vector<float>& td) {
+bool host_is_symmetric(int64_t n, const int64_t* ip, const int32_t* ix, const float* dv,
+                       const std::vector<int64_t>& tp, const std::vector<int32_t>& tx,
+                       const std::vector<float>& td) {
   // A == A^T iff row r of A equals row r of A^T as (sorted col, value) multisets.
   for (int64_t r = 0; r < n; ++r) {
     const int64_t a0 = ip[r], a1 = ip[r + 1], b0 = tp[r], b1 = tp[r + 1];
@@ -265,21 +437,42 @@ bool host_is_symmetric(int64_t n, int64_t nnz, const int64_t* ip, const int32_t*
   return true;
 }
 
+// upload rows [r0, r0 + nr) of a CSR (global column indices kept) into (ip, ix, dv) buffers
+void upload_rows(hipStream_t st, int64_t r0, int64_t nr, const int64_t* ip, const int32_t* ix,
+                 const float* dv, DevBuf& dip, DevBuf& dix, DevBuf& ddv, int64_t& nnz_out) {
+  const int64_t p0 = ip[r0], p1 = ip[r0 + nr];
+  nnz_out = p1 - p0;
+  std::vector<int64_t> lip(nr + 1);
+  for (int64_t r = 0; r <= nr; ++r) lip[r] = ip[r0 + r] - p0;
+  dip.ensure(sizeof(int64_t) * (nr + 1));
+  dix.ensure(sizeof(int32_t) * std::max<int64_t>(nnz_out, 1));
+  ddv.ensure(sizeof(float) * std::max<int64_t>(nnz_out, 1));
+  HIPCHK(hipMemcpyAsync(dip.p, lip.data(), sizeof(int64_t) * (nr + 1), hipMemcpyHostToDevice, st));
+  if (nnz_out) {
+    HIPCHK(hipMemcpyAsync(dix.p, ix + p0, sizeof(int32_t) * nnz_out, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(ddv.p, dv + p0, sizeof(float) * nnz_out, hipMemcpyHostToDevice, st));
+  }
+  HIPCHK(hipStreamSynchronize(st));  // lip dies here
+}
+
 // ---- the eigensolver ----------------------------------------------------------------------
 struct Eig {
   n2v2r_handle* h;
   hipStream_t st;
-  int64_t n;
+  int64_t n;        // local rows
+  int64_t npad;     // local rows incl. padding (panel allocation)
+  int64_t row0;     // global index of local row 0
   int K;
   int b;            // block width
   int nb_max;       // max basis blocks
   int pb;           // kept blocks at restart
   int d;
   uint64_t seed;
-  std::vector<std::unique_ptr<DevBuf>> pool;  // all N x b blocks
+  std::vector<std::unique_ptr<DevBuf>> pool;  // all npad x b blocks
   std::vector<float*> freelist;
   std::vector<float*> Q, W;                   // current basis / images
-  std::vector<std::unique_ptr<DevBuf>> zk;    // K stage-1 panels
+  std::vector<std::unique_ptr<DevBuf>> zk;    // K stage-1 panels (local)
+  DevBuf zg;                                  // K gathered stage-1 panels
   DevBuf rinv, flg, anyflag, gsmall, csmall;
   n2v2r_eig_stats* stats;
   double t_spmm = 0, t_ortho = 0;
@@ -290,7 +483,7 @@ struct Eig {
   float* take() {
     if (freelist.empty()) {
       pool.emplace_back(new DevBuf());
-      pool.back()->ensure(sizeof(float) * n * b);
+      pool.back()->ensure(sizeof(float) * npad * b, st);
       return pool.back()->as<float>();
     }
     float* p = freelist.back();
@@ -321,64 +514,79 @@ struct Eig {
     return L;
   }
 
-  // W = M X = sum_k A_k (A_k^T X)
+  // TN over local rows, summed over ranks
+  void tn(const BlockList& A, const BlockList& B, double* out, const int* cond) {
+    HIPCHK(n2v2r_launch_ts_tn(A, B, n, h->partial.as<double>(), h->partial_elems, out, cond, st));
+    if (h->comm)
+      h->allreduce_f64(out, (size_t)A.count * A.width * B.count * B.width);
+  }
+
+  // W = M X = sum_k A_k (A_k^T X); X, W local, gathered panels for the column side
   void apply_M(const float* X, float* Wout) {
     const double t0 = now_ms();
-    for (int k0 = 0; k0 < K; k0 += SPMM_MAX_LAYERS) {
-      const int kc = std::min(SPMM_MAX_LAYERS, K - k0);
-      SpmmArgs a{};
-      a.K = kc;
-      a.sum = 0;
-      a.ldx = b;
-      a.ldy = b;
-      a.colscale = nullptr;
-      for (int k = 0; k < kc; ++k) {
-        a.A[k] = h->layers[k0 + k]->csr_t();
-        a.X[k] = X;
-        a.Y[k] = zk[k]->as<float>();
-      }
-      HIPCHK(n2v2r_launch_spmm(a, b, st));
-      SpmmArgs s{};
-      s.K = kc;
-      s.sum = 1;
-      s.ldx = b;
-      s.ldy = b;
-      s.colscale = nullptr;
-      for (int k = 0; k < kc; ++k) {
-        s.A[k] = h->layers[k0 + k]->csr();
+    const int64_t ng = (int64_t)h->world * npad;  // rows of a gathered panel
+    const float* xg = X;
+    if (h->comm) {
+      float* xgb = h->gath.as<float>();
+      h->gather_panel(X, xgb, b);
+      xg = xgb;
+    }
+    SpmmArgs a{};
+    a.K = K;
+    a.sum = 0;
+    a.ldx = b;
+    a.ldy = b;
+    a.colscale = nullptr;
+    for (int k = 0; k < K; ++k) {
+      a.A[k] = h->layers[k]->csr_t();
+      a.X[k] = xg;
+      a.Y[k] = zk[k]->as<float>();
+    }
+    HIPCHK(n2v2r_launch_spmm(a, b, st));
+    SpmmArgs s{};
+    s.K = K;
+    s.sum = 1;
+    s.ldx = b;
+    s.ldy = b;
+    s.colscale = nullptr;
+    for (int k = 0; k < K; ++k) {
+      s.A[k] = h->layers[k]->csr();
+      if (h->comm) {
+        float* zgk = zg.as<float>() + (size_t)k * ng * b;
+        h->gather_panel(zk[k]->as<float>(), zgk, b);
+        s.X[k] = zgk;
+      } else {
         s.X[k] = zk[k]->as<float>();
       }
-      s.Y[0] = Wout;
-      if (k0 > 0) throw StatusFail{N2V2R_ERR_BAD_ARG, "more than 8 layers not supported yet"};
-      HIPCHK(n2v2r_launch_spmm(s, b, st));
-      for (int k = 0; k < kc; ++k) {
-        const double nnz = (double)h->layers[k0 + k]->nnz;
-        algo_bytes += 2.0 * (8.0 * nnz + 4.0 * (n + 1) + 8.0 * n * b);
-      }
-      launches += 2;
     }
+    s.Y[0] = Wout;
+    HIPCHK(n2v2r_launch_spmm(s, b, st));
+    for (int k = 0; k < K; ++k) {
+      const double nnz = (double)h->layers[k]->nnz;
+      algo_bytes += 2.0 * (8.0 * nnz + 4.0 * (n + 1) + 8.0 * n * b);
+    }
+    launches += 2;
     t_spmm += now_ms() - t0;
   }
 
-  // One fused BCGS + CholQR pass: G = [Q Z]^T Z -> F -> Z <- [Q Z] F, refill deficient columns.
-  // `cond` (device int, nullptr = always) skips the whole pass when zero.
+  // One fused BCGS + CholQR pass: G = [Q Z]^T Z -> R^{-1} -> Z <- [Q Z] [-C R^{-1}; R^{-1}],
+  // refill deficient columns.  `cond` (device int, nullptr = always) skips the pass when zero.
   void pip_pass(float* Z, const std::vector<float*>& basis, const int* cond, int* flags_out,
                 int* any_out) {
     const int nq = (int)basis.size();
     std::vector<float*> qz(basis);
     qz.push_back(Z);
     const BlockList L = blocks(qz, 0, nq + 1);
-    HIPCHK(n2v2r_launch_ts_tn(L, one(Z), n, h->partial.as<double>(), h->partial_elems,
-                              gsmall.as<double>(), cond, st));
-    HIPCHK(n2v2r_launch_pip_chol(gsmall.as<double>(), nq * b, b, csmall.as<float>(), flags_out,
+    tn(L, one(Z), gsmall.as<double>(), cond);
+    HIPCHK(n2v2r_launch_pip_chol(gsmall.as<double>(), nq * b, b, rinv.as<double>(), flags_out,
                                  any_out, cond, st));
-    HIPCHK(n2v2r_launch_ts_nn(L, csmall.as<float>(), b, b, out_one(Z), one(nullptr), 1.f, 0.f, n,
-                              cond, st));
-    HIPCHK(n2v2r_launch_fill_normal(Z, b, n, seed ^ (0xABCDull + ++fill_counter), flags_out,
-                                    any_out, st));
+    // rank-deficient columns (flags_out) are refilled with random values by the same launch
+    HIPCHK(n2v2r_launch_pip_apply(L, gsmall.as<double>(), rinv.as<double>(), nq * b, b,
+                                  out_one(Z), n, cond, flags_out,
+                                  seed ^ (0xABCDull + ++fill_counter), row0, st));
   }
 
-  // orthonormalise Z against Q[0..nq) and within itself: two fused passes (BCGS-PIP2), a third
+  // orthonormalise Z against `basis` and within itself: two fused passes (BCGS-PIP2), a third
   // only when the second one had to refill a rank-deficient column.
   void orthonormalize(float* Z, const std::vector<float*>& basis) {
     const double t0 = now_ms();
@@ -392,7 +600,7 @@ struct Eig {
   void expand_one(const float* w_from, const std::vector<float*>& basis, std::vector<float*>& qs,
                   std::vector<float*>& ws) {
     float* z = take();
-    HIPCHK(hipMemcpyAsync(z, w_from, sizeof(float) * n * b, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(z, w_from, sizeof(float) * npad * b, hipMemcpyDeviceToDevice, st));
     orthonormalize(z, basis);
     float* w = take();
     apply_M(z, w);
@@ -409,6 +617,7 @@ struct Eig {
     b = o.block ? o.block : 8;
     if (b != 8 && b != 16 && b != 32 && b != 64)
       throw StatusFail{N2V2R_ERR_BAD_ARG, "block must be 8, 16, 32 or 64"};
+    const int64_t nglob = h->n;
     // small graphs: shrink the block until the Krylov space fits well inside R^n
     int keep = 0, maxc = 0;
     for (;; b /= 2) {
@@ -417,7 +626,7 @@ struct Eig {
       maxc = o.max_basis ? o.max_basis : std::max(keep + 3 * b, (16 * keep) / 5);
       maxc = ((maxc + b - 1) / b) * b;
       const int cap =
-          (int)std::min<int64_t>((n / 2) / b * b, (int64_t)(N2V2R_MAX_BLOCKS - 1) * b);
+          (int)std::min<int64_t>((nglob / 2) / b * b, (int64_t)(N2V2R_MAX_BLOCKS - 1) * b);
       if (maxc > cap) maxc = cap;
       if (maxc >= keep + b) break;
       if (b == 8)
@@ -429,15 +638,19 @@ struct Eig {
     const int c_max = maxc;
     // scratch
     zk.clear();
-    for (int k = 0; k < std::min(K, SPMM_MAX_LAYERS); ++k) {
+    for (int k = 0; k < K; ++k) {
       zk.emplace_back(new DevBuf());
-      zk.back()->ensure(sizeof(float) * n * b);
+      zk.back()->ensure(sizeof(float) * npad * b);
+    }
+    if (h->comm) {
+      h->gath.ensure(sizeof(float) * h->world * npad * b);
+      zg.ensure(sizeof(float) * (size_t)K * h->world * npad * b);
     }
     h->partial_elems = std::max<size_t>(4096ull * 1024ull, (size_t)c_max * c_max * 8);
     h->partial.ensure(sizeof(double) * h->partial_elems);
     gsmall.ensure(sizeof(double) * (size_t)c_max * c_max);
     csmall.ensure(sizeof(float) * (size_t)c_max * c_max);
-    rinv.ensure(sizeof(float) * 64 * 64);
+    rinv.ensure(sizeof(double) * 64 * 64);
     flg.ensure(sizeof(int) * 256);
     anyflag.ensure(sizeof(int) * 4);
     h->theta.ensure(sizeof(double) * c_max);
@@ -446,9 +659,9 @@ struct Eig {
     std::vector<double> Sh((size_t)c_max * keep), wh(keep);
     std::vector<double> res2(keep);
 
-    // start block
+    // start block (counter-based: the same values whatever the row partition)
     float* q0 = take();
-    HIPCHK(n2v2r_launch_fill_normal(q0, b, n, seed, nullptr, nullptr, st));
+    HIPCHK(n2v2r_launch_fill_normal(q0, b, n, seed, nullptr, nullptr, (uint64_t)row0 * b, st));
     Q.assign(1, q0);
     orthonormalize(q0, {});
     W.assign(1, take());
@@ -468,79 +681,36 @@ struct Eig {
     HIPCHK(hipHostMalloc((void**)&Hh, sizeof(double) * (size_t)c_max * c_max, 0));
     HIPCHK(hipHostMalloc((void**)&Sf, sizeof(float) * (size_t)c_max * keep, 0));
     struct PinnedFree {
-      double* h;
+      double* hh;
       float* s;
       ~PinnedFree() {
-        if (h) (void)hipHostFree(h);
+        if (hh) (void)hipHostFree(hh);
         if (s) (void)hipHostFree(s);
       }
     } pinned_guard{Hh, Sf};
-    hipEvent_t ev_h, ev_e0, ev_e1;
-    HIPCHK(hipEventCreateWithFlags(&ev_h, hipEventDisableTiming));
-    HIPCHK(hipEventCreate(&ev_e0));
-    HIPCHK(hipEventCreate(&ev_e1));
-    struct EvFree {
-      hipEvent_t a, b, c;
-      ~EvFree() {
-        (void)hipEventDestroy(a);
-        (void)hipEventDestroy(b);
-        (void)hipEventDestroy(c);
-      }
-    } ev_guard{ev_h, ev_e0, ev_e1};
-    // extra blocks expanded (against the old basis) while the host solves the projected
-    // problem; adapted so that their GPU time covers the host Rayleigh-Ritz time
-    int extras = 0;
-    if (o.overlap == -2) extras = std::max(1, std::min(nb_max - pb - 1, (nb_max - pb) / 2));
-    if (o.overlap > 0) extras = std::min(o.overlap, nb_max - pb - 1);
-    const bool adaptive = o.overlap == -2;
-    double t_blk_est = 0.0;
     for (;; ++cycle) {
-      const double tcy0 = now_ms();
-      int nexp = 0;
       while ((int)Q.size() < nb_max) {
         expand_one(W.back(), Q, Q, W);
         ++apps;
-        ++nexp;
       }
       const int nq = (int)Q.size();
       const int c = nq * b;
-      // H = Q^T W -> pinned host, then the host solves it on a worker thread
-      HIPCHK(n2v2r_launch_ts_tn(blocks(Q, 0, nq), blocks(W, 0, nq), n, h->partial.as<double>(),
-                                h->partial_elems, gsmall.as<double>(), nullptr, st));
+      // H = Q^T W
+      tn(blocks(Q, 0, nq), blocks(W, 0, nq), gsmall.as<double>(), nullptr);
       HIPCHK(hipMemcpyAsync(Hh, gsmall.as<double>(), sizeof(double) * c * c,
                             hipMemcpyDeviceToHost, st));
-      HIPCHK(hipEventRecord(ev_h, st));
-      double rr_ms = 0.0;
-      int rr_status = 0;
-      std::thread rr([&]() {
-        if (hipEventSynchronize(ev_h) != hipSuccess) {
-          rr_status = -1;
-          return;
+      HIPCHK(hipStreamSynchronize(st));
+      const double tr0 = now_ms();
+      for (int i = 0; i < c; ++i)
+        for (int j = 0; j < i; ++j) {
+          const double sv = 0.5 * (Hh[(size_t)i * c + j] + Hh[(size_t)j * c + i]);
+          Hh[(size_t)i * c + j] = sv;
+          Hh[(size_t)j * c + i] = sv;
         }
-        const double tr0 = now_ms();
-        for (int i = 0; i < c; ++i)
-          for (int j = 0; j < i; ++j) {
-            const double sv = 0.5 * (Hh[(size_t)i * c + j] + Hh[(size_t)j * c + i]);
-            Hh[(size_t)i * c + j] = sv;
-            Hh[(size_t)j * c + i] = sv;
-          }
-        rr_status = n2v2r_host_sym_eig_top(c, Hh, keep, wh.data(), Sh.data());
-        for (size_t i = 0; i < (size_t)c * keep; ++i) Sf[i] = (float)Sh[i];
-        rr_ms = now_ms() - tr0;
-      });
-      // meanwhile: continue the Krylov sequence against the un-restarted basis
-      std::vector<float*> E, EW, basis_e(Q);
-      HIPCHK(hipEventRecord(ev_e0, st));
-      for (int i = 0; i < extras; ++i) {
-        expand_one(i == 0 ? W.back() : EW.back(), basis_e, E, EW);
-        basis_e.push_back(E.back());
-        ++apps;
-      }
-      HIPCHK(hipEventRecord(ev_e1, st));
-      rr.join();
-      if (rr_status != 0)
+      if (n2v2r_host_sym_eig_top(c, Hh, keep, wh.data(), Sh.data()) != 0)
         throw StatusFail{N2V2R_ERR_NO_CONVERGENCE, "Rayleigh-Ritz eigensolve failed"};
-      t_rr += rr_ms;
+      for (size_t i = 0; i < (size_t)c * keep; ++i) Sf[i] = (float)Sh[i];
+      t_rr += now_ms() - tr0;
       HIPCHK(hipMemcpyAsync(csmall.as<float>(), Sf, sizeof(float) * c * keep,
                             hipMemcpyHostToDevice, st));
       HIPCHK(hipMemcpyAsync(h->theta.as<double>(), wh.data(), sizeof(double) * keep,
@@ -564,28 +734,18 @@ struct Eig {
         // G slice: columns [q0b*b, q0b*b + nt*b) of S (ld = keep)
         const float* g = csmall.as<float>() + q0b * b;
         HIPCHK(n2v2r_launch_ts_nn(blocks(Q, 0, nq), g, keep, nt * b, ox, one(nullptr), 1.f, 0.f, n,
-                                  nullptr, st));
+                                  nullptr, nullptr, 0, st));
         HIPCHK(n2v2r_launch_ts_nn(blocks(W, 0, nq), g, keep, nt * b, omx, one(nullptr), 1.f, 0.f,
-                                  n, nullptr, st));
+                                  n, nullptr, nullptr, 0, st));
       }
       HIPCHK(n2v2r_launch_resid(blocks(X, 0, pb), blocks(MX, 0, pb), h->theta.as<double>(), n,
                                 h->partial.as<double>(), h->partial_elems, h->resid.as<double>(),
                                 st));
+      h->allreduce_f64(h->resid.as<double>(), keep);
       HIPCHK(hipMemcpyAsync(res2.data(), h->resid.as<double>(), sizeof(double) * keep,
                             hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
       t_ortho += now_ms() - to0;
-      // adapt the overlap: enough extra blocks that their GPU time covers the host solve
-      if (extras > 0 && adaptive) {
-        float ems = 0.f;
-        HIPCHK(hipEventElapsedTime(&ems, ev_e0, ev_e1));
-        const double per_blk = std::max(1e-3, (double)ems / extras);
-        t_blk_est = t_blk_est > 0 ? 0.5 * (t_blk_est + per_blk) : per_blk;
-        const int want = (int)std::ceil(1.1 * rr_ms / t_blk_est);
-        extras = std::max(1, std::min(nb_max - pb - 1, want));
-      }
-      (void)tcy0;
-      (void)nexp;
       maxres = 0;
       conv = 0;
       const double th1 = std::max(wh[0], 1e-300);
@@ -608,17 +768,11 @@ struct Eig {
           }
         }
       }
-      if (done) {
-        for (float* p : E) give(p);
-        for (float* p : EW) give(p);
-        break;
-      }
-      // restart: [X | extras]; the extras are orthogonal to the old basis, hence to X.
-      // Without overlap, the classic Krylov-Schur next block (W_last against the old basis).
-      if (E.empty()) {
-        expand_one(W.back(), Q, E, EW);
-        ++apps;
-      }
+      if (done) break;
+      // restart: [X | orth(W_last) against the old basis] (thick restart)
+      std::vector<float*> E, EW;
+      expand_one(W.back(), Q, E, EW);
+      ++apps;
       for (float* p : Q) give(p);
       for (float* p : W) give(p);
       Q.assign(X.begin(), X.end());
@@ -631,7 +785,7 @@ struct Eig {
     for (int q = 0; q * b < d; ++q) {
       const int cols = std::min(b, d - q * b);
       HIPCHK(hipMemcpy2DAsync(Uout + q * b, sizeof(float) * ldu, X[q], sizeof(float) * b,
-                              sizeof(float) * cols, n, hipMemcpyDeviceToDevice, st));
+                              sizeof(float) * cols, npad, hipMemcpyDeviceToDevice, st));
     }
     HIPCHK(hipStreamSynchronize(st));
     if (stats) {
@@ -652,12 +806,27 @@ struct Eig {
   }
 };
 
+n2v2r_handle* new_handle(int device) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return nullptr;
+  if (device < 0 || device >= count) return nullptr;
+  auto* h = new (std::nothrow) n2v2r_handle();
+  if (!h) return nullptr;
+  h->device = device;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return nullptr;
+  }
+  return h;
+}
+
 }  // namespace
 
 // ======================================================================================
 extern "C" {
 
-const char* n2v2r_version(void) { return "n2v2r-mi355x 0.1.0 (gfx950)"; }
+const char* n2v2r_version(void) { return "n2v2r-mi355x 0.2.0 (gfx950)"; }
 
 int n2v2r_create(int device, n2v2r_handle** out) {
   if (!out) return N2V2R_ERR_BAD_ARG;
@@ -665,15 +834,78 @@ int n2v2r_create(int device, n2v2r_handle** out) {
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return N2V2R_ERR_HIP;
   if (device < 0 || device >= count) return N2V2R_ERR_BAD_ARG;
-  auto* h = new (std::nothrow) n2v2r_handle();
-  if (!h) return N2V2R_ERR_OUT_OF_MEMORY;
-  h->device = device;
-  if (hipSetDevice(device) != hipSuccess ||
-      hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete h;
+  n2v2r_handle* h = new_handle(device);
+  if (!h) return N2V2R_ERR_HIP;
+  *out = h;
+  return N2V2R_OK;
+}
+
+int n2v2r_comm_unique_id(char* out, size_t len) {
+  if (!out || len < sizeof(ncclUniqueId)) return N2V2R_ERR_BAD_ARG;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return N2V2R_ERR_HIP;
+  std::memcpy(out, &id, sizeof(id));
+  return N2V2R_OK;
+}
+
+int n2v2r_create_rccl(int device, int rank, int world, const char* unique_id,
+                      n2v2r_handle** out) {
+  if (!out || !unique_id || world < 1 || rank < 0 || rank >= world) return N2V2R_ERR_BAD_ARG;
+  *out = nullptr;
+  n2v2r_handle* h = new_handle(device);
+  if (!h) return N2V2R_ERR_HIP;
+  auto c = std::make_unique<RcclComm>();
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id, sizeof(id));
+  c->rank = rank;
+  c->world = world;
+  if (ncclCommInitRank(&c->c, world, id, rank) != ncclSuccess) {
+    n2v2r_destroy(h);
     return N2V2R_ERR_HIP;
   }
+  h->rank = rank;
+  h->world = world;
+  h->comm = std::move(c);
   *out = h;
+  return N2V2R_OK;
+}
+
+int n2v2r_simgroup_create(int world, n2v2r_simgroup** out) {
+  if (!out || world < 1) return N2V2R_ERR_BAD_ARG;
+  auto* g = new (std::nothrow) n2v2r_simgroup();
+  if (!g) return N2V2R_ERR_OUT_OF_MEMORY;
+  g->world = world;
+  g->ptrs.assign(world, nullptr);
+  g->host.resize(world);
+  *out = g;
+  return N2V2R_OK;
+}
+
+void n2v2r_simgroup_destroy(n2v2r_simgroup* g) { delete g; }
+
+int n2v2r_create_sim(int device, n2v2r_simgroup* g, int rank, n2v2r_handle** out) {
+  if (!out || !g || rank < 0 || rank >= g->world) return N2V2R_ERR_BAD_ARG;
+  *out = nullptr;
+  n2v2r_handle* h = new_handle(device);
+  if (!h) return N2V2R_ERR_HIP;
+  auto c = std::make_unique<ThreadComm>();
+  c->g = g;
+  c->rank = rank;
+  c->world = g->world;
+  h->rank = rank;
+  h->world = g->world;
+  h->comm = std::move(c);
+  *out = h;
+  return N2V2R_OK;
+}
+
+int n2v2r_dist_info(const n2v2r_handle* h, int* rank, int* world, int64_t* row0,
+                    int64_t* n_local) {
+  if (!h) return N2V2R_ERR_BAD_ARG;
+  if (rank) *rank = h->rank;
+  if (world) *world = h->world;
+  if (row0) *row0 = h->row0;
+  if (n_local) *n_local = h->nloc;
   return N2V2R_OK;
 }
 
@@ -682,6 +914,7 @@ void n2v2r_destroy(n2v2r_handle* h) {
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   h->layers.clear();
+  h->comm.reset();
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -710,7 +943,7 @@ int n2v2r_set_num_layers(n2v2r_handle* h, int num_layers, int64_t n) {
       return N2V2R_ERR_BAD_ARG;
     }
     h->K = num_layers;
-    h->n = n;
+    h->set_partition(n);
     h->layers.clear();
     for (int k = 0; k < num_layers; ++k) h->layers.emplace_back(new LayerDev());
     h->have_embedding = false;
@@ -741,43 +974,47 @@ int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const in
         return N2V2R_ERR_BAD_ARG;
       }
     LayerDev& L = *h->layers[k];
-    L.n_rows = n;
-    L.nnz = nnz;
-    L.indptr.ensure(sizeof(int64_t) * (n + 1));
-    L.indices.ensure(sizeof(int32_t) * std::max<int64_t>(nnz, 1));
-    L.data.ensure(sizeof(float) * std::max<int64_t>(nnz, 1));
-    HIPCHK(hipMemcpyAsync(L.indptr.p, indptr, sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice,
-                          h->stream));
-    if (nnz) {
-      HIPCHK(hipMemcpyAsync(L.indices.p, indices, sizeof(int32_t) * nnz, hipMemcpyHostToDevice,
-                            h->stream));
-      HIPCHK(hipMemcpyAsync(L.data.p, data, sizeof(float) * nnz, hipMemcpyHostToDevice,
-                            h->stream));
-    }
+    L.n_rows = h->nloc;
+    upload_rows(h->stream, h->row0, h->nloc, indptr, indices, data, L.indptr, L.indices, L.data,
+                L.nnz);
     bool sym = symmetric == N2V2R_SYM_YES;
-    std::vector<int64_t> tp;
-    std::vector<int32_t> tx;
-    std::vector<float> td;
     if (symmetric != N2V2R_SYM_YES) {
+      std::vector<int64_t> tp;
+      std::vector<int32_t> tx;
+      std::vector<float> td;
       host_transpose(n, nnz, indptr, indices, data, tp, tx, td);
       if (symmetric == N2V2R_SYM_DETECT)
-        sym = host_is_symmetric(n, nnz, indptr, indices, data, tp, tx, td);
+        sym = host_is_symmetric(n, indptr, indices, data, tp, tx, td);
+      if (!sym)
+        upload_rows(h->stream, h->row0, h->nloc, tp.data(), tx.data(), td.data(), L.t_indptr,
+                    L.t_indices, L.t_data, L.t_nnz);
     }
     L.symmetric = sym;
-    if (!sym) {
-      L.t_indptr.ensure(sizeof(int64_t) * (n + 1));
-      L.t_indices.ensure(sizeof(int32_t) * std::max<int64_t>(nnz, 1));
-      L.t_data.ensure(sizeof(float) * std::max<int64_t>(nnz, 1));
-      HIPCHK(hipMemcpyAsync(L.t_indptr.p, tp.data(), sizeof(int64_t) * (n + 1),
-                            hipMemcpyHostToDevice, h->stream));
-      if (nnz) {
-        HIPCHK(hipMemcpyAsync(L.t_indices.p, tx.data(), sizeof(int32_t) * nnz,
-                              hipMemcpyHostToDevice, h->stream));
-        HIPCHK(hipMemcpyAsync(L.t_data.p, td.data(), sizeof(float) * nnz, hipMemcpyHostToDevice,
-                              h->stream));
-      }
+    L.loaded = true;
+    h->have_embedding = false;
+    return N2V2R_OK;
+  });
+}
+
+int n2v2r_set_layer_csr_rows(n2v2r_handle* h, int k, int64_t n, int64_t row0, int64_t n_rows,
+                             int64_t nnz, const int64_t* indptr, const int32_t* indices,
+                             const float* data) {
+  return guarded(h, [&]() -> int {
+    if (k < 0 || k >= h->K || n != h->n || row0 != h->row0 || n_rows != h->nloc || nnz < 0 ||
+        !indptr || (nnz > 0 && (!indices || !data)) || indptr[0] != 0 || indptr[n_rows] != nnz) {
+      h->set_err("bad local CSR rows for layer %d (expected rows [%lld, %lld))", k,
+                 (long long)h->row0, (long long)(h->row0 + h->nloc));
+      return N2V2R_ERR_BAD_ARG;
     }
-    HIPCHK(hipStreamSynchronize(h->stream));  // host vectors die here
+    for (int64_t p = 0; p < nnz; ++p)
+      if (indices[p] < 0 || indices[p] >= n) {
+        h->set_err("layer %d: column index out of range", k);
+        return N2V2R_ERR_BAD_ARG;
+      }
+    LayerDev& L = *h->layers[k];
+    L.n_rows = h->nloc;
+    upload_rows(h->stream, 0, n_rows, indptr, indices, data, L.indptr, L.indices, L.data, L.nnz);
+    L.symmetric = true;
     L.loaded = true;
     h->have_embedding = false;
     return N2V2R_OK;
@@ -805,22 +1042,32 @@ int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_sta
     Eig eig{};
     eig.h = h;
     eig.st = h->stream;
-    eig.n = h->n;
+    eig.n = h->nloc;
+    eig.npad = h->npad;
+    eig.row0 = h->row0;
     eig.K = h->K;
     eig.stats = stats;
     const int ldu = ((d + 63) / 64) * 64;  // a multiple of every block width
-    h->U.ensure(sizeof(float) * h->n * ldu);
-    HIPCHK(hipMemsetAsync(h->U.p, 0, sizeof(float) * h->n * ldu, h->stream));
+    h->U.ensure(sizeof(float) * h->npad * ldu);
+    HIPCHK(hipMemsetAsync(h->U.p, 0, sizeof(float) * h->npad * ldu, h->stream));
     std::vector<double> theta;
     const int st = eig.run(d, o, theta, h->U.as<float>(), ldu);
     const int b = eig.b;
     // deterministic signs: largest-magnitude entry of every column of U positive
-    h->partial.ensure(sizeof(double) * 1024 * (size_t)ldu);
+    h->keys.ensure(sizeof(unsigned long long) * 1024 * (size_t)ldu);
+    h->best.ensure(sizeof(unsigned long long) * ldu);
     h->colscale.ensure(sizeof(float) * ldu);
-    HIPCHK(n2v2r_launch_sign_convention(h->U.as<float>(), ldu, h->n, d,
-                                        h->partial.as<unsigned long long>(),
-                                        h->partial.bytes / sizeof(unsigned long long),
-                                        h->colscale.as<float>(), h->stream));
+    HIPCHK(n2v2r_launch_colmax_keys(h->U.as<float>(), ldu, h->nloc, d, h->row0,
+                                    h->keys.as<unsigned long long>(), 1024 * (size_t)ldu,
+                                    h->best.as<unsigned long long>(), h->stream));
+    if (h->comm)
+      h->comm->allreduce_max_u64(h->best.as<unsigned long long>(), ldu, h->stream);
+    HIPCHK(n2v2r_launch_colmax_sign(h->best.as<unsigned long long>(), ldu, h->U.as<float>(), ldu, d,
+                                    h->row0, h->nloc, h->colscale.as<float>(), h->stream));
+    if (h->comm)
+      h->comm->allreduce_sum_f32(h->colscale.as<float>(), ldu, h->stream);
+    HIPCHK(n2v2r_launch_scale_cols(h->U.as<float>(), ldu, h->npad, h->colscale.as<float>(),
+                                   h->stream));
     // Y_k = A_k^T U diag(theta)^(-1/4)  (sigma = sqrt(theta); V sqrt(sigma) = A^T U sigma^-1/2)
     h->d = d;
     h->ldy = ldu;
@@ -830,10 +1077,16 @@ int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_sta
       h->sigma[j] = std::sqrt(std::max(theta[j], 0.0));
       sc[j] = h->sigma[j] > 0 ? (float)(1.0 / std::sqrt(h->sigma[j])) : 0.f;
     }
-    h->colscale.ensure(sizeof(float) * ldu);
     HIPCHK(hipMemcpyAsync(h->colscale.p, sc.data(), sizeof(float) * ldu, hipMemcpyHostToDevice,
                           h->stream));
-    h->Y.ensure(sizeof(float) * (size_t)h->K * h->n * ldu);
+    const float* ug = h->U.as<float>();
+    DevBuf ugath;
+    if (h->comm) {
+      ugath.ensure(sizeof(float) * h->world * h->npad * ldu);
+      h->gather_panel(h->U.as<float>(), ugath.as<float>(), ldu);
+      ug = ugath.as<float>();
+    }
+    h->Y.ensure(sizeof(float) * (size_t)h->K * h->npad * ldu);
     for (int q = 0; q * b < ldu; ++q) {
       SpmmArgs a{};
       a.K = h->K;
@@ -843,8 +1096,8 @@ int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_sta
       a.colscale = h->colscale.as<float>() + q * b;
       for (int k = 0; k < h->K; ++k) {
         a.A[k] = h->layers[k]->csr_t();
-        a.X[k] = h->U.as<float>() + q * b;
-        a.Y[k] = h->Y.as<float>() + (size_t)k * h->n * ldu + q * b;
+        a.X[k] = ug + q * b;
+        a.Y[k] = h->Y.as<float>() + (size_t)k * h->npad * ldu + q * b;
       }
       HIPCHK(n2v2r_launch_spmm(a, b, h->stream));
     }
@@ -858,6 +1111,7 @@ int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_sta
   });
 }
 
+// local rows (row0 .. row0 + n_local) on a distributed handle
 int n2v2r_get_embedding(n2v2r_handle* h, float* Y) {
   return guarded(h, [&]() -> int {
     if (!h->have_embedding) {
@@ -865,9 +1119,9 @@ int n2v2r_get_embedding(n2v2r_handle* h, float* Y) {
       return N2V2R_ERR_NOT_READY;
     }
     for (int k = 0; k < h->K; ++k)
-      HIPCHK(hipMemcpy2DAsync(Y + (size_t)k * h->n * h->d, sizeof(float) * h->d,
-                              h->Y.as<float>() + (size_t)k * h->n * h->ldy,
-                              sizeof(float) * h->ldy, sizeof(float) * h->d, h->n,
+      HIPCHK(hipMemcpy2DAsync(Y + (size_t)k * h->nloc * h->d, sizeof(float) * h->d,
+                              h->Y.as<float>() + (size_t)k * h->npad * h->ldy,
+                              sizeof(float) * h->ldy, sizeof(float) * h->d, h->nloc,
                               hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     return N2V2R_OK;
@@ -881,9 +1135,9 @@ int n2v2r_get_left_embedding(n2v2r_handle* h, float* X) {
       return N2V2R_ERR_NOT_READY;
     }
     HIPCHK(hipMemcpy2DAsync(X, sizeof(float) * h->d, h->U.as<float>(), sizeof(float) * h->ldy,
-                            sizeof(float) * h->d, h->n, hipMemcpyDeviceToHost, h->stream));
+                            sizeof(float) * h->d, h->nloc, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
-    for (int64_t i = 0; i < h->n; ++i)
+    for (int64_t i = 0; i < h->nloc; ++i)
       for (int j = 0; j < h->d; ++j) X[i * h->d + j] *= (float)std::sqrt(h->sigma[j]);
     return N2V2R_OK;
   });
@@ -903,8 +1157,12 @@ int n2v2r_get_singular_values(n2v2r_handle* h, double* s) {
 int n2v2r_set_embedding(n2v2r_handle* h, int num_layers, int64_t n, int d, const float* Y) {
   return guarded(h, [&]() -> int {
     if (num_layers < 1 || n < 1 || d < 1 || !Y) return N2V2R_ERR_BAD_ARG;
+    if (h->comm) {
+      h->err = "set_embedding is single-GPU only";
+      return N2V2R_ERR_BAD_ARG;
+    }
     h->K = num_layers;
-    h->n = n;
+    h->set_partition(n);
     h->d = d;
     h->ldy = d;
     h->Y.ensure(sizeof(float) * (size_t)num_layers * n * d);
@@ -1017,15 +1275,34 @@ int n2v2r_rank(n2v2r_handle* h, int strategy, const int* dims, int n_dims, const
     }
     const int ncmp = (int)layer_i.size();
     const int C = plan.n_cols;
-    h->D.ensure(sizeof(double) * (size_t)ncmp * C * h->n);
-    h->borda.ensure(sizeof(int64_t) * (size_t)ncmp * h->n);
+    const int64_t n = h->n;
+    h->D.ensure(sizeof(double) * (size_t)ncmp * C * n);
+    h->borda.ensure(sizeof(int64_t) * (size_t)ncmp * n);
     const double t0 = now_ms();
-    for (int c = 0; c < ncmp; ++c)
-      HIPCHK(n2v2r_launch_distances(h->Y.as<float>(), h->K, h->n, h->ldy, strategy, layer_i[c],
-                                    plan, h->D.as<double>() + (size_t)c * C * h->n, h->stream));
+    if (!h->comm) {
+      for (int c = 0; c < ncmp; ++c)
+        HIPCHK(n2v2r_launch_distances(h->Y.as<float>(), h->K, n, h->ldy, h->npad, strategy,
+                                      layer_i[c], plan, h->D.as<double>() + (size_t)c * C * n, n,
+                                      h->stream));
+    } else {
+      // local rows -> [ncmp][C][npad], then every column gathered into the global table
+      h->Dloc.ensure(sizeof(double) * (size_t)ncmp * C * h->npad);
+      h->Dgat.ensure(sizeof(double) * (size_t)h->world * h->npad);
+      for (int c = 0; c < ncmp; ++c)
+        HIPCHK(n2v2r_launch_distances(h->Y.as<float>(), h->K, h->nloc, h->ldy, h->npad, strategy,
+                                      layer_i[c], plan,
+                                      h->Dloc.as<double>() + (size_t)c * C * h->npad, h->npad,
+                                      h->stream));
+      for (int s = 0; s < ncmp * C; ++s) {
+        h->comm->allgather(h->Dloc.as<double>() + (size_t)s * h->npad, h->Dgat.p,
+                           sizeof(double) * h->npad, h->stream);
+        HIPCHK(hipMemcpyAsync(h->D.as<double>() + (size_t)s * n, h->Dgat.p, sizeof(double) * n,
+                              hipMemcpyDeviceToDevice, h->stream));
+      }
+    }
     HIPCHK(hipStreamSynchronize(h->stream));
     const double t1 = now_ms();
-    run_borda(h, h->D.as<double>(), h->n, ncmp * C, C, h->borda.as<int64_t>());
+    run_borda(h, h->D.as<double>(), n, ncmp * C, C, h->borda.as<int64_t>());
     HIPCHK(hipStreamSynchronize(h->stream));
     h->ms_dist = t1 - t0;
     h->ms_borda = now_ms() - t1;
@@ -1100,13 +1377,20 @@ int n2v2r_borda_columns(n2v2r_handle* h, const double* D, int64_t n, int n_cols,
   });
 }
 
+// float32 column sums of layer k for all N nodes (row sums of the local rows of A^T, gathered)
 int n2v2r_column_sums(n2v2r_handle* h, int k, float* out) {
   return guarded(h, [&]() -> int {
     if (k < 0 || k >= h->K || !out || !h->layers[k]->loaded) return N2V2R_ERR_BAD_ARG;
-    DevBuf o;
-    o.ensure(sizeof(float) * h->n);
+    DevBuf o, g;
+    o.ensure(sizeof(float) * h->npad);
     HIPCHK(n2v2r_launch_row_sums(h->layers[k]->csr_t(), o.as<float>(), h->stream));
-    HIPCHK(hipMemcpyAsync(out, o.p, sizeof(float) * h->n, hipMemcpyDeviceToHost, h->stream));
+    const float* src = o.as<float>();
+    if (h->comm) {
+      g.ensure(sizeof(float) * h->world * h->npad);
+      h->comm->allgather(o.p, g.p, sizeof(float) * h->npad, h->stream);
+      src = g.as<float>();
+    }
+    HIPCHK(hipMemcpyAsync(out, src, sizeof(float) * h->n, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     return N2V2R_OK;
   });
@@ -1116,7 +1400,7 @@ int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, con
                      float* Y, double* avg_ms, double* algo_bytes) {
   return guarded(h, [&]() -> int {
     if (k < 0 || k >= h->K || !h->layers[k]->loaded || (b != 8 && b != 16 && b != 32 && b != 64) ||
-        reps < 1 || !X)
+        reps < 1 || !X || h->comm)
       return N2V2R_ERR_BAD_ARG;
     const LayerDev& L = *h->layers[k];
     DevBuf xd, yd;
@@ -1146,7 +1430,7 @@ int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, con
     (void)hipEventDestroy(e1);
     if (avg_ms) *avg_ms = (double)ms / reps;
     if (algo_bytes)
-      *algo_bytes = 8.0 * (double)L.nnz + 4.0 * (double)(h->n + 1) + 8.0 * (double)h->n * b;
+      *algo_bytes = 8.0 * (double)a.A[0].nnz + 4.0 * (double)(h->n + 1) + 8.0 * (double)h->n * b;
     if (Y)
       HIPCHK(hipMemcpyAsync(Y, yd.p, sizeof(float) * h->n * b, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));

@@ -26,12 +26,12 @@ __device__ __forceinline__ double clip02_keep_nan(double x) {
 
 // Y: [K][N][ldy] fp32.  Comparison layer i; strategy picks embed_one.  Out: [C][N] fp64.
 __global__ __launch_bounds__(256) void distances_kernel(const float* __restrict__ Y, int K,
-                                                        int64_t n, int64_t ldy, int strategy,
-                                                        int layer_i, DistPlan plan,
-                                                        double* __restrict__ out) {
+                                                        int64_t n, int64_t ldy, int64_t lrows,
+                                                        int strategy, int layer_i, DistPlan plan,
+                                                        double* __restrict__ out, int64_t ldo) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
-  const int64_t lstride = n * ldy;
+  const int64_t lstride = lrows * ldy;  // rows per layer block of Y (>= n when padded)
   const float* y2 = Y + (int64_t)layer_i * lstride + r * ldy;
   double suv = 0, suu = 0, svv = 0, sdd = 0, su = 0, sv = 0;
   int next = 0;
@@ -93,17 +93,19 @@ __global__ __launch_bounds__(256) void distances_kernel(const float* __restrict_
         }
         res = clip02_keep_nan(1.0 - cuv / sqrt(cuu * cvv));
       }
-      out[(int64_t)plan.col_out[next] * n + r] = res;
+      out[(int64_t)plan.col_out[next] * ldo + r] = res;
       ++next;
     }
   }
 }
 
+// Y: [K][lrows][ldy]; the first n rows are computed; column c of the output at out + c * ldo
 extern "C" hipError_t n2v2r_launch_distances(const float* Y, int K, int64_t n, int64_t ldy,
-                                             int strategy, int layer_i, const DistPlan& plan,
-                                             double* out, hipStream_t stream) {
+                                             int64_t lrows, int strategy, int layer_i,
+                                             const DistPlan& plan, double* out, int64_t ldo,
+                                             hipStream_t stream) {
   hipLaunchKernelGGL(distances_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                     Y, K, n, ldy, strategy, layer_i, plan, out);
+                     Y, K, n, ldy, lrows, strategy, layer_i, plan, out, ldo);
   return hipGetLastError();
 }
 

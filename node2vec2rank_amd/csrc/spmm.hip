@@ -15,6 +15,9 @@
 #include "common.h"
 
 #define SPMM_MAX_LAYERS 8
+#ifndef N2V2R_SPMM_WGS
+#define N2V2R_SPMM_WGS 2048  // workgroups per launch (8 per CU); rows are grid-strided
+#endif
 
 struct SpmmArgs {
   CsrDev A[SPMM_MAX_LAYERS];
@@ -93,31 +96,35 @@ __global__ __launch_bounds__(256) void spmm_csr_panel_kernel(SpmmArgs args) {
   const int lane = threadIdx.x & 63;
   const int k0 = args.sum ? 0 : (int)blockIdx.y;
   const int64_t n = args.A[k0].n_rows;
-  const int64_t wave_row0 = ((int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * RPW;
-  if (wave_row0 >= n) return;
-  const int64_t row = wave_row0 + lane / L;
-  const bool row_ok = row < n;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  if (args.sum) {
-    for (int k = 0; k < args.K; ++k)
-      spmm_row_accumulate<B, RPW>(args.A[k], args.X[k], args.ldx, row, row_ok, lane, acc);
-  } else {
-    spmm_row_accumulate<B, RPW>(args.A[k0], args.X[k0], args.ldx, row, row_ok, lane, acc);
-  }
-#pragma unroll
-  for (int m = LPN; m < L; m <<= 1) {
-    acc.x += __shfl_xor(acc.x, m, 64);
-    acc.y += __shfl_xor(acc.y, m, 64);
-    acc.z += __shfl_xor(acc.z, m, 64);
-    acc.w += __shfl_xor(acc.w, m, 64);
-  }
   const int li = lane % L;
-  if (row_ok && li < LPN) {
-    if (args.colscale) {
-      f32x4 sc = *reinterpret_cast<const f32x4*>(args.colscale + li * 4);
-      acc *= sc;
+  // grid-stride over row groups: a bounded number of long-lived workgroups (measured 4-7 %
+  // faster than one short workgroup per 4 x RPW rows)
+  const int64_t nwaves_total = (int64_t)gridDim.x * (blockDim.x / 64);
+  for (int64_t wid = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+       wid * RPW < n; wid += nwaves_total) {
+    const int64_t row = wid * RPW + lane / L;
+    const bool row_ok = row < n;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (args.sum) {
+      for (int k = 0; k < args.K; ++k)
+        spmm_row_accumulate<B, RPW>(args.A[k], args.X[k], args.ldx, row, row_ok, lane, acc);
+    } else {
+      spmm_row_accumulate<B, RPW>(args.A[k0], args.X[k0], args.ldx, row, row_ok, lane, acc);
     }
-    *reinterpret_cast<f32x4*>(args.Y[k0] + row * args.ldy + li * 4) = acc;
+#pragma unroll
+    for (int m = LPN; m < L; m <<= 1) {
+      acc.x += __shfl_xor(acc.x, m, 64);
+      acc.y += __shfl_xor(acc.y, m, 64);
+      acc.z += __shfl_xor(acc.z, m, 64);
+      acc.w += __shfl_xor(acc.w, m, 64);
+    }
+    if (row_ok && li < LPN) {
+      if (args.colscale) {
+        f32x4 sc = *reinterpret_cast<const f32x4*>(args.colscale + li * 4);
+        acc *= sc;
+      }
+      *reinterpret_cast<f32x4*>(args.Y[k0] + row * args.ldy + li * 4) = acc;
+    }
   }
 }
 
@@ -125,7 +132,10 @@ template <int B, int RPW>
 static void launch_spmm_t(const SpmmArgs& args, hipStream_t stream) {
   const int64_t n = args.A[0].n_rows;
   const int64_t waves = (n + RPW - 1) / RPW;
-  dim3 grid((unsigned)((waves + 3) / 4), args.sum ? 1 : args.K);
+  int64_t wgs = (waves + 3) / 4;
+  const int64_t cap = (int64_t)N2V2R_SPMM_WGS / (args.sum ? 1 : args.K);
+  if (wgs > cap) wgs = cap;
+  dim3 grid((unsigned)wgs, args.sum ? 1 : args.K);
   hipLaunchKernelGGL((spmm_csr_panel_kernel<B, RPW>), grid, dim3(256), 0, stream, args);
 }
 

@@ -1,0 +1,169 @@
+"""Row-partitioned UASE + ranking on one MI355X.
+
+W ranks run as threads of this process on device 0 through the in-process thread communicator
+(RCCL refuses two ranks on one device); each rank owns rows [g R, (g+1) R), R = ceil(N / W), of
+every layer and of every Krylov block, gathers panels per SpMM stage and all-reduces the small
+Gram / projection / residual reductions, exactly as the RCCL ranks do.  The RCCL communicator
+itself is exercised at world size 1 (every collective still goes through RCCL).
+
+Checks: every rank ends with identical distances and Borda; the partitioned result matches the
+single-GPU engine and the reference's golden vectors within the UASE tolerances of
+test_gpu_parity.py (reductions are summed in a different order, so not bit-exact)."""
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import fixture_layers, load_fixture
+from oracle import n2v2r_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_ranks(world, fn, timeout=300):
+    from node2vec2rank_amd import _lib
+    group = _lib.SimGroup(world)
+    out = [None] * world
+    errs = []
+
+    def work(r):
+        try:
+            eng = _lib.Engine.sim(0, group, r)
+            out[r] = fn(eng, r)
+            eng.close()
+        except BaseException as e:  # noqa: BLE001 - reported below
+            errs.append((r, repr(e)))
+
+    ts = [threading.Thread(target=work, args=(r,), daemon=True) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout)
+    assert not any(t.is_alive() for t in ts), "distributed ranks hung"
+    group.close()
+    assert not errs, errs
+    return out
+
+
+def _fit_rank(layers, d, dims, metrics, strategy, seed, rows_only=False):
+    def fn(eng, r):
+        if rows_only:
+            n = layers[0].shape[0]
+            eng.set_layer_rows(n, len(layers), [])  # sets the partition first
+            _, _, row0, nl = eng.dist_info()
+            eng.set_layer_rows(n, len(layers), [A[row0:row0 + nl] for A in layers])
+        else:
+            eng.set_layers(layers)
+        st = eng.uase(d, seed=seed)
+        ncmp, _ = eng.rank(strategy, dims, metrics)
+        return dict(info=eng.dist_info(), stats=st, Y=eng.embedding(), X=eng.left_embedding(),
+                    s=eng.singular_values(),
+                    D=[eng.distances(c) for c in range(ncmp)],
+                    B=[eng.borda(c) for c in range(ncmp)],
+                    cs=[eng.column_sums(k) for k in range(len(layers))])
+    return fn
+
+
+def _single(engine, layers, d, dims, metrics, strategy, seed):
+    engine.set_layers(layers)
+    engine.uase(d, seed=seed)
+    ncmp, _ = engine.rank(strategy, dims, metrics)
+    return dict(Y=engine.embedding(), s=engine.singular_values(),
+                D=[engine.distances(c) for c in range(ncmp)],
+                B=[engine.borda(c) for c in range(ncmp)])
+
+
+def _concat(res):
+    Y = np.concatenate([r["Y"] for r in res], axis=1)
+    X = np.concatenate([r["X"] for r in res], axis=0)
+    return Y, X
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("name", ["er_cfg1", "k4_strategies", "directed_weighted"])
+def test_partitioned_matches_reference(engine, name, world):
+    fx = load_fixture(name)
+    layers = fixture_layers(fx)
+    n = layers[0].shape[0]
+    d = int(fx["dims"].max())
+    dims = [int(x) for x in fx["dims"]]
+    metrics = [str(x) for x in fx["metrics"]]
+    strategy = str(fx["strategies"][0])
+    seed = int(fx["seed"])
+    res = _run_ranks(world, _fit_rank(layers, d, dims, metrics, strategy, seed))
+    # partition: contiguous equal blocks covering [0, n)
+    R = -(-n // world)
+    for g, r in enumerate(res):
+        assert r["info"][:3] == (g, world, min(n, g * R))
+    assert sum(r["info"][3] for r in res) == n
+    # identical global results on every rank
+    for r in res[1:]:
+        np.testing.assert_array_equal(r["s"], res[0]["s"])
+        for c in range(len(r["D"])):
+            np.testing.assert_array_equal(r["D"][c], res[0]["D"][c])
+            np.testing.assert_array_equal(r["B"][c], res[0]["B"][c])
+    Y, _ = _concat(res)
+    # vs the reference (golden): same bar as the single-GPU test
+    np.testing.assert_allclose(res[0]["s"], fx["sigma"], rtol=2e-5)
+    Ya, _, _ = orc.uase(layers, d, seed=seed + 1)
+    env = np.abs(orc.align_signs(Ya, fx["Y"]) - fx["Y"]).max() / np.abs(fx["Y"]).max()
+    err = np.abs(orc.align_signs(Y.astype(np.float64), fx["Y"]) - fx["Y"]).max() \
+        / np.abs(fx["Y"]).max()
+    assert err <= max(5e-4, 3 * env), (name, world, err, env)
+    # vs the single-GPU engine: same signs (deterministic convention), close values
+    one = _single(engine, layers, d, dims, metrics, strategy, seed)
+    np.testing.assert_allclose(res[0]["s"], one["s"], rtol=1e-5)
+    assert np.abs(Y - one["Y"]).max() <= max(5e-4, 3 * env) * np.abs(one["Y"]).max()
+    # Borda is a pure function of D (bit-exact given identical D)
+    for c in range(len(one["D"])):
+        assert np.all(engine.borda_columns(res[0]["D"][c]) == res[0]["B"][c])
+    # column sums are global and exact
+    for k, A in enumerate(layers):
+        np.testing.assert_allclose(res[0]["cs"][k], np.asarray(A.sum(axis=0)).ravel(),
+                                   rtol=1e-6, atol=1e-6)
+
+
+def test_partitioned_er_large_rows_ingest(engine):
+    """N=20k ER, d=16, 4 ranks, local-rows ingest (no global CSR handed to the engine)."""
+    from node2vec2rank_amd import synthetic
+    layers = synthetic.er_layers(20_000, 12.0, 2, seed_base=5150)
+    d, dims, metrics = 16, [4, 16], ["cosine", "euclidean"]
+    res = _run_ranks(4, _fit_rank(layers, d, dims, metrics, "sequential", 9, rows_only=True))
+    one = _single(engine, layers, d, dims, metrics, "sequential", 9)
+    Y, X = _concat(res)
+    np.testing.assert_allclose(res[0]["s"], one["s"], rtol=1e-5)
+    for r in res:
+        st = r["stats"]
+        assert st["converged"] == d or st["stagnated"] == 1, st
+    # Ritz residual of the gathered result in fp64
+    M = sum((A @ A.T) for A in layers)
+    U = X / np.sqrt(res[0]["s"])[None, :]
+    R = M @ U.astype(np.float64) - U * (res[0]["s"] ** 2)[None, :]
+    assert np.abs(R).max() / res[0]["s"][0] ** 2 < 1e-4
+    assert np.abs(Y - one["Y"]).max() <= 2e-3 * np.abs(one["Y"]).max()
+    from scipy.stats import kendalltau
+    assert kendalltau(res[0]["B"][0], one["B"][0]).statistic > 0.99
+
+
+def test_rccl_world1(engine):
+    """Every collective routed through RCCL at world size 1 (init, all-gather of panels and of
+    the distance columns, all-reduces of Gram / residual / sign keys)."""
+    from node2vec2rank_amd import _lib
+    fx = load_fixture("er_cfg1")
+    layers = fixture_layers(fx)
+    d = int(fx["dims"].max())
+    dims = [int(x) for x in fx["dims"]]
+    metrics = [str(x) for x in fx["metrics"]]
+    strategy = str(fx["strategies"][0])
+    seed = int(fx["seed"])
+    uid = _lib.comm_unique_id()
+    eng = _lib.Engine.rccl(0, 0, 1, uid)
+    try:
+        res = _fit_rank(layers, d, dims, metrics, strategy, seed)(eng, 0)
+    finally:
+        eng.close()
+    one = _single(engine, layers, d, dims, metrics, strategy, seed)
+    np.testing.assert_allclose(res["s"], one["s"], rtol=1e-6)
+    assert np.abs(res["Y"] - one["Y"]).max() <= 1e-4 * np.abs(one["Y"]).max()
+    for c in range(len(one["D"])):
+        np.testing.assert_allclose(res["D"][c], one["D"][c], rtol=1e-6, atol=1e-9)
