@@ -1,6 +1,7 @@
 """Benchmark: nodes ranked/s of the fit-and-rank path on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg1|cfg4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg1|cfg4|cfg5]
+                    [--mode auto|replicas|partitioned]
 
 One step = ``fit_transform_rank()`` + ``aggregate_transform()`` of the engine on one synthetic
 2-layer graph whose CSR layers are already resident in HBM: UASE (block Krylov-Schur on the
@@ -8,9 +9,15 @@ GPU), distances for every (dim, metric) column, Borda, and the copy of the dista
 Borda scores back to the host (what the reference API returns).  Default workload is
 BASELINE.json configs[1] (cfg2: 2-layer ER N=100k, avg-deg 20, d=64).
 
-Multi-GPU (torchrun, one process per GPU): every rank ranks its own independent graph
-(different generator seeds): no data-path collective ("scaling": "weak", replicas).  A gloo
-group provides the barrier and the max-over-ranks of the timed region.
+Multi-GPU (torchrun, one process per GPU), two modes:
+  * replicas (default for cfg1/2/4): every rank ranks its own independent graph (different
+    generator seeds), no data-path collective, "scaling": "weak";
+  * partitioned (default for cfg5): ONE graph row-partitioned over the ranks (RCCL communicator
+    of the engine: panel all-gathers per SpMM stage, all-reduce of the Gram / Rayleigh-Ritz /
+    residual reductions), every rank builds only its own rows (counter-based ER generator),
+    "scaling": "strong".
+A gloo group provides the barrier, the max-over-ranks of the timed region and the broadcast
+of the RCCL unique id.
 
 Extra JSON fields: ``roofline`` (SpMM kernel, HIP-event timed on the engine stream at the
 Krylov panel width) and ``cpu_baseline`` (the reference algorithm restated in oracle/, on a
@@ -37,7 +44,11 @@ CONFIGS = {
     "cfg4": dict(n=1_000_000, avg_deg=50.0, dims=[8, 16, 32, 64, 128], d=128,
                  desc="cfg4: 2-layer ER N=1M avg-deg 50, dims {8,16,32,64,128} x "
                       "{cosine,euclidean}, sequential"),
+    "cfg5": dict(n=10_000_000, avg_deg=30.0, dims=[128], d=128, mode="partitioned",
+                 desc="cfg5: 2-layer ER N=10M avg-deg 30, d=128, cosine+euclidean, sequential, "
+                      "row-partitioned"),
 }
+CPU_SAMPLE = {"cfg1": 1000, "cfg2": 50_000, "cfg4": 20_000, "cfg5": 20_000}
 METRICS = ["cosine", "euclidean"]
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
@@ -81,6 +92,13 @@ class _Group:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
 
+    def bcast_bytes(self, b: bytes | None) -> bytes:
+        if not self.dist:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
     def close(self):
         if self.dist:
             self.dist.destroy_process_group()
@@ -95,12 +113,13 @@ def _torch_sync():
         pass
 
 
-def run_step(eng, cfg, seed):
+def run_step(eng, cfg, seed, fetch=True):
     st = eng.uase(cfg["d"], seed=seed)
     ncmp, _ = eng.rank("sequential", cfg["dims"], METRICS)
     out = []
-    for c in range(ncmp):
-        out.append((eng.distances(c), eng.borda(c)))
+    if fetch:  # the reference API hands the distance table and the Borda scores to the caller
+        for c in range(ncmp):
+            out.append((eng.distances(c), eng.borda(c)))
     return st, out
 
 
@@ -124,13 +143,19 @@ def cpu_baseline(sample_n=20_000, avg_deg=20.0, d=64, dims=(64,)):
     total = t3 - t0
     return {
         "value": sample_n / total, "unit": "nodes/s", "cores": 1, "kind": "port",
-        "sample": (f"2-layer ER N={sample_n} avg-deg {avg_deg:g}, d={d}, cosine+euclidean "
-                   f"(the bench workload at {sample_n / 100_000:g}x its nodes; the Borda "
-                   f"stage is O(C N^2) so the full-size rate is lower), oracle faithful mode, "
-                   f"1 thread"),
+        "sample": (f"2-layer ER N={sample_n} avg-deg {avg_deg:g}, d={d}, dims {list(dims)} x "
+                   f"cosine+euclidean (the bench workload's graph family at fewer nodes; the "
+                   f"Borda stage is O(C N^2) so the full-size rate is lower), oracle faithful "
+                   f"mode, 1 thread"),
         "stages_s": {"svds": round(t1 - t0, 3), "distances": round(t2 - t1, 3),
                      "borda": round(t3 - t2, 3)},
     }
+
+
+def _layers_partitioned(cfg, row0, n_local):
+    from node2vec2rank_amd import synthetic
+    return [synthetic.er_layer_rows(cfg["n"], cfg["avg_deg"], 2000 + k, row0, n_local)
+            for k in range(2)]
 
 
 def main():
@@ -139,8 +164,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--mode", default="auto", choices=["auto", "replicas", "partitioned"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=50_000)
+    ap.add_argument("--cpu-sample", type=int, default=0)
     args = ap.parse_args()
 
     world, rank, local = _dist_env()
@@ -148,43 +174,65 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     group = _Group(world)
     cfg = CONFIGS[args.config]
+    mode = args.mode if args.mode != "auto" else cfg.get("mode", "replicas")
 
     from node2vec2rank_amd import _lib, synthetic
-    eng = _lib.Engine(local)
-    layers = synthetic.er_layers(cfg["n"], cfg["avg_deg"], 2, seed_base=1000 + 17 * rank)
-    nnz = [int(a.nnz) for a in layers]
-    eng.set_layers(layers)  # CSR -> HBM, untimed (inputs resident when timing starts)
-    seed = 42 + rank
+    t_build = time.perf_counter()
+    if mode == "partitioned":
+        if world > 1:
+            uid = group.bcast_bytes(_lib.comm_unique_id() if rank == 0 else None)
+            eng = _lib.Engine.rccl(local, rank, world, uid)
+        else:
+            eng = _lib.Engine(local)
+        eng.set_layer_rows(cfg["n"], 2, [])  # partition first
+        _, _, row0, n_local = eng.dist_info()
+        local_layers = _layers_partitioned(cfg, row0, n_local)
+        nnz = [int(group.sum(float(a.nnz))) for a in local_layers]
+        eng.set_layer_rows(cfg["n"], 2, local_layers)  # local CSR rows -> HBM, untimed
+        del local_layers
+        seed = 42
+        nodes_per_step = float(cfg["n"])  # one graph, ranked once, over all ranks
+    else:
+        eng = _lib.Engine(local)
+        layers = synthetic.er_layers(cfg["n"], cfg["avg_deg"], 2, seed_base=1000 + 17 * rank)
+        nnz = [int(a.nnz) for a in layers]
+        eng.set_layers(layers)  # CSR -> HBM, untimed (inputs resident when timing starts)
+        del layers
+        seed = 42 + rank
+        nodes_per_step = group.sum(float(cfg["n"]))  # every rank ranks its own graph
+    t_build = time.perf_counter() - t_build
+    fetch = mode == "replicas" or rank == 0
 
     for _ in range(args.warmup):
-        run_step(eng, cfg, seed)
+        run_step(eng, cfg, seed, fetch)
     eng.synchronize()
     _torch_sync()
     group.barrier()
     t0 = time.perf_counter()
     stats = None
     for _ in range(args.steps):
-        stats, _ = run_step(eng, cfg, seed)
+        stats, _ = run_step(eng, cfg, seed, fetch)
     eng.synchronize()
     _torch_sync()
     group.barrier()
     elapsed = time.perf_counter() - t0
     elapsed_max = group.max(elapsed)
     ncmp = 1
-    nodes_total = group.sum(float(cfg["n"] * ncmp * args.steps))
-    value = nodes_total / elapsed_max
+    value = nodes_per_step * ncmp * args.steps / elapsed_max
 
     # dominant kernel: the CSR x panel SpMM at the Krylov panel width, HIP events on the
-    # engine stream (same launch configuration as inside UASE)
+    # engine stream (same launch configuration as inside UASE; this rank's rows when
+    # partitioned)
     b = 8  # the Krylov block width UASE runs with (engine default)
     X = np.random.default_rng(0).standard_normal((cfg["n"], b)).astype(np.float32)
     _, spmm_ms, spmm_bytes = eng.bench_spmm(0, X, reps=50, want_y=False)
+    del X
     achieved = spmm_bytes / (spmm_ms * 1e-3) / 1e9
     ms_dist, ms_borda = eng.rank_timing()
 
     traffic = None
     tpath = os.path.join(REPO, "profiles", "spmm_traffic.json")
-    if os.path.exists(tpath):
+    if os.path.exists(tpath) and world == 1:
         try:
             t = json.load(open(tpath))
             if t.get("config") == args.config and int(t.get("b", -1)) == b:
@@ -192,6 +240,10 @@ def main():
         except Exception:
             traffic = None
 
+    if mode == "partitioned":
+        par = f"row-partitioned x{world} (RCCL)" if world > 1 else "row-partitioned x1"
+    else:
+        par = f"replicas x{world}" if world > 1 else "single"
     result = {
         "metric": "nodes ranked/sec (fit_transform_rank + aggregate_transform)",
         "value": round(value, 1),
@@ -201,25 +253,29 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if mode == "partitioned" else "weak",
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic",
         "config": {"workload": cfg["desc"], "nodes": cfg["n"], "layers": 2,
                    "avg_degree": cfg["avg_deg"], "nnz_per_layer": nnz, "embed_dim": cfg["d"],
                    "columns": len(cfg["dims"]) * len(METRICS), "comparisons": ncmp,
-                   "parallelism": f"replicas x{world}" if world > 1 else "single"},
+                   "parallelism": par},
         "roofline": {"bound": "hbm", "kernel": f"spmm_csr_panel_kernel<{b},*>",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "algo_bytes_per_launch": spmm_bytes, "avg_launch_ms": round(spmm_ms, 5)},
         "eig": {k: (float(f"{v:.4g}") if isinstance(v, float) else v) for k, v in stats.items()},
         "rank_ms": {"distances": round(ms_dist, 3), "borda": round(ms_borda, 3)},
+        "setup_s": round(t_build, 2),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(sample_n=args.cpu_sample)
+        result["cpu_baseline"] = cpu_baseline(
+            sample_n=args.cpu_sample or CPU_SAMPLE[args.config], avg_deg=cfg["avg_deg"],
+            d=cfg["d"], dims=tuple(cfg["dims"]))
     if rank == 0:
         print(json.dumps(result), flush=True)
+    eng.close()
     group.close()
 
 

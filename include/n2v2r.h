@@ -140,8 +140,10 @@ int n2v2r_synchronize(n2v2r_handle* h);
 
 /* SpMM kernel alone (tests + roofline): Y = A_k X (transpose = 0) or A_k^T X (1) for a host
  * N x b panel X (b = 8, 16, 32 or 64), timed with HIP events on the engine stream over `reps`
- * launches after one warm-up (single-GPU handles only).  avg_ms = mean launch duration; algo_bytes = SURVEY 8(d) bytes
- * per launch (8 nnz + 4 (N+1) + 8 N b).  Y may be NULL. */
+ * launches after one warm-up.  avg_ms = mean launch duration; algo_bytes = SURVEY 8(d) bytes
+ * per launch (8 nnz + 4 (N+1) + 8 N b).  On a partitioned handle A_k means this rank's rows:
+ * X is the global N x b panel, Y its n_local x b rows, bytes 8 nnz_loc + 4 (n_loc+1) +
+ * 4 (N + n_loc) b.  Y may be NULL. */
 int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, const float* X,
                      float* Y, double* avg_ms, double* algo_bytes);
 

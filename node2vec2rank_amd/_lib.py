@@ -391,7 +391,7 @@ class Engine:
         """Time the SpMM kernel alone (HIP events on the engine stream)."""
         X = np.ascontiguousarray(X, dtype=np.float32)
         n, b = X.shape
-        Y = np.empty_like(X) if want_y else None
+        Y = np.empty((self._n_local(), b), dtype=np.float32) if want_y else None
         ms, by = ctypes.c_double(), ctypes.c_double()
         yp = Y.ctypes.data_as(ctypes.c_void_p) if want_y else None
         self._check(self.lib.n2v2r_bench_spmm(self.h, int(k), int(bool(transpose)), int(b),

@@ -1400,12 +1400,12 @@ int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, con
                      float* Y, double* avg_ms, double* algo_bytes) {
   return guarded(h, [&]() -> int {
     if (k < 0 || k >= h->K || !h->layers[k]->loaded || (b != 8 && b != 16 && b != 32 && b != 64) ||
-        reps < 1 || !X || h->comm)
+        reps < 1 || !X)
       return N2V2R_ERR_BAD_ARG;
     const LayerDev& L = *h->layers[k];
     DevBuf xd, yd;
     xd.ensure(sizeof(float) * h->n * b);
-    yd.ensure(sizeof(float) * h->n * b);
+    yd.ensure(sizeof(float) * std::max<int64_t>(h->nloc, 1) * b);
     HIPCHK(hipMemcpyAsync(xd.p, X, sizeof(float) * h->n * b, hipMemcpyHostToDevice, h->stream));
     SpmmArgs a{};
     a.K = 1;
@@ -1430,9 +1430,11 @@ int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, con
     (void)hipEventDestroy(e1);
     if (avg_ms) *avg_ms = (double)ms / reps;
     if (algo_bytes)
-      *algo_bytes = 8.0 * (double)a.A[0].nnz + 4.0 * (double)(h->n + 1) + 8.0 * (double)h->n * b;
+      *algo_bytes = 8.0 * (double)a.A[0].nnz + 4.0 * (double)(h->nloc + 1) +
+                    4.0 * (double)(h->n + h->nloc) * b;
     if (Y)
-      HIPCHK(hipMemcpyAsync(Y, yd.p, sizeof(float) * h->n * b, hipMemcpyDeviceToHost, h->stream));
+      HIPCHK(hipMemcpyAsync(Y, yd.p, sizeof(float) * h->nloc * b, hipMemcpyDeviceToHost,
+                            h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     return N2V2R_OK;
   });

@@ -37,6 +37,55 @@ def er_layers(n: int, avg_deg: float, num_layers: int = 2, seed_base: int = 1000
     return [er_layer(n, avg_deg, seed_base + k) for k in range(num_layers)]
 
 
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _splitmix64(x: np.ndarray) -> np.ndarray:
+    x = x + np.uint64(0x9E3779B97F4A7C15)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def er_layer_rows(n: int, avg_deg: float, seed: int, row0: int = 0, n_rows: int | None = None,
+                  chunk: int = 1 << 23, dtype=np.float32) -> sp.csr_matrix:
+    """Rows [row0, row0 + n_rows) of a symmetric ER layer whose edges are counter-based:
+    edge e (0 <= e < N avg_deg / 2) joins splitmix64 draws i(e), j(e).  Every rank of a
+    row-partitioned run builds only its own rows (scanning the edge counter in chunks, memory
+    O(local nnz)), and the union over ranks is exactly ``er_layer_rows(n, avg_deg, seed)``.
+    Self loops dropped, duplicate pairs merged, weights 1.0 (same recipe as ``er_layer``, a
+    different random stream)."""
+    if n_rows is None:
+        n_rows = n - row0
+    row1 = row0 + n_rows
+    m = int(round(n * avg_deg / 2.0))
+    s = np.uint64(seed & 0xFFFFFFFFFFFFFFFF)
+    nn = np.uint64(n)
+    keys = []
+    with np.errstate(over="ignore"):
+        for e0 in range(0, m, chunk):
+            e = np.arange(e0, min(m, e0 + chunk), dtype=np.uint64)
+            h1 = _splitmix64(s ^ (e * np.uint64(0x2545F4914F6CDD1D)))
+            h2 = _splitmix64(h1)
+            i = ((h1 >> np.uint64(32)) * nn) >> np.uint64(32)
+            j = ((h2 >> np.uint64(32)) * nn) >> np.uint64(32)
+            i = i.astype(np.int64)
+            j = j.astype(np.int64)
+            ok = i != j
+            i, j = i[ok], j[ok]
+            a = (i >= row0) & (i < row1)
+            b = (j >= row0) & (j < row1)
+            keys.append((i[a] - row0) * n + j[a])
+            keys.append((j[b] - row0) * n + i[b])
+    key = np.unique(np.concatenate(keys)) if keys else np.zeros(0, np.int64)
+    rows = key // n
+    cols = (key % n).astype(np.int32)
+    indptr = np.zeros(n_rows + 1, dtype=np.int64)
+    np.cumsum(np.bincount(rows, minlength=n_rows), out=indptr[1:])
+    return sp.csr_matrix((np.ones(key.shape[0], dtype=dtype), cols, indptr),
+                         shape=(n_rows, n))
+
+
 def er_layer_p(n: int, p: float, seed: int) -> sp.csr_matrix:
     """ER with edge probability p (BASELINE cfg1: N=1000, p=0.01)."""
     return er_layer(n, p * (n - 1), seed)
