@@ -147,6 +147,12 @@ int n2v2r_synchronize(n2v2r_handle* h);
 int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, const float* X,
                      float* Y, double* avg_ms, double* algo_bytes);
 
+/* Rayleigh-Ritz stage alone (tests): top-p eigenpairs of a host symmetric c x c fp64 matrix H
+ * (3 <= c <= 768) through UASE's own path (GPU Householder tridiagonalisation, host QL +
+ * inverse iteration on T, GPU back-transform).  w: p eigenvalues, descending; S: c x p
+ * row-major fp32 eigenvectors (the Ritz coefficients UASE consumes). */
+int n2v2r_rr_top(n2v2r_handle* h, int c, const double* H, int p, double* w, float* S);
+
 #ifdef __cplusplus
 }
 #endif

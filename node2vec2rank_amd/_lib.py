@@ -38,6 +38,7 @@ EXPORTED = [
     "n2v2r_synchronize", "n2v2r_bench_spmm",
     "n2v2r_comm_unique_id", "n2v2r_create_rccl", "n2v2r_simgroup_create",
     "n2v2r_simgroup_destroy", "n2v2r_create_sim", "n2v2r_dist_info", "n2v2r_set_layer_csr_rows",
+    "n2v2r_rr_top",
 ]
 UNIQUE_ID_BYTES = 128
 
@@ -116,6 +117,7 @@ def load(path: str | None = None):
             "n2v2r_bench_spmm": (_i, [_vp, _i, _i, _i, _i, _p(np.float32), _vp,
                                       ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_double)]),
+            "n2v2r_rr_top": (_i, [_vp, _i, _p(np.float64), _i, _p(np.float64), _p(np.float32)]),
             "n2v2r_comm_unique_id": (_i, [ctypes.c_char_p, ctypes.c_size_t]),
             "n2v2r_create_rccl": (_i, [_i, _i, _i, ctypes.c_char_p, ctypes.POINTER(_vp)]),
             "n2v2r_simgroup_create": (_i, [_i, ctypes.POINTER(_vp)]),
@@ -398,6 +400,16 @@ class Engine:
                                               int(reps), X, yp, ctypes.byref(ms),
                                               ctypes.byref(by)), "bench_spmm")
         return Y, ms.value, by.value
+
+    def rr_top(self, H, p: int):
+        """Rayleigh-Ritz stage alone: top-p eigenpairs of symmetric H (GPU tridiagonalisation,
+        host tridiagonal solve, GPU back-transform).  Returns (w, S)."""
+        H = np.ascontiguousarray(H, dtype=np.float64)
+        c = H.shape[0]
+        w = np.empty(p, dtype=np.float64)
+        S = np.empty((c, p), dtype=np.float32)
+        self._check(self.lib.n2v2r_rr_top(self.h, c, H, int(p), w, S), "rr_top")
+        return w, S
 
     def synchronize(self):
         self._check(self.lib.n2v2r_synchronize(self.h), "synchronize")

@@ -115,10 +115,113 @@ __global__ __launch_bounds__(256) void reduce_chunks_kernel(const double* __rest
   if (lane == 0) out[e] = s;
 }
 
+// Narrow right-hand side (one JB = 8/16-wide block B, the Gram step of the orthogonalisation
+// G = [Q Z]^T Z): VALU form.  Lane owns 4 consecutive columns of A (one 16-B load per row,
+// a wave covers 256 columns = 1 KB of every row), the B row is wave-uniform (scalar loads,
+// read once per row instead of once per 32-column tile), 4 x JB fp32 accumulators per lane.
+// The 4 waves take contiguous quarters of the workgroup's row chunk and are folded through
+// LDS in fixed order into one fp64 partial per chunk.
+template <int JB>
+__global__ __launch_bounds__(256) void ts_tn_narrow_kernel(BlockList A, const float* __restrict__ Bz,
+                                                           int64_t n, int64_t rows_per_chunk,
+                                                           int u, double* __restrict__ partial,
+                                                           const int* cond) {
+  if (cond && *cond == 0) return;
+  extern __shared__ float tn_red[];  // [4][256 * 4][JB]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: B rows via SMEM
+  const int ca = A.count * A.width;
+  const int col0 = (u * 64 + lane) * 4;  // this lane's first column
+  const bool colok = col0 < ca;
+  const float* ab = colok ? A.blk[col0 / A.width] + (col0 % A.width) : A.blk[0];
+  const int64_t lda = A.width;
+  const int64_t c0 = (int64_t)blockIdx.x * rows_per_chunk;
+  int64_t c1 = c0 + rows_per_chunk;
+  if (c1 > n) c1 = n;
+  const int64_t per_wave = (rows_per_chunk + 3) / 4;
+  int64_t r0 = c0 + wave * per_wave;
+  int64_t r1 = r0 + per_wave;
+  if (r1 > c1) r1 = c1;
+  float acc[4][JB];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < JB; ++j) acc[i][j] = 0.f;
+  int64_t r = r0;
+  for (; r + 4 <= r1; r += 4) {
+    f32x4 a[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      a[t] = colok ? *reinterpret_cast<const f32x4*>(ab + (r + t) * lda) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float* zr = Bz + (r + t) * JB;
+#pragma unroll
+      for (int j = 0; j < JB; ++j) {
+        const float zj = zr[j];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][j] += a[t][i] * zj;
+      }
+    }
+  }
+  for (; r < r1; ++r) {
+    const f32x4 a = colok ? *reinterpret_cast<const f32x4*>(ab + r * lda) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const float* zr = Bz + r * JB;
+#pragma unroll
+    for (int j = 0; j < JB; ++j) {
+      const float zj = zr[j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][j] += a[i] * zj;
+    }
+  }
+  // fold the 4 waves (fixed order) and write this chunk's fp64 partial [ca][JB]
+  float* mine = tn_red + (size_t)wave * 256 * JB;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < JB; ++j) mine[(lane * 4 + i) * JB + j] = acc[i][j];
+  __syncthreads();
+  double* out = partial + (int64_t)blockIdx.x * ca * JB;
+  for (int e = threadIdx.x; e < 256 * JB; e += 256) {
+    const int cl = e / JB;  // column within this 256-column group
+    const int col = u * 256 + cl;
+    if (col >= ca) continue;
+    const double s = (double)tn_red[e] + (double)tn_red[256 * JB + e] +
+                     (double)tn_red[2 * 256 * JB + e] + (double)tn_red[3 * 256 * JB + e];
+    out[(int64_t)col * JB + (e % JB)] = s;
+  }
+}
+
 extern "C" hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n,
                                          double* partial, size_t partial_elems, double* out,
                                          const int* cond, hipStream_t stream) {
   const int ca = A.count * A.width, cb = B.count * B.width;
+  if (B.count == 1 && (B.width == 8 || B.width == 16) && A.width % 4 == 0) {
+    // narrow form: ~1024 workgroups of >= 256 rows, partials within the buffer
+    const int64_t elems = (int64_t)ca * cb;
+    int64_t nchunks = (n + 255) / 256;
+    if (nchunks > 1024) nchunks = 1024;
+    if ((size_t)(nchunks * elems) > partial_elems) nchunks = (int64_t)(partial_elems / elems);
+    if (nchunks < 1) return hipErrorInvalidValue;
+    const int64_t rows_per_chunk = (n + nchunks - 1) / nchunks;
+    nchunks = (n + rows_per_chunk - 1) / rows_per_chunk;
+    const int groups = (ca + 255) / 256;
+    for (int u = 0; u < groups; ++u) {
+      // each 256-column group writes its own columns of every chunk's partial
+      const size_t lds = sizeof(float) * 4 * 256 * B.width;
+      if (B.width == 8)
+        hipLaunchKernelGGL(ts_tn_narrow_kernel<8>, dim3((unsigned)nchunks), dim3(256), lds, stream,
+                           A, B.blk[0], n, rows_per_chunk, u, partial, cond);
+      else
+        hipLaunchKernelGGL(ts_tn_narrow_kernel<16>, dim3((unsigned)nchunks), dim3(256), lds,
+                           stream, A, B.blk[0], n, rows_per_chunk, u, partial, cond);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((elems + 3) / 4)), dim3(256), 0,
+                       stream, partial, (int)nchunks, elems, out, cond);
+    return hipGetLastError();
+  }
   const int nti = (ca + 31) / 32, ntj = (cb + 31) / 32;
   const int ntiles = nti * ntj;
   // chunk count: ~1024 workgroups with >= 512 rows per chunk, partials within the buffer

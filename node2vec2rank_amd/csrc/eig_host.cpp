@@ -19,12 +19,12 @@ namespace {
 // on the tridiagonal (d, e): the factorisation grows one extra superdiagonal.
 void tri_shift_solve(int n, const double* d, const double* e, double lambda, double tiny,
                      double* b, std::vector<double>& wk) {
-  wk.resize(4 * (size_t)n);
+  wk.resize(5 * (size_t)n);
   double* dg = wk.data();        // diagonal of U
   double* u1 = dg + n;           // first superdiagonal of U
   double* u2 = u1 + n;           // second superdiagonal of U
   double* lm = u2 + n;           // multipliers
-  std::vector<char> swp(n, 0);
+  double* swp = lm + n;          // 1.0 where rows i, i+1 were interchanged
   // working copies of the current row
   double a = d[0] - lambda;      // current diagonal candidate
   double c = (n > 1) ? e[0] : 0.0;  // current super
@@ -36,7 +36,7 @@ void tri_shift_solve(int n, const double* d, const double* e, double lambda, dou
       if (std::fabs(a) < tiny) a = (a < 0 ? -tiny : tiny);
       const double m = sub / a;
       lm[i] = m;
-      swp[i] = 0;
+      swp[i] = 0.0;
       dg[i] = a;
       u1[i] = c;
       u2[i] = 0.0;
@@ -46,7 +46,7 @@ void tri_shift_solve(int n, const double* d, const double* e, double lambda, dou
       // swap rows i and i+1
       const double m = a / sub;
       lm[i] = m;
-      swp[i] = 1;
+      swp[i] = 1.0;
       dg[i] = sub;
       u1[i] = nd;
       u2[i] = ns;
@@ -58,7 +58,7 @@ void tri_shift_solve(int n, const double* d, const double* e, double lambda, dou
   dg[n - 1] = a;
   // forward substitution with the row interchanges
   for (int i = 0; i < n - 1; ++i) {
-    if (swp[i]) std::swap(b[i], b[i + 1]);
+    if (swp[i] != 0.0) std::swap(b[i], b[i + 1]);
     b[i + 1] -= lm[i] * b[i];
   }
   // back substitution
@@ -68,6 +68,111 @@ void tri_shift_solve(int n, const double* d, const double* e, double lambda, dou
 }
 
 }  // namespace
+
+// Top-p eigenpairs of the symmetric tridiagonal T = tridiag(e, d, e) (d: n, e: n-1).
+// w[p] descending; Y: p x n, row j = unit eigenvector of w[j] (column-major n x p).
+extern "C" int n2v2r_host_tridiag_eig_top(int n, const double* d_in, const double* e_in, int p,
+                                          double* w, double* Y) {
+  if (n <= 0 || p <= 0 || p > n) return 1;
+  std::vector<double> d(d_in, d_in + n), e(std::max(n - 1, 1), 0.0);
+  for (int i = 0; i < n - 1; ++i) e[i] = e_in[i];
+  // --- 2. all eigenvalues of T by implicit QL (no vectors), keep the p largest --------
+  const double eps = 2.220446049250313e-16;
+  double tnorm = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double r = (i > 0 ? std::fabs(e[i - 1]) : 0.0) + (i < n - 1 ? std::fabs(e[i]) : 0.0);
+    tnorm = std::max(tnorm, std::fabs(d[i]) + r);
+  }
+  {
+    std::vector<double> dd(d), ee(n, 0.0);
+    for (int i = 0; i < n - 1; ++i) ee[i] = e[i];
+    for (int l = 0; l < n; ++l) {
+      int iter = 0;
+      int m;
+      do {
+        for (m = l; m < n - 1; ++m) {
+          const double s = std::fabs(dd[m]) + std::fabs(dd[m + 1]);
+          if (std::fabs(ee[m]) <= eps * s) break;
+        }
+        if (m != l) {
+          if (++iter > 60) break;
+          double g = (dd[l + 1] - dd[l]) / (2.0 * ee[l]);
+          double r = std::sqrt(g * g + 1.0);
+          g = dd[m] - dd[l] + ee[l] / (g + (g >= 0 ? std::fabs(r) : -std::fabs(r)));
+          double s = 1.0, c = 1.0, pp = 0.0;
+          int i;
+          bool underflow = false;
+          for (i = m - 1; i >= l; --i) {
+            double f = s * ee[i];
+            const double bb = c * ee[i];
+            r = std::sqrt(f * f + g * g);  // |f|, |g| << 1e150 here: no hypot needed
+            ee[i + 1] = r;
+            if (r == 0.0) {
+              dd[i + 1] -= pp;
+              ee[m] = 0.0;
+              underflow = true;
+              break;
+            }
+            s = f / r;
+            c = g / r;
+            g = dd[i + 1] - pp;
+            r = (dd[i] - g) * s + 2.0 * c * bb;
+            pp = s * r;
+            dd[i + 1] = g + pp;
+            g = c * r - bb;
+          }
+          if (underflow) continue;
+          dd[l] -= pp;
+          ee[l] = g;
+          ee[m] = 0.0;
+        }
+      } while (m != l);
+    }
+    std::sort(dd.begin(), dd.end(), [](double a, double b) { return a > b; });
+    for (int j = 0; j < p; ++j) w[j] = dd[j];
+  }
+
+  // --- 3. inverse iteration ----------------------------------------------------------
+  std::vector<double> x(n), wk;
+  double* T = Y;  // column j at T[j*n]
+  // fp64 inverse iteration leaves vectors of eigenvalues delta apart orthogonal to
+  // ~eps ||T|| / delta, so only near-degenerate ones (delta <= 1e-7 ||T||) need Gram-Schmidt;
+  // LAPACK's 1e-3 ||T|| lumps the whole bulk edge of a Krylov projection into one cluster.
+  const double clus = 1e-7 * std::max(tnorm, 1e-300);
+  const double tiny = std::max(eps * tnorm, 1e-300);
+  int cluster_start = 0;
+  uint64_t seed = 0x9E3779B97F4A7C15ull;
+  for (int j = 0; j < p; ++j) {
+    if (j > 0 && std::fabs(w[j - 1] - w[j]) > clus) cluster_start = j;
+    // perturb identical eigenvalues slightly, as dstein does
+    double lam = w[j];
+    for (int i = 0; i < n; ++i) {
+      seed = seed * 6364136223846793005ull + 1442695040888963407ull;
+      x[i] = ((double)(seed >> 11) / 9007199254740992.0) - 0.5;
+    }
+    for (int it = 0; it < 3; ++it) {
+      tri_shift_solve(n, d.data(), e.data(), lam, tiny, x.data(), wk);
+      // MGS against the previous members of the cluster
+      for (int q = cluster_start; q < j; ++q) {
+        const double* tq = &T[(size_t)q * n];
+        double s = 0.0;
+        for (int i = 0; i < n; ++i) s += tq[i] * x[i];
+        for (int i = 0; i < n; ++i) x[i] -= s * tq[i];
+      }
+      double nr = 0.0;
+      for (int i = 0; i < n; ++i) nr += x[i] * x[i];
+      nr = std::sqrt(nr);
+      if (!(nr > 0)) {
+        x[j % n] = 1.0;
+        nr = 1.0;
+      }
+      for (int i = 0; i < n; ++i) x[i] /= nr;
+    }
+    std::memcpy(&T[(size_t)j * n], x.data(), sizeof(double) * n);
+  }
+
+  return 0;
+}
 
 // A: n x n row-major symmetric (destroyed).  Returns 0 on success.
 // w[p]: eigenvalues, descending.  Z: n x p row-major, column j = eigenvector of w[j].
@@ -139,100 +244,9 @@ extern "C" int n2v2r_host_sym_eig_top(int n, double* A, int p, double* w, double
   }
   d[n - 1] = A[(size_t)(n - 1) * n + (n - 1)];
 
-  // --- 2. all eigenvalues of T by implicit QL (no vectors), keep the p largest --------
-  const double eps = 2.220446049250313e-16;
-  double tnorm = 0.0;
-  for (int i = 0; i < n; ++i) {
-    const double r = (i > 0 ? std::fabs(e[i - 1]) : 0.0) + (i < n - 1 ? std::fabs(e[i]) : 0.0);
-    tnorm = std::max(tnorm, std::fabs(d[i]) + r);
-  }
-  {
-    std::vector<double> dd(d), ee(n, 0.0);
-    for (int i = 0; i < n - 1; ++i) ee[i] = e[i];
-    for (int l = 0; l < n; ++l) {
-      int iter = 0;
-      int m;
-      do {
-        for (m = l; m < n - 1; ++m) {
-          const double s = std::fabs(dd[m]) + std::fabs(dd[m + 1]);
-          if (std::fabs(ee[m]) <= eps * s) break;
-        }
-        if (m != l) {
-          if (++iter > 60) break;
-          double g = (dd[l + 1] - dd[l]) / (2.0 * ee[l]);
-          double r = std::hypot(g, 1.0);
-          g = dd[m] - dd[l] + ee[l] / (g + (g >= 0 ? std::fabs(r) : -std::fabs(r)));
-          double s = 1.0, c = 1.0, pp = 0.0;
-          int i;
-          bool underflow = false;
-          for (i = m - 1; i >= l; --i) {
-            double f = s * ee[i];
-            const double bb = c * ee[i];
-            r = std::hypot(f, g);
-            ee[i + 1] = r;
-            if (r == 0.0) {
-              dd[i + 1] -= pp;
-              ee[m] = 0.0;
-              underflow = true;
-              break;
-            }
-            s = f / r;
-            c = g / r;
-            g = dd[i + 1] - pp;
-            r = (dd[i] - g) * s + 2.0 * c * bb;
-            pp = s * r;
-            dd[i + 1] = g + pp;
-            g = c * r - bb;
-          }
-          if (underflow) continue;
-          dd[l] -= pp;
-          ee[l] = g;
-          ee[m] = 0.0;
-        }
-      } while (m != l);
-    }
-    std::sort(dd.begin(), dd.end(), [](double a, double b) { return a > b; });
-    for (int j = 0; j < p; ++j) w[j] = dd[j];
-  }
-
-  // --- 3. inverse iteration ----------------------------------------------------------
-  std::vector<double> x(n), wk;
+  // --- 2./3. eigenpairs of T -------------------------------------------------------
   std::vector<double> T(n * (size_t)p);  // column j at T[j*n]
-  // fp64 inverse iteration leaves vectors of eigenvalues delta apart orthogonal to
-  // ~eps ||T|| / delta, so only near-degenerate ones (delta <= 1e-7 ||T||) need Gram-Schmidt;
-  // LAPACK's 1e-3 ||T|| lumps the whole bulk edge of a Krylov projection into one cluster.
-  const double clus = 1e-7 * std::max(tnorm, 1e-300);
-  const double tiny = std::max(eps * tnorm, 1e-300);
-  int cluster_start = 0;
-  uint64_t seed = 0x9E3779B97F4A7C15ull;
-  for (int j = 0; j < p; ++j) {
-    if (j > 0 && std::fabs(w[j - 1] - w[j]) > clus) cluster_start = j;
-    // perturb identical eigenvalues slightly, as dstein does
-    double lam = w[j];
-    for (int i = 0; i < n; ++i) {
-      seed = seed * 6364136223846793005ull + 1442695040888963407ull;
-      x[i] = ((double)(seed >> 11) / 9007199254740992.0) - 0.5;
-    }
-    for (int it = 0; it < 4; ++it) {
-      tri_shift_solve(n, d.data(), e.data(), lam, tiny, x.data(), wk);
-      // MGS against the previous members of the cluster
-      for (int q = cluster_start; q < j; ++q) {
-        const double* tq = &T[(size_t)q * n];
-        double s = 0.0;
-        for (int i = 0; i < n; ++i) s += tq[i] * x[i];
-        for (int i = 0; i < n; ++i) x[i] -= s * tq[i];
-      }
-      double nr = 0.0;
-      for (int i = 0; i < n; ++i) nr += x[i] * x[i];
-      nr = std::sqrt(nr);
-      if (!(nr > 0)) {
-        x[j % n] = 1.0;
-        nr = 1.0;
-      }
-      for (int i = 0; i < n; ++i) x[i] /= nr;
-    }
-    std::memcpy(&T[(size_t)j * n], x.data(), sizeof(double) * n);
-  }
+  if (n2v2r_host_tridiag_eig_top(n, d.data(), e.data(), p, w, T.data()) != 0) return 1;
 
   // --- 4. back-transformation: z <- H_0 H_1 ... H_{n-3} z ------------------------------
   for (int k = n - 3; k >= 0; --k) {

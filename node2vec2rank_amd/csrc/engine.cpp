@@ -106,6 +106,13 @@ hipError_t n2v2r_launch_radix_pass(const uint64_t* kin, const int32_t* pin, uint
 hipError_t n2v2r_launch_borda_finish(const int32_t* sorted_idx, int64_t n, int nseg, int ncols,
                                      int32_t* pos, int64_t* borda, hipStream_t stream);
 int n2v2r_host_sym_eig_top(int n, double* A, int p, double* w, double* Z);
+int n2v2r_host_tridiag_eig_top(int n, const double* d, const double* e, int p, double* w,
+                               double* Y);
+hipError_t n2v2r_launch_rr_tridiag(double* A, int c, double* d, double* e, double* tau, double* V,
+                                   hipStream_t stream);
+hipError_t n2v2r_launch_rr_backtransform(const double* V, const double* tau, int c,
+                                         const double* Y, int p, float* S, int lds,
+                                         hipStream_t stream);
 }
 
 namespace {
@@ -474,6 +481,7 @@ struct Eig {
   std::vector<std::unique_ptr<DevBuf>> zk;    // K stage-1 panels (local)
   DevBuf zg;                                  // K gathered stage-1 panels
   DevBuf rinv, flg, anyflag, gsmall, csmall;
+  DevBuf tri, refl, ytri;                     // GPU Rayleigh-Ritz: [d|e|tau], reflectors, Y_T
   n2v2r_eig_stats* stats;
   double t_spmm = 0, t_ortho = 0;
   int64_t launches = 0;
@@ -650,13 +658,16 @@ struct Eig {
     h->partial.ensure(sizeof(double) * h->partial_elems);
     gsmall.ensure(sizeof(double) * (size_t)c_max * c_max);
     csmall.ensure(sizeof(float) * (size_t)c_max * c_max);
+    tri.ensure(sizeof(double) * 3 * (size_t)c_max);
+    refl.ensure(sizeof(double) * (size_t)c_max * c_max);
+    ytri.ensure(sizeof(double) * (size_t)c_max * keep);
     rinv.ensure(sizeof(double) * 64 * 64);
     flg.ensure(sizeof(int) * 256);
     anyflag.ensure(sizeof(int) * 4);
     h->theta.ensure(sizeof(double) * c_max);
     h->resid.ensure(sizeof(double) * c_max);
 
-    std::vector<double> Sh((size_t)c_max * keep), wh(keep);
+    std::vector<double> wh(keep);
     std::vector<double> res2(keep);
 
     // start block (counter-based: the same values whatever the row partition)
@@ -677,17 +688,17 @@ struct Eig {
     double t_rr = 0;
     // pinned host staging for the projected matrix and the Ritz coefficients
     double* Hh = nullptr;
-    float* Sf = nullptr;
-    HIPCHK(hipHostMalloc((void**)&Hh, sizeof(double) * (size_t)c_max * c_max, 0));
-    HIPCHK(hipHostMalloc((void**)&Sf, sizeof(float) * (size_t)c_max * keep, 0));
+    double* Yh = nullptr;
+    HIPCHK(hipHostMalloc((void**)&Hh, sizeof(double) * 2 * (size_t)c_max, 0));
+    HIPCHK(hipHostMalloc((void**)&Yh, sizeof(double) * (size_t)c_max * keep, 0));
     struct PinnedFree {
       double* hh;
-      float* s;
+      double* y;
       ~PinnedFree() {
         if (hh) (void)hipHostFree(hh);
-        if (s) (void)hipHostFree(s);
+        if (y) (void)hipHostFree(y);
       }
-    } pinned_guard{Hh, Sf};
+    } pinned_guard{Hh, Yh};
     for (;; ++cycle) {
       while ((int)Q.size() < nb_max) {
         expand_one(W.back(), Q, Q, W);
@@ -695,26 +706,24 @@ struct Eig {
       }
       const int nq = (int)Q.size();
       const int c = nq * b;
-      // H = Q^T W
+      // H = Q^T W (fp64, all-reduced) -> tridiagonal on the GPU -> host QL + inverse
+      // iteration on T (O(c keep)) -> back-transform on the GPU into the fp32 Ritz
+      // coefficients S (c x keep, ld keep)
       tn(blocks(Q, 0, nq), blocks(W, 0, nq), gsmall.as<double>(), nullptr);
-      HIPCHK(hipMemcpyAsync(Hh, gsmall.as<double>(), sizeof(double) * c * c,
-                            hipMemcpyDeviceToHost, st));
+      double* trid = tri.as<double>();
+      HIPCHK(n2v2r_launch_rr_tridiag(gsmall.as<double>(), c, trid, trid + c_max, trid + 2 * c_max,
+                                     refl.as<double>(), st));
+      HIPCHK(hipMemcpyAsync(Hh, trid, sizeof(double) * 2 * c_max, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
       const double tr0 = now_ms();
-      for (int i = 0; i < c; ++i)
-        for (int j = 0; j < i; ++j) {
-          const double sv = 0.5 * (Hh[(size_t)i * c + j] + Hh[(size_t)j * c + i]);
-          Hh[(size_t)i * c + j] = sv;
-          Hh[(size_t)j * c + i] = sv;
-        }
-      if (n2v2r_host_sym_eig_top(c, Hh, keep, wh.data(), Sh.data()) != 0)
+      if (n2v2r_host_tridiag_eig_top(c, Hh, Hh + c_max, keep, wh.data(), Yh) != 0)
         throw StatusFail{N2V2R_ERR_NO_CONVERGENCE, "Rayleigh-Ritz eigensolve failed"};
-      for (size_t i = 0; i < (size_t)c * keep; ++i) Sf[i] = (float)Sh[i];
       t_rr += now_ms() - tr0;
-      HIPCHK(hipMemcpyAsync(csmall.as<float>(), Sf, sizeof(float) * c * keep,
-                            hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(ytri.p, Yh, sizeof(double) * c * keep, hipMemcpyHostToDevice, st));
       HIPCHK(hipMemcpyAsync(h->theta.as<double>(), wh.data(), sizeof(double) * keep,
                             hipMemcpyHostToDevice, st));
+      HIPCHK(n2v2r_launch_rr_backtransform(refl.as<double>(), trid + 2 * c_max, c,
+                                           ytri.as<double>(), keep, csmall.as<float>(), keep, st));
       // Ritz vectors X = Q S, MX = W S (keep columns, pb blocks)
       for (int q = 0; q < pb; ++q) {
         X[q] = take();
@@ -1391,6 +1400,37 @@ int n2v2r_column_sums(n2v2r_handle* h, int k, float* out) {
       src = g.as<float>();
     }
     HIPCHK(hipMemcpyAsync(out, src, sizeof(float) * h->n, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return N2V2R_OK;
+  });
+}
+
+// Rayleigh-Ritz stage alone (tests): top-p eigenpairs of a host symmetric c x c matrix through
+// the same GPU tridiagonalisation + host tridiagonal solve + GPU back-transform as UASE.
+int n2v2r_rr_top(n2v2r_handle* h, int c, const double* H, int p, double* w, float* S) {
+  return guarded(h, [&]() -> int {
+    if (c < 3 || c > 768 || p < 1 || p > c || !H || !w || !S) return N2V2R_ERR_BAD_ARG;
+    DevBuf a, tri, refl, y, s;
+    a.ensure(sizeof(double) * c * c);
+    tri.ensure(sizeof(double) * 3 * c);
+    refl.ensure(sizeof(double) * c * c);
+    y.ensure(sizeof(double) * c * p);
+    s.ensure(sizeof(float) * c * p);
+    HIPCHK(hipMemcpyAsync(a.p, H, sizeof(double) * c * c, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));  // pageable source: complete before the kernel
+    double* t = tri.as<double>();
+    HIPCHK(n2v2r_launch_rr_tridiag(a.as<double>(), c, t, t + c, t + 2 * c, refl.as<double>(),
+                                   h->stream));
+    std::vector<double> de(2 * c), yh((size_t)c * p);
+    HIPCHK(hipMemcpyAsync(de.data(), t, sizeof(double) * 2 * c, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    if (n2v2r_host_tridiag_eig_top(c, de.data(), de.data() + c, p, w, yh.data()) != 0)
+      return N2V2R_ERR_NO_CONVERGENCE;
+    HIPCHK(hipMemcpyAsync(y.p, yh.data(), sizeof(double) * c * p, hipMemcpyHostToDevice,
+                          h->stream));
+    HIPCHK(n2v2r_launch_rr_backtransform(refl.as<double>(), t + 2 * c, c, y.as<double>(), p,
+                                         s.as<float>(), p, h->stream));
+    HIPCHK(hipMemcpyAsync(S, s.p, sizeof(float) * c * p, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     return N2V2R_OK;
   });

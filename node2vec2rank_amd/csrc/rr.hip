@@ -1,0 +1,444 @@
+// Rayleigh-Ritz on the GPU for the block Krylov-Schur eigensolver: the projected matrix
+// H = Q^T M Q (c x c fp64, c <= 768) never leaves the device except as its tridiagonal.
+//
+//   rr_tridiag_kernel    Householder reduction H = P T P^T (one workgroup of 1024 threads,
+//                        H L2-resident, full symmetric storage; per step ONE fused pass
+//                        reads and writes the trailing block: rank-2 update of step k +
+//                        column-oriented matvec of step k+1).  Outputs d, e (T), tau and the
+//                        reflectors V (row k = v_k, v_k[0] = 1).
+//   (host)               eigenvalues of T by implicit QL + inverse iteration for the top p
+//                        (n2v2r_host_tridiag_eig_top, eig_host.cpp): O(c p) work.
+//   rr_backtransform     S = P Y for the p wanted eigenvectors Y of T: one workgroup per 8
+//                        columns applies the c-2 reflectors as compact-WY blocks of 32, last
+//                        block first, and writes S as the fp32 Ritz coefficient matrix
+//                        (c x ld) the NN kernels consume.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#define RR_MAXC 768
+#define RR_BT_COLS 8
+
+namespace {
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// block-wide sum of one double per thread (fixed order: waves folded in index order)
+template <int NW>
+__device__ __forceinline__ double block_sum(double v, double* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) s += red[w];
+  return s;
+}
+
+}  // namespace
+
+// Fused column-oriented Householder tridiagonalisation.  H is symmetric, so p = B v is also
+// B^T v = sum_r v[r] B[r][:]: lanes own columns, waves own rows, every row is read as
+// coalesced 8-B loads and accumulated without cross-lane reductions.  One pass per step does
+// the rank-2 update of step k AND the matvec of step k+1 (whose reflector comes from the
+// updated first row, formed just before the pass): B is read once and written once per step.
+//   LDS: v, w (step k), vn, p (step k+1), part[NW][c] (per-wave matvec partials).
+template <int TMAX, int NT, bool PAIRS>
+__global__ __launch_bounds__(NT) void rr_tridiag_kernel(double* __restrict__ A, int c,
+                                                                    double* __restrict__ dd,
+                                                                    double* __restrict__ ee,
+                                                                    double* __restrict__ tau,
+                                                                    double* __restrict__ V) {
+  constexpr int NW = NT / 64;
+  extern __shared__ double lds[];
+  double* v = lds;              // [c]
+  double* w = v + c;            // [c]
+  double* vn = w + c;           // [c]
+  double* p = vn + c;           // [c]
+  double* part = p + c;         // [NW][c]
+  __shared__ double red[NW];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  for (int64_t q = tid; q < (int64_t)c * c; q += NT) {
+    const int i = (int)(q / c), j = (int)(q % c);
+    if (j < i) {
+      const double s = 0.5 * (A[(int64_t)i * c + j] + A[(int64_t)j * c + i]);
+      A[(int64_t)i * c + j] = s;
+      A[(int64_t)j * c + i] = s;
+    }
+  }
+  __syncthreads();
+
+  // reflector from x (length m, in `dst`, overwritten by v, v[0] = 1); returns tau, sets beta
+  // Every thread owns the entries i = tid (mod NT) of dst (it wrote them, or the caller
+  // synchronised), so only the block reduction needs barriers.
+  auto make_reflector = [&](double* dst, int m, int k) -> double {
+    double part2 = 0.0;
+    for (int i = tid; i < m; i += NT)
+      if (i > 0) part2 += dst[i] * dst[i];
+    const double x0 = dst[0];
+    const double sig = block_sum<NW>(part2, red);
+    double t = 0.0, beta = x0, scale = 0.0;
+    if (sig != 0.0) {
+      const double nrm = sqrt(x0 * x0 + sig);
+      beta = (x0 >= 0) ? -nrm : nrm;
+      t = (beta - x0) / beta;
+      scale = 1.0 / (x0 - beta);
+    }
+    double* vk = V + (int64_t)k * c;
+    for (int i = tid; i < m; i += NT) {
+      const double vi = (i == 0) ? 1.0 : dst[i] * scale;
+      dst[i] = vi;
+      vk[i] = vi;
+    }
+    if (tid == 0) {
+      ee[k] = beta;
+      tau[k] = t;
+    }
+    __syncthreads();
+    return t;
+  };
+
+  // ---- step 0: reflector from row 0, p = tau B v with B = A[1.., 1..] (matvec only)
+  int m = c - 1;
+  for (int i = tid; i < m; i += NT) v[i] = A[1 + i];
+  if (tid == 0) dd[0] = A[0];
+  __syncthreads();  // v[0] is read by every thread
+  double t = make_reflector(v, m, 0);
+  {
+    double acc[TMAX];
+#pragma unroll
+    for (int q = 0; q < TMAX; ++q) acc[q] = 0.0;
+    for (int r = wave; r < m; r += NW) {
+      const double* br = A + (int64_t)(1 + r) * c + 1;
+      const double vr = v[r];
+#pragma unroll
+      for (int q = 0; q < TMAX; ++q) {
+        const int j = lane + 64 * q;
+        if (j < m) acc[q] += br[j] * vr;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < TMAX; ++q) {
+      const int j = lane + 64 * q;
+      if (j < m) part[wave * c + j] = acc[q];
+    }
+    __syncthreads();
+    for (int j = tid; j < m; j += NT) {
+      double s2 = 0.0;
+#pragma unroll
+      for (int wv = 0; wv < NW; ++wv) s2 += part[wv * c + j];
+      p[j] = t * s2;
+    }
+    __syncthreads();
+  }
+
+  for (int k = 0; k < c - 2; ++k) {
+    const int o = k + 1;  // B = A[o.., o..], m = c - o rows
+    // w = p - (t/2)(p.v) v
+    double pp = 0.0;
+    for (int i = tid; i < m; i += NT) pp += p[i] * v[i];
+    const double pvv = block_sum<NW>(pp, red);
+    const double half = 0.5 * t * pvv;
+    for (int i = tid; i < m; i += NT) w[i] = p[i] - half * v[i];
+    __syncthreads();
+    // updated first row of B: diagonal d[o] and x' = B[0][1..] (the next reflector's input)
+    const double* b0 = A + (int64_t)o * c + o;
+    if (tid == 0) dd[o] = b0[0] - 2.0 * v[0] * w[0];
+    const int mn = m - 1;
+    for (int j = tid; j < mn; j += NT)
+      vn[j] = b0[1 + j] - v[0] * w[1 + j] - w[0] * v[1 + j];
+    __syncthreads();
+    if (mn == 1) {  // k = c - 3: the last 2 x 2 block
+      if (tid == 0) {
+        ee[o] = vn[0];
+        tau[o] = 0.0;
+        const double b11 = A[(int64_t)(o + 1) * c + o + 1];
+        dd[o + 1] = b11 - 2.0 * v[1] * w[1];
+      }
+      break;
+    }
+    const double tn = make_reflector(vn, mn, o);
+    // fused pass over rows r = 1..m-1: B[r][1..] -= v[r] w + w[r] v; p' += vn[r-1] B'[r][1..]
+    if (PAIRS) {
+      // 16-B accesses: lane owns absolute column pairs (J, J+1), J even, J >= jb
+      const int jb = (o + 1) & ~1;
+      double vj[TMAX], wj[TMAX], acc[TMAX];
+      int rel[TMAX];
+#pragma unroll
+      for (int q = 0; q < TMAX; ++q) {
+        const int J = jb + 2 * (lane + 64 * (q >> 1)) + (q & 1);
+        rel[q] = J - (o + 1);  // column 1 + rel of B; valid for 0 <= rel < mn
+        const bool ok = rel[q] >= 0 && rel[q] < mn;
+        vj[q] = ok ? v[1 + rel[q]] : 0.0;
+        wj[q] = ok ? w[1 + rel[q]] : 0.0;
+        acc[q] = 0.0;
+      }
+#pragma unroll 4
+      for (int r = 1 + wave; r < m; r += NW) {
+        double* rowp = A + (int64_t)(o + r) * c;
+        const double vr = v[r], wr = w[r], vnr = vn[r - 1];
+#pragma unroll
+        for (int q2 = 0; q2 < TMAX; q2 += 2) {
+          const int J = jb + 2 * (lane + 64 * (q2 >> 1));
+          if (J < c) {
+            double2 b2 = *reinterpret_cast<const double2*>(rowp + J);
+            double bx = b2.x, by = b2.y;
+            if (rel[q2] >= 0) {
+              bx -= vr * wj[q2] + wr * vj[q2];
+              acc[q2] += bx * vnr;
+            }
+            by -= vr * wj[q2 + 1] + wr * vj[q2 + 1];
+            acc[q2 + 1] += by * vnr;
+            *reinterpret_cast<double2*>(rowp + J) = make_double2(bx, by);
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < TMAX; ++q)
+        if (rel[q] >= 0 && rel[q] < mn) part[wave * c + rel[q]] = acc[q];
+    } else {
+      double vj[TMAX], wj[TMAX], acc[TMAX];
+#pragma unroll
+      for (int q = 0; q < TMAX; ++q) {
+        const int j = 1 + lane + 64 * q;
+        vj[q] = (j < m) ? v[j] : 0.0;
+        wj[q] = (j < m) ? w[j] : 0.0;
+        acc[q] = 0.0;
+      }
+#pragma unroll 4
+      for (int r = 1 + wave; r < m; r += NW) {
+        double* br = A + (int64_t)(o + r) * c + o + 1;
+        const double vr = v[r], wr = w[r], vnr = vn[r - 1];
+#pragma unroll
+        for (int q = 0; q < TMAX; ++q) {
+          const int j = lane + 64 * q;  // column 1 + j of B
+          if (j < mn) {
+            const double b = br[j] - vr * wj[q] - wr * vj[q];
+            br[j] = b;
+            acc[q] += b * vnr;
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < TMAX; ++q) {
+        const int j = lane + 64 * q;
+        if (j < mn) part[wave * c + j] = acc[q];
+      }
+    }
+    __syncthreads();
+    for (int j = tid; j < mn; j += NT) {
+      double s2 = 0.0;
+#pragma unroll
+      for (int wv = 0; wv < NW; ++wv) s2 += part[wv * c + j];
+      p[j] = tn * s2;
+      v[j] = vn[j];
+    }
+    // no barrier: the next pp and w loops read only this thread's own entries of p and v
+    t = tn;
+    m = mn;
+  }
+}
+
+// Y: p eigenvectors of T, column-major (vector j at Y[j * c]).  S[i * lds + j] = (P Y)[i][j],
+// P = H_0 H_1 ... H_{c-3}.  Blocked (compact WY): the reflectors are taken BT_NB at a time,
+// last block first; for the block H_k0 ... H_k1-1 = I - W T W^T (T upper triangular, the
+// forward column-wise LAPACK larft recurrence, built from the block's Gram matrix W^T W) the
+// update is z <- z - W (T (W^T z)).  One workgroup per RR_BT_COLS columns keeps its columns in
+// LDS; about 4 barriers per block instead of 2 per reflector.
+#define BT_NB 32
+#define BT_CH 128
+__global__ __launch_bounds__(256) void rr_backtransform_kernel(const double* __restrict__ V,
+                                                               const double* __restrict__ tau,
+                                                               int c, const double* __restrict__ Y,
+                                                               int p, float* __restrict__ S,
+                                                               int lds) {
+  __shared__ double z[RR_BT_COLS][RR_MAXC + 1];  // +1: the 8 columns fall in distinct banks
+  __shared__ double Wc[BT_NB][BT_CH + 1];         // staged rows of the block's reflectors
+  __shared__ double G[BT_NB][BT_NB + 1];
+  __shared__ double T[BT_NB][BT_NB + 1];
+  __shared__ double WZ[BT_NB][RR_BT_COLS];
+  __shared__ double U[BT_NB][RR_BT_COLS];
+  const int tid = threadIdx.x;
+  const int j0 = blockIdx.x * RR_BT_COLS;
+  const int nj = (p - j0) < RR_BT_COLS ? (p - j0) : RR_BT_COLS;
+  for (int q = tid; q < RR_BT_COLS * c; q += 256) {
+    const int jj = q / c, i = q % c;
+    z[jj][i] = (jj < nj) ? Y[(int64_t)(j0 + jj) * c + i] : 0.0;
+  }
+  __syncthreads();
+  // thread roles in the dot phase: (a, jj) = (tid / 8, tid % 8) for W^T z; Gram pairs
+  // (a, bb), bb < a, enumerated e = tid and tid + 256
+  const int wa = tid / RR_BT_COLS, wj = tid % RR_BT_COLS;
+  int ga[2], gb[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    int e = tid + 256 * h, a = 1;
+    while (e >= a) {  // row a holds a pairs (bb = 0 .. a-1)
+      e -= a;
+      ++a;
+    }
+    ga[h] = a;
+    gb[h] = e;
+  }
+  const int nref = c - 2;  // reflectors 0 .. c-3 (v_k acts on indices k+1 .. c-1)
+  for (int kb = ((nref - 1) / BT_NB) * BT_NB; kb >= 0; kb -= BT_NB) {
+    const int nb = (nref - kb) < BT_NB ? (nref - kb) : BT_NB;
+    double wz = 0.0, g0 = 0.0, g1 = 0.0;
+    for (int ich = kb + 1; ich < c; ich += BT_CH) {
+      const int len = (c - ich) < BT_CH ? (c - ich) : BT_CH;
+      // fixed trip count, unrolled: all 16 loads of a thread are in flight together
+#pragma unroll 8
+      for (int it = 0; it < BT_NB * BT_CH / 256; ++it) {
+        const int q = tid + 256 * it;
+        const int a = q / BT_CH, ii = q % BT_CH;
+        const int k = kb + a, i = ich + ii;
+        // the address is clamped in-bounds: the unrolled select may issue the load regardless
+        const bool ok = a < nb && ii < len && i >= k + 1;
+        const double x = V[ok ? (int64_t)k * c + (i - k - 1) : 0];
+        Wc[a][ii] = ok ? x : 0.0;
+      }
+      __syncthreads();
+      // three independent dot products per thread, each split over 4 accumulators, so the
+      // LDS loads of successive terms overlap instead of forming one dependent chain
+      // (Wc is zero past len, z is read only below c)
+      {
+        const double* wr = Wc[wa < nb ? wa : 0];
+        const double* zr = &z[wj][ich];
+        const double* a0 = Wc[ga[0] < nb ? ga[0] : 0];
+        const double* b0 = Wc[gb[0]];
+        const double* a1 = Wc[ga[1] < nb ? ga[1] : 0];
+        const double* b1 = Wc[gb[1] < BT_NB ? gb[1] : 0];
+        double s0[4] = {0.0, 0.0, 0.0, 0.0}, s1[4] = {0.0, 0.0, 0.0, 0.0};
+        double s2[4] = {0.0, 0.0, 0.0, 0.0};
+        const int len4 = len & ~3;
+        for (int ii = 0; ii < len4; ii += 4) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            s0[u] += wr[ii + u] * zr[ii + u];
+            s1[u] += a0[ii + u] * b0[ii + u];
+            s2[u] += a1[ii + u] * b1[ii + u];
+          }
+        }
+        for (int ii = len4; ii < len; ++ii) {
+          s0[0] += wr[ii] * zr[ii];
+          s1[0] += a0[ii] * b0[ii];
+          s2[0] += a1[ii] * b1[ii];
+        }
+        if (wa < nb) wz += (s0[0] + s0[1]) + (s0[2] + s0[3]);
+        if (ga[0] < nb) g0 += (s1[0] + s1[1]) + (s1[2] + s1[3]);
+        if (ga[1] < nb) g1 += (s2[0] + s2[1]) + (s2[2] + s2[3]);
+      }
+      __syncthreads();
+    }
+    if (wa < nb) WZ[wa][wj] = wz;
+    if (ga[0] < nb) G[gb[0]][ga[0]] = g0;
+    if (ga[1] < nb) G[gb[1]][ga[1]] = g1;
+    __syncthreads();
+    // T (forward larft): lane r builds row r alone (its own LDS row, 4 partial sums),
+    // T[r][i] = -tau_i sum_{q=r}^{i-1} T[r][q] G[q][i]
+    if (tid < nb) {
+      const int r = tid;
+      T[r][r] = tau[kb + r];
+      for (int i = r + 1; i < nb; ++i) {
+        double sa[4] = {0.0, 0.0, 0.0, 0.0};
+        int q = r;
+        for (; q + 4 <= i; q += 4) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) sa[u] += T[r][q + u] * G[q + u][i];
+        }
+        for (; q < i; ++q) sa[0] += T[r][q] * G[q][i];
+        T[r][i] = -tau[kb + i] * ((sa[0] + sa[1]) + (sa[2] + sa[3]));
+      }
+    }
+    __syncthreads();
+    if (wa < nb) {
+      double sacc = 0.0;
+      for (int bb = wa; bb < nb; ++bb) sacc += T[wa][bb] * WZ[bb][wj];
+      U[wa][wj] = sacc;
+    }
+    __syncthreads();
+    // z[:, i] -= sum_a w_a[i] U[a][:] for i > kb
+    for (int i = kb + 1 + tid; i < c; i += 256) {
+      double acc[RR_BT_COLS];
+#pragma unroll
+      for (int jj = 0; jj < RR_BT_COLS; ++jj) acc[jj] = 0.0;
+      const int amax = (i - kb - 1) < nb ? (i - kb - 1) : nb - 1;  // w_a[i] != 0 iff i >= kb+a+1
+#pragma unroll 1
+      for (int h = 0; h < BT_NB; h += 8) {
+        double wv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {  // 8 loads in flight before the FMAs
+          const int a = h + u, k = kb + a;
+          const bool ok = a <= amax;  // clamped address, as above
+          const double x = V[ok ? (int64_t)k * c + (i - k - 1) : 0];
+          wv[u] = ok ? x : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+          for (int jj = 0; jj < RR_BT_COLS; ++jj) acc[jj] += wv[u] * U[h + u][jj];
+      }
+#pragma unroll
+      for (int jj = 0; jj < RR_BT_COLS; ++jj) z[jj][i] -= acc[jj];
+    }
+    __syncthreads();
+  }
+  for (int q = tid; q < RR_BT_COLS * c; q += 256) {
+    const int i = q / RR_BT_COLS, jj = q % RR_BT_COLS;
+    if (jj < nj) S[(int64_t)i * lds + j0 + jj] = (float)z[jj][i];
+  }
+}
+
+extern "C" hipError_t n2v2r_launch_rr_tridiag(double* A, int c, double* d, double* e, double* tau,
+                                              double* V, hipStream_t stream) {
+  if (c < 3 || c > RR_MAXC) return hipErrorInvalidValue;
+  // 1024 threads up to c = 512; 512 threads (twice the registers per lane) beyond.  Even c
+  // (every UASE basis: c = blocks x b): 16-B column-pair accesses.
+  static bool attr_set = false;
+  const int cap = 160 * 1024 - 1024;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)rr_tridiag_kernel<4, 1024, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+    (void)hipFuncSetAttribute((const void*)rr_tridiag_kernel<8, 1024, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+    (void)hipFuncSetAttribute((const void*)rr_tridiag_kernel<12, 512, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+    (void)hipFuncSetAttribute((const void*)rr_tridiag_kernel<4, 1024, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+    (void)hipFuncSetAttribute((const void*)rr_tridiag_kernel<8, 1024, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+    (void)hipFuncSetAttribute((const void*)rr_tridiag_kernel<12, 512, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+    attr_set = true;
+  }
+  const dim3 g(1);
+  const bool even = (c % 2) == 0;
+  const size_t l1024 = sizeof(double) * c * 20, l512 = sizeof(double) * c * 12;
+#define RR_TRI_LAUNCH(TM, NT_, PR, L)                                                           \
+  hipLaunchKernelGGL((rr_tridiag_kernel<TM, NT_, PR>), g, dim3(NT_), L, stream, A, c, d, e, tau, V)
+  if (c <= 256) {
+    if (even) RR_TRI_LAUNCH(4, 1024, true, l1024); else RR_TRI_LAUNCH(4, 1024, false, l1024);
+  } else if (c <= 512) {
+    if (even) RR_TRI_LAUNCH(8, 1024, true, l1024); else RR_TRI_LAUNCH(8, 1024, false, l1024);
+  } else {
+    if (even) RR_TRI_LAUNCH(12, 512, true, l512); else RR_TRI_LAUNCH(12, 512, false, l512);
+  }
+#undef RR_TRI_LAUNCH
+  return hipGetLastError();
+}
+
+extern "C" hipError_t n2v2r_launch_rr_backtransform(const double* V, const double* tau, int c,
+                                                    const double* Y, int p, float* S, int lds,
+                                                    hipStream_t stream) {
+  if (c < 3 || c > RR_MAXC || p < 1 || p > c) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rr_backtransform_kernel, dim3((unsigned)((p + RR_BT_COLS - 1) / RR_BT_COLS)),
+                     dim3(256), 0, stream, V, tau, c, Y, p, S, lds);
+  return hipGetLastError();
+}

@@ -110,10 +110,13 @@ def test_partitioned_matches_reference(engine, name, world):
     err = np.abs(orc.align_signs(Y.astype(np.float64), fx["Y"]) - fx["Y"]).max() \
         / np.abs(fx["Y"]).max()
     assert err <= max(5e-4, 3 * env), (name, world, err, env)
-    # vs the single-GPU engine: same signs (deterministic convention), close values
+    # vs the single-GPU engine: close values.  Signs are compared after alignment: the
+    # largest-|u| sign convention can pick a different row when two entries of a column tie
+    # to within the fp32 noise of the two (differently ordered) reductions.
     one = _single(engine, layers, d, dims, metrics, strategy, seed)
     np.testing.assert_allclose(res[0]["s"], one["s"], rtol=1e-5)
-    assert np.abs(Y - one["Y"]).max() <= max(5e-4, 3 * env) * np.abs(one["Y"]).max()
+    Yal = orc.align_signs(Y.astype(np.float64), one["Y"].astype(np.float64))
+    assert np.abs(Yal - one["Y"]).max() <= max(5e-4, 3 * env) * np.abs(one["Y"]).max()
     # Borda is a pure function of D (bit-exact given identical D)
     for c in range(len(one["D"])):
         assert np.all(engine.borda_columns(res[0]["D"][c]) == res[0]["B"][c])
@@ -140,7 +143,8 @@ def test_partitioned_er_large_rows_ingest(engine):
     U = X / np.sqrt(res[0]["s"])[None, :]
     R = M @ U.astype(np.float64) - U * (res[0]["s"] ** 2)[None, :]
     assert np.abs(R).max() / res[0]["s"][0] ** 2 < 1e-4
-    assert np.abs(Y - one["Y"]).max() <= 2e-3 * np.abs(one["Y"]).max()
+    Yal = orc.align_signs(Y.astype(np.float64), one["Y"].astype(np.float64))
+    assert np.abs(Yal - one["Y"]).max() <= 2e-3 * np.abs(one["Y"]).max()
     from scipy.stats import kendalltau
     assert kendalltau(res[0]["B"][0], one["B"][0]).statistic > 0.99
 

@@ -277,3 +277,24 @@ def test_uase_block_widths(engine, name, block):
     env, _ = _envelope(layers, d, int(fx["seed"]))
     err = np.abs(Ya - fx["Y"]).max() / np.abs(fx["Y"]).max()
     assert err <= max(5e-4, 3 * env), (name, block, err, env)
+
+
+# ----------------------------------------------------------------------------- Rayleigh-Ritz
+@pytest.mark.parametrize("c,p", [(40, 12), (256, 80), (300, 100), (512, 160), (600, 150), (768, 200)])
+def test_rayleigh_ritz_stage(engine, c, p):
+    """GPU tridiagonalisation + host tridiagonal solve + GPU back-transform vs numpy eigh,
+    including a tight cluster (gaps 1e-9 relative) and an exactly repeated eigenvalue."""
+    rng = np.random.default_rng(c)
+    ev = np.sort(rng.random(c))[::-1] * 100.0
+    ev[3:8] = ev[3] - 1e-7 * np.arange(5)
+    ev[10] = ev[11]
+    Q, _ = np.linalg.qr(rng.standard_normal((c, c)))
+    H = (Q * ev) @ Q.T
+    H = H + 1e-12 * rng.standard_normal((c, c))  # not exactly symmetric, as QtW is not
+    w, S = engine.rr_top(H, p)
+    ref = np.sort(np.linalg.eigvalsh(0.5 * (H + H.T)))[::-1][:p]
+    np.testing.assert_allclose(w, ref, rtol=0, atol=1e-10 * ref[0])
+    S = S.astype(np.float64)
+    assert np.abs(S.T @ S - np.eye(p)).max() < 5e-6
+    Hs = 0.5 * (H + H.T)
+    assert np.abs(Hs @ S - S * w).max() < 5e-6 * ref[0]
