@@ -41,6 +41,9 @@ CONFIGS = {
                  desc="cfg1: 2-layer ER N=1000 p=0.01, d=8, cosine+euclidean, sequential"),
     "cfg2": dict(n=100_000, avg_deg=20.0, dims=[64], d=64,
                  desc="cfg2: 2-layer ER N=100k avg-deg 20, d=64, cosine+euclidean, sequential"),
+    "cfg3": dict(n=20_000, layers=4, dense=True, dims=[256], d=256, avg_deg=None,
+                 desc="cfg3: 4-layer dense |corrcoef| N=20k (N x 200 Gaussian), d=256, "
+                      "cosine+euclidean, sequential, dense MFMA path"),
     "cfg4": dict(n=1_000_000, avg_deg=50.0, dims=[8, 16, 32, 64, 128], d=128,
                  desc="cfg4: 2-layer ER N=1M avg-deg 50, dims {8,16,32,64,128} x "
                       "{cosine,euclidean}, sequential"),
@@ -48,7 +51,7 @@ CONFIGS = {
                  desc="cfg5: 2-layer ER N=10M avg-deg 30, d=128, cosine+euclidean, sequential, "
                       "row-partitioned"),
 }
-CPU_SAMPLE = {"cfg1": 1000, "cfg2": 50_000, "cfg4": 20_000, "cfg5": 20_000}
+CPU_SAMPLE = {"cfg1": 1000, "cfg2": 50_000, "cfg3": 2_000, "cfg4": 20_000, "cfg5": 20_000}
 METRICS = ["cosine", "euclidean"]
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
@@ -123,14 +126,18 @@ def run_step(eng, cfg, seed, fetch=True):
     return st, out
 
 
-def cpu_baseline(sample_n=20_000, avg_deg=20.0, d=64, dims=(64,)):
+def cpu_baseline(sample_n=20_000, avg_deg=20.0, d=64, dims=(64,), dense_layers=0):
     """Reference algorithm (oracle/, faithful mode) on a bounded sample, 1 thread:
     ARPACK svds + per-row scipy distances + the O(C N^2) list.index Borda."""
+    import scipy.sparse as sp
     from threadpoolctl import threadpool_limits
 
     from node2vec2rank_amd import synthetic
     from oracle import n2v2r_oracle as orc
-    layers = synthetic.er_layers(sample_n, avg_deg, 2, seed_base=7000)
+    if dense_layers:
+        layers = [sp.csc_matrix(a) for a in synthetic.corr_layers(sample_n, dense_layers)]
+    else:
+        layers = synthetic.er_layers(sample_n, avg_deg, 2, seed_base=7000)
     with threadpool_limits(1):
         t0 = time.time()
         Y, _, _ = orc.uase(layers, d, seed=42)
@@ -141,12 +148,13 @@ def cpu_baseline(sample_n=20_000, avg_deg=20.0, d=64, dims=(64,)):
             orc.borda_reference_loop(D)
         t3 = time.time()
     total = t3 - t0
+    fam = (f"{dense_layers}-layer dense |corrcoef| N={sample_n}" if dense_layers else
+           f"2-layer ER N={sample_n} avg-deg {avg_deg:g}")
     return {
-        "value": sample_n / total, "unit": "nodes/s", "cores": 1, "kind": "port",
-        "sample": (f"2-layer ER N={sample_n} avg-deg {avg_deg:g}, d={d}, dims {list(dims)} x "
-                   f"cosine+euclidean (the bench workload's graph family at fewer nodes; the "
-                   f"Borda stage is O(C N^2) so the full-size rate is lower), oracle faithful "
-                   f"mode, 1 thread"),
+        "value": sample_n * len(ranks) / total, "unit": "nodes/s", "cores": 1, "kind": "port",
+        "sample": (f"{fam}, d={d}, dims {list(dims)} x cosine+euclidean (the bench workload's "
+                   f"graph family at fewer nodes; the Borda stage is O(C N^2) so the "
+                   f"full-size rate is lower), oracle faithful mode, 1 thread"),
         "stages_s": {"svds": round(t1 - t0, 3), "distances": round(t2 - t1, 3),
                      "borda": round(t3 - t2, 3)},
     }
@@ -192,6 +200,14 @@ def main():
         del local_layers
         seed = 42
         nodes_per_step = float(cfg["n"])  # one graph, ranked once, over all ranks
+    elif cfg.get("dense"):
+        eng = _lib.Engine(local)
+        layers = synthetic.corr_layers(cfg["n"], cfg["layers"], seed_base=17 * rank)
+        nnz = [int(cfg["n"]) ** 2] * cfg["layers"]
+        eng.set_layers(layers, storage="dense", symmetric=1)  # dense fp32 -> HBM, untimed
+        del layers
+        seed = 42 + rank
+        nodes_per_step = group.sum(float(cfg["n"]))
     else:
         eng = _lib.Engine(local)
         layers = synthetic.er_layers(cfg["n"], cfg["avg_deg"], 2, seed_base=1000 + 17 * rank)
@@ -217,13 +233,13 @@ def main():
     group.barrier()
     elapsed = time.perf_counter() - t0
     elapsed_max = group.max(elapsed)
-    ncmp = 1
+    ncmp = eng.ncmp  # comparisons per step (K - 1 for "sequential")
     value = nodes_per_step * ncmp * args.steps / elapsed_max
 
     # dominant kernel: the CSR x panel SpMM at the Krylov panel width, HIP events on the
     # engine stream (same launch configuration as inside UASE; this rank's rows when
     # partitioned)
-    b = 8  # the Krylov block width UASE runs with (engine default)
+    b = 32 if cfg.get("dense") else 8  # the Krylov panel width UASE runs with (engine default)
     X = np.random.default_rng(0).standard_normal((cfg["n"], b)).astype(np.float32)
     _, spmm_ms, spmm_bytes = eng.bench_spmm(0, X, reps=50, want_y=False)
     del X
@@ -257,11 +273,13 @@ def main():
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic",
-        "config": {"workload": cfg["desc"], "nodes": cfg["n"], "layers": 2,
+        "config": {"workload": cfg["desc"], "nodes": cfg["n"], "layers": cfg.get("layers", 2),
                    "avg_degree": cfg["avg_deg"], "nnz_per_layer": nnz, "embed_dim": cfg["d"],
                    "columns": len(cfg["dims"]) * len(METRICS), "comparisons": ncmp,
                    "parallelism": par},
-        "roofline": {"bound": "hbm", "kernel": f"spmm_csr_panel_kernel<{b},*>",
+        "roofline": {"bound": "hbm",
+                     "kernel": ("dense_gemm_kernel<1> (A_k X, MFMA f32)" if cfg.get("dense")
+                                else f"spmm_csr_panel_kernel<{b},*>"),
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "algo_bytes_per_launch": spmm_bytes, "avg_launch_ms": round(spmm_ms, 5)},
@@ -272,7 +290,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(
             sample_n=args.cpu_sample or CPU_SAMPLE[args.config], avg_deg=cfg["avg_deg"],
-            d=cfg["d"], dims=tuple(cfg["dims"]))
+            d=cfg["d"], dims=tuple(cfg["dims"]),
+            dense_layers=cfg["layers"] if cfg.get("dense") else 0)
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

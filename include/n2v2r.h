@@ -105,6 +105,11 @@ int n2v2r_dist_info(const n2v2r_handle* h, int* rank, int* world, int64_t* row0,
 int n2v2r_set_num_layers(n2v2r_handle* h, int num_layers, int64_t n);
 int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const int64_t* indptr,
                         const int32_t* indices, const float* data, int symmetric);
+/* dense layer (BASELINE cfg3, co-expression networks): A row-major n x n fp32 on the host.
+ * Stored dense in HBM (this rank's rows; A^T rows as well unless symmetric); the Gram
+ * application becomes dense MFMA GEMMs.  All layers of a handle are CSR or all dense.
+ * symmetric: N2V2R_SYM_* (DETECT compares A with A^T on the GPU). */
+int n2v2r_set_layer_dense(n2v2r_handle* h, int k, int64_t n, const float* A, int symmetric);
 /* distributed ingest without the global CSR on every rank: the caller's own rows
  * [row0, row0 + n_rows) (must equal n2v2r_dist_info's) of a SYMMETRIC layer, indptr local
  * (starting at 0), column indices global. */

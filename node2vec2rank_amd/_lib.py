@@ -38,7 +38,7 @@ EXPORTED = [
     "n2v2r_synchronize", "n2v2r_bench_spmm",
     "n2v2r_comm_unique_id", "n2v2r_create_rccl", "n2v2r_simgroup_create",
     "n2v2r_simgroup_destroy", "n2v2r_create_sim", "n2v2r_dist_info", "n2v2r_set_layer_csr_rows",
-    "n2v2r_rr_top",
+    "n2v2r_rr_top", "n2v2r_set_layer_dense",
 ]
 UNIQUE_ID_BYTES = 128
 
@@ -118,6 +118,7 @@ def load(path: str | None = None):
                                       ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_double)]),
             "n2v2r_rr_top": (_i, [_vp, _i, _p(np.float64), _i, _p(np.float64), _p(np.float32)]),
+            "n2v2r_set_layer_dense": (_i, [_vp, _i, _i64, _p(np.float32), _i]),
             "n2v2r_comm_unique_id": (_i, [ctypes.c_char_p, ctypes.c_size_t]),
             "n2v2r_create_rccl": (_i, [_i, _i, _i, ctypes.c_char_p, ctypes.POINTER(_vp)]),
             "n2v2r_simgroup_create": (_i, [_i, ctypes.POINTER(_vp)]),
@@ -248,9 +249,33 @@ class Engine:
         raise RuntimeError(msg)
 
     # -- layers ----------------------------------------------------------------------------
-    def set_layers(self, layers, symmetric=SYM_DETECT):
-        """layers: list of scipy.sparse matrices (any format) or dense arrays, N x N."""
+    def set_layers(self, layers, symmetric=SYM_DETECT, storage="auto"):
+        """layers: list of scipy.sparse matrices (any format) or dense arrays, N x N.
+
+        storage: "csr", "dense" (fp32 N x N in HBM, MFMA GEMMs) or "auto" (dense when every
+        layer is a dense array with more than 1/4 of its entries non-zero)."""
         import scipy.sparse as sp
+        if storage == "auto":
+            storage = "csr"
+            if all(not sp.issparse(a) for a in layers):
+                arrs = [np.asarray(a) for a in layers]
+                if all(np.count_nonzero(a) > a.size // 4 for a in arrs):
+                    storage = "dense"
+        if storage == "dense":
+            arrs = [np.ascontiguousarray(np.asarray(a.todense() if sp.issparse(a) else a),
+                                         dtype=np.float32) for a in layers]
+            n = arrs[0].shape[0]
+            for a in arrs:
+                if a.shape != (n, n):
+                    raise ValueError("all layers must be square and share the node set")
+            self._check(self.lib.n2v2r_set_num_layers(self.h, len(arrs), n), "set_num_layers")
+            for k, a in enumerate(arrs):
+                self._check(self.lib.n2v2r_set_layer_dense(self.h, k, n, a, int(symmetric)),
+                            f"layer {k}")
+            self.n = n
+            self.num_layers = len(arrs)
+            self.storage = "dense"
+            return
         mats = [sp.csr_matrix(a, dtype=np.float32) for a in layers]
         n = mats[0].shape[0]
         for m in mats:
@@ -267,6 +292,7 @@ class Engine:
                                                      data, int(symmetric)), f"layer {k}")
         self.n = n
         self.num_layers = len(mats)
+        self.storage = "csr"
 
     def set_layer_rows(self, n: int, num_layers: int, local_layers):
         """Distributed ingest of symmetric layers from this rank's own rows only:

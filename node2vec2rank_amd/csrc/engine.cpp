@@ -106,6 +106,14 @@ hipError_t n2v2r_launch_radix_pass(const uint64_t* kin, const int32_t* pin, uint
 hipError_t n2v2r_launch_borda_finish(const int32_t* sorted_idx, int64_t n, int nseg, int ncols,
                                      int32_t* pos, int64_t* borda, hipStream_t stream);
 int n2v2r_host_sym_eig_top(int n, double* A, int p, double* w, double* Z);
+hipError_t n2v2r_launch_dense_gemm(const float* A, int64_t lda, int64_t rows, int64_t kdim,
+                                   const float* X, int ldx, int b, float* Y, int64_t ldy,
+                                   float beta, const float* colscale, float* work,
+                                   size_t work_elems, hipStream_t stream);
+hipError_t n2v2r_launch_transpose(const float* in, int64_t ldi, int64_t rows, int64_t cols,
+                                  float* out, int64_t ldo, hipStream_t stream);
+hipError_t n2v2r_launch_mismatch(const float* a, const float* b, int64_t ld, int64_t rows,
+                                 int64_t cols, unsigned long long* count, hipStream_t stream);
 int n2v2r_host_tridiag_eig_top(int n, const double* d, const double* e, int p, double* w,
                                double* Y);
 hipError_t n2v2r_launch_rr_tridiag(double* A, int c, double* d, double* e, double* tau, double* V,
@@ -184,6 +192,12 @@ struct LayerDev {
   int64_t n_rows = 0;                  // local rows
   bool symmetric = true;
   bool loaded = false;
+  // dense layer (cfg3): local rows of A and (directed) of A^T, fp32, leading dimension lda
+  bool dense = false;
+  DevBuf dA, dAT;
+  int64_t lda = 0;
+  const float* dense_a() const { return dA.as<float>(); }
+  const float* dense_at() const { return symmetric ? dA.as<float>() : dAT.as<float>(); }
   CsrDev csr() const {
     return CsrDev{indptr.as<int64_t>(), indices.as<int32_t>(), data.as<float>(), n_rows, nnz};
   }
@@ -343,6 +357,20 @@ struct n2v2r_handle {
   DevBuf colscale;          // fp32
   DevBuf keys, best;        // sign convention
   DevBuf gath;              // gathered panels
+  DevBuf dense_work;        // split-K slabs of the dense GEMM
+  size_t dense_work_elems = 0;
+  bool dense_layers() const { return !layers.empty() && layers[0]->dense; }
+  // Y (nloc x b, ld ldy) = beta Y + colscale .* (A_loc X_global) for dense layer rows
+  void dense_apply(const float* Aloc, int64_t lda, const float* X, int ldx, int b, float* Y,
+                   int64_t ldy, float beta, const float* colscale) {
+    const size_t need = (size_t)std::max<int64_t>(nloc, 1) * b * 8;
+    if (dense_work_elems < need) {
+      dense_work.ensure(sizeof(float) * need);
+      dense_work_elems = need;
+    }
+    HIPCHK(n2v2r_launch_dense_gemm(Aloc, lda, nloc, n, X, ldx, b, Y, ldy, beta, colscale,
+                                   dense_work.as<float>(), dense_work_elems, stream));
+  }
   DevBuf rs_keys[2], rs_idx[2], rs_pos, rs_hist, rs_or, rs_and;
 
 
@@ -539,6 +567,27 @@ struct Eig {
       h->gather_panel(X, xgb, b);
       xg = xgb;
     }
+    if (h->dense_layers()) {
+      // Z_k = A_k^T X, W = sum_k A_k Z_k (fixed layer order), dense GEMMs on the local rows
+      for (int k = 0; k < K; ++k) {
+        const LayerDev& L = *h->layers[k];
+        h->dense_apply(L.dense_at(), L.lda, xg, b, b, zk[k]->as<float>(), b, 0.f, nullptr);
+      }
+      for (int k = 0; k < K; ++k) {
+        const LayerDev& L = *h->layers[k];
+        const float* zin = zk[k]->as<float>();
+        if (h->comm) {
+          float* zgk = zg.as<float>() + (size_t)k * ng * b;
+          h->gather_panel(zk[k]->as<float>(), zgk, b);
+          zin = zgk;
+        }
+        h->dense_apply(L.dense_a(), L.lda, zin, b, b, Wout, b, k == 0 ? 0.f : 1.f, nullptr);
+        algo_bytes += 2.0 * (4.0 * (double)n * (double)h->n + 8.0 * (double)n * b);
+      }
+      launches += 2 * K;
+      t_spmm += now_ms() - t0;
+      return;
+    }
     SpmmArgs a{};
     a.K = K;
     a.sum = 0;
@@ -622,7 +671,9 @@ struct Eig {
     seed = o.seed ? o.seed : 0x5EEDull;
     const double tol = o.tol > 0 ? o.tol : 1e-6;
     const int max_restarts = o.max_restarts > 0 ? o.max_restarts : 2000;
-    b = o.block ? o.block : 8;
+    // default panel width: 8 for CSR layers (vector-applications grow with b); 32 for dense
+    // layers, where one application streams all of A whatever b is (HBM-bound up to b = 32)
+    b = o.block ? o.block : (h->dense_layers() ? 32 : 8);
     if (b != 8 && b != 16 && b != 32 && b != 64)
       throw StatusFail{N2V2R_ERR_BAD_ARG, "block must be 8, 16, 32 or 64"};
     const int64_t nglob = h->n;
@@ -636,6 +687,7 @@ struct Eig {
       const int cap =
           (int)std::min<int64_t>((nglob / 2) / b * b, (int64_t)(N2V2R_MAX_BLOCKS - 1) * b);
       if (maxc > cap) maxc = cap;
+      if (maxc > 768) maxc = 768 / b * b;  // Rayleigh-Ritz kernels: c <= 768
       if (maxc >= keep + b) break;
       if (b == 8)
         throw StatusFail{N2V2R_ERR_BAD_ARG,
@@ -982,7 +1034,13 @@ int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const in
         h->set_err("layer %d: column index out of range", k);
         return N2V2R_ERR_BAD_ARG;
       }
+    for (int j = 0; j < h->K; ++j)
+      if (j != k && h->layers[j]->loaded && h->layers[j]->dense) {
+        h->err = "layers must be all CSR or all dense";
+        return N2V2R_ERR_BAD_ARG;
+      }
     LayerDev& L = *h->layers[k];
+    L.dense = false;
     L.n_rows = h->nloc;
     upload_rows(h->stream, h->row0, h->nloc, indptr, indices, data, L.indptr, L.indices, L.data,
                 L.nnz);
@@ -997,6 +1055,55 @@ int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const in
       if (!sym)
         upload_rows(h->stream, h->row0, h->nloc, tp.data(), tx.data(), td.data(), L.t_indptr,
                     L.t_indices, L.t_data, L.t_nnz);
+    }
+    L.symmetric = sym;
+    L.loaded = true;
+    h->have_embedding = false;
+    return N2V2R_OK;
+  });
+}
+
+int n2v2r_set_layer_dense(n2v2r_handle* h, int k, int64_t n, const float* A, int symmetric) {
+  return guarded(h, [&]() -> int {
+    if (k < 0 || k >= h->K || n != h->n || !A) {
+      h->set_err("bad dense arguments for layer %d", k);
+      return N2V2R_ERR_BAD_ARG;
+    }
+    for (int j = 0; j < h->K; ++j)
+      if (j != k && h->layers[j]->loaded && !h->layers[j]->dense) {
+        h->err = "layers must be all CSR or all dense";
+        return N2V2R_ERR_BAD_ARG;
+      }
+    LayerDev& L = *h->layers[k];
+    L.dense = true;
+    L.n_rows = h->nloc;
+    L.lda = (n + 63) / 64 * 64;
+    const int64_t nl = std::max<int64_t>(h->nloc, 1);
+    L.dA.ensure(sizeof(float) * nl * L.lda);
+    HIPCHK(hipMemcpy2D(L.dA.p, sizeof(float) * L.lda, A + h->row0 * n, sizeof(float) * n,
+                       sizeof(float) * n, h->nloc, hipMemcpyHostToDevice));
+    bool sym = symmetric == N2V2R_SYM_YES;
+    if (!sym) {
+      // A^T rows [row0, row0 + nloc) = columns of A: stage all of A once, transpose the block
+      DevBuf full;
+      full.ensure(sizeof(float) * n * L.lda);
+      HIPCHK(hipMemcpy2D(full.p, sizeof(float) * L.lda, A, sizeof(float) * n, sizeof(float) * n,
+                         n, hipMemcpyHostToDevice));
+      L.dAT.ensure(sizeof(float) * nl * L.lda);
+      HIPCHK(n2v2r_launch_transpose(full.as<float>() + h->row0, L.lda, n, h->nloc,
+                                    L.dAT.as<float>(), L.lda, h->stream));
+      if (symmetric == N2V2R_SYM_DETECT) {
+        DevBuf cnt;
+        cnt.ensure(sizeof(unsigned long long));
+        HIPCHK(n2v2r_launch_mismatch(L.dA.as<float>(), L.dAT.as<float>(), L.lda, h->nloc, n,
+                                     cnt.as<unsigned long long>(), h->stream));
+        unsigned long long mism = 0;
+        HIPCHK(hipMemcpyAsync(&mism, cnt.p, sizeof(mism), hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        sym = mism == 0;
+      }
+      HIPCHK(hipStreamSynchronize(h->stream));
+      if (sym) L.dAT.release();
     }
     L.symmetric = sym;
     L.loaded = true;
@@ -1096,7 +1203,17 @@ int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_sta
       ug = ugath.as<float>();
     }
     h->Y.ensure(sizeof(float) * (size_t)h->K * h->npad * ldu);
-    for (int q = 0; q * b < ldu; ++q) {
+    if (h->dense_layers()) {
+      for (int k = 0; k < h->K; ++k) {
+        const LayerDev& L = *h->layers[k];
+        // one GEMM per layer over all ldu columns (ldu <= 256: 64-column slices)
+        for (int q = 0; q * 64 < ldu; ++q)
+          h->dense_apply(L.dense_at(), L.lda, ug + q * 64, ldu, std::min(64, ldu - q * 64),
+                         h->Y.as<float>() + (size_t)k * h->npad * ldu + q * 64, ldu, 0.f,
+                         h->colscale.as<float>() + q * 64);
+      }
+    }
+    for (int q = 0; !h->dense_layers() && q * b < ldu; ++q) {
       SpmmArgs a{};
       a.K = h->K;
       a.sum = 0;
@@ -1392,7 +1509,16 @@ int n2v2r_column_sums(n2v2r_handle* h, int k, float* out) {
     if (k < 0 || k >= h->K || !out || !h->layers[k]->loaded) return N2V2R_ERR_BAD_ARG;
     DevBuf o, g;
     o.ensure(sizeof(float) * h->npad);
-    HIPCHK(n2v2r_launch_row_sums(h->layers[k]->csr_t(), o.as<float>(), h->stream));
+    if (h->layers[k]->dense) {
+      DevBuf ones;
+      ones.ensure(sizeof(float) * h->n);
+      std::vector<float> one(h->n, 1.f);
+      HIPCHK(hipMemcpy(ones.p, one.data(), sizeof(float) * h->n, hipMemcpyHostToDevice));
+      h->dense_apply(h->layers[k]->dense_at(), h->layers[k]->lda, ones.as<float>(), 1, 1,
+                     o.as<float>(), 1, 0.f, nullptr);
+    } else {
+      HIPCHK(n2v2r_launch_row_sums(h->layers[k]->csr_t(), o.as<float>(), h->stream));
+    }
     const float* src = o.as<float>();
     if (h->comm) {
       g.ensure(sizeof(float) * h->world * h->npad);
@@ -1447,6 +1573,31 @@ int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, con
     xd.ensure(sizeof(float) * h->n * b);
     yd.ensure(sizeof(float) * std::max<int64_t>(h->nloc, 1) * b);
     HIPCHK(hipMemcpyAsync(xd.p, X, sizeof(float) * h->n * b, hipMemcpyHostToDevice, h->stream));
+    if (L.dense) {
+      // dense layer: the GEMM Y = A_k X (or A_k^T X) over this rank's rows
+      const float* am = transpose ? L.dense_at() : L.dense_a();
+      h->dense_apply(am, L.lda, xd.as<float>(), b, b, yd.as<float>(), b, 0.f, nullptr);
+      hipEvent_t e0, e1;
+      HIPCHK(hipEventCreate(&e0));
+      HIPCHK(hipEventCreate(&e1));
+      HIPCHK(hipEventRecord(e0, h->stream));
+      for (int r = 0; r < reps; ++r)
+        h->dense_apply(am, L.lda, xd.as<float>(), b, b, yd.as<float>(), b, 0.f, nullptr);
+      HIPCHK(hipEventRecord(e1, h->stream));
+      HIPCHK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+      if (avg_ms) *avg_ms = (double)ms / reps;
+      if (algo_bytes)
+        *algo_bytes = 4.0 * (double)h->nloc * (double)h->n + 4.0 * (double)(h->n + h->nloc) * b;
+      if (Y)
+        HIPCHK(hipMemcpyAsync(Y, yd.p, sizeof(float) * h->nloc * b, hipMemcpyDeviceToHost,
+                              h->stream));
+      HIPCHK(hipStreamSynchronize(h->stream));
+      return N2V2R_OK;
+    }
     SpmmArgs a{};
     a.K = 1;
     a.sum = 0;

@@ -1,0 +1,197 @@
+// Dense layers (BASELINE cfg3: K dense fp32 N x N co-expression layers): the Gram application
+// of UASE becomes two dense GEMMs per layer, Z_k = A_k^T X and W = sum_k A_k Z_k, with X an
+// N x b panel.  At b = 8..64 the GEMM streams A once (N^2 fp32) and does 2 N^2 b flops, i.e.
+// 4..32 flop/B: HBM-bound at small b, MFMA-bound near b = 64.
+//
+//   dense_gemm_kernel<NT>  Y[r0:r0+rows, 0:b] (+)= A[rows x kdim] X[kdim x b]:
+//     v_mfma_f32_32x32x2_f32, one wave per 32 output rows x NT*32 columns, 4 waves per WG
+//     (128 rows); A rows read as two 16-B loads per lane covering 16 consecutive k (the k order
+//     inside each 16-group is permuted identically for A and X: lane half h carries k
+//     8h..8h+7, MFMA m sums k = {m, 8+m}); X staged through LDS 64 k-rows at a time (row pitch
+//     padded by 4 floats so the two half-waves hit different banks); split-K over grid.y when
+//     the row tiles alone cannot fill the chip, fp32 partial slabs folded by dense_fold_kernel.
+//   transpose_kernel       32x32 LDS tiles (A^T of a directed layer, once at ingest).
+//   mismatch_kernel        counts A != A^T entries (symmetry detection at ingest).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "common.h"
+
+#define DG_KC 64  // k rows of X staged per LDS round
+
+template <int NT>
+__global__ __launch_bounds__(256) void dense_gemm_kernel(const float* __restrict__ A, int64_t lda,
+                                                         int64_t rows, int64_t kdim,
+                                                         int64_t kper, const float* __restrict__ X,
+                                                         int ldx, int b, float* __restrict__ out,
+                                                         int64_t ldo, int64_t slab) {
+  constexpr int XP = NT * 32 + 4;  // padded LDS row pitch
+  __shared__ float xs[DG_KC][XP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const int64_t r0 = (int64_t)blockIdx.x * 128 + wave * 32;
+  const int64_t row = r0 + i;
+  const bool row_ok = row < rows;
+  const int64_t k_begin = (int64_t)blockIdx.y * kper;
+  int64_t k_end = k_begin + kper;
+  if (k_end > kdim) k_end = kdim;
+  const float* arow = A + (row_ok ? row : 0) * lda;
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x16{0.f};
+  for (int64_t k0 = k_begin; k0 < k_end; k0 += DG_KC) {
+    const int kn = (k_end - k0) < DG_KC ? (int)(k_end - k0) : DG_KC;
+    __syncthreads();
+    for (int e = threadIdx.x; e < DG_KC * NT * 32; e += 256) {
+      const int kk = e / (NT * 32), j = e % (NT * 32);
+      xs[kk][j] = (kk < kn && j < b) ? X[(k0 + kk) * ldx + j] : 0.f;
+    }
+    __syncthreads();
+    if (r0 < rows) {
+      for (int kk = 0; kk < kn; kk += 16) {
+        f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+        const int64_t kg = k0 + kk + 8 * h;
+        if (row_ok) {
+          if (kg + 8 <= k_end) {
+            a0 = *reinterpret_cast<const f32x4*>(arow + kg);
+            a1 = *reinterpret_cast<const f32x4*>(arow + kg + 4);
+          } else {
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+              a0[m] = (kg + m < k_end) ? arow[kg + m] : 0.f;
+              a1[m] = (kg + 4 + m < k_end) ? arow[kg + 4 + m] : 0.f;
+            }
+          }
+        }
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          const float av = m < 4 ? a0[m] : a1[m - 4];
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xs[kk + 8 * h + m][t * 32 + i],
+                                                          acc[t], 0, 0, 0);
+        }
+      }
+    }
+  }
+  if (r0 >= rows) return;
+  float* o = out + (int64_t)blockIdx.y * slab;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int col = t * 32 + i;
+    if (col >= b) continue;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int64_t rr = r0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+      if (rr < rows) o[rr * ldo + col] = acc[t][q];
+    }
+  }
+}
+
+// Y[r][j] = beta * Y[r][j] + s[j] * sum_s P[s][r][j]   (s = colscale, or 1)
+__global__ void dense_fold_kernel(const float* __restrict__ P, int nsplit, int64_t slab,
+                                  int64_t rows, int b, float* __restrict__ Y, int64_t ldy,
+                                  float beta, const float* __restrict__ colscale) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= rows * b) return;
+  const int64_t r = e / b;
+  const int j = (int)(e % b);
+  float s = 0.f;
+  for (int q = 0; q < nsplit; ++q) s += P[q * slab + r * b + j];
+  if (colscale) s *= colscale[j];
+  float* y = Y + r * ldy + j;
+  *y = (beta != 0.f ? beta * *y : 0.f) + s;
+}
+
+// Y (rows x b, ld ldy) = beta * Y + colscale .* (A[rows x kdim] X[kdim x b]).  `work` holds the
+// split-K slabs (>= nsplit * rows * b floats; nullptr forces nsplit = 1 and a direct write,
+// allowed only with beta == 0 and no colscale).
+extern "C" hipError_t n2v2r_launch_dense_gemm(const float* A, int64_t lda, int64_t rows,
+                                              int64_t kdim, const float* X, int ldx, int b,
+                                              float* Y, int64_t ldy, float beta,
+                                              const float* colscale, float* work,
+                                              size_t work_elems, hipStream_t stream) {
+  if (rows <= 0) return hipSuccess;
+  if (b < 1 || b > 64 || lda % 4 != 0 || ((uintptr_t)A & 15) != 0) return hipErrorInvalidValue;
+  const int64_t tiles = (rows + 127) / 128;
+  // split K until ~2 workgroups per CU, 256-aligned k ranges, slabs within `work`
+  int64_t nsplit = 1;
+  if (work) {
+    nsplit = (512 + tiles - 1) / tiles;
+    const int64_t kmax = (kdim + 255) / 256;
+    if (nsplit > kmax) nsplit = kmax;
+    if (nsplit < 1) nsplit = 1;
+    const int64_t cap = (int64_t)(work_elems / (size_t)(rows * b));
+    if (nsplit > cap) nsplit = cap;
+    if (nsplit < 1) return hipErrorInvalidValue;
+  } else if (beta != 0.f || colscale) {
+    return hipErrorInvalidValue;
+  }
+  int64_t kper = (kdim + nsplit - 1) / nsplit;
+  kper = (kper + 15) & ~(int64_t)15;
+  nsplit = (kdim + kper - 1) / kper;
+  float* dst = work ? work : Y;
+  const int64_t ldo = work ? b : ldy;
+  const int64_t slab = work ? rows * b : 0;
+  const dim3 grid((unsigned)tiles, (unsigned)nsplit);
+  if (b <= 32)
+    hipLaunchKernelGGL(dense_gemm_kernel<1>, grid, dim3(256), 0, stream, A, lda, rows, kdim, kper,
+                       X, ldx, b, dst, ldo, slab);
+  else
+    hipLaunchKernelGGL(dense_gemm_kernel<2>, grid, dim3(256), 0, stream, A, lda, rows, kdim, kper,
+                       X, ldx, b, dst, ldo, slab);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !work) return e;
+  const int64_t elems = rows * b;
+  hipLaunchKernelGGL(dense_fold_kernel, dim3((unsigned)((elems + 255) / 256)), dim3(256), 0, stream,
+                     work, (int)nsplit, slab, rows, b, Y, ldy, beta, colscale);
+  return hipGetLastError();
+}
+
+// out[c][r] = in[r][c] for an (rows x cols) block, leading dimensions ldi / ldo
+__global__ void transpose_kernel(const float* __restrict__ in, int64_t ldi, int64_t rows,
+                                 int64_t cols, float* __restrict__ out, int64_t ldo) {
+  __shared__ float t[32][33];
+  const int64_t bx = (int64_t)blockIdx.x * 32, by = (int64_t)blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
+  for (int k = ty; k < 32; k += 8) {
+    const int64_t r = by + k, c = bx + tx;
+    t[k][tx] = (r < rows && c < cols) ? in[r * ldi + c] : 0.f;
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int64_t c = bx + k, r = by + tx;
+    if (c < cols && r < rows) out[c * ldo + r] = t[tx][k];
+  }
+}
+
+extern "C" hipError_t n2v2r_launch_transpose(const float* in, int64_t ldi, int64_t rows,
+                                             int64_t cols, float* out, int64_t ldo,
+                                             hipStream_t stream) {
+  const dim3 grid((unsigned)((cols + 31) / 32), (unsigned)((rows + 31) / 32));
+  hipLaunchKernelGGL(transpose_kernel, grid, dim3(256), 0, stream, in, ldi, rows, cols, out, ldo);
+  return hipGetLastError();
+}
+
+// *count += #{(r, c) : a[r][c] != b[r][c]} over an (rows x cols) block
+__global__ void mismatch_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                int64_t ld, int64_t rows, int64_t cols,
+                                unsigned long long* count) {
+  unsigned long long n = 0;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < rows * cols;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / cols, c = e % cols;
+    n += (a[r * ld + c] != b[r * ld + c]) ? 1ull : 0ull;
+  }
+  for (int o = 32; o >= 1; o >>= 1) n += __shfl_xor(n, o, 64);
+  if ((threadIdx.x & 63) == 0 && n) atomicAdd(count, n);
+}
+
+extern "C" hipError_t n2v2r_launch_mismatch(const float* a, const float* b, int64_t ld,
+                                            int64_t rows, int64_t cols, unsigned long long* count,
+                                            hipStream_t stream) {
+  hipLaunchKernelGGL(mismatch_kernel, dim3(2048), dim3(256), 0, stream, a, b, ld, rows, cols,
+                     count);
+  return hipGetLastError();
+}

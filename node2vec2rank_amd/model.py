@@ -27,11 +27,14 @@ from . import _lib
 
 
 def _as_layer(g):
+    """Layers as the engine takes them: scipy sparse stays sparse (CSR), dense arrays and
+    DataFrames stay dense (the engine stores them dense in HBM when they are more than 1/4
+    non-zero, CSR otherwise)."""
     if isinstance(g, pd.DataFrame):
         g = g.values
     if sp.issparse(g):
         return sp.csr_matrix(g, dtype=np.float32)
-    return sp.csr_matrix(np.asarray(g, dtype=np.float32))
+    return np.ascontiguousarray(np.asarray(g, dtype=np.float32))
 
 
 class N2V2R:

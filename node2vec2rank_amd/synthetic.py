@@ -112,3 +112,23 @@ def sbm_layers(n: int, num_layers: int, k_comm: int = 5, p_in: float = 0.2,
         a = (u | u.T).astype(np.float32)
         layers.append(sp.csr_matrix(a))
     return layers, comm
+
+
+def corr_layer(n: int, samples: int = 200, seed: int = 0) -> np.ndarray:
+    """Dense co-expression layer (BASELINE cfg3): |corrcoef| of an n x samples
+    Gaussian matrix drawn from ``default_rng(seed)``, fp32, symmetric, unit diagonal."""
+    g = np.random.default_rng(seed).standard_normal((n, samples))
+    g -= g.mean(axis=1, keepdims=True)
+    g /= np.linalg.norm(g, axis=1, keepdims=True)
+    c = g @ g.T
+    np.abs(c, out=c)
+    out = c.astype(np.float32)
+    del c
+    # exact symmetry (the GEMM is symmetric up to rounding) and unit diagonal, as corrcoef
+    out = np.triu(out) + np.triu(out, 1).T
+    np.fill_diagonal(out, 1.0)
+    return np.ascontiguousarray(out)
+
+
+def corr_layers(n: int, num_layers: int = 4, samples: int = 200, seed_base: int = 0):
+    return [corr_layer(n, samples, seed_base + k) for k in range(num_layers)]
