@@ -68,7 +68,8 @@ typedef struct {
   int converged;             /* Ritz pairs (of d) that met tol */
   int basis;                 /* max basis columns used */
   double max_residual;       /* max_j<d ||M x_j - theta_j x_j|| / theta_1 */
-  double ms_total, ms_spmm, ms_ortho, ms_rr_host; /* wall-clock split */
+  double ms_total, ms_spmm, ms_ortho, ms_rr_host; /* host wall-clock split (launch time for
+                                                     asynchronous GPU stages) */
   int64_t spmm_launches;     /* SpMM kernel launches (for roofline accounting) */
   double spmm_algo_bytes;    /* sum over launches of the SURVEY 8(d) algorithmic bytes */
   int stagnated;             /* 1: stopped at the fp32 residual floor (flat 8 cycles, <= 100x tol) */
@@ -153,8 +154,8 @@ int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, con
                      float* Y, double* avg_ms, double* algo_bytes);
 
 /* Rayleigh-Ritz stage alone (tests): top-p eigenpairs of a host symmetric c x c fp64 matrix H
- * (3 <= c <= 768) through UASE's own path (GPU Householder tridiagonalisation, host QL +
- * inverse iteration on T, GPU back-transform).  w: p eigenvalues, descending; S: c x p
+ * (3 <= c <= 768) through UASE's own path, all on the GPU (Householder tridiagonalisation,
+ * bisection + inverse iteration on the tridiagonal, compact-WY back-transform).  w: p eigenvalues, descending; S: c x p
  * row-major fp32 eigenvectors (the Ritz coefficients UASE consumes). */
 int n2v2r_rr_top(n2v2r_handle* h, int c, const double* H, int p, double* w, float* S);
 

@@ -429,7 +429,7 @@ class Engine:
 
     def rr_top(self, H, p: int):
         """Rayleigh-Ritz stage alone: top-p eigenpairs of symmetric H (GPU tridiagonalisation,
-        host tridiagonal solve, GPU back-transform).  Returns (w, S)."""
+        bisection + inverse iteration, back-transform).  Returns (w, S)."""
         H = np.ascontiguousarray(H, dtype=np.float64)
         c = H.shape[0]
         w = np.empty(p, dtype=np.float64)

@@ -120,17 +120,18 @@ __global__ __launch_bounds__(256) void reduce_chunks_kernel(const double* __rest
 // a wave covers 256 columns = 1 KB of every row), the B row is wave-uniform (scalar loads,
 // read once per row instead of once per 32-column tile), 4 x JB fp32 accumulators per lane.
 // The 4 waves take contiguous quarters of the workgroup's row chunk and are folded through
-// LDS in fixed order into one fp64 partial per chunk.
+// LDS in fixed order into one fp64 partial per chunk; grid.y = 256-column group.
 template <int JB>
 __global__ __launch_bounds__(256) void ts_tn_narrow_kernel(BlockList A, const float* __restrict__ Bz,
                                                            int64_t n, int64_t rows_per_chunk,
-                                                           int u, double* __restrict__ partial,
+                                                           double* __restrict__ partial,
                                                            const int* cond) {
   if (cond && *cond == 0) return;
   extern __shared__ float tn_red[];  // [4][256 * 4][JB]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: B rows via SMEM
   const int ca = A.count * A.width;
+  const int u = blockIdx.y;               // 256-column group
   const int col0 = (u * 64 + lane) * 4;  // this lane's first column
   const bool colok = col0 < ca;
   const float* ab = colok ? A.blk[col0 / A.width] + (col0 % A.width) : A.blk[0];
@@ -206,18 +207,16 @@ extern "C" hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B,
     const int64_t rows_per_chunk = (n + nchunks - 1) / nchunks;
     nchunks = (n + rows_per_chunk - 1) / rows_per_chunk;
     const int groups = (ca + 255) / 256;
-    for (int u = 0; u < groups; ++u) {
-      // each 256-column group writes its own columns of every chunk's partial
-      const size_t lds = sizeof(float) * 4 * 256 * B.width;
-      if (B.width == 8)
-        hipLaunchKernelGGL(ts_tn_narrow_kernel<8>, dim3((unsigned)nchunks), dim3(256), lds, stream,
-                           A, B.blk[0], n, rows_per_chunk, u, partial, cond);
-      else
-        hipLaunchKernelGGL(ts_tn_narrow_kernel<16>, dim3((unsigned)nchunks), dim3(256), lds,
-                           stream, A, B.blk[0], n, rows_per_chunk, u, partial, cond);
-      hipError_t e = hipGetLastError();
-      if (e != hipSuccess) return e;
-    }
+    const size_t lds = sizeof(float) * 4 * 256 * B.width;
+    const dim3 grid((unsigned)nchunks, (unsigned)groups);
+    if (B.width == 8)
+      hipLaunchKernelGGL(ts_tn_narrow_kernel<8>, grid, dim3(256), lds, stream, A, B.blk[0], n,
+                         rows_per_chunk, partial, cond);
+    else
+      hipLaunchKernelGGL(ts_tn_narrow_kernel<16>, grid, dim3(256), lds, stream, A, B.blk[0], n,
+                         rows_per_chunk, partial, cond);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((elems + 3) / 4)), dim3(256), 0,
                        stream, partial, (int)nchunks, elems, out, cond);
     return hipGetLastError();

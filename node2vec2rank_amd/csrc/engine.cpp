@@ -30,6 +30,7 @@
 #include <cmath>
 #include <condition_variable>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -118,6 +119,8 @@ int n2v2r_host_tridiag_eig_top(int n, const double* d, const double* e, int p, d
                                double* Y);
 hipError_t n2v2r_launch_rr_tridiag(double* A, int c, double* d, double* e, double* tau, double* V,
                                    hipStream_t stream);
+hipError_t n2v2r_launch_rr_tri_eig(const double* d, const double* e, int c, int p, double* w,
+                                   double* Y, double* scratch, hipStream_t stream);
 hipError_t n2v2r_launch_rr_backtransform(const double* V, const double* tau, int c,
                                          const double* Y, int p, float* S, int lds,
                                          hipStream_t stream);
@@ -321,6 +324,19 @@ struct ThreadComm : Comm {
 
 }  // namespace
 
+namespace {
+// Solver buffers kept by the handle across n2v2r_uase calls (repeated fits of the same graph
+// reuse every allocation; the zero-filled padding rows of pool blocks stay zero).
+struct EigWorkspace {
+  std::vector<std::unique_ptr<DevBuf>> pool;  // Krylov blocks, block_bytes each
+  size_t block_bytes = 0;
+  std::vector<std::unique_ptr<DevBuf>> zk;    // K stage-1 panels (local)
+  DevBuf zg;                                  // K gathered stage-1 panels
+  DevBuf rinv, flg, anyflag, gsmall, csmall;
+  DevBuf tri, refl, ytri, tscr;               // GPU Rayleigh-Ritz: [d|e|tau], reflectors, Y_T
+};
+}  // namespace
+
 struct n2v2r_handle {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -357,6 +373,7 @@ struct n2v2r_handle {
   DevBuf colscale;          // fp32
   DevBuf keys, best;        // sign convention
   DevBuf gath;              // gathered panels
+  EigWorkspace ews;         // eigensolver buffers, reused across fits
   DevBuf dense_work;        // split-K slabs of the dense GEMM
   size_t dense_work_elems = 0;
   bool dense_layers() const { return !layers.empty() && layers[0]->dense; }
@@ -503,13 +520,8 @@ struct Eig {
   int pb;           // kept blocks at restart
   int d;
   uint64_t seed;
-  std::vector<std::unique_ptr<DevBuf>> pool;  // all npad x b blocks
   std::vector<float*> freelist;
   std::vector<float*> Q, W;                   // current basis / images
-  std::vector<std::unique_ptr<DevBuf>> zk;    // K stage-1 panels (local)
-  DevBuf zg;                                  // K gathered stage-1 panels
-  DevBuf rinv, flg, anyflag, gsmall, csmall;
-  DevBuf tri, refl, ytri;                     // GPU Rayleigh-Ritz: [d|e|tau], reflectors, Y_T
   n2v2r_eig_stats* stats;
   double t_spmm = 0, t_ortho = 0;
   int64_t launches = 0;
@@ -518,9 +530,9 @@ struct Eig {
 
   float* take() {
     if (freelist.empty()) {
-      pool.emplace_back(new DevBuf());
-      pool.back()->ensure(sizeof(float) * npad * b, st);
-      return pool.back()->as<float>();
+      h->ews.pool.emplace_back(new DevBuf());
+      h->ews.pool.back()->ensure(sizeof(float) * npad * b, st);
+      return h->ews.pool.back()->as<float>();
     }
     float* p = freelist.back();
     freelist.pop_back();
@@ -571,14 +583,14 @@ struct Eig {
       // Z_k = A_k^T X, W = sum_k A_k Z_k (fixed layer order), dense GEMMs on the local rows
       for (int k = 0; k < K; ++k) {
         const LayerDev& L = *h->layers[k];
-        h->dense_apply(L.dense_at(), L.lda, xg, b, b, zk[k]->as<float>(), b, 0.f, nullptr);
+        h->dense_apply(L.dense_at(), L.lda, xg, b, b, h->ews.zk[k]->as<float>(), b, 0.f, nullptr);
       }
       for (int k = 0; k < K; ++k) {
         const LayerDev& L = *h->layers[k];
-        const float* zin = zk[k]->as<float>();
+        const float* zin = h->ews.zk[k]->as<float>();
         if (h->comm) {
-          float* zgk = zg.as<float>() + (size_t)k * ng * b;
-          h->gather_panel(zk[k]->as<float>(), zgk, b);
+          float* zgk = h->ews.zg.as<float>() + (size_t)k * ng * b;
+          h->gather_panel(h->ews.zk[k]->as<float>(), zgk, b);
           zin = zgk;
         }
         h->dense_apply(L.dense_a(), L.lda, zin, b, b, Wout, b, k == 0 ? 0.f : 1.f, nullptr);
@@ -597,7 +609,7 @@ struct Eig {
     for (int k = 0; k < K; ++k) {
       a.A[k] = h->layers[k]->csr_t();
       a.X[k] = xg;
-      a.Y[k] = zk[k]->as<float>();
+      a.Y[k] = h->ews.zk[k]->as<float>();
     }
     HIPCHK(n2v2r_launch_spmm(a, b, st));
     SpmmArgs s{};
@@ -609,11 +621,11 @@ struct Eig {
     for (int k = 0; k < K; ++k) {
       s.A[k] = h->layers[k]->csr();
       if (h->comm) {
-        float* zgk = zg.as<float>() + (size_t)k * ng * b;
-        h->gather_panel(zk[k]->as<float>(), zgk, b);
+        float* zgk = h->ews.zg.as<float>() + (size_t)k * ng * b;
+        h->gather_panel(h->ews.zk[k]->as<float>(), zgk, b);
         s.X[k] = zgk;
       } else {
-        s.X[k] = zk[k]->as<float>();
+        s.X[k] = h->ews.zk[k]->as<float>();
       }
     }
     s.Y[0] = Wout;
@@ -629,27 +641,32 @@ struct Eig {
   // One fused BCGS + CholQR pass: G = [Q Z]^T Z -> R^{-1} -> Z <- [Q Z] [-C R^{-1}; R^{-1}],
   // refill deficient columns.  `cond` (device int, nullptr = always) skips the pass when zero.
   void pip_pass(float* Z, const std::vector<float*>& basis, const int* cond, int* flags_out,
-                int* any_out) {
+                int* any_out, const float* Zin = nullptr) {
+    // Zin (default Z): the block to orthogonalise; the result is written to Z
+    const float* zin = Zin ? Zin : Z;
     const int nq = (int)basis.size();
     std::vector<float*> qz(basis);
-    qz.push_back(Z);
+    qz.push_back(const_cast<float*>(zin));
     const BlockList L = blocks(qz, 0, nq + 1);
-    tn(L, one(Z), gsmall.as<double>(), cond);
-    HIPCHK(n2v2r_launch_pip_chol(gsmall.as<double>(), nq * b, b, rinv.as<double>(), flags_out,
-                                 any_out, cond, st));
+    tn(L, one(zin), h->ews.gsmall.as<double>(), cond);
+    HIPCHK(n2v2r_launch_pip_chol(h->ews.gsmall.as<double>(), nq * b, b, h->ews.rinv.as<double>(),
+                                 flags_out, any_out, cond, st));
     // rank-deficient columns (flags_out) are refilled with random values by the same launch
-    HIPCHK(n2v2r_launch_pip_apply(L, gsmall.as<double>(), rinv.as<double>(), nq * b, b,
-                                  out_one(Z), n, cond, flags_out,
+    HIPCHK(n2v2r_launch_pip_apply(L, h->ews.gsmall.as<double>(), h->ews.rinv.as<double>(), nq * b,
+                                  b, out_one(Z), n, cond, flags_out,
                                   seed ^ (0xABCDull + ++fill_counter), row0, st));
   }
 
-  // orthonormalise Z against `basis` and within itself: two fused passes (BCGS-PIP2), a third
-  // only when the second one had to refill a rank-deficient column.
-  void orthonormalize(float* Z, const std::vector<float*>& basis) {
+  // orthonormalise Zin (default: Z in place) against `basis` and within itself into Z: two
+  // fused passes (BCGS-PIP2), a third only when the second one had to refill a rank-deficient
+  // column.
+  void orthonormalize(float* Z, const std::vector<float*>& basis, const float* Zin = nullptr) {
     const double t0 = now_ms();
-    pip_pass(Z, basis, nullptr, flg.as<int>(), anyflag.as<int>());
-    pip_pass(Z, basis, nullptr, flg.as<int>() + 64, anyflag.as<int>() + 1);
-    pip_pass(Z, basis, anyflag.as<int>() + 1, flg.as<int>() + 128, anyflag.as<int>() + 2);
+    int* flg = h->ews.flg.as<int>();
+    int* any = h->ews.anyflag.as<int>();
+    pip_pass(Z, basis, nullptr, flg, any, Zin);
+    pip_pass(Z, basis, nullptr, flg + 64, any + 1);
+    pip_pass(Z, basis, any + 1, flg + 128, any + 2);
     t_ortho += now_ms() - t0;
   }
 
@@ -657,8 +674,7 @@ struct Eig {
   void expand_one(const float* w_from, const std::vector<float*>& basis, std::vector<float*>& qs,
                   std::vector<float*>& ws) {
     float* z = take();
-    HIPCHK(hipMemcpyAsync(z, w_from, sizeof(float) * npad * b, hipMemcpyDeviceToDevice, st));
-    orthonormalize(z, basis);
+    orthonormalize(z, basis, w_from);  // the first pass reads W_from and writes z: no copy
     float* w = take();
     apply_M(z, w);
     qs.push_back(z);
@@ -697,25 +713,31 @@ struct Eig {
     nb_max = maxc / b;
     const int c_max = maxc;
     // scratch
-    zk.clear();
-    for (int k = 0; k < K; ++k) {
-      zk.emplace_back(new DevBuf());
-      zk.back()->ensure(sizeof(float) * npad * b);
+    // reuse the workspace of the previous fit: every pool block is free again
+    const size_t bb = sizeof(float) * npad * b;
+    if (h->ews.block_bytes != bb) {
+      h->ews.pool.clear();
+      h->ews.block_bytes = bb;
     }
+    freelist.clear();
+    for (auto& blk : h->ews.pool) freelist.push_back(blk->as<float>());
+    while ((int)h->ews.zk.size() < K) h->ews.zk.emplace_back(new DevBuf());
+    for (int k = 0; k < K; ++k) h->ews.zk[k]->ensure(bb);
     if (h->comm) {
       h->gath.ensure(sizeof(float) * h->world * npad * b);
-      zg.ensure(sizeof(float) * (size_t)K * h->world * npad * b);
+      h->ews.zg.ensure(sizeof(float) * (size_t)K * h->world * npad * b);
     }
     h->partial_elems = std::max<size_t>(4096ull * 1024ull, (size_t)c_max * c_max * 8);
     h->partial.ensure(sizeof(double) * h->partial_elems);
-    gsmall.ensure(sizeof(double) * (size_t)c_max * c_max);
-    csmall.ensure(sizeof(float) * (size_t)c_max * c_max);
-    tri.ensure(sizeof(double) * 3 * (size_t)c_max);
-    refl.ensure(sizeof(double) * (size_t)c_max * c_max);
-    ytri.ensure(sizeof(double) * (size_t)c_max * keep);
-    rinv.ensure(sizeof(double) * 64 * 64);
-    flg.ensure(sizeof(int) * 256);
-    anyflag.ensure(sizeof(int) * 4);
+    h->ews.gsmall.ensure(sizeof(double) * (size_t)c_max * c_max);
+    h->ews.csmall.ensure(sizeof(float) * (size_t)c_max * c_max);
+    h->ews.tri.ensure(sizeof(double) * 3 * (size_t)c_max);
+    h->ews.refl.ensure(sizeof(double) * (size_t)c_max * c_max);
+    h->ews.ytri.ensure(sizeof(double) * (size_t)c_max * keep);
+    h->ews.tscr.ensure(sizeof(double) * 6 * (size_t)((keep + 63) / 64 * 64) * c_max);
+    h->ews.rinv.ensure(sizeof(double) * 64 * 64);
+    h->ews.flg.ensure(sizeof(int) * 256);
+    h->ews.anyflag.ensure(sizeof(int) * 4);
     h->theta.ensure(sizeof(double) * c_max);
     h->resid.ensure(sizeof(double) * c_max);
 
@@ -737,20 +759,11 @@ struct Eig {
     std::vector<double> hist_res;
     int stagnated = 0;
     const double t_start = now_ms();
+    static const bool trace = [] {  // N2V2R_TRACE=1: one stderr line per Rayleigh-Ritz cycle
+      const char* e = std::getenv("N2V2R_TRACE");
+      return e && *e && *e != '0';
+    }();
     double t_rr = 0;
-    // pinned host staging for the projected matrix and the Ritz coefficients
-    double* Hh = nullptr;
-    double* Yh = nullptr;
-    HIPCHK(hipHostMalloc((void**)&Hh, sizeof(double) * 2 * (size_t)c_max, 0));
-    HIPCHK(hipHostMalloc((void**)&Yh, sizeof(double) * (size_t)c_max * keep, 0));
-    struct PinnedFree {
-      double* hh;
-      double* y;
-      ~PinnedFree() {
-        if (hh) (void)hipHostFree(hh);
-        if (y) (void)hipHostFree(y);
-      }
-    } pinned_guard{Hh, Yh};
     for (;; ++cycle) {
       while ((int)Q.size() < nb_max) {
         expand_one(W.back(), Q, Q, W);
@@ -758,24 +771,20 @@ struct Eig {
       }
       const int nq = (int)Q.size();
       const int c = nq * b;
-      // H = Q^T W (fp64, all-reduced) -> tridiagonal on the GPU -> host QL + inverse
-      // iteration on T (O(c keep)) -> back-transform on the GPU into the fp32 Ritz
-      // coefficients S (c x keep, ld keep)
-      tn(blocks(Q, 0, nq), blocks(W, 0, nq), gsmall.as<double>(), nullptr);
-      double* trid = tri.as<double>();
-      HIPCHK(n2v2r_launch_rr_tridiag(gsmall.as<double>(), c, trid, trid + c_max, trid + 2 * c_max,
-                                     refl.as<double>(), st));
-      HIPCHK(hipMemcpyAsync(Hh, trid, sizeof(double) * 2 * c_max, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
+      // Rayleigh-Ritz, all on the GPU: H = Q^T W (fp64, all-reduced) -> Householder
+      // tridiagonal -> bisection + inverse iteration on T for the top keep -> back-transform
+      // into the fp32 Ritz coefficients S (c x keep, ld keep); theta stays in HBM until the
+      // residual read-back below
+      tn(blocks(Q, 0, nq), blocks(W, 0, nq), h->ews.gsmall.as<double>(), nullptr);
+      double* trid = h->ews.tri.as<double>();
       const double tr0 = now_ms();
-      if (n2v2r_host_tridiag_eig_top(c, Hh, Hh + c_max, keep, wh.data(), Yh) != 0)
-        throw StatusFail{N2V2R_ERR_NO_CONVERGENCE, "Rayleigh-Ritz eigensolve failed"};
+      HIPCHK(n2v2r_launch_rr_tridiag(h->ews.gsmall.as<double>(), c, trid, trid + c_max, trid + 2 * c_max,
+                                     h->ews.refl.as<double>(), st));
+      HIPCHK(n2v2r_launch_rr_tri_eig(trid, trid + c_max, c, keep, h->theta.as<double>(),
+                                     h->ews.ytri.as<double>(), h->ews.tscr.as<double>(), st));
+      HIPCHK(n2v2r_launch_rr_backtransform(h->ews.refl.as<double>(), trid + 2 * c_max, c,
+                                           h->ews.ytri.as<double>(), keep, h->ews.csmall.as<float>(), keep, st));
       t_rr += now_ms() - tr0;
-      HIPCHK(hipMemcpyAsync(ytri.p, Yh, sizeof(double) * c * keep, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(h->theta.as<double>(), wh.data(), sizeof(double) * keep,
-                            hipMemcpyHostToDevice, st));
-      HIPCHK(n2v2r_launch_rr_backtransform(refl.as<double>(), trid + 2 * c_max, c,
-                                           ytri.as<double>(), keep, csmall.as<float>(), keep, st));
       // Ritz vectors X = Q S, MX = W S (keep columns, pb blocks)
       for (int q = 0; q < pb; ++q) {
         X[q] = take();
@@ -793,7 +802,7 @@ struct Eig {
           omx.blk[t] = MX[q0b + t];
         }
         // G slice: columns [q0b*b, q0b*b + nt*b) of S (ld = keep)
-        const float* g = csmall.as<float>() + q0b * b;
+        const float* g = h->ews.csmall.as<float>() + q0b * b;
         HIPCHK(n2v2r_launch_ts_nn(blocks(Q, 0, nq), g, keep, nt * b, ox, one(nullptr), 1.f, 0.f, n,
                                   nullptr, nullptr, 0, st));
         HIPCHK(n2v2r_launch_ts_nn(blocks(W, 0, nq), g, keep, nt * b, omx, one(nullptr), 1.f, 0.f,
@@ -805,6 +814,8 @@ struct Eig {
       h->allreduce_f64(h->resid.as<double>(), keep);
       HIPCHK(hipMemcpyAsync(res2.data(), h->resid.as<double>(), sizeof(double) * keep,
                             hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(wh.data(), h->theta.as<double>(), sizeof(double) * keep,
+                            hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
       t_ortho += now_ms() - to0;
       maxres = 0;
@@ -815,6 +826,9 @@ struct Eig {
         maxres = std::max(maxres, r);
         if (r <= tol) ++conv;
       }
+      if (trace)
+        fprintf(stderr, "[n2v2r] rank %d cycle %d apps %d c %d max_res %.3e converged %d/%d %.1f ms\n",
+                h->rank, cycle, apps, c, maxres, conv, d, now_ms() - t_start);
       bool done = (conv == d || cycle + 1 >= max_restarts);
       if (!done) {
         // fp32 noise floor: the true residual of W = M Q cannot fall below ~eps32 *
@@ -1547,13 +1561,12 @@ int n2v2r_rr_top(n2v2r_handle* h, int c, const double* H, int p, double* w, floa
     double* t = tri.as<double>();
     HIPCHK(n2v2r_launch_rr_tridiag(a.as<double>(), c, t, t + c, t + 2 * c, refl.as<double>(),
                                    h->stream));
-    std::vector<double> de(2 * c), yh((size_t)c * p);
-    HIPCHK(hipMemcpyAsync(de.data(), t, sizeof(double) * 2 * c, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
-    if (n2v2r_host_tridiag_eig_top(c, de.data(), de.data() + c, p, w, yh.data()) != 0)
-      return N2V2R_ERR_NO_CONVERGENCE;
-    HIPCHK(hipMemcpyAsync(y.p, yh.data(), sizeof(double) * c * p, hipMemcpyHostToDevice,
-                          h->stream));
+    DevBuf wd, scr;
+    wd.ensure(sizeof(double) * p);
+    scr.ensure(sizeof(double) * 6 * (size_t)((p + 63) / 64 * 64) * c);
+    HIPCHK(n2v2r_launch_rr_tri_eig(t, t + c, c, p, wd.as<double>(), y.as<double>(),
+                                   scr.as<double>(), h->stream));
+    HIPCHK(hipMemcpyAsync(w, wd.p, sizeof(double) * p, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(n2v2r_launch_rr_backtransform(refl.as<double>(), t + 2 * c, c, y.as<double>(), p,
                                          s.as<float>(), p, h->stream));
     HIPCHK(hipMemcpyAsync(S, s.p, sizeof(float) * c * p, hipMemcpyDeviceToHost, h->stream));

@@ -16,6 +16,8 @@
 
 #include <cstdint>
 
+#include "common.h"
+
 #define RR_MAXC 768
 #define RR_BT_COLS 8
 
@@ -394,6 +396,220 @@ __global__ __launch_bounds__(256) void rr_backtransform_kernel(const double* __r
     const int i = q / RR_BT_COLS, jj = q % RR_BT_COLS;
     if (jj < nj) S[(int64_t)i * lds + j0 + jj] = (float)z[jj][i];
   }
+}
+
+// ---- eigenpairs of the tridiagonal T on the GPU --------------------------------------------
+// rr_bisect_kernel: one workgroup per wanted eigenvalue (j-th largest, j < p).  Multisection
+// on the Gershgorin interval: each round the 256 threads evaluate the Sturm count (negative
+// pivots of the LDL^T of T - x I, pivots clamped to -pivmin as LAPACK dstebz) at 256 interior
+// points, the interval shrinks 257x; 7 rounds reach fp64 resolution.
+#define RR_BIS_THREADS 256
+__global__ __launch_bounds__(RR_BIS_THREADS) void rr_bisect_kernel(const double* __restrict__ dg,
+                                                                   const double* __restrict__ eg,
+                                                                   int c, int p,
+                                                                   double* __restrict__ w) {
+  __shared__ double d[RR_MAXC], e2[RR_MAXC];
+  __shared__ int cnt[RR_BIS_THREADS];
+  __shared__ double red[4][2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = blockIdx.x;
+  const int a = c - 1 - j;  // ascending index of the wanted eigenvalue
+  double glo = 1e300, ghi = -1e300, emax = 0.0;
+  for (int i = tid; i < c; i += RR_BIS_THREADS) {
+    const double di = dg[i];
+    const double el = i > 0 ? fabs(eg[i - 1]) : 0.0, er = i < c - 1 ? fabs(eg[i]) : 0.0;
+    d[i] = di;
+    e2[i] = i > 0 ? eg[i - 1] * eg[i - 1] : 0.0;
+    glo = fmin(glo, di - el - er);
+    ghi = fmax(ghi, di + el + er);
+    emax = fmax(emax, e2[i]);
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    glo = fmin(glo, __shfl_xor(glo, o, 64));
+    ghi = fmax(ghi, __shfl_xor(ghi, o, 64));
+    emax = fmax(emax, __shfl_xor(emax, o, 64));
+  }
+  if (lane == 0) {
+    red[wave][0] = glo;
+    red[wave][1] = ghi;
+    cnt[wave] = 0;
+  }
+  __syncthreads();
+  double lo = fmin(fmin(red[0][0], red[1][0]), fmin(red[2][0], red[3][0]));
+  double hi = fmax(fmax(red[0][1], red[1][1]), fmax(red[2][1], red[3][1]));
+  const double span = fmax(fabs(lo), fabs(hi));
+  lo -= 2.2e-16 * span * c + 1e-300;
+  hi += 2.2e-16 * span * c + 1e-300;
+  const double pivmin = fmax(1e-300, 2.2e-308 * fmax(1.0, emax));
+  for (int round = 0; round < 8; ++round) {
+    const double x = lo + (hi - lo) * (double)(tid + 1) / (double)(RR_BIS_THREADS + 1);
+    int neg = 0;
+    double q = d[0] - x;
+    if (fabs(q) < pivmin) q = -pivmin;
+    neg += q < 0.0;
+    for (int i = 1; i < c; ++i) {
+      q = (d[i] - x) - e2[i] / q;
+      if (fabs(q) < pivmin) q = -pivmin;
+      neg += q < 0.0;
+    }
+    __syncthreads();
+    cnt[tid] = neg;  // nu(x_t) = #eigenvalues < x_t, nondecreasing in t
+    __syncthreads();
+    // lambda_a lies in (x_{t-1}, x_t] for the first t with nu(x_t) > a
+    int first = RR_BIS_THREADS;
+    for (int t = tid; t < RR_BIS_THREADS; t += RR_BIS_THREADS)
+      if (cnt[t] > a && (t == 0 || cnt[t - 1] <= a)) first = t;
+    for (int o = 32; o >= 1; o >>= 1) first = min(first, __shfl_xor(first, o, 64));
+    __syncthreads();
+    if (lane == 0) cnt[wave] = first;
+    __syncthreads();
+    first = min(min(cnt[0], cnt[1]), min(cnt[2], cnt[3]));
+    const double step = (hi - lo) / (double)(RR_BIS_THREADS + 1);
+    const double nlo = lo + step * first;
+    const double nhi = (first < RR_BIS_THREADS) ? lo + step * (first + 1) : hi;
+    lo = nlo;
+    hi = nhi;
+    if (hi - lo <= 2.2e-16 * fmax(fabs(lo), fabs(hi))) break;
+  }
+  if (tid == 0) w[j] = 0.5 * (lo + hi);
+}
+
+// rr_inviter_kernel: eigenvectors of T for the p wanted eigenvalues (descending).  Thread j
+// handles the cluster starting at j (gap to the previous eigenvalue > clus); the members of a
+// cluster are computed in order by the same thread and Gram-Schmidt'ed against the earlier
+// ones.  Two inverse iterations per vector from a counter-based random start; tridiagonal
+// LU with partial pivoting.  Per-thread vectors live in `scratch` interleaved across threads
+// (element i of thread t at [i * P + t], P = p rounded to 64), so a wave's accesses to step i
+// are one coalesced segment; the recurrences carry their running values in registers.
+// Y: column-major c x p.
+__global__ __launch_bounds__(64) void rr_inviter_kernel(const double* __restrict__ d,
+                                                        const double* __restrict__ e, int c,
+                                                        int p, const double* __restrict__ w,
+                                                        double clus_rel, double* __restrict__ Y,
+                                                        double* __restrict__ scratch) {
+  const int j0 = blockIdx.x * 64 + threadIdx.x;
+  const int P = (p + 63) / 64 * 64;
+  if (j0 >= p) return;
+  double tnorm = 0.0;
+  for (int i = 0; i < c; ++i) {
+    const double r = (i > 0 ? fabs(e[i - 1]) : 0.0) + (i < c - 1 ? fabs(e[i]) : 0.0);
+    tnorm = fmax(tnorm, fabs(d[i]) + r);
+  }
+  const double clus = clus_rel * fmax(tnorm, 1e-300);
+  if (j0 > 0 && fabs(w[j0 - 1] - w[j0]) <= clus) return;  // not a cluster start
+  const double tiny = fmax(2.220446049250313e-16 * tnorm, 1e-300);
+  const int64_t S = (int64_t)P * c;  // one interleaved array
+  double* dgv = scratch + j0;
+  double* u1 = dgv + S;
+  double* u2 = u1 + S;
+  double* lm = u2 + S;
+  double* sw = lm + S;
+  double* x = sw + S;
+#define AT(arr, i) (arr)[(int64_t)(i) * P]
+  for (int j = j0; j < p && (j == j0 || fabs(w[j - 1] - w[j]) <= clus); ++j) {
+    const double lam = w[j];
+    for (int i = 0; i < c; ++i) {
+      const uint64_t hsh = splitmix64(0x9E3779B97F4A7C15ull ^ ((uint64_t)j << 32) ^ (uint64_t)i);
+      AT(x, i) = (double)(hsh >> 11) * (1.0 / 9007199254740992.0) - 0.5;
+    }
+    {  // LU of T - lam I with partial pivoting (one extra superdiagonal)
+      double a = d[0] - lam;
+      double cc = (c > 1) ? e[0] : 0.0;
+      for (int i = 0; i < c - 1; ++i) {
+        const double sub = e[i];
+        const double nd = d[i + 1] - lam;
+        const double ns = (i + 1 < c - 1) ? e[i + 1] : 0.0;
+        if (fabs(a) >= fabs(sub)) {
+          if (fabs(a) < tiny) a = (a < 0 ? -tiny : tiny);
+          const double m = sub / a;
+          AT(lm, i) = m;
+          AT(sw, i) = 0.0;
+          AT(dgv, i) = a;
+          AT(u1, i) = cc;
+          AT(u2, i) = 0.0;
+          a = nd - m * cc;
+          cc = ns;
+        } else {
+          const double m = a / sub;
+          AT(lm, i) = m;
+          AT(sw, i) = 1.0;
+          AT(dgv, i) = sub;
+          AT(u1, i) = nd;
+          AT(u2, i) = ns;
+          a = cc - m * nd;
+          cc = -m * ns;
+        }
+      }
+      if (fabs(a) < tiny) a = (a < 0 ? -tiny : tiny);
+      AT(dgv, c - 1) = a;
+    }
+    // two inverse iterations: the shift is the bisection eigenvalue (fp64-accurate), so the
+    // first solve already amplifies the wanted direction by ~1/eps; the second cleans up
+    for (int it = 0; it < 2; ++it) {
+      // forward substitution with the interchanges: cur = updated x[i]
+      double cur = AT(x, 0);
+#pragma unroll 8
+      for (int i = 0; i < c - 1; ++i) {
+        double nxt = AT(x, i + 1);
+        if (AT(sw, i) != 0.0) {
+          const double t = cur;
+          cur = nxt;
+          nxt = t;
+        }
+        AT(x, i) = cur;
+        cur = nxt - AT(lm, i) * cur;
+      }
+      AT(x, c - 1) = cur;
+      // back substitution, x[i+1], x[i+2] carried in registers
+      double x1 = AT(x, c - 1) / AT(dgv, c - 1);
+      AT(x, c - 1) = x1;
+      double x2 = 0.0;
+      if (c > 1) {
+        const double v = (AT(x, c - 2) - AT(u1, c - 2) * x1) / AT(dgv, c - 2);
+        AT(x, c - 2) = v;
+        x2 = x1;
+        x1 = v;
+      }
+#pragma unroll 8
+      for (int i = c - 3; i >= 0; --i) {
+        const double v = (AT(x, i) - AT(u1, i) * x1 - AT(u2, i) * x2) / AT(dgv, i);
+        AT(x, i) = v;
+        x2 = x1;
+        x1 = v;
+      }
+      for (int q = j0; q < j; ++q) {  // MGS against the earlier members of the cluster
+        const double* y = Y + (int64_t)q * c;
+        double s = 0.0;
+        for (int i = 0; i < c; ++i) s += y[i] * AT(x, i);
+        for (int i = 0; i < c; ++i) AT(x, i) -= s * y[i];
+      }
+      double nr = 0.0;
+      for (int i = 0; i < c; ++i) nr += AT(x, i) * AT(x, i);
+      nr = sqrt(nr);
+      if (!(nr > 0.0)) {
+        for (int i = 0; i < c; ++i) AT(x, i) = (i == j % c) ? 1.0 : 0.0;
+        nr = 1.0;
+      }
+      const double inv = 1.0 / nr;
+      for (int i = 0; i < c; ++i) AT(x, i) *= inv;
+    }
+    double* yj = Y + (int64_t)j * c;
+    for (int i = 0; i < c; ++i) yj[i] = AT(x, i);
+  }
+#undef AT
+}
+
+extern "C" hipError_t n2v2r_launch_rr_tri_eig(const double* d, const double* e, int c, int p,
+                                              double* w, double* Y, double* scratch,
+                                              hipStream_t stream) {
+  if (c < 3 || c > RR_MAXC || p < 1 || p > c) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rr_bisect_kernel, dim3((unsigned)p), dim3(RR_BIS_THREADS), 0, stream, d, e,
+                     c, p, w);
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return err;
+  hipLaunchKernelGGL(rr_inviter_kernel, dim3((unsigned)((p + 63) / 64)), dim3(64), 0, stream, d, e,
+                     c, p, w, 1e-7, Y, scratch);
+  return hipGetLastError();
 }
 
 extern "C" hipError_t n2v2r_launch_rr_tridiag(double* A, int c, double* d, double* e, double* tau,
