@@ -29,6 +29,7 @@ __device__ __forceinline__ float counter_normal(uint64_t seed, uint64_t ctr) {
 
 // ----------------------------------------------------------------------------- ts_tn
 #define TN_WAVES 4
+#define TN_FLUSH 1024  // rows per fp32 partial sum before it is added to the fp64 total
 
 // Column `col` of a block list (nullptr past the last column): per lane, so a 32-wide tile may
 // span several 8/16-wide blocks.
@@ -65,16 +66,29 @@ __global__ __launch_bounds__(256) void ts_tn_kernel(BlockList A, BlockList B, in
   int64_t r1 = r0 + per_wave;
   if (r1 > c1) r1 = c1;
   f32x16 acc = {0.f};
+  double dacc[16];  // fp64 flush of the fp32 MFMA sums every TN_FLUSH rows: bounded fp32 sums
+#pragma unroll
+  for (int q = 0; q < 16; ++q) dacc[q] = 0.0;
   int64_t r = r0;
-  for (; r + 8 <= r1; r += 8) {
-    float a0 = ma * pa[(r + 0 + h) * lda], b0 = mb * pb[(r + 0 + h) * ldb];
-    float a1 = ma * pa[(r + 2 + h) * lda], b1 = mb * pb[(r + 2 + h) * ldb];
-    float a2 = ma * pa[(r + 4 + h) * lda], b2 = mb * pb[(r + 4 + h) * ldb];
-    float a3 = ma * pa[(r + 6 + h) * lda], b3 = mb * pb[(r + 6 + h) * ldb];
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a2, b2, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a3, b3, acc, 0, 0, 0);
+  while (r + 8 <= r1) {
+    int64_t rend = r + TN_FLUSH;
+    if (rend > r1) rend = r1;
+    for (; r + 8 <= rend; r += 8) {
+      float a0 = ma * pa[(r + 0 + h) * lda], b0 = mb * pb[(r + 0 + h) * ldb];
+      float a1 = ma * pa[(r + 2 + h) * lda], b1 = mb * pb[(r + 2 + h) * ldb];
+      float a2 = ma * pa[(r + 4 + h) * lda], b2 = mb * pb[(r + 4 + h) * ldb];
+      float a3 = ma * pa[(r + 6 + h) * lda], b3 = mb * pb[(r + 6 + h) * ldb];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a2, b2, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a3, b3, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      dacc[q] += (double)acc[q];
+      acc[q] = 0.f;
+    }
+    if (rend == r1 || r + 8 > r1) break;
   }
   for (; r < r1; r += 2) {
     const int64_t rr = r + h;
@@ -86,7 +100,7 @@ __global__ __launch_bounds__(256) void ts_tn_kernel(BlockList A, BlockList B, in
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
   }
 #pragma unroll
-  for (int q = 0; q < 16; ++q) red[wave][q][lane] = (double)acc[q];
+  for (int q = 0; q < 16; ++q) red[wave][q][lane] = dacc[q] + (double)acc[q];
   __syncthreads();
   // 256 threads fold 4 waves x 1024 values in fixed order.
   double* out = partial + (int64_t)blockIdx.x * ca * cb;
@@ -121,13 +135,13 @@ __global__ __launch_bounds__(256) void reduce_chunks_kernel(const double* __rest
 // read once per row instead of once per 32-column tile), 4 x JB fp32 accumulators per lane.
 // The 4 waves take contiguous quarters of the workgroup's row chunk and are folded through
 // LDS in fixed order into one fp64 partial per chunk; grid.y = 256-column group.
-template <int JB>
+template <int JB, bool FLUSH>
 __global__ __launch_bounds__(256) void ts_tn_narrow_kernel(BlockList A, const float* __restrict__ Bz,
                                                            int64_t n, int64_t rows_per_chunk,
                                                            double* __restrict__ partial,
                                                            const int* cond) {
   if (cond && *cond == 0) return;
-  extern __shared__ float tn_red[];  // [4][256 * 4][JB]
+  extern __shared__ double tn_red[];  // [4 waves][256 columns][JB]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: B rows via SMEM
   const int ca = A.count * A.width;
@@ -148,8 +162,24 @@ __global__ __launch_bounds__(256) void ts_tn_narrow_kernel(BlockList A, const fl
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < JB; ++j) acc[i][j] = 0.f;
+  double dacc[FLUSH ? 4 : 1][FLUSH ? JB : 1];
+#pragma unroll
+  for (int i = 0; i < (FLUSH ? 4 : 1); ++i)
+#pragma unroll
+    for (int j = 0; j < (FLUSH ? JB : 1); ++j) dacc[i][j] = 0.0;
   int64_t r = r0;
+  int64_t next_flush = r0 + TN_FLUSH;
   for (; r + 4 <= r1; r += 4) {
+    if (FLUSH && r >= next_flush) {  // bounded fp32 partial sums, fp64 totals
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < JB; ++j) {
+          dacc[FLUSH ? i : 0][FLUSH ? j : 0] += (double)acc[i][j];
+          acc[i][j] = 0.f;
+        }
+      next_flush += TN_FLUSH;
+    }
     f32x4 a[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -176,19 +206,21 @@ __global__ __launch_bounds__(256) void ts_tn_narrow_kernel(BlockList A, const fl
     }
   }
   // fold the 4 waves (fixed order) and write this chunk's fp64 partial [ca][JB]
-  float* mine = tn_red + (size_t)wave * 256 * JB;
+  double* mine = tn_red + (size_t)wave * 256 * JB;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < JB; ++j) mine[(lane * 4 + i) * JB + j] = acc[i][j];
+    for (int j = 0; j < JB; ++j)
+      mine[(lane * 4 + i) * JB + j] = (FLUSH ? dacc[FLUSH ? i : 0][FLUSH ? j : 0] : 0.0) +
+                                      (double)acc[i][j];
   __syncthreads();
   double* out = partial + (int64_t)blockIdx.x * ca * JB;
   for (int e = threadIdx.x; e < 256 * JB; e += 256) {
     const int cl = e / JB;  // column within this 256-column group
     const int col = u * 256 + cl;
     if (col >= ca) continue;
-    const double s = (double)tn_red[e] + (double)tn_red[256 * JB + e] +
-                     (double)tn_red[2 * 256 * JB + e] + (double)tn_red[3 * 256 * JB + e];
+    const double s = tn_red[e] + tn_red[256 * JB + e] + tn_red[2 * 256 * JB + e] +
+                     tn_red[3 * 256 * JB + e];
     out[(int64_t)col * JB + (e % JB)] = s;
   }
 }
@@ -207,14 +239,26 @@ extern "C" hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B,
     const int64_t rows_per_chunk = (n + nchunks - 1) / nchunks;
     nchunks = (n + rows_per_chunk - 1) / rows_per_chunk;
     const int groups = (ca + 255) / 256;
-    const size_t lds = sizeof(float) * 4 * 256 * B.width;
+    const size_t lds = sizeof(double) * 4 * 256 * B.width;
     const dim3 grid((unsigned)nchunks, (unsigned)groups);
-    if (B.width == 8)
-      hipLaunchKernelGGL(ts_tn_narrow_kernel<8>, grid, dim3(256), lds, stream, A, B.blk[0], n,
-                         rows_per_chunk, partial, cond);
-    else
-      hipLaunchKernelGGL(ts_tn_narrow_kernel<16>, grid, dim3(256), lds, stream, A, B.blk[0], n,
-                         rows_per_chunk, partial, cond);
+    static bool attr = false;
+    if (!attr) {  // 128 KB of LDS for the 16-wide form
+      (void)hipFuncSetAttribute((const void*)ts_tn_narrow_kernel<16, false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024);
+      (void)hipFuncSetAttribute((const void*)ts_tn_narrow_kernel<16, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024);
+      attr = true;
+    }
+    const bool flush = rows_per_chunk / 4 > TN_FLUSH;  // rows per wave beyond one fp32 span
+#define TN_NARROW(J, F)                                                                    \
+  hipLaunchKernelGGL((ts_tn_narrow_kernel<J, F>), grid, dim3(256), lds, stream, A, B.blk[0], n, \
+                     rows_per_chunk, partial, cond)
+    if (B.width == 8) {
+      if (flush) TN_NARROW(8, true); else TN_NARROW(8, false);
+    } else {
+      if (flush) TN_NARROW(16, true); else TN_NARROW(16, false);
+    }
+#undef TN_NARROW
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((elems + 3) / 4)), dim3(256), 0,

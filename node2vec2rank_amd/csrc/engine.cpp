@@ -832,12 +832,15 @@ struct Eig {
       bool done = (conv == d || cycle + 1 >= max_restarts);
       if (!done) {
         // fp32 noise floor: the true residual of W = M Q cannot fall below ~eps32 *
-        // sqrt(nnz/row) * theta_1.  Stop when the worst residual has not improved by 2% over
-        // 8 cycles and is within 100x of tol.
+        // sqrt(nnz/row) * theta_1.  Stop when the best worst-residual of the last 8 cycles is
+        // not 10% below the best one before them (slow but steady convergence on clustered
+        // spectra keeps going) and it is within 100x of tol.
         hist_res.push_back(maxres);
-        if (hist_res.size() >= 9) {
-          const double prev = *std::min_element(hist_res.end() - 9, hist_res.end() - 1);
-          if (maxres > 0.98 * prev && maxres <= 100.0 * tol) {
+        const size_t W8 = 8;
+        if (hist_res.size() >= 2 * W8) {
+          const double recent = *std::min_element(hist_res.end() - W8, hist_res.end());
+          const double before = *std::min_element(hist_res.begin(), hist_res.end() - W8);
+          if (recent > 0.9 * before && recent <= 100.0 * tol) {
             stagnated = 1;
             done = true;
           }
