@@ -141,6 +141,11 @@ int n2v2r_borda_columns(n2v2r_handle* h, const double* D /* C*N column-major */,
                         int n_cols, int64_t* borda);
 int n2v2r_column_sums(n2v2r_handle* h, int k, float* out /* N */);
 
+/* bipartite projection of a non-square layer (preprocessing_utils.py:16-32): out = W^T W
+ * (n x n) when on_columns, else W W^T (m x m), for a host row-major m x n fp32 W. */
+int n2v2r_project(n2v2r_handle* h, int64_t m, int64_t n, const float* W, int on_columns,
+                  float* out);
+
 /* device sync */
 int n2v2r_synchronize(n2v2r_handle* h);
 

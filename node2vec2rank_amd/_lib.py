@@ -38,7 +38,7 @@ EXPORTED = [
     "n2v2r_synchronize", "n2v2r_bench_spmm",
     "n2v2r_comm_unique_id", "n2v2r_create_rccl", "n2v2r_simgroup_create",
     "n2v2r_simgroup_destroy", "n2v2r_create_sim", "n2v2r_dist_info", "n2v2r_set_layer_csr_rows",
-    "n2v2r_rr_top", "n2v2r_set_layer_dense",
+    "n2v2r_rr_top", "n2v2r_set_layer_dense", "n2v2r_project",
 ]
 UNIQUE_ID_BYTES = 128
 
@@ -119,6 +119,7 @@ def load(path: str | None = None):
                                       ctypes.POINTER(ctypes.c_double)]),
             "n2v2r_rr_top": (_i, [_vp, _i, _p(np.float64), _i, _p(np.float64), _p(np.float32)]),
             "n2v2r_set_layer_dense": (_i, [_vp, _i, _i64, _p(np.float32), _i]),
+            "n2v2r_project": (_i, [_vp, _i64, _i64, _p(np.float32), _i, _p(np.float32)]),
             "n2v2r_comm_unique_id": (_i, [ctypes.c_char_p, ctypes.c_size_t]),
             "n2v2r_create_rccl": (_i, [_i, _i, _i, ctypes.c_char_p, ctypes.POINTER(_vp)]),
             "n2v2r_simgroup_create": (_i, [_i, ctypes.POINTER(_vp)]),
@@ -426,6 +427,18 @@ class Engine:
                                               int(reps), X, yp, ctypes.byref(ms),
                                               ctypes.byref(by)), "bench_spmm")
         return Y, ms.value, by.value
+
+    def project(self, W, on: str = "columns"):
+        """W^T W (on="columns") or W W^T (on="rows") of a dense m x n matrix, fp32 on the GPU."""
+        W = np.ascontiguousarray(np.asarray(W), dtype=np.float32)
+        m, n = W.shape
+        oc = on.casefold() == "columns"
+        if not oc and on.casefold() != "rows":
+            raise ValueError("Unknown projection type, options are columns or rows")
+        k = n if oc else m
+        out = np.empty((k, k), dtype=np.float32)
+        self._check(self.lib.n2v2r_project(self.h, m, n, W, int(oc), out), "project")
+        return out
 
     def rr_top(self, H, p: int):
         """Rayleigh-Ritz stage alone: top-p eigenpairs of symmetric H (GPU tridiagonalisation,

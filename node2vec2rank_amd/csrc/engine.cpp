@@ -1548,6 +1548,42 @@ int n2v2r_column_sums(n2v2r_handle* h, int k, float* out) {
   });
 }
 
+// Bipartite projection (replaces bipartite_to_unipartite_projection, preprocessing_utils.py:16-32,
+// which network_transform applies to non-square layers, :128-130): out = W^T W (n x n,
+// on_columns) or W W^T (m x m) for a host row-major m x n fp32 W, as 64-column MFMA GEMM slices
+// on the GPU (fp32 accumulation; the reference multiplies in the CSV's dtype, float64).
+int n2v2r_project(n2v2r_handle* h, int64_t m, int64_t n, const float* W, int on_columns,
+                  float* out) {
+  return guarded(h, [&]() -> int {
+    if (m < 1 || n < 1 || !W || !out) return N2V2R_ERR_BAD_ARG;
+    const int64_t ldw = (n + 63) / 64 * 64, ldt = (m + 63) / 64 * 64;
+    DevBuf w, wt, o, work;
+    w.ensure(sizeof(float) * m * ldw);
+    wt.ensure(sizeof(float) * n * ldt);
+    HIPCHK(hipMemcpy2D(w.p, sizeof(float) * ldw, W, sizeof(float) * n, sizeof(float) * n, m,
+                       hipMemcpyHostToDevice));
+    HIPCHK(n2v2r_launch_transpose(w.as<float>(), ldw, m, n, wt.as<float>(), ldt, h->stream));
+    // columns: A = W^T (n x m), X = W (m x n);  rows: A = W (m x n), X = W^T (n x m)
+    const float* A = on_columns ? wt.as<float>() : w.as<float>();
+    const int64_t lda = on_columns ? ldt : ldw;
+    const int64_t rows = on_columns ? n : m, kdim = on_columns ? m : n;
+    const float* X = on_columns ? w.as<float>() : wt.as<float>();
+    const int64_t ldx = on_columns ? ldw : ldt;
+    o.ensure(sizeof(float) * rows * rows);
+    const size_t welems = (size_t)rows * 64 * 8;
+    work.ensure(sizeof(float) * welems);
+    for (int64_t j = 0; j < rows; j += 64) {
+      const int bw = (int)std::min<int64_t>(64, rows - j);
+      HIPCHK(n2v2r_launch_dense_gemm(A, lda, rows, kdim, X + j, (int)ldx, bw, o.as<float>() + j,
+                                     rows, 0.f, nullptr, work.as<float>(), welems, h->stream));
+    }
+    HIPCHK(hipMemcpyAsync(out, o.p, sizeof(float) * rows * rows, hipMemcpyDeviceToHost,
+                          h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return N2V2R_OK;
+  });
+}
+
 // Rayleigh-Ritz stage alone (tests): top-p eigenpairs of a host symmetric c x c matrix through
 // the same GPU tridiagonalisation + host tridiagonal solve + GPU back-transform as UASE.
 int n2v2r_rr_top(n2v2r_handle* h, int c, const double* H, int p, double* w, float* S) {
