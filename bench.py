@@ -116,8 +116,8 @@ def _torch_sync():
         pass
 
 
-def run_step(eng, cfg, seed, fetch=True):
-    st = eng.uase(cfg["d"], seed=seed)
+def run_step(eng, cfg, seed, fetch=True, eig=None):
+    st = eng.uase(cfg["d"], seed=seed, **(eig or {}))
     ncmp, _ = eng.rank("sequential", cfg["dims"], METRICS)
     out = []
     if fetch:  # the reference API hands the distance table and the Borda scores to the caller
@@ -175,6 +175,8 @@ def main():
     ap.add_argument("--mode", default="auto", choices=["auto", "replicas", "partitioned"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=0)
+    ap.add_argument("--eig", default="", help='solver knobs as JSON, e.g. {"block": 16, '
+                    '"max_basis": 512, "keep": 320} (default: the engine defaults)')
     args = ap.parse_args()
 
     world, rank, local = _dist_env()
@@ -183,6 +185,7 @@ def main():
     group = _Group(world)
     cfg = CONFIGS[args.config]
     mode = args.mode if args.mode != "auto" else cfg.get("mode", "replicas")
+    eig = json.loads(args.eig) if args.eig else {}
 
     from node2vec2rank_amd import _lib, synthetic
     t_build = time.perf_counter()
@@ -220,14 +223,14 @@ def main():
     fetch = mode == "replicas" or rank == 0
 
     for _ in range(args.warmup):
-        run_step(eng, cfg, seed, fetch)
+        run_step(eng, cfg, seed, fetch, eig)
     eng.synchronize()
     _torch_sync()
     group.barrier()
     t0 = time.perf_counter()
     stats = None
     for _ in range(args.steps):
-        stats, _ = run_step(eng, cfg, seed, fetch)
+        stats, _ = run_step(eng, cfg, seed, fetch, eig)
     eng.synchronize()
     _torch_sync()
     group.barrier()
@@ -239,7 +242,7 @@ def main():
     # dominant kernel: the CSR x panel SpMM at the Krylov panel width, HIP events on the
     # engine stream (same launch configuration as inside UASE; this rank's rows when
     # partitioned)
-    b = 32 if cfg.get("dense") else 8  # the Krylov panel width UASE runs with (engine default)
+    b = int(eig.get("block", 0)) or (32 if cfg.get("dense") else 8)  # the solver's panel width
     X = np.random.default_rng(0).standard_normal((cfg["n"], b)).astype(np.float32)
     _, spmm_ms, spmm_bytes = eng.bench_spmm(0, X, reps=50, want_y=False)
     del X
@@ -284,6 +287,7 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "algo_bytes_per_launch": spmm_bytes, "avg_launch_ms": round(spmm_ms, 5)},
         "eig": {k: (float(f"{v:.4g}") if isinstance(v, float) else v) for k, v in stats.items()},
+        "eig_options": eig,
         "rank_ms": {"distances": round(ms_dist, 3), "borda": round(ms_borda, 3)},
         "setup_s": round(t_build, 2),
     }

@@ -474,45 +474,40 @@ __global__ __launch_bounds__(RR_BIS_THREADS) void rr_bisect_kernel(const double*
   if (tid == 0) w[j] = 0.5 * (lo + hi);
 }
 
-// rr_inviter_kernel: eigenvectors of T for the p wanted eigenvalues (descending).  Thread j
-// handles the cluster starting at j (gap to the previous eigenvalue > clus); the members of a
-// cluster are computed in order by the same thread and Gram-Schmidt'ed against the earlier
-// ones.  Two inverse iterations per vector from a counter-based random start; tridiagonal
-// LU with partial pivoting.  Per-thread vectors live in `scratch` interleaved across threads
-// (element i of thread t at [i * P + t], P = p rounded to 64), so a wave's accesses to step i
-// are one coalesced segment; the recurrences carry their running values in registers.
+// rr_inviter_kernel: eigenvectors of T for the p wanted eigenvalues (descending).  One
+// 64-thread workgroup per cluster start (gap to the previous eigenvalue > clus = 1e-9 ||T||;
+// fp64 inverse iteration leaves vectors of eigenvalues delta apart orthogonal to
+// ~eps ||T|| / delta, so only gaps below that need Gram-Schmidt); the cluster's members are
+// computed in order.  Lane 0 runs the O(c) tridiagonal LU (partial pivoting) and the two
+// inverse-iteration solves with the factors and the iterate in LDS; the whole wave does the
+// Gram-Schmidt against the earlier members (classical, twice per member: one per iteration).
 // Y: column-major c x p.
 __global__ __launch_bounds__(64) void rr_inviter_kernel(const double* __restrict__ d,
                                                         const double* __restrict__ e, int c,
                                                         int p, const double* __restrict__ w,
-                                                        double clus_rel, double* __restrict__ Y,
-                                                        double* __restrict__ scratch) {
-  const int j0 = blockIdx.x * 64 + threadIdx.x;
-  const int P = (p + 63) / 64 * 64;
-  if (j0 >= p) return;
-  double tnorm = 0.0;
-  for (int i = 0; i < c; ++i) {
+                                                        double clus_rel, double* __restrict__ Y) {
+  __shared__ double dgv[RR_MAXC], u1[RR_MAXC], u2[RR_MAXC], lm[RR_MAXC], x[RR_MAXC];
+  __shared__ unsigned char sw[RR_MAXC];
+  __shared__ double proj[64];
+  __shared__ double nrm_s;
+  const int j0 = blockIdx.x;
+  const int lane = threadIdx.x;
+  double tn = 0.0;
+  for (int i = lane; i < c; i += 64) {
     const double r = (i > 0 ? fabs(e[i - 1]) : 0.0) + (i < c - 1 ? fabs(e[i]) : 0.0);
-    tnorm = fmax(tnorm, fabs(d[i]) + r);
+    tn = fmax(tn, fabs(d[i]) + r);
   }
-  const double clus = clus_rel * fmax(tnorm, 1e-300);
-  if (j0 > 0 && fabs(w[j0 - 1] - w[j0]) <= clus) return;  // not a cluster start
-  const double tiny = fmax(2.220446049250313e-16 * tnorm, 1e-300);
-  const int64_t S = (int64_t)P * c;  // one interleaved array
-  double* dgv = scratch + j0;
-  double* u1 = dgv + S;
-  double* u2 = u1 + S;
-  double* lm = u2 + S;
-  double* sw = lm + S;
-  double* x = sw + S;
-#define AT(arr, i) (arr)[(int64_t)(i) * P]
+  for (int o = 32; o >= 1; o >>= 1) tn = fmax(tn, __shfl_xor(tn, o, 64));
+  const double clus = clus_rel * fmax(tn, 1e-300);
+  if (j0 > 0 && fabs(w[j0 - 1] - w[j0]) <= clus) return;  // not a cluster start (uniform)
+  const double tiny = fmax(2.220446049250313e-16 * tn, 1e-300);
   for (int j = j0; j < p && (j == j0 || fabs(w[j - 1] - w[j]) <= clus); ++j) {
     const double lam = w[j];
-    for (int i = 0; i < c; ++i) {
+    for (int i = lane; i < c; i += 64) {
       const uint64_t hsh = splitmix64(0x9E3779B97F4A7C15ull ^ ((uint64_t)j << 32) ^ (uint64_t)i);
-      AT(x, i) = (double)(hsh >> 11) * (1.0 / 9007199254740992.0) - 0.5;
+      x[i] = (double)(hsh >> 11) * (1.0 / 9007199254740992.0) - 0.5;
     }
-    {  // LU of T - lam I with partial pivoting (one extra superdiagonal)
+    if (lane == 0) {  // LU of T - lam I with partial pivoting (one extra superdiagonal)
       double a = d[0] - lam;
       double cc = (c > 1) ? e[0] : 0.0;
       for (int i = 0; i < c - 1; ++i) {
@@ -522,93 +517,111 @@ __global__ __launch_bounds__(64) void rr_inviter_kernel(const double* __restrict
         if (fabs(a) >= fabs(sub)) {
           if (fabs(a) < tiny) a = (a < 0 ? -tiny : tiny);
           const double m = sub / a;
-          AT(lm, i) = m;
-          AT(sw, i) = 0.0;
-          AT(dgv, i) = a;
-          AT(u1, i) = cc;
-          AT(u2, i) = 0.0;
+          lm[i] = m;
+          sw[i] = 0;
+          dgv[i] = a;
+          u1[i] = cc;
+          u2[i] = 0.0;
           a = nd - m * cc;
           cc = ns;
         } else {
           const double m = a / sub;
-          AT(lm, i) = m;
-          AT(sw, i) = 1.0;
-          AT(dgv, i) = sub;
-          AT(u1, i) = nd;
-          AT(u2, i) = ns;
+          lm[i] = m;
+          sw[i] = 1;
+          dgv[i] = sub;
+          u1[i] = nd;
+          u2[i] = ns;
           a = cc - m * nd;
           cc = -m * ns;
         }
       }
       if (fabs(a) < tiny) a = (a < 0 ? -tiny : tiny);
-      AT(dgv, c - 1) = a;
+      dgv[c - 1] = a;
     }
+    __syncthreads();
     // two inverse iterations: the shift is the bisection eigenvalue (fp64-accurate), so the
     // first solve already amplifies the wanted direction by ~1/eps; the second cleans up
     for (int it = 0; it < 2; ++it) {
-      // forward substitution with the interchanges: cur = updated x[i]
-      double cur = AT(x, 0);
-#pragma unroll 8
-      for (int i = 0; i < c - 1; ++i) {
-        double nxt = AT(x, i + 1);
-        if (AT(sw, i) != 0.0) {
-          const double t = cur;
-          cur = nxt;
-          nxt = t;
+      if (lane == 0) {
+        double cur = x[0];
+        for (int i = 0; i < c - 1; ++i) {  // forward substitution with the interchanges
+          double nxt = x[i + 1];
+          if (sw[i]) {
+            const double t = cur;
+            cur = nxt;
+            nxt = t;
+          }
+          x[i] = cur;
+          cur = nxt - lm[i] * cur;
         }
-        AT(x, i) = cur;
-        cur = nxt - AT(lm, i) * cur;
+        x[c - 1] = cur;
+        double x1 = cur / dgv[c - 1];  // back substitution, x[i+1], x[i+2] in registers
+        x[c - 1] = x1;
+        double x2 = 0.0;
+        if (c > 1) {
+          const double v = (x[c - 2] - u1[c - 2] * x1) / dgv[c - 2];
+          x[c - 2] = v;
+          x2 = x1;
+          x1 = v;
+        }
+        for (int i = c - 3; i >= 0; --i) {
+          const double v = (x[i] - u1[i] * x1 - u2[i] * x2) / dgv[i];
+          x[i] = v;
+          x2 = x1;
+          x1 = v;
+        }
       }
-      AT(x, c - 1) = cur;
-      // back substitution, x[i+1], x[i+2] carried in registers
-      double x1 = AT(x, c - 1) / AT(dgv, c - 1);
-      AT(x, c - 1) = x1;
-      double x2 = 0.0;
-      if (c > 1) {
-        const double v = (AT(x, c - 2) - AT(u1, c - 2) * x1) / AT(dgv, c - 2);
-        AT(x, c - 2) = v;
-        x2 = x1;
-        x1 = v;
+      __syncthreads();
+      // classical Gram-Schmidt against the earlier members of the cluster, 64 at a time
+      for (int q0 = j0; q0 < j; q0 += 64) {
+        const int q = q0 + lane;
+        double sdot = 0.0;
+        if (q < j) {
+          const double* y = Y + (int64_t)q * c;
+          for (int i = 0; i < c; ++i) sdot += y[i] * x[i];
+        }
+        proj[lane] = sdot;
+        __syncthreads();
+        const int nq = min(64, j - q0);
+        for (int i = lane; i < c; i += 64) {
+          double acc = 0.0;
+          for (int t = 0; t < nq; ++t) acc += proj[t] * Y[(int64_t)(q0 + t) * c + i];
+          x[i] -= acc;
+        }
+        __syncthreads();
       }
-#pragma unroll 8
-      for (int i = c - 3; i >= 0; --i) {
-        const double v = (AT(x, i) - AT(u1, i) * x1 - AT(u2, i) * x2) / AT(dgv, i);
-        AT(x, i) = v;
-        x2 = x1;
-        x1 = v;
-      }
-      for (int q = j0; q < j; ++q) {  // MGS against the earlier members of the cluster
-        const double* y = Y + (int64_t)q * c;
-        double s = 0.0;
-        for (int i = 0; i < c; ++i) s += y[i] * AT(x, i);
-        for (int i = 0; i < c; ++i) AT(x, i) -= s * y[i];
-      }
-      double nr = 0.0;
-      for (int i = 0; i < c; ++i) nr += AT(x, i) * AT(x, i);
-      nr = sqrt(nr);
+      double s2 = 0.0;
+      for (int i = lane; i < c; i += 64) s2 += x[i] * x[i];
+      for (int o = 32; o >= 1; o >>= 1) s2 += __shfl_xor(s2, o, 64);
+      if (lane == 0) nrm_s = sqrt(s2);
+      __syncthreads();
+      double nr = nrm_s;
       if (!(nr > 0.0)) {
-        for (int i = 0; i < c; ++i) AT(x, i) = (i == j % c) ? 1.0 : 0.0;
+        for (int i = lane; i < c; i += 64) x[i] = (i == j % c) ? 1.0 : 0.0;
         nr = 1.0;
       }
       const double inv = 1.0 / nr;
-      for (int i = 0; i < c; ++i) AT(x, i) *= inv;
+      for (int i = lane; i < c; i += 64) x[i] *= inv;
+      __syncthreads();
     }
     double* yj = Y + (int64_t)j * c;
-    for (int i = 0; i < c; ++i) yj[i] = AT(x, i);
+    for (int i = lane; i < c; i += 64) yj[i] = x[i];
+    __syncthreads();
+    __threadfence_block();
   }
-#undef AT
 }
 
 extern "C" hipError_t n2v2r_launch_rr_tri_eig(const double* d, const double* e, int c, int p,
                                               double* w, double* Y, double* scratch,
                                               hipStream_t stream) {
+  (void)scratch;
   if (c < 3 || c > RR_MAXC || p < 1 || p > c) return hipErrorInvalidValue;
   hipLaunchKernelGGL(rr_bisect_kernel, dim3((unsigned)p), dim3(RR_BIS_THREADS), 0, stream, d, e,
                      c, p, w);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return err;
-  hipLaunchKernelGGL(rr_inviter_kernel, dim3((unsigned)((p + 63) / 64)), dim3(64), 0, stream, d, e,
-                     c, p, w, 1e-7, Y, scratch);
+  hipLaunchKernelGGL(rr_inviter_kernel, dim3((unsigned)p), dim3(64), 0, stream, d, e, c, p, w,
+                     1e-9, Y);
   return hipGetLastError();
 }
 
