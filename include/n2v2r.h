@@ -46,6 +46,9 @@ enum { N2V2R_COSINE = 0, N2V2R_EUCLIDEAN = 1, N2V2R_CORRELATION = 2 };
 /* symmetric hint for n2v2r_set_layer_csr */
 enum { N2V2R_SYM_DETECT = -1, N2V2R_SYM_NO = 0, N2V2R_SYM_YES = 1 };
 
+/* n2v2r_eig_opts.solver_flags */
+enum { N2V2R_EIG_FULL_FIRST_PASS = 1, N2V2R_EIG_DENSE_RR = 2 };
+
 typedef struct n2v2r_handle n2v2r_handle;
 typedef struct n2v2r_simgroup n2v2r_simgroup;
 
@@ -56,10 +59,11 @@ typedef struct {
   int max_restarts;   /* (0 = auto: 2000) */
   double tol;         /* stop when ||M x_j - theta_j x_j|| <= tol * theta_1 for j < d (<=0: 1e-6) */
   uint64_t seed;      /* start block seed */
-  int overlap;        /* EXPERIMENTAL: blocks expanded on the GPU (against the un-restarted basis)
-                         while the host solves the projected problem; 0 = off (default),
-                         k > 0 = fixed, -2 = adaptive.  Breaks the Krylov-Schur structure:
-                         residuals stall near 1e-4, so it is off unless asked for. */
+  int solver_flags;   /* 0 = defaults.  N2V2R_EIG_FULL_FIRST_PASS: orthogonalise every new
+                         block with two full block-Gram-Schmidt passes (instead of a local pass
+                         against the two previous blocks + one full pass);
+                         N2V2R_EIG_DENSE_RR: Rayleigh-Ritz on the dense projected matrix
+                         Q^T M Q (instead of the block-tridiagonal one) */
 } n2v2r_eig_opts;
 
 typedef struct {

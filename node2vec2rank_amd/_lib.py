@@ -51,7 +51,7 @@ class ArpackNoConvergence(RuntimeError):
 class EigOpts(ctypes.Structure):
     _fields_ = [("block", ctypes.c_int), ("max_basis", ctypes.c_int), ("keep", ctypes.c_int),
                 ("max_restarts", ctypes.c_int), ("tol", ctypes.c_double),
-                ("seed", ctypes.c_uint64), ("overlap", ctypes.c_int)]
+                ("seed", ctypes.c_uint64), ("solver_flags", ctypes.c_int)]
 
 
 class EigStats(ctypes.Structure):
@@ -318,9 +318,9 @@ class Engine:
 
     # -- UASE ------------------------------------------------------------------------------
     def uase(self, d: int, block=0, max_basis=0, keep=0, max_restarts=0, tol=0.0, seed=0,
-             overlap=0, raise_on_no_convergence=True):
+             solver_flags=0, raise_on_no_convergence=True):
         o = EigOpts(int(block), int(max_basis), int(keep), int(max_restarts), float(tol),
-                    int(seed) & 0xFFFFFFFFFFFFFFFF, int(overlap))
+                    int(seed) & 0xFFFFFFFFFFFFFFFF, int(solver_flags))
         s = EigStats()
         st = self.lib.n2v2r_uase(self.h, int(d), ctypes.byref(o), ctypes.byref(s))
         if st == ERR_NO_CONVERGENCE and not raise_on_no_convergence:

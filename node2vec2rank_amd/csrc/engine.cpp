@@ -527,6 +527,8 @@ struct Eig {
   int64_t launches = 0;
   double algo_bytes = 0;
   uint64_t fill_counter = 0;
+  int kry0 = 0;             // index of the first Krylov block of the current cycle
+  bool full_first = false;  // N2V2R_EIG_FULL_FIRST_PASS
 
   float* take() {
     if (freelist.empty()) {
@@ -657,24 +659,39 @@ struct Eig {
                                   seed ^ (0xABCDull + ++fill_counter), row0, st));
   }
 
-  // orthonormalise Zin (default: Z in place) against `basis` and within itself into Z: two
-  // fused passes (BCGS-PIP2), a third only when the second one had to refill a rank-deficient
-  // column.
-  void orthonormalize(float* Z, const std::vector<float*>& basis, const float* Zin = nullptr) {
+  // orthonormalise Zin (default: Z in place) against `basis` and within itself into Z.
+  // Default: a first fused pass against `local` only (the blocks W_from = M Q_last couples to in
+  // exact arithmetic: the block three-term recurrence), then one full pass (block CGS2 with a
+  // local first pass: the full pass removes the fp32 loss-of-orthogonality components); a third
+  // full pass only when the second one had to refill a rank-deficient column.  `local` empty or
+  // full_first: the first pass is a full one too (BCGS-PIP2).
+  void orthonormalize(float* Z, const std::vector<float*>& basis, const float* Zin = nullptr,
+                      const std::vector<float*>* local = nullptr) {
     const double t0 = now_ms();
     int* flg = h->ews.flg.as<int>();
     int* any = h->ews.anyflag.as<int>();
-    pip_pass(Z, basis, nullptr, flg, any, Zin);
+    const bool loc = local && !full_first && local->size() < basis.size();
+    pip_pass(Z, loc ? *local : basis, nullptr, flg, any, Zin);
     pip_pass(Z, basis, nullptr, flg + 64, any + 1);
     pip_pass(Z, basis, any + 1, flg + 128, any + 2);
     t_ortho += now_ms() - t0;
+  }
+
+  // blocks M Q[last] couples to: Q[last-1], Q[last]; for the first Krylov block of a cycle
+  // (kry0: the start block, or the block E appended at a thick restart) every block before it
+  // (the kept Ritz vectors X, whose residuals M X - X Theta lie in span(E))
+  std::vector<float*> local_of(const std::vector<float*>& basis) const {
+    const int last = (int)basis.size() - 1;
+    const int lo = last <= kry0 ? 0 : last - 1;
+    return std::vector<float*>(basis.begin() + lo, basis.end());
   }
 
   // z = orth(W_from) against `basis`, w = M z; appended to (qs, ws)
   void expand_one(const float* w_from, const std::vector<float*>& basis, std::vector<float*>& qs,
                   std::vector<float*>& ws) {
     float* z = take();
-    orthonormalize(z, basis, w_from);  // the first pass reads W_from and writes z: no copy
+    const std::vector<float*> loc = local_of(basis);
+    orthonormalize(z, basis, w_from, &loc);  // the first pass reads W_from, writes z: no copy
     float* w = take();
     apply_M(z, w);
     qs.push_back(z);
@@ -685,6 +702,8 @@ struct Eig {
           int ldu) {
     d = d_;
     seed = o.seed ? o.seed : 0x5EEDull;
+    full_first = (o.solver_flags & N2V2R_EIG_FULL_FIRST_PASS) != 0;
+    kry0 = 0;
     const double tol = o.tol > 0 ? o.tol : 1e-6;
     const int max_restarts = o.max_restarts > 0 ? o.max_restarts : 2000;
     // default panel width: 8 for CSR layers (vector-applications grow with b); 32 for dense
@@ -857,6 +876,7 @@ struct Eig {
       W.assign(MX.begin(), MX.end());
       Q.insert(Q.end(), E.begin(), E.end());
       W.insert(W.end(), EW.begin(), EW.end());
+      kry0 = pb;
     }
     // U = first d columns of X (row stride ldu); theta
     theta_out.assign(wh.begin(), wh.begin() + d);
