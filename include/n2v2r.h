@@ -168,6 +168,15 @@ int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, con
  * row-major fp32 eigenvectors (the Ritz coefficients UASE consumes). */
 int n2v2r_rr_top(n2v2r_handle* h, int c, const double* H, int p, double* w, float* S);
 
+/* Banded Rayleigh-Ritz stage alone (tests; block width 8, c <= 512, kp + 8 <= 192): the
+ * projected matrix of a Krylov-Schur cycle given as UASE keeps it.  Basis order [X (kp
+ * columns, diagonal theta_prev), E, Z_2, ...] in 8-wide blocks; hband holds band column
+ * j0 = kp/8 ([X E]^T M E, (kp+8) x 8 row-major) at offset 0, then for every later block j the
+ * 16 x 8 matrix [Q_{j-1} Q_j]^T M Q_j.  Entries outside the band (half-bandwidth 8) are taken
+ * as zero.  Same outputs as n2v2r_rr_top. */
+int n2v2r_rr_band_top(n2v2r_handle* h, int c, int kp, const double* hband, int64_t hband_len,
+                      const double* theta_prev, int p, double* w, float* S);
+
 #ifdef __cplusplus
 }
 #endif

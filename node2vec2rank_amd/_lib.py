@@ -38,7 +38,7 @@ EXPORTED = [
     "n2v2r_synchronize", "n2v2r_bench_spmm",
     "n2v2r_comm_unique_id", "n2v2r_create_rccl", "n2v2r_simgroup_create",
     "n2v2r_simgroup_destroy", "n2v2r_create_sim", "n2v2r_dist_info", "n2v2r_set_layer_csr_rows",
-    "n2v2r_rr_top", "n2v2r_set_layer_dense", "n2v2r_project",
+    "n2v2r_rr_top", "n2v2r_rr_band_top", "n2v2r_set_layer_dense", "n2v2r_project",
 ]
 UNIQUE_ID_BYTES = 128
 
@@ -118,6 +118,8 @@ def load(path: str | None = None):
                                       ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_double)]),
             "n2v2r_rr_top": (_i, [_vp, _i, _p(np.float64), _i, _p(np.float64), _p(np.float32)]),
+            "n2v2r_rr_band_top": (_i, [_vp, _i, _i, _p(np.float64), ctypes.c_int64, _vp, _i,
+                                       _p(np.float64), _p(np.float32)]),
             "n2v2r_set_layer_dense": (_i, [_vp, _i, _i64, _p(np.float32), _i]),
             "n2v2r_project": (_i, [_vp, _i64, _i64, _p(np.float32), _i, _p(np.float32)]),
             "n2v2r_comm_unique_id": (_i, [ctypes.c_char_p, ctypes.c_size_t]),
@@ -448,6 +450,20 @@ class Engine:
         w = np.empty(p, dtype=np.float64)
         S = np.empty((c, p), dtype=np.float32)
         self._check(self.lib.n2v2r_rr_top(self.h, c, H, int(p), w, S), "rr_top")
+        return w, S
+
+    def rr_band_top(self, hband, c: int, kp: int, theta_prev, p: int):
+        """Banded Rayleigh-Ritz stage alone (see n2v2r_rr_band_top).  Returns (w, S)."""
+        hband = np.ascontiguousarray(hband, dtype=np.float64).ravel()
+        tp = None
+        if kp > 0:
+            tp = np.ascontiguousarray(theta_prev, dtype=np.float64)
+        w = np.empty(p, dtype=np.float64)
+        S = np.empty((c, p), dtype=np.float32)
+        self._check(self.lib.n2v2r_rr_band_top(
+            self.h, int(c), int(kp), hband, int(hband.size),
+            None if tp is None else tp.ctypes.data_as(ctypes.c_void_p), int(p), w, S),
+            "rr_band_top")
         return w, S
 
     def synchronize(self):

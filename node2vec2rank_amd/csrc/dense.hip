@@ -568,14 +568,21 @@ __global__ __launch_bounds__(1024) void chol_inv_kernel(const double* __restrict
 // Cholesky P = R^T R and R^{-1} (xinv, fp64 b x b).  The apply pass builds
 // F = [-C R^{-1}; R^{-1}] in LDS and writes Z <- (Z - Q C) R^{-1} in ONE pass over [Q Z].
 // Rank-deficient columns (pivot below 1e-10 max diag) get a zero xinv column and a flag.
+// save (optional): rows [save_row0, save_row0 + save_rows) of G copied out (the banded
+// Rayleigh-Ritz keeps the local first-pass Gram Q_loc^T W_j as its band column j).
 __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict__ G, int c, int b,
                                                         double* __restrict__ xinv, int* flags,
-                                                        int* any_flag, const int* cond) {
+                                                        int* any_flag, const int* cond,
+                                                        double* __restrict__ save, int save_row0,
+                                                        int save_rows) {
   if (cond && *cond == 0) {
     if (threadIdx.x < b) flags[threadIdx.x] = 0;
     if (threadIdx.x == 0) *any_flag = 0;
     return;
   }
+  if (save)
+    for (int e = threadIdx.x; e < save_rows * b; e += blockDim.x)
+      save[e] = G[(int64_t)save_row0 * b + e];
   __shared__ double R[64][65];
   __shared__ double X[64][65];
   __shared__ double part[16][64];
@@ -668,10 +675,11 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
 
 extern "C" hipError_t n2v2r_launch_pip_chol(const double* G, int c, int b, double* xinv,
                                             int* flags, int* any_flag, const int* cond,
+                                            double* save, int save_row0, int save_rows,
                                             hipStream_t stream) {
   if (b > 64) return hipErrorInvalidValue;
   hipLaunchKernelGGL(pip_chol_kernel, dim3(1), dim3(1024), 0, stream, G, c, b, xinv, flags,
-                     any_flag, cond);
+                     any_flag, cond, save, save_row0, save_rows);
   return hipGetLastError();
 }
 

@@ -74,7 +74,13 @@ hipError_t n2v2r_launch_ts_nn(const BlockList& A, const float* G, int ldg, int c
                               int64_t n, const int* cond, const int* flags, uint64_t seed,
                               hipStream_t stream);
 hipError_t n2v2r_launch_pip_chol(const double* G, int c, int b, double* xinv, int* flags,
-                                 int* any_flag, const int* cond, hipStream_t stream);
+                                 int* any_flag, const int* cond, double* save, int save_row0,
+                                 int save_rows, hipStream_t stream);
+hipError_t n2v2r_launch_rr_band(const double* hband, int c, int kp, double* theta, double* AB,
+                                double* Varr, double* taua, double* d, double* e, double* refl,
+                                double* Y, float* S, int ldS, int p, int* err,
+                                hipStream_t stream);
+int n2v2r_rr_band_jm(int c);
 hipError_t n2v2r_launch_pip_apply(const BlockList& QZ, const double* G, const double* xinv,
                                   int c, int b, const OutBlockList& Z, int64_t n, const int* cond,
                                   const int* flags, uint64_t seed, int64_t row0,
@@ -334,6 +340,7 @@ struct EigWorkspace {
   DevBuf zg;                                  // K gathered stage-1 panels
   DevBuf rinv, flg, anyflag, gsmall, csmall;
   DevBuf tri, refl, ytri, tscr;               // GPU Rayleigh-Ritz: [d|e|tau], reflectors, Y_T
+  DevBuf hband, band, varr, taua, rrerr;      // banded RR: band columns, band matrix, arrow
 };
 }  // namespace
 
@@ -529,6 +536,7 @@ struct Eig {
   uint64_t fill_counter = 0;
   int kry0 = 0;             // index of the first Krylov block of the current cycle
   bool full_first = false;  // N2V2R_EIG_FULL_FIRST_PASS
+  bool band_rr = false;     // banded Rayleigh-Ritz (b = 8, c <= 512), else dense
 
   float* take() {
     if (freelist.empty()) {
@@ -643,7 +651,8 @@ struct Eig {
   // One fused BCGS + CholQR pass: G = [Q Z]^T Z -> R^{-1} -> Z <- [Q Z] [-C R^{-1}; R^{-1}],
   // refill deficient columns.  `cond` (device int, nullptr = always) skips the pass when zero.
   void pip_pass(float* Z, const std::vector<float*>& basis, const int* cond, int* flags_out,
-                int* any_out, const float* Zin = nullptr) {
+                int* any_out, const float* Zin = nullptr, double* save = nullptr,
+                int save_row0 = 0, int save_rows = 0) {
     // Zin (default Z): the block to orthogonalise; the result is written to Z
     const float* zin = Zin ? Zin : Z;
     const int nq = (int)basis.size();
@@ -652,7 +661,7 @@ struct Eig {
     const BlockList L = blocks(qz, 0, nq + 1);
     tn(L, one(zin), h->ews.gsmall.as<double>(), cond);
     HIPCHK(n2v2r_launch_pip_chol(h->ews.gsmall.as<double>(), nq * b, b, h->ews.rinv.as<double>(),
-                                 flags_out, any_out, cond, st));
+                                 flags_out, any_out, cond, save, save_row0, save_rows, st));
     // rank-deficient columns (flags_out) are refilled with random values by the same launch
     HIPCHK(n2v2r_launch_pip_apply(L, h->ews.gsmall.as<double>(), h->ews.rinv.as<double>(), nq * b,
                                   b, out_one(Z), n, cond, flags_out,
@@ -665,13 +674,18 @@ struct Eig {
   // local first pass: the full pass removes the fp32 loss-of-orthogonality components); a third
   // full pass only when the second one had to refill a rank-deficient column.  `local` empty or
   // full_first: the first pass is a full one too (BCGS-PIP2).
+  // save (band Rayleigh-Ritz): the first pass's Gram rows of the `local` blocks,
+  // Q_loc^T W_from, are kept as band column j of the projected matrix.
   void orthonormalize(float* Z, const std::vector<float*>& basis, const float* Zin = nullptr,
-                      const std::vector<float*>* local = nullptr) {
+                      const std::vector<float*>* local = nullptr, double* save = nullptr) {
     const double t0 = now_ms();
     int* flg = h->ews.flg.as<int>();
     int* any = h->ews.anyflag.as<int>();
     const bool loc = local && !full_first && local->size() < basis.size();
-    pip_pass(Z, loc ? *local : basis, nullptr, flg, any, Zin);
+    const std::vector<float*>& first = loc ? *local : basis;
+    const int nsave = (save && local) ? (int)local->size() : 0;
+    pip_pass(Z, first, nullptr, flg, any, Zin, nsave ? save : nullptr,
+             ((int)first.size() - nsave) * b, nsave * b);
     pip_pass(Z, basis, nullptr, flg + 64, any + 1);
     pip_pass(Z, basis, any + 1, flg + 128, any + 2);
     t_ortho += now_ms() - t0;
@@ -686,12 +700,23 @@ struct Eig {
     return std::vector<float*>(basis.begin() + lo, basis.end());
   }
 
-  // z = orth(W_from) against `basis`, w = M z; appended to (qs, ws)
+  // offset of band column j (the local Gram of W_j) in the band store: column kry0 holds
+  // [X E]^T W_E ((kry0 + 1) b x b), later ones [Q_{j-1} Q_j]^T W_j (2b x b)
+  size_t band_off(int j) const {
+    if (j == kry0) return 0;
+    return (size_t)(kry0 * b + b) * b + (size_t)(j - kry0 - 1) * 2 * b * b;
+  }
+
+  // z = orth(W_from) against `basis`, w = M z; appended to (qs, ws).  save_band: W_from is the
+  // image of the last basis block; keep its local Gram as a band column.
   void expand_one(const float* w_from, const std::vector<float*>& basis, std::vector<float*>& qs,
-                  std::vector<float*>& ws) {
+                  std::vector<float*>& ws, bool save_band = false) {
     float* z = take();
     const std::vector<float*> loc = local_of(basis);
-    orthonormalize(z, basis, w_from, &loc);  // the first pass reads W_from, writes z: no copy
+    double* save = (save_band && band_rr)
+                       ? h->ews.hband.as<double>() + band_off((int)basis.size() - 1)
+                       : nullptr;
+    orthonormalize(z, basis, w_from, &loc, save);  // first pass reads W_from, writes z: no copy
     float* w = take();
     apply_M(z, w);
     qs.push_back(z);
@@ -717,7 +742,13 @@ struct Eig {
     for (;; b /= 2) {
       keep = o.keep ? o.keep : std::max(d + 16, (d * 5) / 4);
       keep = ((keep + b - 1) / b) * b;
-      maxc = o.max_basis ? o.max_basis : std::max(keep + 3 * b, (16 * keep) / 5);
+      // default basis: 3.2 keep for the dense Rayleigh-Ritz (its cost grows as c^3); 4.8 keep
+      // (<= 512) for the banded one (b = 8), where fewer, longer cycles win (cfg2: 14 cycles
+      // at c = 256, 7 at c = 384, 13 % fewer block applications)
+      const bool band_ok = b == 8 && !(o.solver_flags & N2V2R_EIG_DENSE_RR);
+      maxc = o.max_basis ? o.max_basis
+                         : (band_ok ? std::min(512, std::max(keep + 3 * b, (24 * keep) / 5))
+                                    : std::max(keep + 3 * b, (16 * keep) / 5));
       maxc = ((maxc + b - 1) / b) * b;
       const int cap =
           (int)std::min<int64_t>((nglob / 2) / b * b, (int64_t)(N2V2R_MAX_BLOCKS - 1) * b);
@@ -751,7 +782,8 @@ struct Eig {
     h->ews.gsmall.ensure(sizeof(double) * (size_t)c_max * c_max);
     h->ews.csmall.ensure(sizeof(float) * (size_t)c_max * c_max);
     h->ews.tri.ensure(sizeof(double) * 3 * (size_t)c_max);
-    h->ews.refl.ensure(sizeof(double) * (size_t)c_max * c_max);
+    h->ews.refl.ensure(sizeof(double) * std::max<size_t>((size_t)c_max * c_max,
+                                                        (size_t)c_max * (c_max / 8 + 2) * 9));
     h->ews.ytri.ensure(sizeof(double) * (size_t)c_max * keep);
     h->ews.tscr.ensure(sizeof(double) * 6 * (size_t)((keep + 63) / 64 * 64) * c_max);
     h->ews.rinv.ensure(sizeof(double) * 64 * 64);
@@ -759,6 +791,15 @@ struct Eig {
     h->ews.anyflag.ensure(sizeof(int) * 4);
     h->theta.ensure(sizeof(double) * c_max);
     h->resid.ensure(sizeof(double) * c_max);
+    band_rr = b == 8 && !(o.solver_flags & N2V2R_EIG_DENSE_RR) && c_max <= 512 &&
+              keep + 8 <= 192;
+    if (band_rr) {
+      h->ews.hband.ensure(sizeof(double) * ((size_t)(keep + b) * b + (size_t)nb_max * 2 * b * b));
+      h->ews.band.ensure(sizeof(double) * (size_t)c_max * (b + 1));
+      h->ews.varr.ensure(sizeof(double) * (size_t)(keep + b) * (keep + b));
+      h->ews.taua.ensure(sizeof(double) * (size_t)(keep + b));
+      h->ews.rrerr.ensure(sizeof(int) * 4);
+    }
 
     std::vector<double> wh(keep);
     std::vector<double> res2(keep);
@@ -785,30 +826,51 @@ struct Eig {
     double t_rr = 0;
     for (;; ++cycle) {
       while ((int)Q.size() < nb_max) {
-        expand_one(W.back(), Q, Q, W);
+        expand_one(W.back(), Q, Q, W, /*save_band=*/true);
         ++apps;
       }
       const int nq = (int)Q.size();
       const int c = nq * b;
-      // Rayleigh-Ritz, all on the GPU: H = Q^T W (fp64, all-reduced) -> Householder
-      // tridiagonal -> bisection + inverse iteration on T for the top keep -> back-transform
-      // into the fp32 Ritz coefficients S (c x keep, ld keep); theta stays in HBM until the
-      // residual read-back below
-      tn(blocks(Q, 0, nq), blocks(W, 0, nq), h->ews.gsmall.as<double>(), nullptr);
-      double* trid = h->ews.tri.as<double>();
-      const double tr0 = now_ms();
-      HIPCHK(n2v2r_launch_rr_tridiag(h->ews.gsmall.as<double>(), c, trid, trid + c_max, trid + 2 * c_max,
-                                     h->ews.refl.as<double>(), st));
-      HIPCHK(n2v2r_launch_rr_tri_eig(trid, trid + c_max, c, keep, h->theta.as<double>(),
-                                     h->ews.ytri.as<double>(), h->ews.tscr.as<double>(), st));
-      HIPCHK(n2v2r_launch_rr_backtransform(h->ews.refl.as<double>(), trid + 2 * c_max, c,
-                                           h->ews.ytri.as<double>(), keep, h->ews.csmall.as<float>(), keep, st));
-      t_rr += now_ms() - tr0;
-      // Ritz vectors X = Q S, MX = W S (keep columns, pb blocks)
       for (int q = 0; q < pb; ++q) {
         X[q] = take();
         MX[q] = take();
       }
+      bool dense_rr = !band_rr;
+      int rr_err = 0;
+    rayleigh_ritz:
+      {
+      // Rayleigh-Ritz, all on the GPU, into the fp32 Ritz coefficients S (c x keep, ld keep)
+      // and theta (kept in HBM until the residual read-back below).
+      //   banded: the band columns saved by the expansions (+ the last block's, computed
+      //     here) -> arrow reduction + bulge chasing -> bisection -> band inverse iteration;
+      //   dense: H = Q^T W (fp64, all-reduced) -> Householder tridiagonal -> bisection +
+      //     inverse iteration on T -> compact-WY back-transform.
+      double* trid = h->ews.tri.as<double>();
+      const double tr0 = now_ms();
+      if (!dense_rr) {
+        const std::vector<float*> loc = local_of(Q);
+        tn(blocks(loc, 0, (int)loc.size()), one(W.back()),
+           h->ews.hband.as<double>() + band_off(nq - 1), nullptr);
+        HIPCHK(hipMemsetAsync(h->ews.rrerr.as<int>(), 0, sizeof(int), st));
+        HIPCHK(n2v2r_launch_rr_band(h->ews.hband.as<double>(), c, kry0 * b, h->theta.as<double>(),
+                                    h->ews.band.as<double>(), h->ews.varr.as<double>(),
+                                    h->ews.taua.as<double>(), trid, trid + c_max,
+                                    h->ews.refl.as<double>(), h->ews.ytri.as<double>(),
+                                    h->ews.csmall.as<float>(), keep, keep,
+                                    h->ews.rrerr.as<int>(), st));
+      } else {
+        tn(blocks(Q, 0, nq), blocks(W, 0, nq), h->ews.gsmall.as<double>(), nullptr);
+        HIPCHK(n2v2r_launch_rr_tridiag(h->ews.gsmall.as<double>(), c, trid, trid + c_max,
+                                       trid + 2 * c_max, h->ews.refl.as<double>(), st));
+        HIPCHK(n2v2r_launch_rr_tri_eig(trid, trid + c_max, c, keep, h->theta.as<double>(),
+                                       h->ews.ytri.as<double>(), h->ews.tscr.as<double>(), st));
+        HIPCHK(n2v2r_launch_rr_backtransform(h->ews.refl.as<double>(), trid + 2 * c_max, c,
+                                             h->ews.ytri.as<double>(), keep,
+                                             h->ews.csmall.as<float>(), keep, st));
+      }
+      t_rr += now_ms() - tr0;
+      }
+      // Ritz vectors X = Q S, MX = W S (keep columns, pb blocks)
       const double to0 = now_ms();
       const int per_launch = std::max(1, 128 / b);  // output blocks per ts_nn launch (<= 128 cols)
       for (int q0b = 0; q0b < pb; q0b += per_launch) {
@@ -835,8 +897,17 @@ struct Eig {
                             hipMemcpyDeviceToHost, st));
       HIPCHK(hipMemcpyAsync(wh.data(), h->theta.as<double>(), sizeof(double) * keep,
                             hipMemcpyDeviceToHost, st));
+      if (!dense_rr)
+        HIPCHK(hipMemcpyAsync(&rr_err, h->ews.rrerr.as<int>(), sizeof(int),
+                              hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
       t_ortho += now_ms() - to0;
+      if (rr_err && !dense_rr) {  // the bulge chase gave up (should not happen): dense RR
+        if (trace) fprintf(stderr, "[n2v2r] banded Rayleigh-Ritz failed, dense fallback\n");
+        dense_rr = true;
+        rr_err = 0;
+        goto rayleigh_ritz;
+      }
       maxres = 0;
       conv = 0;
       const double th1 = std::max(wh[0], 1e-300);
@@ -1630,6 +1701,46 @@ int n2v2r_rr_top(n2v2r_handle* h, int c, const double* H, int p, double* w, floa
                                          s.as<float>(), p, h->stream));
     HIPCHK(hipMemcpyAsync(S, s.p, sizeof(float) * c * p, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
+    return N2V2R_OK;
+  });
+}
+
+int n2v2r_rr_band_top(n2v2r_handle* h, int c, int kp, const double* hband, int64_t hband_len,
+                      const double* theta_prev, int p, double* w, float* S) {
+  return guarded(h, [&]() -> int {
+    const int b = 8;
+    if (c < 3 || c > 512 || c % b || kp % b || kp + b > 192 || kp >= c || p < 1 || p > c ||
+        !hband || !w || !S || (kp > 0 && !theta_prev))
+      return N2V2R_ERR_BAD_ARG;
+    const int64_t need = (int64_t)(kp + b) * b + (int64_t)(c / b - kp / b - 1) * 2 * b * b;
+    if (hband_len < need) return N2V2R_ERR_BAD_ARG;
+    DevBuf hb, th, ab, va, ta, tri, y, s, er, rf;
+    rf.ensure(sizeof(double) * c * n2v2r_rr_band_jm(c) * 9);
+    hb.ensure(sizeof(double) * hband_len);
+    th.ensure(sizeof(double) * c);
+    ab.ensure(sizeof(double) * c * (b + 1));
+    va.ensure(sizeof(double) * (kp + b) * (kp + b));
+    ta.ensure(sizeof(double) * (kp + b));
+    tri.ensure(sizeof(double) * 2 * c);
+    y.ensure(sizeof(double) * c * p);
+    s.ensure(sizeof(float) * c * p);
+    er.ensure(sizeof(int));
+    HIPCHK(hipMemcpyAsync(hb.p, hband, sizeof(double) * hband_len, hipMemcpyHostToDevice,
+                          h->stream));
+    if (kp > 0)
+      HIPCHK(hipMemcpyAsync(th.p, theta_prev, sizeof(double) * kp, hipMemcpyHostToDevice,
+                            h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));  // pageable sources: complete before the kernels
+    HIPCHK(n2v2r_launch_rr_band(hb.as<double>(), c, kp, th.as<double>(), ab.as<double>(),
+                                va.as<double>(), ta.as<double>(), tri.as<double>(),
+                                tri.as<double>() + c, rf.as<double>(), y.as<double>(),
+                                s.as<float>(), p, p, er.as<int>(), h->stream));
+    int e = 0;
+    HIPCHK(hipMemcpyAsync(&e, er.p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipMemcpyAsync(w, th.p, sizeof(double) * p, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipMemcpyAsync(S, s.p, sizeof(float) * c * p, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    if (e) throw StatusFail{N2V2R_ERR_NO_CONVERGENCE, "banded Rayleigh-Ritz: bulge chase aborted"};
     return N2V2R_OK;
   });
 }

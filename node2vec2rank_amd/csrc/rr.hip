@@ -625,6 +625,23 @@ extern "C" hipError_t n2v2r_launch_rr_tri_eig(const double* d, const double* e, 
   return hipGetLastError();
 }
 
+extern "C" hipError_t n2v2r_launch_rr_bisect(const double* d, const double* e, int c, int p,
+                                             double* w, hipStream_t stream) {
+  if (c < 3 || c > RR_MAXC || p < 1 || p > c) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rr_bisect_kernel, dim3((unsigned)p), dim3(RR_BIS_THREADS), 0, stream, d, e,
+                     c, p, w);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t n2v2r_launch_rr_tri_inviter(const double* d, const double* e, int c, int p,
+                                                  const double* w, double* Y,
+                                                  hipStream_t stream) {
+  if (c < 3 || c > RR_MAXC || p < 1 || p > c) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rr_inviter_kernel, dim3((unsigned)p), dim3(64), 0, stream, d, e, c, p, w,
+                     1e-9, Y);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t n2v2r_launch_rr_tridiag(double* A, int c, double* d, double* e, double* tau,
                                               double* V, hipStream_t stream) {
   if (c < 3 || c > RR_MAXC) return hipErrorInvalidValue;

@@ -1,0 +1,621 @@
+// Banded Rayleigh-Ritz for the block Krylov-Schur eigensolver (block width b = 8).
+//
+// In exact arithmetic the projected matrix of a Krylov-Schur cycle, in the basis order
+// [X (kept Ritz vectors, kp columns), E, Z_2, ..., Z_m] (b-wide blocks), is
+//   * block tridiagonal on the Krylov blocks: diagonal blocks Q_j^T M Q_j, sub-diagonal blocks
+//     R_j = Q_j^T M Q_{j-1} upper triangular (the Cholesky factors of the orthogonalisation);
+//   * diag(Theta) on X (the previous Ritz values), coupled only to E (M X = X Theta + E B).
+// Every entry it needs is a by-product of the expansion: the local first orthogonalisation
+// pass of block j computes [Q_{j-1} Q_j]^T W_j (or [X E]^T W_E), saved as "band column" j.
+// Off-band entries are rounding noise at the fp32 level of the basis and are dropped.
+//
+//   rr_arrow_kernel    [[Theta, B^T], [B, A_E]] -> half-bandwidth b by an offset-b Householder
+//                      reduction of its index reversal (E untouched), packed in LDS; the
+//                      reflectors are kept for the back-transform of the X rows.
+//   rr_chase_kernel    band (half-bandwidth 8) -> tridiagonal by bulge chasing, LDS-resident:
+//                      one wave per sweep (lane = one entry of an 8 x 8 window), sweep i+1
+//                      pipelined two steps behind sweep i through LDS progress counters.
+//   rr_bisect_kernel, rr_inviter_kernel (rr.hip)  top-p eigenpairs of the tridiagonal.
+//   rr_band_back       eigenvectors back through the chase (one sweep = a block-diagonal
+//                      product of 8 x 8 reflectors, applied in parallel) and the arrow
+//                      reflectors; fp32 Ritz coefficients S written.
+// Cost is O(c^2 b) + O(kp^3) instead of the O(c^3) dense tridiagonalisation.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "common.h"
+
+#define RB_W 8
+#define RB_MAXC 512
+#define RB_MAXNA 192
+#define RB_DONE_ALL 0x3fffffff
+
+namespace {
+
+__device__ __forceinline__ void house_params(double x0, double sig, double& tau, double& beta,
+                                             double& scale) {
+  if (sig == 0.0) {
+    tau = 0.0;
+    beta = x0;
+    scale = 0.0;
+    return;
+  }
+  const double nrm = sqrt(x0 * x0 + sig);
+  beta = (x0 >= 0.0) ? -nrm : nrm;
+  tau = (beta - x0) / beta;
+  scale = 1.0 / (x0 - beta);
+}
+
+template <int CTRL>
+__device__ __forceinline__ double rb_dpp(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// sum over the 8 lanes of a lane's row group (all 8 get it)
+__device__ __forceinline__ double rb_row_sum(double v) {
+  v += rb_dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += rb_dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += rb_dpp<0x141>(v);  // row_half_mirror
+  return v;
+}
+
+// sum over the wave: 16-lane rows by DPP, then the 4 rows by two lane exchanges
+__device__ __forceinline__ double rb_wave_sum(double v) {
+  v = rb_row_sum(v);
+  v += rb_dpp<0x140>(v);  // row_mirror: the two 8-lane halves of a row
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+// sum over the workgroup, fixed order; red must hold 16 doubles
+__device__ __forceinline__ double rb_block_sum(double v, double* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v = rb_wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  double s = 0.0;
+  const int nw = blockDim.x >> 6;
+  for (int w = 0; w < nw; ++w) s += red[w];
+  return s;
+}
+
+}  // namespace
+
+// ---- arrow -> band ----------------------------------------------------------------------
+// GE: (kp + 8) x 8 row-major = [X E]^T W_E (rows 0..kp-1: B^T, rows kp..: A_E).
+// R = J A J in packed lower storage; step k annihilates R[k+8+1.., k] with a reflector on the
+// trailing indices k+8.. (u = [0 x 7, v] over T = R[k+1.., k+1..]).  1024 threads, 4 per row of
+// T (row-wise loops over the packed rows).
+// Outputs: AB rows 0..na-1 (band of A' = J R J, AB[i][kd] = A'[i][i-kd]), reflectors
+// Varr[k][0..m) (v_0 = 1), taua[k].
+__global__ __launch_bounds__(1024) void rr_arrow_kernel(const double* __restrict__ theta, int kp,
+                                                       const double* __restrict__ GE,
+                                                       double* __restrict__ AB,
+                                                       double* __restrict__ Varr,
+                                                       double* __restrict__ taua) {
+  constexpr int W = RB_W;
+  extern __shared__ double lds[];
+  const int na = kp + W;
+  double* R = lds;                  // packed lower, row i at i (i + 1) / 2
+  double* u = R + na * (na + 1) / 2;
+  double* p = u + na;
+  __shared__ double red[16];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < na; i += blockDim.x) {
+    const int a = na - 1 - i;
+    double* row = R + i * (i + 1) / 2;
+    for (int j = 0; j <= i; ++j) {
+      const int bc = na - 1 - j;  // natural indices, a <= bc
+      double v;
+      if (bc < kp)
+        v = (a == bc) ? theta[a] : 0.0;
+      else if (a < kp)
+        v = GE[a * W + (bc - kp)];
+      else
+        v = 0.5 * (GE[a * W + (bc - kp)] + GE[bc * W + (a - kp)]);
+      row[j] = v;
+    }
+  }
+  __syncthreads();
+  for (int k = 0; k + W + 1 < na; ++k) {
+    const int m = na - k - W;  // reflector length (>= 2)
+    const int nT = na - k - 1;
+    const int o = k + 1;       // T[i][j] = R[o + i][o + j]
+    double part = 0.0;
+    for (int t = 1 + tid; t < m; t += blockDim.x) {
+      const int row = k + W + t;
+      const double x = R[row * (row + 1) / 2 + k];
+      part += x * x;
+    }
+    const double sig = rb_block_sum(part, red);
+    const double x0 = R[(k + W) * (k + W + 1) / 2 + k];
+    double tau, beta, scale;
+    house_params(x0, sig, tau, beta, scale);
+    for (int t = tid; t < nT; t += blockDim.x) {
+      double val = 0.0;
+      if (t == W - 1) {
+        val = 1.0;
+      } else if (t > W - 1) {
+        const int row = o + t;
+        val = R[row * (row + 1) / 2 + k] * scale;
+      }
+      u[t] = val;
+    }
+    __syncthreads();
+    for (int t = tid; t < m; t += blockDim.x) {
+      const int row = k + W + t;
+      Varr[(int64_t)k * na + t] = u[W - 1 + t];
+      R[row * (row + 1) / 2 + k] = (t == 0) ? beta : 0.0;
+    }
+    if (tid == 0) taua[k] = tau;
+    if (tau == 0.0) {
+      __syncthreads();
+      continue;
+    }
+    // p = tau T u over u's support j >= W-1: row part (j <= i) + column part (j > i),
+    // 4 threads per row (slice sl takes j = sl mod 4), incremental packed offsets
+    {
+      const int ri = tid >> 2, sl = tid & 3;
+      double a0 = 0.0, a1 = 0.0;
+      if (ri < nT) {
+        const int gi = o + ri;
+        const double* rowp = R + gi * (gi + 1) / 2 + o;
+        int j = W - 1 + sl;
+        for (; j + 4 <= ri; j += 8) {
+          a0 += rowp[j] * u[j];
+          a1 += rowp[j + 4] * u[j + 4];
+        }
+        for (; j <= ri; j += 4) a0 += rowp[j] * u[j];
+        const int j1 = (ri + 1 > W - 1) ? ri + 1 : W - 1;
+        j = j1 + ((sl - j1) & 3);
+        int gj = o + j;
+        int off = gj * (gj + 1) / 2 + gi;  // R[gj][gi]; R[gj + 4][gi] = off + 4 gj + 10
+        for (; j + 4 < nT; j += 8) {
+          a0 += R[off] * u[j];
+          a1 += R[off + 4 * gj + 10] * u[j + 4];
+          off += 8 * gj + 36;
+          gj += 8;
+        }
+        for (; j < nT; j += 4) {
+          a0 += R[off] * u[j];
+          off += 4 * gj + 10;
+          gj += 4;
+        }
+      }
+      double acc = a0 + a1;
+      acc += __shfl_xor(acc, 1, 64);
+      acc += __shfl_xor(acc, 2, 64);
+      if (ri < nT && sl == 0) p[ri] = tau * acc;
+    }
+    __syncthreads();
+    double pp = 0.0;
+    for (int t = tid; t < nT; t += blockDim.x) pp += p[t] * u[t];
+    const double K = 0.5 * tau * rb_block_sum(pp, red);
+    for (int t = tid; t < nT; t += blockDim.x) p[t] -= K * u[t];  // w
+    __syncthreads();
+    {
+      const int ri = tid >> 2, sl = tid & 3;
+      if (ri < nT) {
+        const int gi = o + ri;
+        double* rowp = R + gi * (gi + 1) / 2 + o;
+        const double ui = u[ri], wi = p[ri];
+        int j = sl;
+        for (; j + 4 <= ri; j += 8) {
+          const double r0 = rowp[j] - (ui * p[j] + wi * u[j]);
+          const double r1 = rowp[j + 4] - (ui * p[j + 4] + wi * u[j + 4]);
+          rowp[j] = r0;
+          rowp[j + 4] = r1;
+        }
+        for (; j <= ri; j += 4) rowp[j] -= ui * p[j] + wi * u[j];
+      }
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < na * (W + 1); e += blockDim.x) {
+    const int a = e / (W + 1), kd = e % (W + 1);
+    if (a - kd < 0) {
+      AB[e] = 0.0;
+      continue;
+    }
+    const int i = na - 1 - a + kd, j = na - 1 - a;  // i >= j
+    AB[e] = R[i * (i + 1) / 2 + j];
+  }
+}
+
+// ---- band -> tridiagonal ----------------------------------------------------------------
+// L (LDS): lower band + bulge, L[row * 17 + (row - col)], distance 0..15.
+// hband: band column j at offset 0 (j = kry0, (kp + 8) x 8 rows) or
+// (kp + 8) * 8 + (j - kry0 - 1) * 128 ([Q_{j-1} Q_j]^T W_j, 16 x 8).
+// AB (global, c x 9): rows < na were written by rr_arrow_kernel (kp > 0); the rest is
+// assembled here.
+// One wave per sweep, lane (r, q) = (lane / 8, lane % 8) holds entry (r, q) of the 8 x 8 window;
+// row sums over q use DPP (quad_perm + row_half_mirror), the other exchanges go through a
+// per-wave LDS scratch (gather of a column / transpose), so a chase step is ~4 LDS round trips.
+// Step j of sweep i is written to refl[(i * jm + j) * 9] (v[0..8), tau) for the back-transform.
+__device__ __forceinline__ bool rb_wait(int* done, int prev, int need, int* abort_flag) {
+  if (prev < 0) return true;
+  for (int it = 0;; ++it) {
+    const int v = __hip_atomic_load(&done[prev], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (v >= need) return true;
+    if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+    if (it > (1 << 22)) {
+      __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+__device__ __forceinline__ void rb_mark(int* done, int i, int v) {
+  __hip_atomic_store(&done[i], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+
+// compiler barrier for LDS exchanges inside one wave (LDS executes a wave's accesses in order)
+__device__ __forceinline__ void rb_cbar() { asm volatile("" ::: "memory"); }
+
+// One wave runs 8 consecutive sweeps in lockstep: lane (g, r) = (lane / 8, lane % 8) holds row r
+// of sweep g's current window (8 doubles of the off-diagonal block O and of the diagonal block
+// D in registers); at lockstep time T sweep g performs its step T - 2g, so sweep g+1 always runs
+// two steps behind sweep g (the dependency of the pipelined chase) and concurrently running
+// steps touch disjoint entries.  Column gathers / transposes go through a per-group LDS
+// scratch.  The first sweep of a group waits for the previous group (another wave) through
+// done[] (steps completed per sweep).  A step is: right-apply the previous reflector to O,
+// new reflector from O's first column, left-apply, two-sided update of D; step 0 is the same
+// with O = the column being annihilated.
+#define RB_CH_WAVES 4
+__global__ __launch_bounds__(RB_CH_WAVES * 64) void rr_chase_kernel(
+    const double* __restrict__ hband, int c, int kp, double* __restrict__ AB,
+    double* __restrict__ dd, double* __restrict__ ee, double* __restrict__ refl, int jm,
+    int* __restrict__ err) {
+  constexpr int W = RB_W, S = 2 * W + 1, GS = 80;
+  extern __shared__ double L[];
+  __shared__ int done[RB_MAXC];
+  __shared__ int abort_flag;
+  __shared__ double scratch[RB_CH_WAVES * 8 * GS];
+  const int tid = threadIdx.x;
+  const int na = kp > 0 ? kp + W : 0;
+  const int j0 = kp / W;
+  const int base1 = (kp + W) * W;
+  for (int e = tid; e < c * S; e += blockDim.x) L[e] = 0.0;
+  for (int e = tid; e < c; e += blockDim.x) done[e] = 0;
+  if (tid == 0) abort_flag = 0;
+  __syncthreads();
+  for (int e = tid; e < c * (W + 1); e += blockDim.x) {
+    const int i = e / (W + 1), kd = e % (W + 1);
+    const int col = i - kd;
+    double v = 0.0;
+    if (col >= 0) {
+      if (i < na) {
+        v = AB[e];
+      } else {
+        const int j = i / W, r = i % W;
+        const int nloc = (j == j0) ? (kp + W) : 2 * W;
+        const double* G = hband + (j == j0 ? 0 : base1 + (j - j0 - 1) * 2 * W * W);
+        if (col >= j * W) {
+          const int cc = col - j * W;
+          v = 0.5 * (G[(nloc - W + r) * W + cc] + G[(nloc - W + cc) * W + r]);
+        } else {
+          const int cc = col - (j - 1) * W;  // r <= cc: R_j upper triangular
+          v = G[cc * W + r];
+        }
+        AB[e] = v;
+      }
+    } else if (i >= na) {
+      AB[e] = 0.0;
+    }
+    L[i * S + kd] = v;
+  }
+  __syncthreads();
+  const int wave = tid >> 6, lane = tid & 63;
+  const int nwaves = blockDim.x >> 6;
+  const int g = lane >> 3, r = lane & 7;
+  double* gs = scratch + (wave * 8 + g) * GS;  // [0,64) transpose, [64,72) gather, [72,80) u
+  const int nsw = c - 2;                       // sweeps 0 .. c-3
+  bool aborted = false;
+  for (int G = wave; G * 8 < nsw && !aborted; G += nwaves) {
+    const int i = G * 8 + g;
+    bool fin = !(i < nsw);
+    int s = i + 1, m = (c - 1 - i) < W ? (c - 1 - i) : W;  // rows of the previous reflector
+    if (!fin && m < 2) fin = true;
+    if (fin && i < c && r == 0) done[i] = RB_DONE_ALL;
+    double vp[W];
+#pragma unroll
+    for (int t = 0; t < W; ++t) vp[t] = 0.0;
+    double taup = 0.0;
+    for (int T = 0;; ++T) {
+      if (__ballot(!fin) == 0) break;
+      const int j = T - 2 * g;
+      bool act = !fin && j >= 0;
+      int R0 = 0, MR = 0, C0 = 0, NC = 0;
+      if (act) {
+        if (j == 0) {
+          R0 = i + 1;
+          MR = m;
+          C0 = i;
+          NC = 1;
+        } else {
+          R0 = s + m;
+          C0 = s;
+          NC = m;
+          if (R0 >= c) {
+            fin = true;
+            act = false;
+            if (r == 0) __hip_atomic_store(&done[i], RB_DONE_ALL, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+          } else {
+            MR = (c - R0) < W ? (c - R0) : W;
+          }
+        }
+      }
+      // the group's first sweep waits for the previous group's last sweep (another wave)
+      if (act && g == 0 && i > 0) {
+        for (int it = 0;; ++it) {
+          const int v = __hip_atomic_load(&done[i - 1], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (v >= j + 2) break;
+          if (__hip_atomic_load(&abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ||
+              it > (1 << 22)) {
+            __hip_atomic_store(&abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            aborted = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      if (__ballot(aborted) != 0) {
+        aborted = true;
+        break;
+      }
+      rb_cbar();
+      if (act) {
+        const bool rv = r < MR;
+        const int d0 = R0 - C0 + r;
+        double O[W], D[W];
+#pragma unroll
+        for (int t = 0; t < W; ++t) {
+          O[t] = (rv && t < NC) ? L[(R0 + r) * S + (d0 - t)] : 0.0;
+          const int hi = r > t ? r : t, lo = r > t ? t : r;
+          D[t] = (rv && t < MR) ? L[(R0 + hi) * S + (hi - lo)] : 0.0;
+        }
+        // right-apply the previous reflector (acts on O's columns)
+        double tt = 0.0;
+#pragma unroll
+        for (int t = 0; t < W; ++t) tt += O[t] * vp[t];
+        tt *= taup;
+#pragma unroll
+        for (int t = 0; t < W; ++t) O[t] -= tt * vp[t];
+        // reflector from O's first column
+        gs[64 + r] = rv ? O[0] : 0.0;
+        rb_cbar();
+        double x[W];
+#pragma unroll
+        for (int t = 0; t < W; ++t) x[t] = gs[64 + t];
+        double sig = 0.0;
+#pragma unroll
+        for (int t = 1; t < W; ++t) sig += x[t] * x[t];
+        double tau2, beta2, scale2;
+        house_params(x[0], sig, tau2, beta2, scale2);
+        double v2[W];
+#pragma unroll
+        for (int t = 0; t < W; ++t) v2[t] = (t == 0) ? 1.0 : x[t] * scale2;
+        const double v2r = (r == 0) ? 1.0 : (rv ? O[0] * scale2 : 0.0);
+        // left-apply: u_q = sum_r v2_r O[r][q] through an LDS transpose
+#pragma unroll
+        for (int t = 0; t < W; ++t) gs[r * 8 + t] = v2r * O[t];
+        rb_cbar();
+        double um = 0.0;
+#pragma unroll
+        for (int t = 0; t < W; ++t) um += gs[t * 8 + r];
+        gs[72 + r] = um;
+        rb_cbar();
+#pragma unroll
+        for (int t = 0; t < W; ++t) O[t] -= tau2 * v2r * gs[72 + t];
+        O[0] = (r == 0) ? beta2 : 0.0;
+#pragma unroll
+        for (int t = 0; t < W; ++t)
+          if (rv && t < NC) L[(R0 + r) * S + (d0 - t)] = O[t];
+        // two-sided update of D
+        double pr = 0.0;
+#pragma unroll
+        for (int t = 0; t < W; ++t) pr += D[t] * v2[t];
+        pr *= tau2;
+        rb_cbar();
+        gs[64 + r] = pr;
+        rb_cbar();
+        double ks = 0.0, ps[W];
+#pragma unroll
+        for (int t = 0; t < W; ++t) {
+          ps[t] = gs[64 + t];
+          ks += ps[t] * v2[t];
+        }
+        const double K = 0.5 * tau2 * ks;
+        const double wr = pr - K * v2r;
+#pragma unroll
+        for (int t = 0; t < W; ++t) {
+          D[t] -= v2r * (ps[t] - K * v2[t]) + wr * v2[t];
+          if (rv && t < MR && t <= r) L[(R0 + r) * S + (r - t)] = D[t];
+        }
+        // record the reflector for the back-transform
+        double* slot = refl + ((int64_t)i * jm + j) * 9;
+        slot[r] = v2r;
+        if (r == 0) slot[8] = tau2;
+#pragma unroll
+        for (int t = 0; t < W; ++t) vp[t] = v2[t];
+        taup = tau2;
+        s = R0;
+        m = MR;
+        rb_cbar();
+        if (r == 0)
+          __hip_atomic_store(&done[i], j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      rb_cbar();
+    }
+    if (!aborted && !fin) fin = true;
+    if (!aborted && r == 0 && i < nsw)
+      __hip_atomic_store(&done[i], RB_DONE_ALL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  __syncthreads();
+  if (abort_flag) {
+    if (tid == 0) *err = 1;
+    return;
+  }
+  for (int i = tid; i < c; i += blockDim.x) {
+    dd[i] = L[i * S];
+    if (i < c - 1) ee[i] = L[(i + 1) * S + 1];
+  }
+}
+
+// ---- back-transform ---------------------------------------------------------------------
+// Eigenvectors z of the tridiagonal (Y, column-major c x p) -> eigenvectors of the projected
+// matrix: y = B_0 B_1 ... B_{c-3} z (sweep i's reflectors act on disjoint consecutive windows
+// i+1+8j.., so B_i is block diagonal: lane j applies window j), then the X rows through the
+// arrow reflectors; written as fp32 S (c x p, ld ldS).  One wave per eigenvector; y is kept
+// residue-major in LDS (entry t at (t % 8) * sb + t / 8, sb odd), so the 8 entries of a window
+// are read by all lanes without bank conflicts; the reflectors of RB_BT_CH sweeps are staged
+// through LDS at a time.
+#define RB_BT_CH 16
+__global__ __launch_bounds__(64) void rr_band_back_kernel(const double* __restrict__ Y, int c,
+                                                          int p, const double* __restrict__ refl,
+                                                          int jm, int kp,
+                                                          const double* __restrict__ Varr,
+                                                          const double* __restrict__ taua,
+                                                          float* __restrict__ S, int ldS) {
+  constexpr int W = RB_W;
+  extern __shared__ double lds[];
+  const int sb = (c / W) | 1;
+  double* y = lds;                              // [8][sb]
+  double* rf = y + (size_t)W * sb;              // [RB_BT_CH][jm * 9]
+  const int lane = threadIdx.x;
+  const int vec = blockIdx.x;
+  for (int t = lane; t < c; t += 64) y[(t & 7) * sb + (t >> 3)] = Y[(int64_t)vec * c + t];
+  const int nsw = c - 2;  // sweeps 0 .. c-3
+  for (int ch = ((nsw - 1) / RB_BT_CH) * RB_BT_CH; ch >= 0; ch -= RB_BT_CH) {
+    const int nch = (nsw - ch) < RB_BT_CH ? (nsw - ch) : RB_BT_CH;
+    __syncthreads();
+    {  // stage the chunk's reflectors: 16-B loads, 8 in flight per lane
+      const int n2 = (nch * jm * 9) / 2;
+      const double2* src = reinterpret_cast<const double2*>(refl + (int64_t)ch * jm * 9);
+      double2* dst = reinterpret_cast<double2*>(rf);
+      int e = lane;
+      for (; e + 7 * 64 < n2; e += 8 * 64) {
+        double2 t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = src[e + u * 64];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) dst[e + u * 64] = t[u];
+      }
+      for (; e < n2; e += 64) dst[e] = src[e];
+      if (lane == 0 && (nch * jm * 9) % 2) rf[nch * jm * 9 - 1] = refl[(int64_t)(ch + nch) * jm * 9 - 1];
+    }
+    __syncthreads();
+    for (int ii = nch - 1; ii >= 0; --ii) {
+      const int i = ch + ii;
+      if (c - 1 - i < 2) continue;
+      const int nsteps = (c - (i + 1) + W - 1) / W;
+      for (int j = lane; j < nsteps; j += 64) {
+        const int s = i + 1 + j * W;
+        const int m = (c - s) < W ? (c - s) : W;
+        const double* rv = rf + ((int64_t)ii * jm + j) * 9;
+        const double tau = rv[8];
+        double yv[W], vv[W];
+        double dot = 0.0;
+#pragma unroll
+        for (int t = 0; t < W; ++t) {
+          const int idx = s + t;
+          vv[t] = (t < m) ? rv[t] : 0.0;
+          yv[t] = (t < m) ? y[(idx & 7) * sb + (idx >> 3)] : 0.0;
+          dot += vv[t] * yv[t];
+        }
+        dot *= tau;
+#pragma unroll
+        for (int t = 0; t < W; ++t) {
+          const int idx = s + t;
+          if (t < m) y[(idx & 7) * sb + (idx >> 3)] = yv[t] - dot * vv[t];
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // X rows: y[0..na) <- J Q J y[0..na)
+  if (kp > 0) {
+    const int na = kp + W, nref = na - W - 1;
+    for (int k = nref - 1; k >= 0; --k) {
+      const double tau = taua[k];
+      if (tau == 0.0) continue;
+      const int m = na - k - W;
+      const double* vk = Varr + (int64_t)k * na;
+      double dot = 0.0;
+      for (int t = lane; t < m; t += 64) {
+        const int idx = na - 1 - k - W - t;
+        dot += vk[t] * y[(idx & 7) * sb + (idx >> 3)];
+      }
+      dot = wave_sum_f64(dot);
+      for (int t = lane; t < m; t += 64) {
+        const int idx = na - 1 - k - W - t;
+        y[(idx & 7) * sb + (idx >> 3)] -= tau * dot * vk[t];
+      }
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  for (int t = lane; t < c; t += 64)
+    S[(int64_t)t * ldS + vec] = (float)y[(t & 7) * sb + (t >> 3)];
+}
+
+extern "C" hipError_t n2v2r_launch_rr_bisect(const double* d, const double* e, int c, int p,
+                                             double* w, hipStream_t stream);
+extern "C" hipError_t n2v2r_launch_rr_tri_inviter(const double* d, const double* e, int c, int p,
+                                                  const double* w, double* Y,
+                                                  hipStream_t stream);
+
+// reflector slots per sweep of the bulge chase
+extern "C" int n2v2r_rr_band_jm(int c) { return c / RB_W + 2; }
+
+// Banded Rayleigh-Ritz: top-p Ritz pairs from the saved band columns.  theta: in = previous
+// Ritz values (kp of them, the diagonal of the X block), out = p new ones (descending).
+// refl: c * jm * 9 doubles (jm = n2v2r_rr_band_jm(c)).
+extern "C" hipError_t n2v2r_launch_rr_band(const double* hband, int c, int kp, double* theta,
+                                           double* AB, double* Varr, double* taua, double* d,
+                                           double* e, double* refl, double* Y, float* S, int ldS,
+                                           int p, int* err, hipStream_t stream) {
+  if (c < 3 || c > RB_MAXC || c % RB_W || kp % RB_W || kp + RB_W > RB_MAXNA || p < 1 || p > c)
+    return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)rr_arrow_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 2048);
+    (void)hipFuncSetAttribute((const void*)rr_chase_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 46 * 1024);
+    (void)hipFuncSetAttribute((const void*)rr_band_back_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 2048);
+    attr = true;
+  }
+  const int jm = n2v2r_rr_band_jm(c);
+  if (kp > 0) {
+    const int na = kp + RB_W;
+    const size_t lds = sizeof(double) * ((size_t)na * (na + 1) / 2 + 2 * (size_t)na);
+    hipLaunchKernelGGL(rr_arrow_kernel, dim3(1), dim3(1024), lds, stream, theta, kp, hband, AB,
+                       Varr, taua);
+    hipError_t er = hipGetLastError();
+    if (er != hipSuccess) return er;
+  }
+  const size_t lch = sizeof(double) * (size_t)c * (2 * RB_W + 1);
+  hipLaunchKernelGGL(rr_chase_kernel, dim3(1), dim3(RB_CH_WAVES * 64), lch, stream, hband, c, kp,
+                     AB, d, e, refl, jm, err);
+  hipError_t er = hipGetLastError();
+  if (er != hipSuccess) return er;
+  er = n2v2r_launch_rr_bisect(d, e, c, p, theta, stream);
+  if (er != hipSuccess) return er;
+  er = n2v2r_launch_rr_tri_inviter(d, e, c, p, theta, Y, stream);
+  if (er != hipSuccess) return er;
+  const size_t lbt = sizeof(double) * ((size_t)RB_W * ((c / RB_W) | 1) + (size_t)RB_BT_CH * jm * 9);
+  hipLaunchKernelGGL(rr_band_back_kernel, dim3((unsigned)p), dim3(64), lbt, stream, Y, c, p, refl,
+                     jm, kp, Varr, taua, S, ldS);
+  return hipGetLastError();
+}

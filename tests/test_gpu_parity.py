@@ -298,3 +298,60 @@ def test_rayleigh_ritz_stage(engine, c, p):
     assert np.abs(S.T @ S - np.eye(p)).max() < 5e-6
     Hs = 0.5 * (H + H.T)
     assert np.abs(Hs @ S - S * w).max() < 5e-6 * ref[0]
+
+
+def _band_problem(c, kp, seed, cluster=False, decoupled=0):
+    """A projected matrix with the Krylov-Schur structure (see n2v2r_rr_band_top) and its
+    band columns as UASE saves them."""
+    b = 8
+    rng = np.random.default_rng(seed)
+    nb, j0 = c // b, kp // b
+    H = np.zeros((c, c))
+    theta = None
+    cols = []
+    if kp:
+        theta = np.sort(rng.random(kp))[::-1] * 50.0 + 10.0
+        if cluster:
+            theta[5:12] = theta[5] - 1e-9 * np.arange(7)  # a tight cluster of kept Ritz values
+            theta[20] = theta[21]
+        H[:kp, :kp] = np.diag(theta)
+    for j in range(j0, nb):
+        o = j * b
+        D = rng.standard_normal((b, b)) * 3.0
+        D = D + D.T
+        H[o:o + b, o:o + b] = D
+        Dn = D + 1e-13 * rng.standard_normal((b, b))  # Q^T W is not exactly symmetric
+        if j == j0:
+            if kp:
+                BT = rng.standard_normal((kp, b))
+                if decoupled:
+                    BT[:decoupled] *= 1e-9  # converged Ritz vectors: tiny residual couplings
+                H[:kp, o:o + b] = BT
+                H[o:o + b, :kp] = BT.T
+                cols.append(np.vstack([BT, Dn]))
+            else:
+                cols.append(Dn)
+        else:
+            R = np.triu(rng.standard_normal((b, b)))
+            H[o:o + b, o - b:o] = R
+            H[o - b:o, o:o + b] = R.T
+            cols.append(np.vstack([R.T, Dn]))
+    hband = np.concatenate([m.ravel() for m in cols])
+    return H, hband, theta
+
+
+@pytest.mark.parametrize("c,kp,p,cluster,decoupled", [
+    (40, 0, 12, False, 0), (256, 0, 80, False, 0), (256, 80, 80, False, 0),
+    (256, 80, 80, True, 30), (384, 160, 160, False, 0), (512, 184, 184, True, 100),
+    (96, 80, 80, False, 0)])
+def test_rayleigh_ritz_band_stage(engine, c, kp, p, cluster, decoupled):
+    """Banded Rayleigh-Ritz (arrow reduction, bulge chasing, bisection, band inverse
+    iteration, arrow back-transform) vs numpy eigh of the same structured matrix."""
+    H, hband, theta = _band_problem(c, kp, seed=c + kp, cluster=cluster, decoupled=decoupled)
+    w, S = engine.rr_band_top(hband, c, kp, theta, p)
+    ref = np.sort(np.linalg.eigvalsh(H))[::-1][:p]
+    scale = np.abs(ref).max()
+    np.testing.assert_allclose(w, ref, rtol=0, atol=1e-10 * scale)
+    S = S.astype(np.float64)
+    assert np.abs(S.T @ S - np.eye(p)).max() < 5e-6
+    assert np.abs(H @ S - S * w).max() < 5e-6 * scale
