@@ -169,7 +169,9 @@ __global__ __launch_bounds__(256) void ts_tn_narrow_kernel(BlockList A, const fl
     for (int j = 0; j < (FLUSH ? JB : 1); ++j) dacc[i][j] = 0.0;
   int64_t r = r0;
   int64_t next_flush = r0 + TN_FLUSH;
-  for (; r + 4 <= r1; r += 4) {
+  // 8 rows per step: 8 independent 16-B loads per lane in flight (the chunk grid is only
+  // ~1.5 waves per SIMD at N = 100k, so the loads in flight per wave set the bandwidth)
+  for (; r + 8 <= r1; r += 8) {
     if (FLUSH && r >= next_flush) {  // bounded fp32 partial sums, fp64 totals
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -180,12 +182,12 @@ __global__ __launch_bounds__(256) void ts_tn_narrow_kernel(BlockList A, const fl
         }
       next_flush += TN_FLUSH;
     }
-    f32x4 a[4];
+    f32x4 a[8];
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 8; ++t)
       a[t] = colok ? *reinterpret_cast<const f32x4*>(ab + (r + t) * lda) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < 8; ++t) {
       const float* zr = Bz + (r + t) * JB;
 #pragma unroll
       for (int j = 0; j < JB; ++j) {
@@ -401,7 +403,29 @@ __global__ __launch_bounds__(256) void ts_nn_rows_kernel(BlockList A, Coef F, in
 #pragma unroll
   for (int j = 0; j < CB; ++j) acc[j] = 0.f;
   const int w = A.width;
-  for (int q = 0; q < A.count; ++q) {
+  int q = 0;
+  if (w == CB) {  // Krylov blocks: 4 blocks (4 x CB/4 16-B loads) in flight per step
+    constexpr int NL = CB / 4;
+    for (; q + 4 <= A.count; q += 4) {
+      f32x4 a4[4][NL];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int l = 0; l < NL; ++l)
+          a4[u][l] = *reinterpret_cast<const f32x4*>(A.blk[q + u] + row * (int64_t)CB + 4 * l);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int l = 0; l < NL; ++l) {
+          const float* g = gs + ((q + u) * CB + 4 * l) * CB;
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int j = 0; j < CB; ++j) acc[j] += a4[u][l][m] * g[m * CB + j];
+        }
+    }
+  }
+  for (; q < A.count; ++q) {
     const float* ap = A.blk[q] + row * (int64_t)w;
     for (int kk = 0; kk < w; kk += 4) {
       const f32x4 a4 = *reinterpret_cast<const f32x4*>(ap + kk);
@@ -460,13 +484,14 @@ extern "C" hipError_t n2v2r_launch_ts_nn(const BlockList& A, const float* G, int
   return launch_nn(A, F, cb, O, C, alpha, beta, n, cond, flags, seed, 0, stream);
 }
 
-// Z <- [Q Z] [-C R^{-1}; R^{-1}] (fused BCGS + CholQR apply), C = G[0:c], R^{-1} = xinv.
-extern "C" hipError_t n2v2r_launch_pip_apply(const BlockList& QZ, const double* G,
-                                             const double* xinv, int c, int b,
+// Z <- [Q Z] F, F = [-C R^{-1}; R^{-1}] (fp32 (c + b) x b, formed by pip_chol): the fused
+// BCGS + CholQR apply.
+extern "C" hipError_t n2v2r_launch_pip_apply(const BlockList& QZ, const float* Fm, int c, int b,
                                              const OutBlockList& Z, int64_t n, const int* cond,
                                              const int* flags, uint64_t seed, int64_t row0,
                                              hipStream_t stream) {
-  const Coef F{nullptr, 0, G, xinv, c};
+  (void)c;
+  const Coef F{Fm, b, nullptr, nullptr, 0};
   BlockList none{};
   return launch_nn(QZ, F, b, Z, none, 1.f, 0.f, n, cond, flags, seed, row0, stream);
 }
@@ -570,11 +595,13 @@ __global__ __launch_bounds__(1024) void chol_inv_kernel(const double* __restrict
 // Rank-deficient columns (pivot below 1e-10 max diag) get a zero xinv column and a flag.
 // save (optional): rows [save_row0, save_row0 + save_rows) of G copied out (the banded
 // Rayleigh-Ritz keeps the local first-pass Gram Q_loc^T W_j as its band column j).
+// fout (optional): F = [-C R^{-1}; R^{-1}] as fp32 ((c + b) x b, flagged columns zero), the
+// coefficient matrix of the apply pass, formed here once instead of in every apply workgroup.
 __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict__ G, int c, int b,
                                                         double* __restrict__ xinv, int* flags,
                                                         int* any_flag, const int* cond,
                                                         double* __restrict__ save, int save_row0,
-                                                        int save_rows) {
+                                                        int save_rows, float* __restrict__ fout) {
   if (cond && *cond == 0) {
     if (threadIdx.x < b) flags[threadIdx.x] = 0;
     if (threadIdx.x == 0) *any_flag = 0;
@@ -616,12 +643,12 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
     }
   }
   for (int e = tid; e < bb; e += nt) X[e / b][e % b] = (e / b == e % b) ? 1.0 : 0.0;
+  if (tid < 64) bad[tid] = 0;
   __syncthreads();
-  if (tid >= 64) return;  // O(b^3), b <= 64: one wave from here on
+  // O(b^3), b <= 64: wave 0 works, the other waves only keep the barriers
+  const bool w0 = tid < 64;
   const int nw = 64;
-  bad[tid] = 0;
-  __syncthreads();
-  {
+  if (w0) {
     double m = (tid < b) ? R[tid][tid] : 0.0;
     for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
     if (tid == 0) dmax = m;
@@ -639,47 +666,73 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
       }
     }
     __syncthreads();
-    const double pj = piv[j];
-    const int isbad = bad[j];
-    for (int cc = j + tid; cc < b; cc += nw)
-      R[j][cc] = isbad ? (cc == j ? 1.0 : 0.0) : (cc == j ? pj : R[j][cc] / pj);
+    if (w0) {
+      const double pj = piv[j];
+      const int isbad = bad[j];
+      for (int cc = j + tid; cc < b; cc += nw)
+        R[j][cc] = isbad ? (cc == j ? 1.0 : 0.0) : (cc == j ? pj : R[j][cc] / pj);
+    }
     __syncthreads();
-    const int m = b - j - 1;
-    for (int e = tid; e < m * m; e += nw) {
-      const int r = j + 1 + e / m, cc = j + 1 + e % m;
-      if (cc >= r) R[r][cc] -= R[j][r] * R[j][cc];
+    if (w0) {
+      const int m = b - j - 1;
+      for (int e = tid; e < m * m; e += nw) {
+        const int r = j + 1 + e / m, cc = j + 1 + e % m;
+        if (cc >= r) R[r][cc] -= R[j][r] * R[j][cc];
+      }
     }
     __syncthreads();
   }
   for (int j = b - 1; j >= 0; --j) {
-    const double inv = 1.0 / R[j][j];
-    for (int cc = tid; cc < b; cc += nw) X[j][cc] *= inv;
-    __syncthreads();
-    for (int e = tid; e < j * b; e += nw) {
-      const int r = e / b, cc = e % b;
-      X[r][cc] -= R[r][j] * X[j][cc];
+    if (w0) {
+      const double inv = 1.0 / R[j][j];
+      for (int cc = tid; cc < b; cc += nw) X[j][cc] *= inv;
     }
     __syncthreads();
+    if (w0)
+      for (int e = tid; e < j * b; e += nw) {
+        const int r = e / b, cc = e % b;
+        X[r][cc] -= R[r][j] * X[j][cc];
+      }
+    __syncthreads();
   }
-  for (int e = tid; e < bb; e += nw) {
-    const int r = e / b, cc = e % b;
-    xinv[e] = bad[cc] ? 0.0 : X[r][cc];
+  if (w0) {
+    for (int e = tid; e < bb; e += nw) {
+      const int r = e / b, cc = e % b;
+      xinv[e] = bad[cc] ? 0.0 : X[r][cc];
+    }
+    if (tid < b) flags[tid] = bad[tid];
+    if (tid == 0) {
+      int any = 0;
+      for (int j = 0; j < b; ++j) any |= bad[j];
+      *any_flag = any;
+    }
   }
-  if (tid < b) flags[tid] = bad[tid];
-  if (tid == 0) {
-    int any = 0;
-    for (int j = 0; j < b; ++j) any |= bad[j];
-    *any_flag = any;
+  if (fout) {  // every thread: F[k][j] = -sum_{m <= j} C[k][m] X[m][j]; F[c + i][j] = X[i][j]
+    for (int e = tid; e < (c + b) * b; e += nt) {
+      const int k = e / b, j = e % b;
+      float v = 0.f;
+      if (!bad[j]) {
+        if (k >= c) {
+          v = (float)X[k - c][j];
+        } else {
+          const double* crow = G + (int64_t)k * b;
+          double sacc = 0.0;
+          for (int m = 0; m <= j; ++m) sacc -= crow[m] * X[m][j];
+          v = (float)sacc;
+        }
+      }
+      fout[e] = v;
+    }
   }
 }
 
 extern "C" hipError_t n2v2r_launch_pip_chol(const double* G, int c, int b, double* xinv,
                                             int* flags, int* any_flag, const int* cond,
                                             double* save, int save_row0, int save_rows,
-                                            hipStream_t stream) {
+                                            float* fout, hipStream_t stream) {
   if (b > 64) return hipErrorInvalidValue;
   hipLaunchKernelGGL(pip_chol_kernel, dim3(1), dim3(1024), 0, stream, G, c, b, xinv, flags,
-                     any_flag, cond, save, save_row0, save_rows);
+                     any_flag, cond, save, save_row0, save_rows, fout);
   return hipGetLastError();
 }
 

@@ -75,14 +75,14 @@ hipError_t n2v2r_launch_ts_nn(const BlockList& A, const float* G, int ldg, int c
                               hipStream_t stream);
 hipError_t n2v2r_launch_pip_chol(const double* G, int c, int b, double* xinv, int* flags,
                                  int* any_flag, const int* cond, double* save, int save_row0,
-                                 int save_rows, hipStream_t stream);
+                                 int save_rows, float* fout, hipStream_t stream);
 hipError_t n2v2r_launch_rr_band(const double* hband, int c, int kp, double* theta, double* AB,
                                 double* Varr, double* taua, double* d, double* e, double* refl,
                                 double* Y, float* S, int ldS, int p, int* err,
                                 hipStream_t stream);
 int n2v2r_rr_band_jm(int c);
-hipError_t n2v2r_launch_pip_apply(const BlockList& QZ, const double* G, const double* xinv,
-                                  int c, int b, const OutBlockList& Z, int64_t n, const int* cond,
+hipError_t n2v2r_launch_pip_apply(const BlockList& QZ, const float* F, int c, int b,
+                                  const OutBlockList& Z, int64_t n, const int* cond,
                                   const int* flags, uint64_t seed, int64_t row0,
                                   hipStream_t stream);
 hipError_t n2v2r_launch_fill_normal(float* blk, int w, int64_t n, uint64_t seed, const int* flags,
@@ -341,6 +341,7 @@ struct EigWorkspace {
   DevBuf rinv, flg, anyflag, gsmall, csmall;
   DevBuf tri, refl, ytri, tscr;               // GPU Rayleigh-Ritz: [d|e|tau], reflectors, Y_T
   DevBuf hband, band, varr, taua, rrerr;      // banded RR: band columns, band matrix, arrow
+  DevBuf fcoef;                               // fp32 [-C R^-1; R^-1] of the apply pass
 };
 }  // namespace
 
@@ -661,11 +662,11 @@ struct Eig {
     const BlockList L = blocks(qz, 0, nq + 1);
     tn(L, one(zin), h->ews.gsmall.as<double>(), cond);
     HIPCHK(n2v2r_launch_pip_chol(h->ews.gsmall.as<double>(), nq * b, b, h->ews.rinv.as<double>(),
-                                 flags_out, any_out, cond, save, save_row0, save_rows, st));
+                                 flags_out, any_out, cond, save, save_row0, save_rows,
+                                 h->ews.fcoef.as<float>(), st));
     // rank-deficient columns (flags_out) are refilled with random values by the same launch
-    HIPCHK(n2v2r_launch_pip_apply(L, h->ews.gsmall.as<double>(), h->ews.rinv.as<double>(), nq * b,
-                                  b, out_one(Z), n, cond, flags_out,
-                                  seed ^ (0xABCDull + ++fill_counter), row0, st));
+    HIPCHK(n2v2r_launch_pip_apply(L, h->ews.fcoef.as<float>(), nq * b, b, out_one(Z), n, cond,
+                                  flags_out, seed ^ (0xABCDull + ++fill_counter), row0, st));
   }
 
   // orthonormalise Zin (default: Z in place) against `basis` and within itself into Z.
@@ -787,6 +788,7 @@ struct Eig {
     h->ews.ytri.ensure(sizeof(double) * (size_t)c_max * keep);
     h->ews.tscr.ensure(sizeof(double) * 6 * (size_t)((keep + 63) / 64 * 64) * c_max);
     h->ews.rinv.ensure(sizeof(double) * 64 * 64);
+    h->ews.fcoef.ensure(sizeof(float) * (size_t)(c_max + 64) * 64);
     h->ews.flg.ensure(sizeof(int) * 256);
     h->ews.anyflag.ensure(sizeof(int) * 4);
     h->theta.ensure(sizeof(double) * c_max);
