@@ -123,8 +123,17 @@ __global__ __launch_bounds__(256) void reduce_chunks_kernel(const double* __rest
   const int lane = threadIdx.x & 63;
   const int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (e >= elems) return;
-  double s = 0.0;
-  for (int c = lane; c < nchunks; c += 64) s += partial[(int64_t)c * elems + e];
+  // 4 independent loads in flight per lane (fixed summation order: deterministic)
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  int c = lane;
+  for (; c + 192 < nchunks; c += 256) {
+    s0 += partial[(int64_t)c * elems + e];
+    s1 += partial[(int64_t)(c + 64) * elems + e];
+    s2 += partial[(int64_t)(c + 128) * elems + e];
+    s3 += partial[(int64_t)(c + 192) * elems + e];
+  }
+  for (; c < nchunks; c += 64) s0 += partial[(int64_t)c * elems + e];
+  double s = (s0 + s1) + (s2 + s3);
   s = wave_sum_f64(s);
   if (lane == 0) out[e] = s;
 }
@@ -227,10 +236,127 @@ __global__ __launch_bounds__(256) void ts_tn_narrow_kernel(BlockList A, const fl
   }
 }
 
+// Gram step for 8-wide basis blocks and an 8-wide right-hand side (G = [Q Z]^T Z at b = 8):
+// every wave-instruction reads whole 128-B lines.  A wave owns 8 blocks; lane =
+// (block: 3 bits, column half h: 1 bit, row offset ro: 2 bits), so for one load the 4 lanes of
+// a (block, h) pair read rows r..r+3 of that block = one 128-B line, and each lane also loads
+// its row of Z (4 distinct 32-B rows per instruction, shared by all blocks).  4 row-quads per
+// step (16 rows, 12 x 16-B loads per lane in flight); fp32 sums flushed to fp64 every 1024
+// rows; the 4 row offsets are folded by DPP at the end and each chunk writes its fp64 partial
+// [ca][8] (no LDS, no cross-wave fold).
+__global__ __launch_bounds__(256) void ts_tn_lines_kernel(BlockList A, const float* __restrict__ Bz,
+                                                          int64_t n, int64_t rows_per_chunk,
+                                                          double* __restrict__ partial,
+                                                          const int* cond) {
+  if (cond && *cond == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int blk = ((int)blockIdx.y * 4 + wave) * 8 + (lane >> 3);
+  const int h = (lane >> 2) & 1, ro = lane & 3;
+  const bool bok = blk < A.count;
+  if (__ballot(bok) == 0) return;  // a wave past the last block
+  const float* ab = (bok ? A.blk[blk] : A.blk[0]) + 4 * h;
+  const int64_t c0 = (int64_t)blockIdx.x * rows_per_chunk;
+  int64_t c1 = c0 + rows_per_chunk;
+  if (c1 > n) c1 = n;
+  float acc[4][8];
+  double dacc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      acc[i][j] = 0.f;
+      dacc[i][j] = 0.0;
+    }
+  int64_t r = c0;
+  int since = 0;
+  for (; r + 16 <= c1; r += 16) {
+    f32x4 a[4], z0[4], z1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t rr = r + 4 * u + ro;
+      a[u] = bok ? *reinterpret_cast<const f32x4*>(ab + rr * 8) : f32x4{0.f, 0.f, 0.f, 0.f};
+      z0[u] = *reinterpret_cast<const f32x4*>(Bz + rr * 8);
+      z1[u] = *reinterpret_cast<const f32x4*>(Bz + rr * 8 + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[i][j] += a[u][i] * z0[u][j];
+          acc[i][4 + j] += a[u][i] * z1[u][j];
+        }
+      }
+    if (++since == 64) {  // 1024 rows: bounded fp32 partial sums
+      since = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          dacc[i][j] += (double)acc[i][j];
+          acc[i][j] = 0.f;
+        }
+    }
+  }
+  for (; r < c1; r += 4) {
+    const int64_t rr = r + ro;
+    if (rr < c1) {
+      const f32x4 a1 = bok ? *reinterpret_cast<const f32x4*>(ab + rr * 8) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 y0 = *reinterpret_cast<const f32x4*>(Bz + rr * 8);
+      const f32x4 y1 = *reinterpret_cast<const f32x4*>(Bz + rr * 8 + 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[i][j] += a1[i] * y0[j];
+          acc[i][4 + j] += a1[i] * y1[j];
+        }
+    }
+  }
+  double* out = partial + (int64_t)blockIdx.x * ((int64_t)A.count * 8) * 8;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      double v = dacc[i][j] + (double)acc[i][j];
+      // fold the 4 row offsets (lane bits 0, 1) in fixed order: quad_perm xor 1, xor 2
+      const int lo1 = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0xB1, 0xF, 0xF, false);
+      const int hi1 = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0xB1, 0xF, 0xF, false);
+      v += __hiloint2double(hi1, lo1);
+      const int lo2 = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x4E, 0xF, 0xF, false);
+      const int hi2 = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x4E, 0xF, 0xF, false);
+      v += __hiloint2double(hi2, lo2);
+      if (bok && ro == 0) out[(int64_t)(blk * 8 + 4 * h + i) * 8 + j] = v;
+    }
+}
+
 extern "C" hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n,
                                          double* partial, size_t partial_elems, double* out,
                                          const int* cond, hipStream_t stream) {
   const int ca = A.count * A.width, cb = B.count * B.width;
+  if (B.count == 1 && B.width == 8 && A.width == 8) {
+    // line form: ~2048 waves, >= 64 rows per chunk, partials within the buffer
+    const int64_t elems = (int64_t)ca * cb;
+    const int groups = (A.count + 7) / 8;
+    int64_t nchunks = 2048 / groups;
+    if (nchunks < 1) nchunks = 1;
+    if (nchunks > (n + 63) / 64) nchunks = (n + 63) / 64;
+    if ((size_t)(nchunks * elems) > partial_elems) nchunks = (int64_t)(partial_elems / elems);
+    if (nchunks < 1) return hipErrorInvalidValue;
+    int64_t rows_per_chunk = (n + nchunks - 1) / nchunks;
+    rows_per_chunk = (rows_per_chunk + 15) & ~(int64_t)15;
+    nchunks = (n + rows_per_chunk - 1) / rows_per_chunk;
+    const dim3 grid((unsigned)nchunks, (unsigned)((groups + 3) / 4));
+    hipLaunchKernelGGL(ts_tn_lines_kernel, grid, dim3(256), 0, stream, A, B.blk[0], n,
+                       rows_per_chunk, partial, cond);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((elems + 3) / 4)), dim3(256), 0,
+                       stream, partial, (int)nchunks, elems, out, cond);
+    return hipGetLastError();
+  }
   if (B.count == 1 && (B.width == 8 || B.width == 16) && A.width % 4 == 0) {
     // narrow form: ~1024 workgroups of >= 256 rows, partials within the buffer
     const int64_t elems = (int64_t)ca * cb;
@@ -601,7 +727,8 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
                                                         double* __restrict__ xinv, int* flags,
                                                         int* any_flag, const int* cond,
                                                         double* __restrict__ save, int save_row0,
-                                                        int save_rows, float* __restrict__ fout) {
+                                                        int save_rows, float* __restrict__ fout,
+                                                        int stage, int* sticky) {
   if (cond && *cond == 0) {
     if (threadIdx.x < b) flags[threadIdx.x] = 0;
     if (threadIdx.x == 0) *any_flag = 0;
@@ -610,6 +737,19 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
   if (save)
     for (int e = threadIdx.x; e < save_rows * b; e += blockDim.x)
       save[e] = G[(int64_t)save_row0 * b + e];
+  // G staged through LDS when it fits (b = 8: (c + 8) x 8 doubles <= 50 KB): the P and F loops
+  // below then read LDS instead of issuing dependent L2 loads
+  extern __shared__ double gstage[];
+  const double* Gs = G;
+  if (stage) {
+    const int n2 = ((c + b) * b) / 2;
+    const double2* src = reinterpret_cast<const double2*>(G);
+    double2* dst = reinterpret_cast<double2*>(gstage);
+    for (int e = threadIdx.x; e < n2; e += blockDim.x) dst[e] = src[e];
+    if (threadIdx.x == 0 && ((c + b) * b) % 2) gstage[(c + b) * b - 1] = G[(c + b) * b - 1];
+    __syncthreads();
+    Gs = gstage;
+  }
   __shared__ double R[64][65];
   __shared__ double X[64][65];
   __shared__ double part[16][64];
@@ -624,21 +764,21 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
     double acc = 0.0;
     if (e < bb) {
       const int i = e / b, j = e % b;
-      for (int k = slice; k < c; k += 16) acc += G[(int64_t)k * b + i] * G[(int64_t)k * b + j];
+      for (int k = slice; k < c; k += 16) acc += Gs[(int64_t)k * b + i] * Gs[(int64_t)k * b + j];
     }
     part[slice][e] = acc;
     __syncthreads();
     if (tid < bb) {
       const int i = tid / b, j = tid % b;
-      double s = 0.5 * (G[(int64_t)(c + i) * b + j] + G[(int64_t)(c + j) * b + i]);
+      double s = 0.5 * (Gs[(int64_t)(c + i) * b + j] + Gs[(int64_t)(c + j) * b + i]);
       for (int sl = 0; sl < 16; ++sl) s -= part[sl][tid];
       R[i][j] = s;
     }
   } else {
     for (int e = tid; e < bb; e += nt) {
       const int i = e / b, j = e % b;
-      double s = 0.5 * (G[(int64_t)(c + i) * b + j] + G[(int64_t)(c + j) * b + i]);
-      for (int k = 0; k < c; ++k) s -= G[(int64_t)k * b + i] * G[(int64_t)k * b + j];
+      double s = 0.5 * (Gs[(int64_t)(c + i) * b + j] + Gs[(int64_t)(c + j) * b + i]);
+      for (int k = 0; k < c; ++k) s -= Gs[(int64_t)k * b + i] * Gs[(int64_t)k * b + j];
       R[i][j] = s;
     }
   }
@@ -705,6 +845,7 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
       int any = 0;
       for (int j = 0; j < b; ++j) any |= bad[j];
       *any_flag = any;
+      if (any && sticky) *sticky = 1;
     }
   }
   if (fout) {  // every thread: F[k][j] = -sum_{m <= j} C[k][m] X[m][j]; F[c + i][j] = X[i][j]
@@ -715,7 +856,7 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
         if (k >= c) {
           v = (float)X[k - c][j];
         } else {
-          const double* crow = G + (int64_t)k * b;
+          const double* crow = Gs + (int64_t)k * b;
           double sacc = 0.0;
           for (int m = 0; m <= j; ++m) sacc -= crow[m] * X[m][j];
           v = (float)sacc;
@@ -729,10 +870,12 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
 extern "C" hipError_t n2v2r_launch_pip_chol(const double* G, int c, int b, double* xinv,
                                             int* flags, int* any_flag, const int* cond,
                                             double* save, int save_row0, int save_rows,
-                                            float* fout, hipStream_t stream) {
+                                            float* fout, int* sticky, hipStream_t stream) {
   if (b > 64) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pip_chol_kernel, dim3(1), dim3(1024), 0, stream, G, c, b, xinv, flags,
-                     any_flag, cond, save, save_row0, save_rows, fout);
+  const size_t gbytes = sizeof(double) * (size_t)(c + b) * b;
+  const int stage = gbytes <= 56 * 1024 ? 1 : 0;
+  hipLaunchKernelGGL(pip_chol_kernel, dim3(1), dim3(1024), stage ? gbytes : 0, stream, G, c, b,
+                     xinv, flags, any_flag, cond, save, save_row0, save_rows, fout, stage, sticky);
   return hipGetLastError();
 }
 

@@ -75,7 +75,7 @@ hipError_t n2v2r_launch_ts_nn(const BlockList& A, const float* G, int ldg, int c
                               hipStream_t stream);
 hipError_t n2v2r_launch_pip_chol(const double* G, int c, int b, double* xinv, int* flags,
                                  int* any_flag, const int* cond, double* save, int save_row0,
-                                 int save_rows, float* fout, hipStream_t stream);
+                                 int save_rows, float* fout, int* sticky, hipStream_t stream);
 hipError_t n2v2r_launch_rr_band(const double* hband, int c, int kp, double* theta, double* AB,
                                 double* Varr, double* taua, double* d, double* e, double* refl,
                                 double* Y, float* S, int ldS, int p, int* err,
@@ -653,7 +653,7 @@ struct Eig {
   // refill deficient columns.  `cond` (device int, nullptr = always) skips the pass when zero.
   void pip_pass(float* Z, const std::vector<float*>& basis, const int* cond, int* flags_out,
                 int* any_out, const float* Zin = nullptr, double* save = nullptr,
-                int save_row0 = 0, int save_rows = 0) {
+                int save_row0 = 0, int save_rows = 0, int* sticky = nullptr) {
     // Zin (default Z): the block to orthogonalise; the result is written to Z
     const float* zin = Zin ? Zin : Z;
     const int nq = (int)basis.size();
@@ -663,7 +663,7 @@ struct Eig {
     tn(L, one(zin), h->ews.gsmall.as<double>(), cond);
     HIPCHK(n2v2r_launch_pip_chol(h->ews.gsmall.as<double>(), nq * b, b, h->ews.rinv.as<double>(),
                                  flags_out, any_out, cond, save, save_row0, save_rows,
-                                 h->ews.fcoef.as<float>(), st));
+                                 h->ews.fcoef.as<float>(), sticky, st));
     // rank-deficient columns (flags_out) are refilled with random values by the same launch
     HIPCHK(n2v2r_launch_pip_apply(L, h->ews.fcoef.as<float>(), nq * b, b, out_one(Z), n, cond,
                                   flags_out, seed ^ (0xABCDull + ++fill_counter), row0, st));
@@ -677,8 +677,12 @@ struct Eig {
   // full_first: the first pass is a full one too (BCGS-PIP2).
   // save (band Rayleigh-Ritz): the first pass's Gram rows of the `local` blocks,
   // Q_loc^T W_from, are kept as band column j of the projected matrix.
+  // lazy: no third pass; a refill in the second pass sets the cycle's sticky flag instead and
+  // the cycle is expanded again with the third pass (rank deficiency after a local + full pass
+  // is rare: it saves four launches per block).
   void orthonormalize(float* Z, const std::vector<float*>& basis, const float* Zin = nullptr,
-                      const std::vector<float*>* local = nullptr, double* save = nullptr) {
+                      const std::vector<float*>* local = nullptr, double* save = nullptr,
+                      bool lazy = false) {
     const double t0 = now_ms();
     int* flg = h->ews.flg.as<int>();
     int* any = h->ews.anyflag.as<int>();
@@ -687,8 +691,9 @@ struct Eig {
     const int nsave = (save && local) ? (int)local->size() : 0;
     pip_pass(Z, first, nullptr, flg, any, Zin, nsave ? save : nullptr,
              ((int)first.size() - nsave) * b, nsave * b);
-    pip_pass(Z, basis, nullptr, flg + 64, any + 1);
-    pip_pass(Z, basis, any + 1, flg + 128, any + 2);
+    pip_pass(Z, basis, nullptr, flg + 64, any + 1, nullptr, nullptr, 0, 0,
+             lazy ? any + 3 : nullptr);
+    if (!lazy) pip_pass(Z, basis, any + 1, flg + 128, any + 2);
     t_ortho += now_ms() - t0;
   }
 
@@ -711,13 +716,13 @@ struct Eig {
   // z = orth(W_from) against `basis`, w = M z; appended to (qs, ws).  save_band: W_from is the
   // image of the last basis block; keep its local Gram as a band column.
   void expand_one(const float* w_from, const std::vector<float*>& basis, std::vector<float*>& qs,
-                  std::vector<float*>& ws, bool save_band = false) {
+                  std::vector<float*>& ws, bool save_band = false, bool lazy = false) {
     float* z = take();
     const std::vector<float*> loc = local_of(basis);
     double* save = (save_band && band_rr)
                        ? h->ews.hband.as<double>() + band_off((int)basis.size() - 1)
                        : nullptr;
-    orthonormalize(z, basis, w_from, &loc, save);  // first pass reads W_from, writes z: no copy
+    orthonormalize(z, basis, w_from, &loc, save, lazy);  // reads W_from, writes z: no copy
     float* w = take();
     apply_M(z, w);
     qs.push_back(z);
@@ -730,6 +735,8 @@ struct Eig {
     seed = o.seed ? o.seed : 0x5EEDull;
     full_first = (o.solver_flags & N2V2R_EIG_FULL_FIRST_PASS) != 0;
     kry0 = 0;
+    bool lazy = true;
+    const bool test_redo = (o.solver_flags & N2V2R_EIG_TEST_REDO_CYCLE) != 0;
     const double tol = o.tol > 0 ? o.tol : 1e-6;
     const int max_restarts = o.max_restarts > 0 ? o.max_restarts : 2000;
     // default panel width: 8 for CSR layers (vector-applications grow with b); 32 for dense
@@ -827,8 +834,10 @@ struct Eig {
     }();
     double t_rr = 0;
     for (;; ++cycle) {
+      const int q_start = (int)Q.size();
+      if (lazy) HIPCHK(hipMemsetAsync(h->ews.anyflag.as<int>() + 3, 0, sizeof(int), st));
       while ((int)Q.size() < nb_max) {
-        expand_one(W.back(), Q, Q, W, /*save_band=*/true);
+        expand_one(W.back(), Q, Q, W, /*save_band=*/true, lazy);
         ++apps;
       }
       const int nq = (int)Q.size();
@@ -902,6 +911,10 @@ struct Eig {
       if (!dense_rr)
         HIPCHK(hipMemcpyAsync(&rr_err, h->ews.rrerr.as<int>(), sizeof(int),
                               hipMemcpyDeviceToHost, st));
+      int refilled = 0;
+      if (lazy)
+        HIPCHK(hipMemcpyAsync(&refilled, h->ews.anyflag.as<int>() + 3, sizeof(int),
+                              hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
       t_ortho += now_ms() - to0;
       if (rr_err && !dense_rr) {  // the bulge chase gave up (should not happen): dense RR
@@ -909,6 +922,24 @@ struct Eig {
         dense_rr = true;
         rr_err = 0;
         goto rayleigh_ritz;
+      }
+      if (test_redo && cycle == 0 && lazy) refilled = 1;  // tests: exercise the recovery
+      if (refilled) {  // a second pass refilled a column: expand this cycle again, 3 passes
+        if (trace) fprintf(stderr, "[n2v2r] rank-deficient block, cycle %d expanded again\n", cycle);
+        for (int q = 0; q < pb; ++q) {
+          give(X[q]);
+          give(MX[q]);
+        }
+        for (int q = q_start; q < nq; ++q) {
+          give(Q[q]);
+          give(W[q]);
+        }
+        apps -= nq - q_start;
+        Q.resize(q_start);
+        W.resize(q_start);
+        lazy = false;
+        --cycle;
+        continue;
       }
       maxres = 0;
       conv = 0;

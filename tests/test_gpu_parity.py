@@ -355,3 +355,50 @@ def test_rayleigh_ritz_band_stage(engine, c, kp, p, cluster, decoupled):
     S = S.astype(np.float64)
     assert np.abs(S.T @ S - np.eye(p)).max() < 5e-6
     assert np.abs(H @ S - S * w).max() < 5e-6 * scale
+
+
+def test_uase_rank_deficient_krylov(engine):
+    """Disjoint cliques: M has two distinct eigenvalues per component size, so the block Krylov
+    space breaks down after a few blocks and the orthogonalisation has to refill rank-deficient
+    columns (random restarts inside the basis).  Singular values must still match scipy and U
+    must be orthonormal with small residuals."""
+    import scipy.sparse.linalg as sla
+    rng = np.random.default_rng(5)
+    sizes = [5] * 60 + [7] * 40 + [9] * 20 + [3] * 100  # 1,060 nodes, 4 clique sizes
+    layers = []
+    for k in range(2):
+        perm = rng.permutation(sum(sizes))
+        blocks = []
+        off = 0
+        for sz in sizes:
+            blocks.append(np.full((sz, sz), 1.0) - np.eye(sz))
+            off += sz
+        A = sp.block_diag(blocks).tocsr().astype(np.float32)
+        A = A[perm][:, perm]  # hide the block structure from the row order
+        layers.append(sp.csr_matrix(A))
+    d = 12
+    engine.set_layers(layers)
+    st = engine.uase(d, seed=3, raise_on_no_convergence=False)
+    s = engine.singular_values()
+    M = sum((A @ A.T).astype(np.float64) for A in layers)
+    ev = np.sort(sla.eigsh(M, k=d + 4, which="LA")[0])[::-1][:d]
+    np.testing.assert_allclose(s, np.sqrt(ev), rtol=1e-4)
+    X = engine.left_embedding().astype(np.float64) / np.sqrt(s)[None, :]  # U sqrt(sigma) -> U
+    assert np.abs(X.T @ X - np.eye(d)).max() < 1e-4
+    R = M @ X - X * (s ** 2)[None, :]
+    assert np.linalg.norm(R, axis=0).max() <= 1e-4 * s[0] ** 2, st
+
+
+def test_uase_cycle_redo_path(engine):
+    """The recovery after a rank-deficient second pass (the cycle expanded again with three
+    passes) gives the same Ritz values as the normal path."""
+    fx = load_fixture("er_cfg1")
+    layers = fixture_layers(fx)
+    engine.set_layers(layers)
+    d = int(fx["dims"].max())
+    engine.uase(d, seed=7)
+    s0 = engine.singular_values()
+    st = engine.uase(d, seed=7, solver_flags=4)
+    np.testing.assert_allclose(engine.singular_values(), s0, rtol=1e-5)
+    np.testing.assert_allclose(engine.singular_values(), fx["sigma"], rtol=2e-5)
+    assert st["converged"] == d
