@@ -22,6 +22,7 @@ struct CsrDev {
   const float* data;
   int64_t n_rows;
   int64_t nnz;
+  int unit;  // every stored value is 1.0f (unweighted graph): the SpMM skips the value stream
 };
 
 // Up to this many basis blocks are addressed through a by-value pointer table.

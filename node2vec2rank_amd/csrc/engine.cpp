@@ -199,6 +199,7 @@ struct LayerDev {
   DevBuf t_indptr, t_indices, t_data;  // local rows of A^T when A is not symmetric
   int64_t nnz = 0, t_nnz = 0;
   int64_t n_rows = 0;                  // local rows
+  bool unit = false, t_unit = false;   // all stored values 1.0f
   bool symmetric = true;
   bool loaded = false;
   // dense layer (cfg3): local rows of A and (directed) of A^T, fp32, leading dimension lda
@@ -208,12 +209,13 @@ struct LayerDev {
   const float* dense_a() const { return dA.as<float>(); }
   const float* dense_at() const { return symmetric ? dA.as<float>() : dAT.as<float>(); }
   CsrDev csr() const {
-    return CsrDev{indptr.as<int64_t>(), indices.as<int32_t>(), data.as<float>(), n_rows, nnz};
+    return CsrDev{indptr.as<int64_t>(), indices.as<int32_t>(), data.as<float>(), n_rows, nnz,
+                  unit ? 1 : 0};
   }
   CsrDev csr_t() const {
     if (symmetric) return csr();
     return CsrDev{t_indptr.as<int64_t>(), t_indices.as<int32_t>(), t_data.as<float>(), n_rows,
-                  t_nnz};
+                  t_nnz, t_unit ? 1 : 0};
   }
 };
 
@@ -497,11 +499,14 @@ bool host_is_symmetric(int64_t n, const int64_t* ip, const int32_t* ix, const fl
   return true;
 }
 
-// upload rows [r0, r0 + nr) of a CSR (global column indices kept) into (ip, ix, dv) buffers
-void upload_rows(hipStream_t st, int64_t r0, int64_t nr, const int64_t* ip, const int32_t* ix,
+// upload rows [r0, r0 + nr) of a CSR (global column indices kept) into (ip, ix, dv) buffers;
+// returns whether every uploaded value is 1.0f (an unweighted graph: the SpMM skips values)
+bool upload_rows(hipStream_t st, int64_t r0, int64_t nr, const int64_t* ip, const int32_t* ix,
                  const float* dv, DevBuf& dip, DevBuf& dix, DevBuf& ddv, int64_t& nnz_out) {
   const int64_t p0 = ip[r0], p1 = ip[r0 + nr];
   nnz_out = p1 - p0;
+  bool unit = true;
+  for (int64_t p = p0; p < p1 && unit; ++p) unit = dv[p] == 1.0f;
   std::vector<int64_t> lip(nr + 1);
   for (int64_t r = 0; r <= nr; ++r) lip[r] = ip[r0 + r] - p0;
   dip.ensure(sizeof(int64_t) * (nr + 1));
@@ -513,6 +518,17 @@ void upload_rows(hipStream_t st, int64_t r0, int64_t nr, const int64_t* ip, cons
     HIPCHK(hipMemcpyAsync(ddv.p, dv + p0, sizeof(float) * nnz_out, hipMemcpyHostToDevice, st));
   }
   HIPCHK(hipStreamSynchronize(st));  // lip dies here
+  return unit;
+}
+
+// Algorithmic HBM bytes of one CSR x panel SpMM over `rows` rows (for this
+// storage format): column indices 4 B/nnz, values 4 B/nnz unless the layer is unweighted (the
+// kernel then skips them), int64 row pointers, the N x b panel read once and the rows x b
+// output written once.  The gathered panel rows (4 b B per nnz, served by L2 / Infinity Cache)
+// are not counted.
+double spmm_algo_bytes(int64_t nnz, bool unit, int64_t rows, int64_t panel_rows, int b) {
+  return (unit ? 4.0 : 8.0) * (double)nnz + 8.0 * (double)(rows + 1) +
+         4.0 * (double)(panel_rows + rows) * b;
 }
 
 // ---- the eigensolver ----------------------------------------------------------------------
@@ -642,8 +658,10 @@ struct Eig {
     s.Y[0] = Wout;
     HIPCHK(n2v2r_launch_spmm(s, b, st));
     for (int k = 0; k < K; ++k) {
-      const double nnz = (double)h->layers[k]->nnz;
-      algo_bytes += 2.0 * (8.0 * nnz + 4.0 * (n + 1) + 8.0 * n * b);
+      const LayerDev& L = *h->layers[k];
+      algo_bytes += spmm_algo_bytes(L.nnz, L.unit, n, n, b) +
+                    spmm_algo_bytes(L.symmetric ? L.nnz : L.t_nnz,
+                                    L.symmetric ? L.unit : L.t_unit, n, n, b);
     }
     launches += 2;
     t_spmm += now_ms() - t0;
@@ -1183,8 +1201,8 @@ int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const in
     LayerDev& L = *h->layers[k];
     L.dense = false;
     L.n_rows = h->nloc;
-    upload_rows(h->stream, h->row0, h->nloc, indptr, indices, data, L.indptr, L.indices, L.data,
-                L.nnz);
+    L.unit = upload_rows(h->stream, h->row0, h->nloc, indptr, indices, data, L.indptr, L.indices,
+                         L.data, L.nnz);
     bool sym = symmetric == N2V2R_SYM_YES;
     if (symmetric != N2V2R_SYM_YES) {
       std::vector<int64_t> tp;
@@ -1194,8 +1212,8 @@ int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const in
       if (symmetric == N2V2R_SYM_DETECT)
         sym = host_is_symmetric(n, indptr, indices, data, tp, tx, td);
       if (!sym)
-        upload_rows(h->stream, h->row0, h->nloc, tp.data(), tx.data(), td.data(), L.t_indptr,
-                    L.t_indices, L.t_data, L.t_nnz);
+        L.t_unit = upload_rows(h->stream, h->row0, h->nloc, tp.data(), tx.data(), td.data(),
+                               L.t_indptr, L.t_indices, L.t_data, L.t_nnz);
     }
     L.symmetric = sym;
     L.loaded = true;
@@ -1270,7 +1288,8 @@ int n2v2r_set_layer_csr_rows(n2v2r_handle* h, int k, int64_t n, int64_t row0, in
       }
     LayerDev& L = *h->layers[k];
     L.n_rows = h->nloc;
-    upload_rows(h->stream, 0, n_rows, indptr, indices, data, L.indptr, L.indices, L.data, L.nnz);
+    L.unit = upload_rows(h->stream, 0, n_rows, indptr, indices, data, L.indptr, L.indices, L.data,
+                         L.nnz);
     L.symmetric = true;
     L.loaded = true;
     h->have_embedding = false;
@@ -1837,8 +1856,7 @@ int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, con
     (void)hipEventDestroy(e1);
     if (avg_ms) *avg_ms = (double)ms / reps;
     if (algo_bytes)
-      *algo_bytes = 8.0 * (double)a.A[0].nnz + 4.0 * (double)(h->nloc + 1) +
-                    4.0 * (double)(h->n + h->nloc) * b;
+      *algo_bytes = spmm_algo_bytes(a.A[0].nnz, a.A[0].unit != 0, h->nloc, h->n, b);
     if (Y)
       HIPCHK(hipMemcpyAsync(Y, yd.p, sizeof(float) * h->nloc * b, hipMemcpyDeviceToHost,
                             h->stream));

@@ -11,7 +11,9 @@
 // There is no LDS staging: an ER/co-expression row's columns are uniformly random, so a
 // workgroup has no panel reuse to stage; reuse comes from L2 / Infinity Cache.
 //
-// Algorithmic bytes per launch: 8*nnz + 4*(N+1) + 4*N*B (read) + 4*N*B (write).
+// Algorithmic bytes per launch (this format): 8*nnz (4*nnz for an unweighted
+// layer: no value stream) + 8*(N+1) (int64 row pointers) + 4*N*B (panel read once) + 4*N*B
+// (output written); the gathered panel rows (4*B per nnz) come from L2 / Infinity Cache.
 #include "common.h"
 
 #define SPMM_MAX_LAYERS 8
@@ -64,7 +66,7 @@ __device__ __forceinline__ void spmm_row_accumulate(const CsrDev& A, const float
     float valv = 0.f;
     if (off + li < len) {
       colv = A.indices[beg + off + li];
-      valv = A.data[beg + off + li];
+      valv = A.unit ? 1.f : A.data[beg + off + li];  // unweighted layers: no value stream
     }
     int64_t rem = maxlen - off;
     const int nn = (int)(rem < L ? rem : L);

@@ -10,7 +10,7 @@ pytestmark = pytest.mark.gpu
 
 
 # ----------------------------------------------------------------------------- SpMM
-@pytest.mark.parametrize("b", [32, 64])
+@pytest.mark.parametrize("b", [8, 16, 32, 64])
 @pytest.mark.parametrize("name", ["er_cfg1", "directed_weighted", "demo"])
 def test_spmm_matches_scipy(engine, name, b):
     fx = load_fixture(name)
@@ -21,10 +21,36 @@ def test_spmm_matches_scipy(engine, name, b):
     for k, A in enumerate(layers):
         for tr in (False, True):
             Y, ms, by = engine.bench_spmm(k, X, transpose=tr, reps=2)
-            ref = (A.T if tr else A).astype(np.float64) @ X.astype(np.float64)
-            scale = np.abs(A).astype(np.float64) @ np.abs(X).astype(np.float64)
+            M = A.T if tr else A
+            ref = M.astype(np.float64) @ X.astype(np.float64)
+            scale = np.abs(M).astype(np.float64) @ np.abs(X).astype(np.float64)
             assert np.all(np.abs(Y - ref) <= 1e-5 * scale + 1e-6), (name, k, tr)
             assert ms > 0 and by > 0
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+def test_spmm_b8_long_rows_and_empty_rows(engine, weighted):
+    """The B = 8 pipelined kernel: rows longer than 32 (the non-pipelined remainder), empty
+    rows, an odd row count, unit (unweighted) and weighted values."""
+    rng = np.random.default_rng(11)
+    n = 3001
+    deg = rng.integers(0, 90, size=n)
+    deg[::7] = 0
+    rows = np.repeat(np.arange(n), deg)
+    cols = rng.integers(0, n, size=rows.size)
+    vals = rng.standard_normal(rows.size).astype(np.float32) if weighted else np.ones(rows.size, np.float32)
+    A = sp.csr_matrix((vals, (rows, cols)), shape=(n, n))
+    A.sum_duplicates()
+    if not weighted:
+        A.data[:] = 1.0
+    engine.set_layers([A, A.T.tocsr()], symmetric=0)
+    X = rng.standard_normal((n, 8)).astype(np.float32)
+    for tr in (False, True):
+        Y, _, _ = engine.bench_spmm(0, X, transpose=tr, reps=2)
+        M = A.T if tr else A
+        ref = M.astype(np.float64) @ X.astype(np.float64)
+        scale = np.abs(M).astype(np.float64) @ np.abs(X).astype(np.float64)
+        assert np.all(np.abs(Y - ref) <= 1e-5 * scale + 1e-6), tr
 
 
 # ----------------------------------------------------------------------------- UASE
