@@ -247,6 +247,10 @@ def main():
     _, spmm_ms, spmm_bytes = eng.bench_spmm(0, X, reps=50, want_y=False)
     del X
     achieved = spmm_bytes / (spmm_ms * 1e-3) / 1e9
+    # panel rows gathered per launch (4 b bytes per nnz, served by L2 / Infinity Cache): not
+    # HBM bytes, reported beside the roofline
+    gathered = (None if cfg.get("dense") else
+                4.0 * b * float(nnz[0]) / max(1, world if mode == "partitioned" else 1))
     ms_dist, ms_borda = eng.rank_timing()
 
     traffic = None
@@ -285,7 +289,10 @@ def main():
                                 else f"spmm_csr_panel_kernel<{b},*>"),
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "algo_bytes_per_launch": spmm_bytes, "avg_launch_ms": round(spmm_ms, 5)},
+                     "algo_bytes_per_launch": spmm_bytes, "avg_launch_ms": round(spmm_ms, 5),
+                     "gathered_bytes_per_launch": gathered,
+                     "gather_GBps": (None if gathered is None else
+                                     round(gathered / (spmm_ms * 1e-3) / 1e9, 1))},
         "eig": {k: (float(f"{v:.4g}") if isinstance(v, float) else v) for k, v in stats.items()},
         "eig_options": eig,
         "rank_ms": {"distances": round(ms_dist, 3), "borda": round(ms_borda, 3)},
