@@ -785,57 +785,53 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
   for (int e = tid; e < bb; e += nt) X[e / b][e % b] = (e / b == e % b) ? 1.0 : 0.0;
   if (tid < 64) bad[tid] = 0;
   __syncthreads();
-  // O(b^3), b <= 64: wave 0 works, the other waves only keep the barriers
-  const bool w0 = tid < 64;
-  const int nw = 64;
-  if (w0) {
-    double m = (tid < b) ? R[tid][tid] : 0.0;
-    for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
-    if (tid == 0) dmax = m;
-  }
-  __syncthreads();
-  const double tiny = 1e-10 * dmax;
-  for (int j = 0; j < b; ++j) {
-    if (tid == 0) {
-      const double p = R[j][j];
-      if (!(p > tiny)) {
-        bad[j] = 1;
-        piv[j] = 0.0;
-      } else {
-        piv[j] = sqrt(p);
-      }
+  // O(b^3), b <= 64: wave 0 alone, synchronised as a wave (LDS executes a wave's accesses in
+  // order; the waits only keep the compiler from reordering), the other waves wait at the
+  // barrier below -- no block-wide barrier per elimination step
+  if (tid < 64) {
+    const int nw = 64;
+#define PIP_WSYNC() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+    {
+      double m = (tid < b) ? R[tid][tid] : 0.0;
+      for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+      if (tid == 0) dmax = m;
     }
-    __syncthreads();
-    if (w0) {
+    PIP_WSYNC();
+    const double tiny = 1e-10 * dmax;
+    for (int j = 0; j < b; ++j) {
+      if (tid == 0) {
+        const double p = R[j][j];
+        if (!(p > tiny)) {
+          bad[j] = 1;
+          piv[j] = 0.0;
+        } else {
+          piv[j] = sqrt(p);
+        }
+      }
+      PIP_WSYNC();
       const double pj = piv[j];
       const int isbad = bad[j];
       for (int cc = j + tid; cc < b; cc += nw)
         R[j][cc] = isbad ? (cc == j ? 1.0 : 0.0) : (cc == j ? pj : R[j][cc] / pj);
-    }
-    __syncthreads();
-    if (w0) {
+      PIP_WSYNC();
       const int m = b - j - 1;
       for (int e = tid; e < m * m; e += nw) {
         const int r = j + 1 + e / m, cc = j + 1 + e % m;
         if (cc >= r) R[r][cc] -= R[j][r] * R[j][cc];
       }
+      PIP_WSYNC();
     }
-    __syncthreads();
-  }
-  for (int j = b - 1; j >= 0; --j) {
-    if (w0) {
+    for (int j = b - 1; j >= 0; --j) {
       const double inv = 1.0 / R[j][j];
       for (int cc = tid; cc < b; cc += nw) X[j][cc] *= inv;
-    }
-    __syncthreads();
-    if (w0)
+      PIP_WSYNC();
       for (int e = tid; e < j * b; e += nw) {
         const int r = e / b, cc = e % b;
         X[r][cc] -= R[r][j] * X[j][cc];
       }
-    __syncthreads();
-  }
-  if (w0) {
+      PIP_WSYNC();
+    }
+#undef PIP_WSYNC
     for (int e = tid; e < bb; e += nw) {
       const int r = e / b, cc = e % b;
       xinv[e] = bad[cc] ? 0.0 : X[r][cc];
@@ -848,6 +844,7 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
       if (any && sticky) *sticky = 1;
     }
   }
+  __syncthreads();
   if (fout) {  // every thread: F[k][j] = -sum_{m <= j} C[k][m] X[m][j]; F[c + i][j] = X[i][j]
     for (int e = tid; e < (c + b) * b; e += nt) {
       const int k = e / b, j = e % b;
