@@ -17,6 +17,9 @@
 //           random values by fill_flagged so the next CGS pass can orthogonalise them.
 #include "common.h"
 
+#include <cstdlib>
+#include <cstring>
+
 // ----------------------------------------------------------------------------- helpers
 // N(0,1) deviate from a counter (Box-Muller on two splitmix64 draws)
 __device__ __forceinline__ float counter_normal(uint64_t seed, uint64_t ctr) {
@@ -332,10 +335,154 @@ __global__ __launch_bounds__(256) void ts_tn_lines_kernel(BlockList A, const flo
     }
 }
 
+// Gram step for 8-wide basis blocks and an 8-wide right-hand side, streaming form: one wave
+// per basis block and row chunk, lane = (column half h = lane >> 5, row offset rl = lane & 31),
+// so every wave-instruction reads 32 consecutive 32-B rows of ONE block (1 KB contiguous; the
+// line form above touched 8 blocks x 128 B per instruction, which halves the HBM rate).  Each
+// lane also loads its Z row (32 B, shared by the h pair).  TS_U row-steps (128 rows) per
+// iteration keep 12 x 16-B loads per lane in flight.  A chunk holds at most 8192 rows, so every
+// lane sums at most 256 products per entry in fp32; the 32 row lanes are then folded in fp64
+// by a fixed reduce-scatter (xor 1, 2, 4, 8, 16): after it lane rl holds entry
+// v = bitrev5(rl) of its half, and the wave writes its 64 fp64 partials as one contiguous run.
+// Chunks with the same rows run on one XCD (nchunks % 8 == 0, workgroup id = y * nchunks + x),
+// so each XCD's L2 fetches a Z chunk once for all of its column groups.
+#define TS_U 4
+#define TS_MAX_CHUNK 8192
+template <int MASK>
+__device__ __forceinline__ double xor_lanes_f64(double v) {
+  // lane ^ MASK within 32-lane halves (ds_swizzle bitmask mode: and 0x1F, xor MASK)
+  const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), 0x1F | (MASK << 10));
+  const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), 0x1F | (MASK << 10));
+  return __hiloint2double(hi, lo);
+}
+
+template <int BIT, int HALF>
+__device__ __forceinline__ void rs_step(double* v, int rl) {
+  // v[0..2*HALF): keep the half selected by lane bit BIT, add the partner's copy of it
+  const bool up = (rl >> BIT) & 1;
+#pragma unroll
+  for (int k = 0; k < HALF; ++k) {
+    const double mine = up ? v[k + HALF] : v[k];
+    const double give = up ? v[k] : v[k + HALF];
+    v[k] = mine + xor_lanes_f64<1 << BIT>(give);
+  }
+}
+
+__global__ __launch_bounds__(256) void ts_tn_stream_kernel(BlockList A, const float* __restrict__ Bz,
+                                                           int64_t n, int64_t rows_per_chunk,
+                                                           double* __restrict__ partial,
+                                                           const int* cond) {
+  if (cond && *cond == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int blk = (int)blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (blk >= A.count) return;  // wave-uniform; no block barrier below
+  const int h = lane >> 5, rl = lane & 31;
+  const float* ab = A.blk[blk] + 4 * h;
+  const int64_t c0 = (int64_t)blockIdx.x * rows_per_chunk;
+  int64_t c1 = c0 + rows_per_chunk;
+  if (c1 > n) c1 = n;
+  float acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
+  int64_t r = c0;
+  for (; r + 32 * TS_U <= c1; r += 32 * TS_U) {
+    f32x4 a[TS_U], z0[TS_U], z1[TS_U];
+#pragma unroll
+    for (int u = 0; u < TS_U; ++u) {
+      const int64_t rr = r + 32 * u + rl;
+      a[u] = *reinterpret_cast<const f32x4*>(ab + rr * 8);
+      z0[u] = *reinterpret_cast<const f32x4*>(Bz + rr * 8);
+      z1[u] = *reinterpret_cast<const f32x4*>(Bz + rr * 8 + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < TS_U; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[i][j] += a[u][i] * z0[u][j];
+          acc[i][4 + j] += a[u][i] * z1[u][j];
+        }
+  }
+  for (; r < c1; r += 32) {
+    const int64_t rr = r + rl;
+    if (rr < c1) {
+      const f32x4 a1 = *reinterpret_cast<const f32x4*>(ab + rr * 8);
+      const f32x4 y0 = *reinterpret_cast<const f32x4*>(Bz + rr * 8);
+      const f32x4 y1 = *reinterpret_cast<const f32x4*>(Bz + rr * 8 + 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[i][j] += a1[i] * y0[j];
+          acc[i][4 + j] += a1[i] * y1[j];
+        }
+    }
+  }
+  double v[32];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[i * 8 + j] = (double)acc[i][j];
+  rs_step<0, 16>(v, rl);
+  rs_step<1, 8>(v, rl);
+  rs_step<2, 4>(v, rl);
+  rs_step<3, 2>(v, rl);
+  rs_step<4, 1>(v, rl);
+  // lane rl now holds entry e = bitrev5(rl) = (i, j) = (e >> 3, e & 7) of its column half
+  const int e = ((rl & 1) << 4) | ((rl & 2) << 2) | (rl & 4) | ((rl & 8) >> 2) | ((rl & 16) >> 4);
+  double* out = partial + (int64_t)blockIdx.x * ((int64_t)A.count * 8) * 8;
+  out[(int64_t)blk * 64 + 32 * h + e] = v[0];
+}
+
+// Gram-kernel selection for 8-wide blocks: streaming form unless N2V2R_TN_FORM=lines;
+// N2V2R_TN_WAVES overrides the streaming form's wave target (tuning runs)
+static bool tn_stream_form() {
+  static const int v = [] {
+    const char* s = getenv("N2V2R_TN_FORM");
+    return (s && strcmp(s, "lines") == 0) ? 0 : 1;
+  }();
+  return v != 0;
+}
+static int64_t tn_stream_waves() {
+  static const int64_t v = [] {
+    const char* s = getenv("N2V2R_TN_WAVES");
+    return (int64_t)(s ? atoll(s) : 4096);
+  }();
+  return v;
+}
+
 extern "C" hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n,
                                          double* partial, size_t partial_elems, double* out,
                                          const int* cond, hipStream_t stream) {
   const int ca = A.count * A.width, cb = B.count * B.width;
+  int64_t s_chunks = 0, s_rows = 0;
+  if (B.count == 1 && B.width == 8 && A.width == 8 && tn_stream_form()) {
+    // streaming form: ~tn_stream_waves() (4096) waves, chunks of <= TS_MAX_CHUNK rows, nchunks % 8 == 0
+    s_chunks = (tn_stream_waves() + A.count - 1) / A.count;
+    const int64_t lo = (n + TS_MAX_CHUNK - 1) / TS_MAX_CHUNK, hi = (n + 255) / 256;
+    if (s_chunks > hi) s_chunks = hi;
+    if (s_chunks < lo) s_chunks = lo;
+    s_chunks = (s_chunks + 7) & ~(int64_t)7;
+    s_rows = ((n + s_chunks - 1) / s_chunks + 31) & ~(int64_t)31;
+    s_chunks = (n + s_rows - 1) / s_rows;
+    // partials must fit the buffer; otherwise the line form below takes it
+    if ((size_t)(s_chunks * ca * cb) > partial_elems || s_rows > TS_MAX_CHUNK) s_chunks = 0;
+  }
+  if (s_chunks > 0) {
+    const int64_t elems = (int64_t)ca * cb;
+    const int64_t nchunks = s_chunks, rows_per_chunk = s_rows;
+    const dim3 grid((unsigned)nchunks, (unsigned)((A.count + 3) / 4));
+    hipLaunchKernelGGL(ts_tn_stream_kernel, grid, dim3(256), 0, stream, A, B.blk[0], n,
+                       rows_per_chunk, partial, cond);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((elems + 3) / 4)), dim3(256), 0,
+                       stream, partial, (int)nchunks, elems, out, cond);
+    return hipGetLastError();
+  }
   if (B.count == 1 && B.width == 8 && A.width == 8) {
     // line form: ~2048 waves, >= 64 rows per chunk, partials within the buffer
     const int64_t elems = (int64_t)ca * cb;
