@@ -1030,6 +1030,166 @@ extern "C" hipError_t n2v2r_launch_chol_inv(const double* G, int b, float* Rinv,
   return hipGetLastError();
 }
 
+// ----------------------------------------------------------------------------- fused PIP pass
+// One launch per BCGS-PIP pass at b = 8 (replaces pip_chol + the apply): every workgroup stages
+// the Gram G = [Q Z]^T Z ((c + 8) x 8 fp64, C = Q^T Z its first c rows) in LDS, forms
+// P = Z^T Z - C^T C (4 k-slices, fixed fold order), factors P = R^T R and inverts R with wave 0
+// lane-parallel (lane = (i, j) entry, pivots by readlane, row/column operands by shuffles: no
+// block barrier per step), then streams its 256 rows: Z <- (Z - Q C) R^{-1}, flagged columns
+// refilled by counter deviates.  Every workgroup forms the same R from the same G (the
+// factorisation is deterministic); workgroup 0 alone writes flags / any_flag / sticky / save.
+// Same pivot rule as pip_chol_kernel (pivot <= 1e-10 max diag: unit row, zero R^{-1} column).
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
+
+__global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float* Zin, float* Zout,
+                                                        const double* __restrict__ G, int c,
+                                                        int64_t n, const int* cond, int* flags,
+                                                        int* any_flag, double* save, int save_row0,
+                                                        int save_rows, int* sticky, uint64_t seed,
+                                                        int64_t row0) {
+  const int tid = threadIdx.x;
+  const bool lead = blockIdx.x == 0;
+  if (cond && *cond == 0) {
+    if (lead && tid < 8) flags[tid] = 0;
+    if (lead && tid == 0) *any_flag = 0;
+    return;
+  }
+  // one LDS array: gd (c + 8) x 8 fp64 | part 4 x 64 fp64 | cf c x 8 fp32 | rv 8 x 8 fp32 | mask
+  extern __shared__ __attribute__((aligned(16))) double pf_lds[];
+  double* gd = pf_lds;
+  double* part = gd + (c + 8) * 8;
+  float* cf = reinterpret_cast<float*>(part + 256);
+  float* rv = cf + c * 8;
+  int* badw = reinterpret_cast<int*>(rv + 64);
+  const int ne2 = (c + 8) * 4;  // double2 count
+  for (int e = tid; e < ne2; e += 256)
+    reinterpret_cast<double2*>(gd)[e] = reinterpret_cast<const double2*>(G)[e];
+  __syncthreads();
+  if (save && lead)
+    for (int e = tid; e < save_rows * 8; e += 256) save[e] = gd[save_row0 * 8 + e];
+  for (int e = tid; e < c * 8; e += 256) cf[e] = (float)gd[e];
+  {
+    const int e = tid & 63, sl = tid >> 6, i = e >> 3, j = e & 7;
+    double acc = 0.0;
+    for (int k = sl; k < c; k += 4) acc += gd[k * 8 + i] * gd[k * 8 + j];
+    part[sl * 64 + e] = acc;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int i = tid >> 3, j = tid & 7;
+    double v = 0.5 * (gd[(c + i) * 8 + j] + gd[(c + j) * 8 + i]);
+    v = v - part[tid] - part[64 + tid] - part[128 + tid] - part[192 + tid];
+    double dmax = 0.0;
+#pragma unroll
+    for (int d = 0; d < 8; ++d) dmax = fmax(dmax, readlane_f64(v, d * 9));
+    const double tiny = 1e-10 * dmax;
+    int bad = 0;
+    // right-looking Cholesky: row jj of R = row jj of the Schur complement / sqrt(pivot)
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const double p = readlane_f64(v, jj * 9);
+      const bool bj = !(p > tiny);
+      const double piv = bj ? 0.0 : sqrt(p);
+      bad |= (int)bj << jj;
+      if (i == jj) v = (j < jj) ? 0.0 : bj ? (j == jj ? 1.0 : 0.0) : (j == jj ? piv : v / piv);
+      const double rjr = __shfl(v, jj * 8 + i, 64);
+      const double rjc = __shfl(v, jj * 8 + j, 64);
+      if (i > jj && j >= i) v -= rjr * rjc;
+    }
+    // Gauss-Jordan on [R | I] from the last row up: x <- R^{-1}
+    double x = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+    for (int jj = 7; jj >= 0; --jj) {
+      const double inv = 1.0 / readlane_f64(v, jj * 9);
+      if (i == jj) x *= inv;
+      const double xj = __shfl(x, jj * 8 + j, 64);
+      const double rij = __shfl(v, i * 8 + jj, 64);
+      if (i < jj) x -= rij * xj;
+    }
+    rv[tid] = ((bad >> j) & 1) ? 0.f : (float)x;
+    if (tid == 0) badw[0] = bad;
+    if (lead) {
+      if (tid < 8) flags[tid] = (bad >> tid) & 1;
+      if (tid == 0) {
+        *any_flag = bad != 0;
+        if (bad && sticky) *sticky = 1;
+      }
+    }
+  }
+  __syncthreads();
+  const int64_t row = (int64_t)blockIdx.x * 256 + tid;
+  if (row >= n) return;
+  float acc[8];
+  {
+    const f32x4 z0 = *reinterpret_cast<const f32x4*>(Zin + row * 8);
+    const f32x4 z1 = *reinterpret_cast<const f32x4*>(Zin + row * 8 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc[j] = z0[j];
+      acc[4 + j] = z1[j];
+    }
+  }
+  int q = 0;
+  for (; q + 4 <= Q.count; q += 4) {  // 4 blocks (8 x 16-B loads) in flight per step
+    f32x4 a4[4][2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int l = 0; l < 2; ++l)
+        a4[u][l] = *reinterpret_cast<const f32x4*>(Q.blk[q + u] + row * 8 + 4 * l);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int l = 0; l < 2; ++l) {
+        const float* g = cf + ((q + u) * 8 + 4 * l) * 8;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] -= a4[u][l][m] * g[m * 8 + j];
+      }
+  }
+  for (; q < Q.count; ++q) {
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+      const f32x4 a4 = *reinterpret_cast<const f32x4*>(Q.blk[q] + row * 8 + 4 * l);
+      const float* g = cf + (q * 8 + 4 * l) * 8;
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] -= a4[m] * g[m * 8 + j];
+    }
+  }
+  const int bad = badw[0];
+  float o[8];
+#pragma unroll
+  for (int jo = 0; jo < 8; ++jo) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j <= jo; ++j) s += acc[j] * rv[j * 8 + jo];
+    o[jo] = ((bad >> jo) & 1) ? counter_normal(seed, (uint64_t)(row0 + row) * 64 + jo) : s;
+  }
+  *reinterpret_cast<f32x4*>(Zout + row * 8) = f32x4{o[0], o[1], o[2], o[3]};
+  *reinterpret_cast<f32x4*>(Zout + row * 8 + 4) = f32x4{o[4], o[5], o[6], o[7]};
+}
+
+extern "C" hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zin, float* Zout,
+                                             const double* G, int c, int64_t n, const int* cond,
+                                             int* flags, int* any_flag, double* save,
+                                             int save_row0, int save_rows, int* sticky,
+                                             uint64_t seed, int64_t row0, hipStream_t stream) {
+  if (Q.width != 8 || c != Q.count * 8) return hipErrorInvalidValue;
+  const size_t lds = sizeof(double) * ((size_t)(c + 8) * 8 + 256) + sizeof(float) * ((size_t)c * 8 + 64) + 16;
+  if (lds > 64 * 1024) return hipErrorInvalidValue;
+  const unsigned grid = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(pip_fused_kernel, dim3(grid ? grid : 1), dim3(256), lds, stream, Q, Zin, Zout, G, c, n,
+                     cond, flags, any_flag, save, save_row0, save_rows, sticky, seed, row0);
+  return hipGetLastError();
+}
+
 // Fill an N x W block with N(0,1) deviates: all columns (flags == nullptr) or only flagged ones.
 __global__ void fill_normal_kernel(float* __restrict__ blk, int w, int64_t n, uint64_t seed,
                                    const int* flags, const int* cond, uint64_t ctr0) {

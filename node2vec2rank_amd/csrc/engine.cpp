@@ -81,6 +81,18 @@ hipError_t n2v2r_launch_rr_band(const double* hband, int c, int kp, double* thet
                                 double* Y, float* S, int ldS, int p, int* err,
                                 hipStream_t stream);
 int n2v2r_rr_band_jm(int c);
+// b = 8 PIP passes use the fused Cholesky + apply launch unless N2V2R_PIP_FUSED=0 (A/B runs)
+static bool pip_fused() {
+  static const bool v = [] {
+    const char* s = std::getenv("N2V2R_PIP_FUSED");
+    return !(s && s[0] == '0');
+  }();
+  return v;
+}
+hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zin, float* Zout,
+                                  const double* G, int c, int64_t n, const int* cond, int* flags,
+                                  int* any_flag, double* save, int save_row0, int save_rows,
+                                  int* sticky, uint64_t seed, int64_t row0, hipStream_t stream);
 hipError_t n2v2r_launch_pip_apply(const BlockList& QZ, const float* F, int c, int b,
                                   const OutBlockList& Z, int64_t n, const int* cond,
                                   const int* flags, uint64_t seed, int64_t row0,
@@ -679,6 +691,13 @@ struct Eig {
     qz.push_back(const_cast<float*>(zin));
     const BlockList L = blocks(qz, 0, nq + 1);
     tn(L, one(zin), h->ews.gsmall.as<double>(), cond);
+    if (b == 8 && nq * b <= 512 && pip_fused()) {
+      // b = 8: the Cholesky step runs inside the apply launch (every workgroup factors G)
+      HIPCHK(n2v2r_launch_pip_fused(blocks(qz, 0, nq), zin, Z, h->ews.gsmall.as<double>(), nq * b,
+                                    n, cond, flags_out, any_out, save, save_row0, save_rows,
+                                    sticky, seed ^ (0xABCDull + ++fill_counter), row0, st));
+      return;
+    }
     HIPCHK(n2v2r_launch_pip_chol(h->ews.gsmall.as<double>(), nq * b, b, h->ews.rinv.as<double>(),
                                  flags_out, any_out, cond, save, save_row0, save_rows,
                                  h->ews.fcoef.as<float>(), sticky, st));
