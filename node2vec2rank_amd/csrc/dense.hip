@@ -608,27 +608,34 @@ __global__ __launch_bounds__(256) void ts_nn_kernel(BlockList A, Coef F, int cb,
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f32x16{0.f};
   const int ca = A.count * A.width;
+  // rows past n read row n-1 (valid address, results not stored); the chunk's 8 A loads are
+  // issued before the F staging so they are in flight across its barriers
+  const int64_t lrow = row_ok ? row : (n > 0 ? n - 1 : 0);
   for (int k0 = 0; k0 < ca; k0 += NN_KCH) {
     const int kn = (ca - k0) < NN_KCH ? (ca - k0) : NN_KCH;
+    f32x4 a4[NN_KCH / 8];
+#pragma unroll
+    for (int s8 = 0; s8 < NN_KCH / 8; ++s8) {
+      int kg = k0 + 8 * s8;
+      if (kg >= ca) kg = ca - 8;
+      a4[s8] = *reinterpret_cast<const f32x4*>(A.blk[kg / A.width] + (kg % A.width) + 4 * h +
+                                               lrow * (int64_t)A.width);
+    }
     __syncthreads();
     for (int e = threadIdx.x; e < NN_KCH * NT * 32; e += blockDim.x) {
       const int k = e / (NT * 32), j = e % (NT * 32);
       fs[k][j] = (k < kn && j < cb) ? coef_at(F, k0 + k, j, cb) : 0.f;
     }
     __syncthreads();
-    if (r0 < n) {
-      for (int kk = 0; kk < kn; kk += 8) {
-        const int kg = k0 + kk;
-        const float* ap = A.blk[kg / A.width] + (kg % A.width) + 4 * h;
-        f32x4 a4 = {0.f, 0.f, 0.f, 0.f};
-        if (row_ok) a4 = *reinterpret_cast<const f32x4*>(ap + row * (int64_t)A.width);
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
+    for (int s8 = 0; s8 < NN_KCH / 8; ++s8) {
+      if (8 * s8 >= kn) break;
 #pragma unroll
-          for (int t = 0; t < NT; ++t)
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[m], fs[kk + 4 * h + m][t * 32 + i],
-                                                           acc[t], 0, 0, 0);
-        }
+      for (int m = 0; m < 4; ++m) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+              a4[s8][m], fs[8 * s8 + 4 * h + m][t * 32 + i], acc[t], 0, 0, 0);
       }
     }
   }
@@ -1121,59 +1128,77 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
     }
   }
   __syncthreads();
-  const int64_t row = (int64_t)blockIdx.x * 256 + tid;
-  if (row >= n) return;
-  float acc[8];
-  {
-    const f32x4 z0 = *reinterpret_cast<const f32x4*>(Zin + row * 8);
-    const f32x4 z1 = *reinterpret_cast<const f32x4*>(Zin + row * 8 + 4);
+  // rows: wave w owns rows 64 w .. 64 w + 63 of the workgroup's 256, lane = (row offset
+  // ro = lane >> 1, column half h = lane & 1) over two 32-row halves u, so one load
+  // instruction reads 32 consecutive 32-B rows of a block (1 KB contiguous)
+  const int lane = tid & 63, h = lane & 1, ro = lane >> 1;
+  const int64_t rbase = (int64_t)blockIdx.x * 256 + (tid >> 6) * 64 + ro;
+  if (rbase >= n) return;
+  const bool ok1 = rbase + 32 < n;
+  const int64_t rw[2] = {rbase, ok1 ? rbase + 32 : rbase};
+  float acc[2][8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      acc[j] = z0[j];
-      acc[4 + j] = z1[j];
+  for (int u = 0; u < 2; ++u) {
+    const f32x4 z = *reinterpret_cast<const f32x4*>(Zin + rw[u] * 8 + 4 * h);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      acc[u][t] = h ? 0.f : z[t];
+      acc[u][4 + t] = h ? z[t] : 0.f;
     }
   }
   int q = 0;
-  for (; q + 4 <= Q.count; q += 4) {  // 4 blocks (8 x 16-B loads) in flight per step
+  for (; q + 4 <= Q.count; q += 4) {  // 4 blocks x 2 rows (8 x 16-B loads) in flight per step
     f32x4 a4[4][2];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int b4 = 0; b4 < 4; ++b4)
 #pragma unroll
-      for (int l = 0; l < 2; ++l)
-        a4[u][l] = *reinterpret_cast<const f32x4*>(Q.blk[q + u] + row * 8 + 4 * l);
+      for (int u = 0; u < 2; ++u)
+        a4[b4][u] = *reinterpret_cast<const f32x4*>(Q.blk[q + b4] + rw[u] * 8 + 4 * h);
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int l = 0; l < 2; ++l) {
-        const float* g = cf + ((q + u) * 8 + 4 * l) * 8;
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc[j] -= a4[u][l][m] * g[m * 8 + j];
-      }
-  }
-  for (; q < Q.count; ++q) {
-#pragma unroll
-    for (int l = 0; l < 2; ++l) {
-      const f32x4 a4 = *reinterpret_cast<const f32x4*>(Q.blk[q] + row * 8 + 4 * l);
-      const float* g = cf + (q * 8 + 4 * l) * 8;
+    for (int b4 = 0; b4 < 4; ++b4) {
+      const float* g = cf + ((q + b4) * 8 + 4 * h) * 8;
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] -= a4[m] * g[m * 8 + j];
+        for (int j = 0; j < 8; ++j) {
+          const float gv = g[m * 8 + j];
+          acc[0][j] -= a4[b4][0][m] * gv;
+          acc[1][j] -= a4[b4][1][m] * gv;
+        }
     }
   }
-  const int bad = badw[0];
-  float o[8];
+  for (; q < Q.count; ++q) {
+    f32x4 a4[2];
 #pragma unroll
-  for (int jo = 0; jo < 8; ++jo) {
-    float s = 0.f;
+    for (int u = 0; u < 2; ++u) a4[u] = *reinterpret_cast<const f32x4*>(Q.blk[q] + rw[u] * 8 + 4 * h);
+    const float* g = cf + (q * 8 + 4 * h) * 8;
 #pragma unroll
-    for (int j = 0; j <= jo; ++j) s += acc[j] * rv[j * 8 + jo];
-    o[jo] = ((bad >> jo) & 1) ? counter_normal(seed, (uint64_t)(row0 + row) * 64 + jo) : s;
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float gv = g[m * 8 + j];
+        acc[0][j] -= a4[0][m] * gv;
+        acc[1][j] -= a4[1][m] * gv;
+      }
   }
-  *reinterpret_cast<f32x4*>(Zout + row * 8) = f32x4{o[0], o[1], o[2], o[3]};
-  *reinterpret_cast<f32x4*>(Zout + row * 8 + 4) = f32x4{o[4], o[5], o[6], o[7]};
+  const int bad = badw[0];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    // the two column halves of a row sit in adjacent lanes: fold them (quad_perm [1,0,3,2])
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      acc[u][j] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(acc[u][j]), 0xB1, 0xF, 0xF, false));
+    float o[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int jo = 4 * h + t;
+      float sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum += (j <= jo) ? acc[u][j] * rv[j * 8 + jo] : 0.f;
+      o[t] = ((bad >> jo) & 1) ? counter_normal(seed, (uint64_t)(row0 + rw[u]) * 64 + jo) : sum;
+    }
+    if (u == 0 || ok1) *reinterpret_cast<f32x4*>(Zout + rw[u] * 8 + 4 * h) = f32x4{o[0], o[1], o[2], o[3]};
+  }
 }
 
 extern "C" hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zin, float* Zout,
