@@ -596,7 +596,7 @@ __global__ __launch_bounds__(256) void ts_nn_kernel(BlockList A, Coef F, int cb,
                                                     int64_t n, const int* cond, const int* flags,
                                                     uint64_t seed, int64_t row0) {
   if (cond && *cond == 0) return;
-  __shared__ float fs[NN_KCH][NT * 32];
+  __shared__ __attribute__((aligned(16))) float fs[NN_KCH][NT * 32];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 32;
@@ -611,6 +611,8 @@ __global__ __launch_bounds__(256) void ts_nn_kernel(BlockList A, Coef F, int cb,
   // rows past n read row n-1 (valid address, results not stored); the chunk's 8 A loads are
   // issued before the F staging so they are in flight across its barriers
   const int64_t lrow = row_ok ? row : (n > 0 ? n - 1 : 0);
+  const bool vec4 = F.G && (F.ldg % 4) == 0 && (cb % 4) == 0 &&
+                    (reinterpret_cast<uintptr_t>(F.G) & 15) == 0;
   for (int k0 = 0; k0 < ca; k0 += NN_KCH) {
     const int kn = (ca - k0) < NN_KCH ? (ca - k0) : NN_KCH;
     f32x4 a4[NN_KCH / 8];
@@ -621,10 +623,30 @@ __global__ __launch_bounds__(256) void ts_nn_kernel(BlockList A, Coef F, int cb,
       a4[s8] = *reinterpret_cast<const f32x4*>(A.blk[kg / A.width] + (kg % A.width) + 4 * h +
                                                lrow * (int64_t)A.width);
     }
-    __syncthreads();
-    for (int e = threadIdx.x; e < NN_KCH * NT * 32; e += blockDim.x) {
-      const int k = e / (NT * 32), j = e % (NT * 32);
-      fs[k][j] = (k < kn && j < cb) ? coef_at(F, k0 + k, j, cb) : 0.f;
+    if (F.G && vec4) {  // plain coefficients, 16-B aligned: 6 float4 loads per thread in flight
+      constexpr int R4 = NT * 8;  // float4 per staged row
+      constexpr int PER = NN_KCH * R4 / 256;
+      f32x4 tv[PER];
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int e = threadIdx.x + u * 256;
+        const int k = e / R4, j = (e % R4) * 4;
+        const bool ok = k < kn && j < cb;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(F.G + (ok ? (int64_t)(k0 + k) * F.ldg + j : 0));
+        tv[u] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int e = threadIdx.x + u * 256;
+        *reinterpret_cast<f32x4*>(&fs[e / R4][(e % R4) * 4]) = tv[u];
+      }
+    } else {
+      __syncthreads();
+      for (int e = threadIdx.x; e < NN_KCH * NT * 32; e += blockDim.x) {
+        const int k = e / (NT * 32), j = e % (NT * 32);
+        fs[k][j] = (k < kn && j < cb) ? coef_at(F, k0 + k, j, cb) : 0.f;
+      }
     }
     __syncthreads();
 #pragma unroll
