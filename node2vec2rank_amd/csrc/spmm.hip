@@ -16,6 +16,8 @@
 // (output written); the gathered panel rows (4*B per nnz) come from L2 / Infinity Cache.
 #include "common.h"
 
+#include <cstdlib>
+
 #define SPMM_MAX_LAYERS 8
 #ifndef N2V2R_SPMM_WGS
 #define N2V2R_SPMM_WGS 2048  // workgroups per launch (8 per CU); rows are grid-strided
@@ -130,6 +132,148 @@ __global__ __launch_bounds__(256) void spmm_csr_panel_kernel(SpmmArgs args) {
   }
 }
 
+// B = 8, software-pipelined: a wave walks its tasks (row group, layer) in order and, while the
+// current task's panel rows are being gathered, already has the next task's row pointers and
+// first SP8_PF x L column indices (and values) in flight.  A row's gathers thus wait on one
+// dependent load (the gather itself) instead of three (row pointer -> index -> gather); rows
+// longer than SP8_PF x L finish in an unpipelined tail loop.  Same lane layout and summation
+// order per row as spmm_csr_panel_kernel<8, RPW> (column halves in lane pairs, NPS panel rows
+// per step, the row group's partial sums folded by xor shuffles).
+#define SP8_PF 2
+template <int RPW>
+__global__ __launch_bounds__(256) void spmm8_pipe_kernel(SpmmArgs args) {
+  constexpr int L = 64 / RPW, NPS = L / 2;
+  const int lane = threadIdx.x & 63;
+  const int g = lane / L, li = lane % L, sub = li & 1;
+  const int srcbase = g * L + (li >> 1);
+  const int K = args.sum ? args.K : 1;
+  const int kfix = args.sum ? 0 : (int)blockIdx.y;
+  const int64_t n = args.A[kfix].n_rows;
+  const int64_t ngroups = (n + RPW - 1) / RPW;
+  const int64_t gstride = (int64_t)gridDim.x * (blockDim.x / 64);
+  int64_t grp = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (grp >= ngroups) return;
+  int k = 0;
+  // current task
+  int64_t row = grp * RPW + g;
+  int64_t beg = 0, len = 0;
+  int idx[SP8_PF];
+  float val[SP8_PF];
+  {
+    const CsrDev& A = args.A[kfix + k];
+    if (row < n) {
+      beg = A.indptr[row];
+      len = A.indptr[row + 1] - beg;
+    }
+#pragma unroll
+    for (int p = 0; p < SP8_PF; ++p) {
+      const bool in = p * L + li < len;
+      idx[p] = in ? A.indices[beg + p * L + li] : 0;
+      val[p] = in ? (A.unit ? 1.f : A.data[beg + p * L + li]) : 0.f;
+    }
+  }
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (;;) {
+    // next task: next layer of this row group (sum mode), else the next row group
+    int nk = k + 1;
+    int64_t ngrp = grp;
+    if (nk == K) {
+      nk = 0;
+      ngrp = grp + gstride;
+    }
+    const bool has_next = ngrp < ngroups;
+    const int64_t nrow = ngrp * RPW + g;
+    const CsrDev& An = args.A[kfix + nk];
+    // 1. the next task's row pointers
+    int64_t nbeg = 0, nend = 0;
+    if (has_next && nrow < n) {
+      nbeg = An.indptr[nrow];
+      nend = An.indptr[nrow + 1];
+    }
+    // 2. the current task's gathers (prefetched indices)
+    const CsrDev& A = args.A[kfix + k];
+    const float* X = args.X[kfix + k];
+    int64_t maxlen = len;
+#pragma unroll
+    for (int m = L; m < 64; m <<= 1) {
+      const int64_t o = __shfl_xor(maxlen, m, 64);
+      maxlen = o > maxlen ? o : maxlen;
+    }
+#pragma unroll
+    for (int s = 0; s < 2 * SP8_PF; ++s) {
+      if (s * NPS >= maxlen) break;
+      const int c0 = __shfl(idx[s >> 1], srcbase + (s & 1) * NPS, 64);
+      const float v0 = __shfl(val[s >> 1], srcbase + (s & 1) * NPS, 64);
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(X + (int64_t)c0 * args.ldx + sub * 4);
+      acc += v0 * x0;
+    }
+    // 3. the next task's first column indices / values
+    const int64_t nlen = nend - nbeg;
+    int nidx[SP8_PF];
+    float nval[SP8_PF];
+#pragma unroll
+    for (int p = 0; p < SP8_PF; ++p) {
+      const bool in = p * L + li < nlen;
+      nidx[p] = in ? An.indices[nbeg + p * L + li] : 0;
+      nval[p] = in ? (An.unit ? 1.f : An.data[nbeg + p * L + li]) : 0.f;
+    }
+    // 4. long rows: the rest of the current task, unpipelined
+    for (int64_t off = SP8_PF * L; off < maxlen; off += L) {
+      int colv = 0;
+      float valv = 0.f;
+      if (off + li < len) {
+        colv = A.indices[beg + off + li];
+        valv = A.unit ? 1.f : A.data[beg + off + li];
+      }
+      const int64_t rem = maxlen - off;
+      const int nn = (int)(rem < L ? rem : L);
+      for (int s = 0; s * NPS < nn; ++s) {
+        const int c0 = __shfl(colv, srcbase + s * NPS, 64);
+        const float v0 = __shfl(valv, srcbase + s * NPS, 64);
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(X + (int64_t)c0 * args.ldx + sub * 4);
+        acc += v0 * x0;
+      }
+    }
+    if (k == K - 1) {  // row complete: fold the row group, store
+#pragma unroll
+      for (int m = 2; m < L; m <<= 1) {
+        acc.x += __shfl_xor(acc.x, m, 64);
+        acc.y += __shfl_xor(acc.y, m, 64);
+        acc.z += __shfl_xor(acc.z, m, 64);
+        acc.w += __shfl_xor(acc.w, m, 64);
+      }
+      if (row < n && li < 2) {
+        if (args.colscale) {
+          const f32x4 sc = *reinterpret_cast<const f32x4*>(args.colscale + li * 4);
+          acc *= sc;
+        }
+        *reinterpret_cast<f32x4*>(args.Y[kfix] + row * args.ldy + li * 4) = acc;
+      }
+      acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (!has_next) break;
+    k = nk;
+    grp = ngrp;
+    row = nrow;
+    beg = nbeg;
+    len = nlen;
+#pragma unroll
+    for (int p = 0; p < SP8_PF; ++p) {
+      idx[p] = nidx[p];
+      val[p] = nval[p];
+    }
+  }
+}
+
+// B = 8 uses the pipelined kernel unless N2V2R_SPMM_PIPE=0 (A/B runs)
+static bool spmm8_pipelined() {
+  static const bool v = [] {
+    const char* s = getenv("N2V2R_SPMM_PIPE");
+    return !(s && s[0] == '0');
+  }();
+  return v;
+}
+
 template <int B, int RPW>
 static void launch_spmm_t(const SpmmArgs& args, hipStream_t stream) {
   const int64_t n = args.A[0].n_rows;
@@ -138,6 +282,12 @@ static void launch_spmm_t(const SpmmArgs& args, hipStream_t stream) {
   const int64_t cap = (int64_t)N2V2R_SPMM_WGS / (args.sum ? 1 : args.K);
   if (wgs > cap) wgs = cap;
   dim3 grid((unsigned)wgs, args.sum ? 1 : args.K);
+  if constexpr (B == 8 && RPW >= 2) {
+    if (spmm8_pipelined()) {
+      hipLaunchKernelGGL((spmm8_pipe_kernel<RPW>), grid, dim3(256), 0, stream, args);
+      return;
+    }
+  }
   hipLaunchKernelGGL((spmm_csr_panel_kernel<B, RPW>), grid, dim3(256), 0, stream, args);
 }
 
