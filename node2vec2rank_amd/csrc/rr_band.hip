@@ -376,12 +376,18 @@ __global__ __launch_bounds__(RB_CH_WAVES * 64) void rr_chase_kernel(
       if (act) {
         const bool rv = r < MR;
         const int d0 = R0 - C0 + r;
+        // branch-free window access: entries outside the window read / write the spare LDS
+        // slot `spare` (past the band) and are masked to zero, so the 16 loads issue together
+        const int spare = c * S;
         double O[W], D[W];
 #pragma unroll
         for (int t = 0; t < W; ++t) {
-          O[t] = (rv && t < NC) ? L[(R0 + r) * S + (d0 - t)] : 0.0;
           const int hi = r > t ? r : t, lo = r > t ? t : r;
-          D[t] = (rv && t < MR) ? L[(R0 + hi) * S + (hi - lo)] : 0.0;
+          const bool oko = rv && t < NC, okd = rv && t < MR;
+          const double ov = L[oko ? (R0 + r) * S + (d0 - t) : spare];
+          const double dv = L[okd ? (R0 + hi) * S + (hi - lo) : spare];
+          O[t] = oko ? ov : 0.0;
+          D[t] = okd ? dv : 0.0;
         }
         // right-apply the previous reflector (acts on O's columns)
         double tt = 0.0;
@@ -418,8 +424,7 @@ __global__ __launch_bounds__(RB_CH_WAVES * 64) void rr_chase_kernel(
         for (int t = 0; t < W; ++t) O[t] -= tau2 * v2r * gs[72 + t];
         O[0] = (r == 0) ? beta2 : 0.0;
 #pragma unroll
-        for (int t = 0; t < W; ++t)
-          if (rv && t < NC) L[(R0 + r) * S + (d0 - t)] = O[t];
+        for (int t = 0; t < W; ++t) L[(rv && t < NC) ? (R0 + r) * S + (d0 - t) : spare] = O[t];
         // two-sided update of D
         double pr = 0.0;
 #pragma unroll
@@ -439,7 +444,7 @@ __global__ __launch_bounds__(RB_CH_WAVES * 64) void rr_chase_kernel(
 #pragma unroll
         for (int t = 0; t < W; ++t) {
           D[t] -= v2r * (ps[t] - K * v2[t]) + wr * v2[t];
-          if (rv && t < MR && t <= r) L[(R0 + r) * S + (r - t)] = D[t];
+          L[(rv && t < MR && t <= r) ? (R0 + r) * S + (r - t) : spare] = D[t];
         }
         // record the reflector for the back-transform
         double* slot = refl + ((int64_t)i * jm + j) * 9;
@@ -605,7 +610,7 @@ extern "C" hipError_t n2v2r_launch_rr_band(const double* hband, int c, int kp, d
     hipError_t er = hipGetLastError();
     if (er != hipSuccess) return er;
   }
-  const size_t lch = sizeof(double) * (size_t)c * (2 * RB_W + 1);
+  const size_t lch = sizeof(double) * ((size_t)c * (2 * RB_W + 1) + 8);  // + the spare slot
   hipLaunchKernelGGL(rr_chase_kernel, dim3(1), dim3(RB_CH_WAVES * 64), lch, stream, hband, c, kp,
                      AB, d, e, refl, jm, err);
   hipError_t er = hipGetLastError();
