@@ -33,18 +33,33 @@
 
 namespace {
 
+__device__ __forceinline__ double rcp_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(r, fma(-x, r, 1.0), r);
+  r = fma(r, fma(-x, r, 1.0), r);
+  return r;
+}
+
+// 8-term dot product as a depth-3 tree (the chase's per-step latency)
+__device__ __forceinline__ double dot8(const double* a, const double* b) {
+  const double p0 = fma(a[0], b[0], a[1] * b[1]), p1 = fma(a[2], b[2], a[3] * b[3]);
+  const double p2 = fma(a[4], b[4], a[5] * b[5]), p3 = fma(a[6], b[6], a[7] * b[7]);
+  return (p0 + p1) + (p2 + p3);
+}
+
 __device__ __forceinline__ void house_params(double x0, double sig, double& tau, double& beta,
                                              double& scale) {
-  if (sig == 0.0) {
-    tau = 0.0;
-    beta = x0;
-    scale = 0.0;
-    return;
-  }
+  // branch-free (sig == 0: the identity reflector tau = 0, beta = x0, scale = 0); two
+  // independent reciprocals (v_rcp_f64 + two Newton steps) instead of two dependent IEEE
+  // divisions: the chase's per-step latency
   const double nrm = sqrt(x0 * x0 + sig);
-  beta = (x0 >= 0.0) ? -nrm : nrm;
-  tau = (beta - x0) / beta;
-  scale = 1.0 / (x0 - beta);
+  const double bt = (x0 >= 0.0) ? -nrm : nrm;
+  const double tc = (bt - x0) * rcp_nr(bt);
+  const double sc = rcp_nr(x0 - bt);
+  const bool z = sig == 0.0;
+  tau = z ? 0.0 : tc;
+  beta = z ? x0 : bt;
+  scale = z ? 0.0 : sc;
 }
 
 template <int CTRL>
@@ -315,7 +330,7 @@ __global__ __launch_bounds__(RB_CH_WAVES * 64) void rr_chase_kernel(
   const int wave = tid >> 6, lane = tid & 63;
   const int nwaves = blockDim.x >> 6;
   const int g = lane >> 3, r = lane & 7;
-  double* gs = scratch + (wave * 8 + g) * GS;  // [0,64) transpose, [64,72) gather, [72,80) u
+  double* gs = scratch + (wave * 8 + g) * GS;  // [0,64) transpose, [64,72) gather / u, [72,80) p
   const int nsw = c - 2;                       // sweeps 0 .. c-3
   bool aborted = false;
   for (int G = wave; G * 8 < nsw && !aborted; G += nwaves) {
@@ -331,27 +346,24 @@ __global__ __launch_bounds__(RB_CH_WAVES * 64) void rr_chase_kernel(
     for (int T = 0;; ++T) {
       if (__ballot(!fin) == 0) break;
       const int j = T - 2 * g;
+      // window of this step, in select form (inactive groups get MR = NC = 0: every access
+      // then goes to the spare slot, the reflector is the identity)
       bool act = !fin && j >= 0;
-      int R0 = 0, MR = 0, C0 = 0, NC = 0;
-      if (act) {
-        if (j == 0) {
-          R0 = i + 1;
-          MR = m;
-          C0 = i;
-          NC = 1;
-        } else {
-          R0 = s + m;
-          C0 = s;
-          NC = m;
-          if (R0 >= c) {
-            fin = true;
-            act = false;
-            if (r == 0) __hip_atomic_store(&done[i], RB_DONE_ALL, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-          } else {
-            MR = (c - R0) < W ? (c - R0) : W;
-          }
-        }
+      const bool first = j == 0;
+      int R0 = first ? i + 1 : s + m;
+      const int C0 = first ? i : s;
+      int NC = first ? 1 : m;
+      int MR = first ? m : ((c - R0) < W ? (c - R0) : W);
+      if (act && !first && R0 >= c) {  // sweep done
+        fin = true;
+        act = false;
+        if (r == 0) __hip_atomic_store(&done[i], RB_DONE_ALL, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      if (!act) {
+        R0 = 0;
+        MR = 0;
+        NC = 0;
       }
       // the group's first sweep waits for the previous group's last sweep (another wave)
       if (act && g == 0 && i > 0) {
@@ -373,7 +385,7 @@ __global__ __launch_bounds__(RB_CH_WAVES * 64) void rr_chase_kernel(
         break;
       }
       rb_cbar();
-      if (act) {
+      {
         const bool rv = r < MR;
         const int d0 = R0 - C0 + r;
         // branch-free window access: entries outside the window read / write the spare LDS
@@ -390,10 +402,7 @@ __global__ __launch_bounds__(RB_CH_WAVES * 64) void rr_chase_kernel(
           D[t] = okd ? dv : 0.0;
         }
         // right-apply the previous reflector (acts on O's columns)
-        double tt = 0.0;
-#pragma unroll
-        for (int t = 0; t < W; ++t) tt += O[t] * vp[t];
-        tt *= taup;
+        const double tt = taup * dot8(O, vp);
 #pragma unroll
         for (int t = 0; t < W; ++t) O[t] -= tt * vp[t];
         // reflector from O's first column
@@ -402,43 +411,39 @@ __global__ __launch_bounds__(RB_CH_WAVES * 64) void rr_chase_kernel(
         double x[W];
 #pragma unroll
         for (int t = 0; t < W; ++t) x[t] = gs[64 + t];
-        double sig = 0.0;
-#pragma unroll
-        for (int t = 1; t < W; ++t) sig += x[t] * x[t];
+        const double sig = ((x[1] * x[1] + x[2] * x[2]) + (x[3] * x[3] + x[4] * x[4])) +
+                           ((x[5] * x[5] + x[6] * x[6]) + x[7] * x[7]);
         double tau2, beta2, scale2;
         house_params(x[0], sig, tau2, beta2, scale2);
         double v2[W];
 #pragma unroll
         for (int t = 0; t < W; ++t) v2[t] = (t == 0) ? 1.0 : x[t] * scale2;
         const double v2r = (r == 0) ? 1.0 : (rv ? O[0] * scale2 : 0.0);
-        // left-apply: u_q = sum_r v2_r O[r][q] through an LDS transpose
+        // one LDS round trip for both the transpose of v2r O (left-apply: u_q = sum_r v2_r
+        // O[r][q]) and p = tau D v2 (two-sided update of D)
+        const double pr = tau2 * dot8(D, v2);
+        rb_cbar();
 #pragma unroll
         for (int t = 0; t < W; ++t) gs[r * 8 + t] = v2r * O[t];
+        gs[72 + r] = pr;
         rb_cbar();
-        double um = 0.0;
+        double ut[W], ps[W];
 #pragma unroll
-        for (int t = 0; t < W; ++t) um += gs[t * 8 + r];
-        gs[72 + r] = um;
+        for (int t = 0; t < W; ++t) {
+          ut[t] = gs[t * 8 + r];
+          ps[t] = gs[72 + t];
+        }
+        const double um = ((ut[0] + ut[1]) + (ut[2] + ut[3])) + ((ut[4] + ut[5]) + (ut[6] + ut[7]));
+        const double ks = dot8(ps, v2);
+        rb_cbar();
+        gs[64 + r] = um;
         rb_cbar();
 #pragma unroll
-        for (int t = 0; t < W; ++t) O[t] -= tau2 * v2r * gs[72 + t];
+        for (int t = 0; t < W; ++t) O[t] -= tau2 * v2r * gs[64 + t];
         O[0] = (r == 0) ? beta2 : 0.0;
 #pragma unroll
         for (int t = 0; t < W; ++t) L[(rv && t < NC) ? (R0 + r) * S + (d0 - t) : spare] = O[t];
         // two-sided update of D
-        double pr = 0.0;
-#pragma unroll
-        for (int t = 0; t < W; ++t) pr += D[t] * v2[t];
-        pr *= tau2;
-        rb_cbar();
-        gs[64 + r] = pr;
-        rb_cbar();
-        double ks = 0.0, ps[W];
-#pragma unroll
-        for (int t = 0; t < W; ++t) {
-          ps[t] = gs[64 + t];
-          ks += ps[t] * v2[t];
-        }
         const double K = 0.5 * tau2 * ks;
         const double wr = pr - K * v2r;
 #pragma unroll
@@ -446,17 +451,19 @@ __global__ __launch_bounds__(RB_CH_WAVES * 64) void rr_chase_kernel(
           D[t] -= v2r * (ps[t] - K * v2[t]) + wr * v2[t];
           L[(rv && t < MR && t <= r) ? (R0 + r) * S + (r - t) : spare] = D[t];
         }
-        // record the reflector for the back-transform
-        double* slot = refl + ((int64_t)i * jm + j) * 9;
-        slot[r] = v2r;
-        if (r == 0) slot[8] = tau2;
+        if (act) {
+          // record the reflector for the back-transform
+          double* slot = refl + ((int64_t)i * jm + j) * 9;
+          slot[r] = v2r;
+          if (r == 0) slot[8] = tau2;
 #pragma unroll
-        for (int t = 0; t < W; ++t) vp[t] = v2[t];
-        taup = tau2;
-        s = R0;
-        m = MR;
+          for (int t = 0; t < W; ++t) vp[t] = v2[t];
+          taup = tau2;
+          s = R0;
+          m = MR;
+        }
         rb_cbar();
-        if (r == 0)
+        if (act && r == 0)
           __hip_atomic_store(&done[i], j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       rb_cbar();
