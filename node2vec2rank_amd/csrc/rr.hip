@@ -474,6 +474,14 @@ __global__ __launch_bounds__(RR_BIS_THREADS) void rr_bisect_kernel(const double*
   if (tid == 0) w[j] = 0.5 * (lo + hi);
 }
 
+// reciprocal to fp64 accuracy: v_rcp_f64 and two Newton steps (off the IEEE-division path)
+__device__ __forceinline__ double inv_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(r, fma(-x, r, 1.0), r);
+  r = fma(r, fma(-x, r, 1.0), r);
+  return r;
+}
+
 // rr_inviter_kernel: eigenvectors of T for the p wanted eigenvalues (descending).  One
 // 64-thread workgroup per cluster start (gap to the previous eigenvalue > clus = 1e-9 ||T||;
 // fp64 inverse iteration leaves vectors of eigenvalues delta apart orthogonal to
@@ -487,6 +495,7 @@ __global__ __launch_bounds__(64) void rr_inviter_kernel(const double* __restrict
                                                         int p, const double* __restrict__ w,
                                                         double clus_rel, double* __restrict__ Y) {
   __shared__ double dgv[RR_MAXC], u1[RR_MAXC], u2[RR_MAXC], lm[RR_MAXC], x[RR_MAXC];
+  __shared__ double rdg[RR_MAXC], ds[RR_MAXC], es[RR_MAXC];
   __shared__ unsigned char sw[RR_MAXC];
   __shared__ double proj[64];
   __shared__ double nrm_s;
@@ -498,6 +507,11 @@ __global__ __launch_bounds__(64) void rr_inviter_kernel(const double* __restrict
     tn = fmax(tn, fabs(d[i]) + r);
   }
   for (int o = 32; o >= 1; o >>= 1) tn = fmax(tn, __shfl_xor(tn, o, 64));
+  for (int i = lane; i < c; i += 64) {
+    ds[i] = d[i];
+    es[i] = i < c - 1 ? e[i] : 0.0;
+  }
+  __syncthreads();
   const double clus = clus_rel * fmax(tn, 1e-300);
   if (j0 > 0 && fabs(w[j0 - 1] - w[j0]) <= clus) return;  // not a cluster start (uniform)
   const double tiny = fmax(2.220446049250313e-16 * tn, 1e-300);
@@ -508,67 +522,101 @@ __global__ __launch_bounds__(64) void rr_inviter_kernel(const double* __restrict
       x[i] = (double)(hsh >> 11) * (1.0 / 9007199254740992.0) - 0.5;
     }
     if (lane == 0) {  // LU of T - lam I with partial pivoting (one extra superdiagonal)
-      double a = d[0] - lam;
-      double cc = (c > 1) ? e[0] : 0.0;
-      for (int i = 0; i < c - 1; ++i) {
-        const double sub = e[i];
-        const double nd = d[i + 1] - lam;
-        const double ns = (i + 1 < c - 1) ? e[i + 1] : 0.0;
-        if (fabs(a) >= fabs(sub)) {
-          if (fabs(a) < tiny) a = (a < 0 ? -tiny : tiny);
-          const double m = sub / a;
+      // branch-free steps; the pivot reciprocal (v_rcp_f64 + Newton) replaces the division on
+      // the serial chain; d / e come from LDS 8 steps ahead of the chain
+      double a = ds[0] - lam;
+      double cc = (c > 1) ? es[0] : 0.0;
+      for (int i0 = 0; i0 < c - 1; i0 += 8) {
+        double dn[8], en[8], en1[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = i0 + u;
+          dn[u] = ds[i + 1 < c ? i + 1 : c - 1];
+          en[u] = es[i < c - 1 ? i : 0];
+          en1[u] = (i + 1 < c - 1) ? es[i + 1] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = i0 + u;
+          if (i >= c - 1) break;
+          const double sub = en[u], nd = dn[u] - lam, ns = en1[u];
+          const bool swp = fabs(a) < fabs(sub);
+          double ag = a;
+          if (fabs(ag) < tiny) ag = (ag < 0 ? -tiny : tiny);
+          const double piv = swp ? sub : ag;
+          const double m = (swp ? a : sub) * inv_nr(piv);
           lm[i] = m;
-          sw[i] = 0;
-          dgv[i] = a;
-          u1[i] = cc;
-          u2[i] = 0.0;
-          a = nd - m * cc;
-          cc = ns;
-        } else {
-          const double m = a / sub;
-          lm[i] = m;
-          sw[i] = 1;
-          dgv[i] = sub;
-          u1[i] = nd;
-          u2[i] = ns;
-          a = cc - m * nd;
-          cc = -m * ns;
+          sw[i] = swp ? 1 : 0;
+          dgv[i] = piv;
+          u1[i] = swp ? nd : cc;
+          u2[i] = swp ? ns : 0.0;
+          const double an = swp ? fma(-m, nd, cc) : fma(-m, cc, nd);
+          cc = swp ? -m * ns : ns;
+          a = an;
         }
       }
       if (fabs(a) < tiny) a = (a < 0 ? -tiny : tiny);
       dgv[c - 1] = a;
     }
     __syncthreads();
+    for (int i = lane; i < c; i += 64) rdg[i] = 1.0 / dgv[i];
+    __syncthreads();
     // two inverse iterations: the shift is the bisection eigenvalue (fp64-accurate), so the
     // first solve already amplifies the wanted direction by ~1/eps; the second cleans up
     for (int it = 0; it < 2; ++it) {
       if (lane == 0) {
+        // forward substitution with the interchanges (x[i+1..] read 8 ahead of the chain)
         double cur = x[0];
-        for (int i = 0; i < c - 1; ++i) {  // forward substitution with the interchanges
-          double nxt = x[i + 1];
-          if (sw[i]) {
-            const double t = cur;
-            cur = nxt;
-            nxt = t;
+        for (int i0 = 0; i0 < c - 1; i0 += 8) {
+          double xn[8], ln[8];
+          int sn[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u < c - 1 ? i0 + u : c - 2;
+            xn[u] = x[i + 1];
+            ln[u] = lm[i];
+            sn[u] = sw[i];
           }
-          x[i] = cur;
-          cur = nxt - lm[i] * cur;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u;
+            if (i >= c - 1) break;
+            const double nxt = sn[u] ? cur : xn[u];
+            const double cv = sn[u] ? xn[u] : cur;
+            x[i] = cv;
+            cur = fma(-ln[u], cv, nxt);
+          }
         }
         x[c - 1] = cur;
-        double x1 = cur / dgv[c - 1];  // back substitution, x[i+1], x[i+2] in registers
+        // back substitution with the pivot reciprocals, x[i+1], x[i+2] in registers
+        double x1 = cur * rdg[c - 1];
         x[c - 1] = x1;
         double x2 = 0.0;
         if (c > 1) {
-          const double v = (x[c - 2] - u1[c - 2] * x1) / dgv[c - 2];
+          const double v = (x[c - 2] - u1[c - 2] * x1) * rdg[c - 2];
           x[c - 2] = v;
           x2 = x1;
           x1 = v;
         }
-        for (int i = c - 3; i >= 0; --i) {
-          const double v = (x[i] - u1[i] * x1 - u2[i] * x2) / dgv[i];
-          x[i] = v;
-          x2 = x1;
-          x1 = v;
+        for (int i0 = c - 3; i0 >= 0; i0 -= 8) {
+          double xv[8], a1[8], a2[8], rv[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int i = i0 - u >= 0 ? i0 - u : 0;
+            xv[u] = x[i];
+            a1[u] = u1[i];
+            a2[u] = u2[i];
+            rv[u] = rdg[i];
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int i = i0 - u;
+            if (i < 0) break;
+            const double v = fma(-a2[u], x2, fma(-a1[u], x1, xv[u])) * rv[u];
+            x[i] = v;
+            x2 = x1;
+            x1 = v;
+          }
         }
       }
       __syncthreads();
