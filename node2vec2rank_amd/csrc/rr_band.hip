@@ -489,95 +489,151 @@ __global__ __launch_bounds__(RB_CH_WAVES * 64) void rr_chase_kernel(
 // i+1+8j.., so B_i is block diagonal: lane j applies window j), then the X rows through the
 // arrow reflectors; written as fp32 S (c x p, ld ldS).  One wave per eigenvector; y is kept
 // residue-major in LDS (entry t at (t % 8) * sb + t / 8, sb odd), so the 8 entries of a window
-// are read by all lanes without bank conflicts; the reflectors of RB_BT_CH sweeps are staged
+// are read by all lanes without bank conflicts; the reflectors are staged
 // through LDS at a time.
-#define RB_BT_CH 16
-__global__ __launch_bounds__(64) void rr_band_back_kernel(const double* __restrict__ Y, int c,
-                                                          int p, const double* __restrict__ refl,
-                                                          int jm, int kp,
-                                                          const double* __restrict__ Varr,
-                                                          const double* __restrict__ taua,
-                                                          float* __restrict__ S, int ldS) {
+// RB_BT_VW eigenvectors per workgroup (one wave each).  The reflectors (chase sweeps in chunks
+// of nch sweeps, then the arrow reflectors in chunks of whole Varr rows) stream through two LDS
+// buffers shared by the workgroup: while the waves apply chunk q, every thread already holds its
+// part of chunk q + 1 in registers (up to RB_BT_PF 16-B loads in flight), stored to the other
+// buffer after the apply.  Window accesses are branch-free (masked lanes use a spare LDS slot);
+// consecutive sweeps of one wave are ordered by the wave's in-order LDS execution.
+#define RB_BT_VW 4
+#define RB_BT_PF 16
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void rb_stage_load(const double* __restrict__ src, int nd, f64x2* r) {
+  const int n2 = nd >> 1;
+#pragma unroll
+  for (int u = 0; u < RB_BT_PF; ++u) {
+    const int e = (int)threadIdx.x + u * 256;
+    r[u] = reinterpret_cast<const f64x2*>(src)[e < n2 ? e : 0];
+  }
+}
+__device__ __forceinline__ void rb_stage_store(double* dst, const double* __restrict__ src, int nd,
+                                               const f64x2* r) {
+  const int n2 = nd >> 1;
+#pragma unroll
+  for (int u = 0; u < RB_BT_PF; ++u) {
+    const int e = (int)threadIdx.x + u * 256;
+    if (e < n2) reinterpret_cast<f64x2*>(dst)[e] = r[u];
+  }
+  if ((nd & 1) && threadIdx.x == 0) dst[nd - 1] = src[nd - 1];
+}
+
+__global__ __launch_bounds__(256) void rr_band_back_kernel(const double* __restrict__ Y, int c,
+                                                           int p, const double* __restrict__ refl,
+                                                           int jm, int kp,
+                                                           const double* __restrict__ Varr,
+                                                           const double* __restrict__ taua,
+                                                           float* __restrict__ S, int ldS, int nch,
+                                                           int bufd) {
   constexpr int W = RB_W;
   extern __shared__ double lds[];
   const int sb = (c / W) | 1;
-  double* y = lds;                              // [8][sb]
-  double* rf = y + (size_t)W * sb;              // [RB_BT_CH][jm * 9]
-  const int lane = threadIdx.x;
-  const int vec = blockIdx.x;
-  for (int t = lane; t < c; t += 64) y[(t & 7) * sb + (t >> 3)] = Y[(int64_t)vec * c + t];
+  const int ys = W * sb + 8;  // per-wave y image + spare slots
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int vec = blockIdx.x * RB_BT_VW + wave;
+  const bool vok = vec < p;
+  double* y = lds + wave * ys;
+  const int spare = W * sb + (lane & 7);
+  double* tau_s = lds + RB_BT_VW * ys;               // arrow reflector taus (RB_MAXNA)
+  double* buf0 = tau_s + RB_MAXNA;                   // two reflector buffers of bufd doubles
+  for (int t = lane; t < c; t += 64) y[(t & 7) * sb + (t >> 3)] = vok ? Y[(int64_t)vec * c + t] : 0.0;
+  if (lane < 8) y[W * sb + lane] = 0.0;  // spare slots stay finite (masked products are 0)
+  const int na = kp > 0 ? kp + W : 0, nref = kp > 0 ? na - W - 1 : 0;
+  for (int k = tid; k < nref; k += 256) tau_s[k] = taua[k];
   const int nsw = c - 2;  // sweeps 0 .. c-3
-  for (int ch = ((nsw - 1) / RB_BT_CH) * RB_BT_CH; ch >= 0; ch -= RB_BT_CH) {
-    const int nch = (nsw - ch) < RB_BT_CH ? (nsw - ch) : RB_BT_CH;
-    __syncthreads();
-    {  // stage the chunk's reflectors: 16-B loads, 8 in flight per lane
-      const int n2 = (nch * jm * 9) / 2;
-      const double2* src = reinterpret_cast<const double2*>(refl + (int64_t)ch * jm * 9);
-      double2* dst = reinterpret_cast<double2*>(rf);
-      int e = lane;
-      for (; e + 7 * 64 < n2; e += 8 * 64) {
-        double2 t[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) t[u] = src[e + u * 64];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) dst[e + u * 64] = t[u];
-      }
-      for (; e < n2; e += 64) dst[e] = src[e];
-      if (lane == 0 && (nch * jm * 9) % 2) rf[nch * jm * 9 - 1] = refl[(int64_t)(ch + nch) * jm * 9 - 1];
+  const int nqc = (nsw - 1) / nch + 1;
+  const int ra = na > 0 ? bufd / na : 1;  // arrow reflectors per chunk
+  const int nqa = nref > 0 ? (nref + ra - 1) / ra : 0;
+  const int nq = nqc + nqa;
+  // chunk q: chase chunks (descending sweeps) then arrow chunks (descending k)
+  auto chunk = [&](int q, const double*& src, int& nd, int& lo, int& cnt) {
+    if (q < nqc) {
+      lo = ((nsw - 1) / nch - q) * nch;
+      cnt = (nsw - lo) < nch ? (nsw - lo) : nch;
+      src = refl + (int64_t)lo * jm * 9;
+      nd = cnt * jm * 9;
+    } else {
+      const int qa = q - nqc;
+      const int hi = nref - qa * ra;
+      lo = hi - ra > 0 ? hi - ra : 0;
+      cnt = hi - lo;
+      src = Varr + (int64_t)lo * na;
+      nd = cnt * na;
     }
-    __syncthreads();
-    for (int ii = nch - 1; ii >= 0; --ii) {
-      const int i = ch + ii;
-      if (c - 1 - i < 2) continue;
-      const int nsteps = (c - (i + 1) + W - 1) / W;
-      for (int j = lane; j < nsteps; j += 64) {
-        const int s = i + 1 + j * W;
-        const int m = (c - s) < W ? (c - s) : W;
-        const double* rv = rf + ((int64_t)ii * jm + j) * 9;
-        const double tau = rv[8];
-        double yv[W], vv[W];
-        double dot = 0.0;
-#pragma unroll
-        for (int t = 0; t < W; ++t) {
-          const int idx = s + t;
-          vv[t] = (t < m) ? rv[t] : 0.0;
-          yv[t] = (t < m) ? y[(idx & 7) * sb + (idx >> 3)] : 0.0;
-          dot += vv[t] * yv[t];
-        }
-        dot *= tau;
-#pragma unroll
-        for (int t = 0; t < W; ++t) {
-          const int idx = s + t;
-          if (t < m) y[(idx & 7) * sb + (idx >> 3)] = yv[t] - dot * vv[t];
-        }
-      }
-      __syncthreads();
-    }
-  }
-  // X rows: y[0..na) <- J Q J y[0..na)
-  if (kp > 0) {
-    const int na = kp + W, nref = na - W - 1;
-    for (int k = nref - 1; k >= 0; --k) {
-      const double tau = taua[k];
-      if (tau == 0.0) continue;
-      const int m = na - k - W;
-      const double* vk = Varr + (int64_t)k * na;
-      double dot = 0.0;
-      for (int t = lane; t < m; t += 64) {
-        const int idx = na - 1 - k - W - t;
-        dot += vk[t] * y[(idx & 7) * sb + (idx >> 3)];
-      }
-      dot = wave_sum_f64(dot);
-      for (int t = lane; t < m; t += 64) {
-        const int idx = na - 1 - k - W - t;
-        y[(idx & 7) * sb + (idx >> 3)] -= tau * dot * vk[t];
-      }
-      __syncthreads();
-    }
+  };
+  f64x2 pf[RB_BT_PF];
+  {
+    const double* src;
+    int nd, lo, cnt;
+    chunk(0, src, nd, lo, cnt);
+    rb_stage_load(src, nd, pf);
+    rb_stage_store(buf0, src, nd, pf);
   }
   __syncthreads();
-  for (int t = lane; t < c; t += 64)
-    S[(int64_t)t * ldS + vec] = (float)y[(t & 7) * sb + (t >> 3)];
+  for (int q = 0; q < nq; ++q) {
+    double* cur = buf0 + (q & 1) * bufd;
+    double* nxt = buf0 + ((q + 1) & 1) * bufd;
+    const double* nsrc = refl;
+    int nnd = 0, nlo, ncnt;
+    if (q + 1 < nq) chunk(q + 1, nsrc, nnd, nlo, ncnt);
+    rb_stage_load(nsrc, nnd, pf);  // in flight during the apply below (nothing after the last)
+    const double* src;
+    int nd, lo, cnt;
+    chunk(q, src, nd, lo, cnt);
+    if (vok && q < nqc) {
+      for (int ii = cnt - 1; ii >= 0; --ii) {
+        const int i = lo + ii;
+        const int nsteps = (c - (i + 1) + W - 1) / W;
+        const bool act = lane < nsteps && c - 1 - i >= 2;
+        const int j = act ? lane : 0;
+        const int s = i + 1 + j * W;
+        const int m = (c - s) < W ? (c - s) : W;
+        const double* rv = cur + ((int64_t)ii * jm + j) * 9;
+        const double tau = act ? rv[8] : 0.0;
+        double yv[W], vv[W];
+        int ad[W];
+#pragma unroll
+        for (int t = 0; t < W; ++t) {
+          // entry s + t = (i + 1 + t) + 8 j: its residue-major slot is a sweep-uniform base + j
+          const int it = i + 1 + t;
+          const bool ok = act && t < m;
+          ad[t] = ok ? (it & 7) * sb + (it >> 3) + j : spare;
+          const double rvt = rv[t];
+          vv[t] = ok ? rvt : 0.0;
+          yv[t] = y[ad[t]];
+        }
+        const double dot = tau * ((fma(vv[0], yv[0], vv[1] * yv[1]) + fma(vv[2], yv[2], vv[3] * yv[3])) +
+                                  (fma(vv[4], yv[4], vv[5] * yv[5]) + fma(vv[6], yv[6], vv[7] * yv[7])));
+#pragma unroll
+        for (int t = 0; t < W; ++t) y[ad[t]] = yv[t] - dot * vv[t];
+        rb_cbar();
+      }
+    } else if (vok) {  // X rows: y[0..na) <- J Q J y[0..na), reflectors k = lo + cnt - 1 .. lo
+      for (int k = lo + cnt - 1; k >= lo; --k) {
+        const double tau = tau_s[k];
+        if (tau == 0.0) continue;
+        const int m = na - k - W;
+        const double* vk = cur + (int64_t)(k - lo) * na;
+        double dot = 0.0;
+        for (int t = lane; t < m; t += 64) {
+          const int idx = na - 1 - k - W - t;
+          dot += vk[t] * y[(idx & 7) * sb + (idx >> 3)];
+        }
+        dot = wave_sum_f64(dot);
+        for (int t = lane; t < m; t += 64) {
+          const int idx = na - 1 - k - W - t;
+          y[(idx & 7) * sb + (idx >> 3)] -= tau * dot * vk[t];
+        }
+        rb_cbar();
+      }
+    }
+    rb_stage_store(nxt, nsrc, nnd, pf);
+    __syncthreads();
+  }
+  if (vok)
+    for (int t = lane; t < c; t += 64)
+      S[(int64_t)t * ldS + vec] = (float)y[(t & 7) * sb + (t >> 3)];
 }
 
 extern "C" hipError_t n2v2r_launch_rr_bisect(const double* d, const double* e, int c, int p,
@@ -626,8 +682,19 @@ extern "C" hipError_t n2v2r_launch_rr_band(const double* hband, int c, int kp, d
   if (er != hipSuccess) return er;
   er = n2v2r_launch_rr_tri_inviter(d, e, c, p, theta, Y, stream);
   if (er != hipSuccess) return er;
-  const size_t lbt = sizeof(double) * ((size_t)RB_W * ((c / RB_W) | 1) + (size_t)RB_BT_CH * jm * 9);
-  hipLaunchKernelGGL(rr_band_back_kernel, dim3((unsigned)p), dim3(64), lbt, stream, Y, c, p, refl,
-                     jm, kp, Varr, taua, S, ldS);
+  // reflector chunk: an even number of sweeps (16-B aligned sources) within the register stage
+  int nch = (2 * 256 * RB_BT_PF) / (jm * 9);
+  if (nch > 16) nch = 16;
+  nch &= ~1;
+  if (nch < 2) return hipErrorInvalidValue;
+  int bufd = nch * jm * 9;
+  if (kp > 0 && bufd < kp + RB_W) bufd = kp + RB_W;
+  bufd = (bufd + 1) & ~1;
+  if (bufd > 2 * 256 * RB_BT_PF) return hipErrorInvalidValue;
+  const size_t lbt = sizeof(double) * ((size_t)RB_BT_VW * (RB_W * ((c / RB_W) | 1) + 8) +
+                                       RB_MAXNA + 2 * (size_t)bufd);
+  hipLaunchKernelGGL(rr_band_back_kernel, dim3((unsigned)((p + RB_BT_VW - 1) / RB_BT_VW)),
+                     dim3(64 * RB_BT_VW), lbt, stream, Y, c, p, refl, jm, kp, Varr, taua, S, ldS,
+                     nch, bufd);
   return hipGetLastError();
 }
