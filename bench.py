@@ -286,7 +286,8 @@ def main():
                    "parallelism": par},
         "roofline": {"bound": "hbm",
                      "kernel": ("dense_gemm_kernel<1> (A_k X, MFMA f32)" if cfg.get("dense")
-                                else f"spmm_csr_panel_kernel<{b},*>"),
+                                else ("spmm8_pipe_kernel<*> (b=8)" if b == 8
+                                      else f"spmm_csr_panel_kernel<{b},*>")),
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "algo_bytes_per_launch": spmm_bytes, "avg_launch_ms": round(spmm_ms, 5),

@@ -33,9 +33,12 @@ for line in open(f"{M}/ptrace.log"):
 rows = []
 traffic = None
 for k in fetch:
-    if "spmm_csr_panel_kernel" not in k:
+    if "spmm8_pipe_kernel" in k:
+        b = 8
+    elif "spmm_csr_panel_kernel" in k:
+        b = int(k.split("<")[1].split(",")[0])
+    else:
         continue
-    b = int(k.split("<")[1].split(",")[0])
     fkb, wkb = med(fetch[k]), med(write.get(k, [0.0]))
     hbm = 2 * fkb * 1024 + wkb * 1024
     avg_ns = float(trace[k]["AverageNs"])
