@@ -124,7 +124,6 @@ hipError_t n2v2r_launch_radix_pass(const uint64_t* kin, const int32_t* pin, uint
                                    hipStream_t stream);
 hipError_t n2v2r_launch_borda_finish(const int32_t* sorted_idx, int64_t n, int nseg, int ncols,
                                      int32_t* pos, int64_t* borda, hipStream_t stream);
-int n2v2r_host_sym_eig_top(int n, double* A, int p, double* w, double* Z);
 hipError_t n2v2r_launch_dense_gemm(const float* A, int64_t lda, int64_t rows, int64_t kdim,
                                    const float* X, int ldx, int b, float* Y, int64_t ldy,
                                    float beta, const float* colscale, float* work,
@@ -133,8 +132,6 @@ hipError_t n2v2r_launch_transpose(const float* in, int64_t ldi, int64_t rows, in
                                   float* out, int64_t ldo, hipStream_t stream);
 hipError_t n2v2r_launch_mismatch(const float* a, const float* b, int64_t ld, int64_t rows,
                                  int64_t cols, unsigned long long* count, hipStream_t stream);
-int n2v2r_host_tridiag_eig_top(int n, const double* d, const double* e, int p, double* w,
-                               double* Y);
 hipError_t n2v2r_launch_rr_tridiag(double* A, int c, double* d, double* e, double* tau, double* V,
                                    hipStream_t stream);
 hipError_t n2v2r_launch_rr_tri_eig(const double* d, const double* e, int c, int p, double* w,
@@ -822,7 +819,11 @@ struct Eig {
       h->gath.ensure(sizeof(float) * h->world * npad * b);
       h->ews.zg.ensure(sizeof(float) * (size_t)K * h->world * npad * b);
     }
+    // chunk partials: also the streaming Gram form at b = 8 (chunks of <= 8192 rows, rounded to
+    // a multiple of 8, (c + b) x b fp64 each)
     h->partial_elems = std::max<size_t>(4096ull * 1024ull, (size_t)c_max * c_max * 8);
+    h->partial_elems = std::max<size_t>(h->partial_elems,
+                                        (size_t)((n + 8191) / 8192 + 16) * (c_max + b) * b);
     h->partial.ensure(sizeof(double) * h->partial_elems);
     h->ews.gsmall.ensure(sizeof(double) * (size_t)c_max * c_max);
     h->ews.csmall.ensure(sizeof(float) * (size_t)c_max * c_max);

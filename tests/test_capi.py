@@ -50,27 +50,3 @@ def test_null_handle_is_rejected():
     assert lib.n2v2r_synchronize(None) == _lib.ERR_BAD_ARG
 
 
-@pytest.mark.parametrize("c,p", [(3, 3), (40, 12), (200, 64)])
-def test_host_rayleigh_ritz_eigensolver(c, p):
-    """The host Rayleigh-Ritz solver (tridiagonalisation + QL + inverse iteration) vs LAPACK,
-    including a cluster of near-equal eigenvalues."""
-    from node2vec2rank_amd import _lib
-    f = _lib.load().n2v2r_host_sym_eig_top
-    f.restype = ctypes.c_int
-    f.argtypes = [ctypes.c_int, np.ctypeslib.ndpointer(np.float64), ctypes.c_int,
-                  np.ctypeslib.ndpointer(np.float64), np.ctypeslib.ndpointer(np.float64)]
-    rng = np.random.default_rng(c)
-    Q, _ = np.linalg.qr(rng.standard_normal((c, c)))
-    ev = np.sort(rng.standard_normal(c)) * 10
-    k = min(4, c)
-    ev[-k:] = ev[-1] + np.arange(k) * 1e-9
-    a = (Q * ev) @ Q.T
-    a = 0.5 * (a + a.T)
-    A = a.copy()
-    w = np.zeros(p)
-    Z = np.zeros((c, p))
-    assert f(c, A, p, w, Z) == 0
-    wr = np.linalg.eigvalsh(a)[::-1][:p]
-    np.testing.assert_allclose(w, wr, atol=1e-11)
-    assert np.abs(a @ Z - Z * w).max() < 1e-10
-    assert np.abs(Z.T @ Z - np.eye(p)).max() < 1e-10
