@@ -86,18 +86,6 @@ __device__ __forceinline__ double rb_wave_sum(double v) {
   return v;
 }
 
-// sum over the workgroup, fixed order; red must hold 16 doubles
-__device__ __forceinline__ double rb_block_sum(double v, double* red) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  v = rb_wave_sum(v);
-  __syncthreads();
-  if (lane == 0) red[wave] = v;
-  __syncthreads();
-  double s = 0.0;
-  const int nw = blockDim.x >> 6;
-  for (int w = 0; w < nw; ++w) s += red[w];
-  return s;
-}
 
 }  // namespace
 
@@ -119,7 +107,6 @@ __global__ __launch_bounds__(1024) void rr_arrow_kernel(const double* __restrict
   double* R = lds;                  // packed lower, row i at i (i + 1) / 2
   double* u = R + na * (na + 1) / 2;
   double* p = u + na;
-  __shared__ double red[16];
   const int tid = threadIdx.x;
   for (int i = tid; i < na; i += blockDim.x) {
     const int a = na - 1 - i;
@@ -137,17 +124,21 @@ __global__ __launch_bounds__(1024) void rr_arrow_kernel(const double* __restrict
     }
   }
   __syncthreads();
+  // three block barriers per step: every wave forms the reflector itself (sig by its own wave
+  // sum, no block reduction), w = p - K u is formed on the fly, and column k is rewritten only
+  // after every wave has read it
+  const int lane = tid & 63;
   for (int k = 0; k + W + 1 < na; ++k) {
     const int m = na - k - W;  // reflector length (>= 2)
     const int nT = na - k - 1;
     const int o = k + 1;       // T[i][j] = R[o + i][o + j]
     double part = 0.0;
-    for (int t = 1 + tid; t < m; t += blockDim.x) {
+    for (int t = 1 + lane; t < m; t += 64) {
       const int row = k + W + t;
       const double x = R[row * (row + 1) / 2 + k];
       part += x * x;
     }
-    const double sig = rb_block_sum(part, red);
+    const double sig = rb_wave_sum(part);
     const double x0 = R[(k + W) * (k + W + 1) / 2 + k];
     double tau, beta, scale;
     house_params(x0, sig, tau, beta, scale);
@@ -160,14 +151,14 @@ __global__ __launch_bounds__(1024) void rr_arrow_kernel(const double* __restrict
         val = R[row * (row + 1) / 2 + k] * scale;
       }
       u[t] = val;
-    }
-    __syncthreads();
-    for (int t = tid; t < m; t += blockDim.x) {
-      const int row = k + W + t;
-      Varr[(int64_t)k * na + t] = u[W - 1 + t];
-      R[row * (row + 1) / 2 + k] = (t == 0) ? beta : 0.0;
+      if (t >= W - 1) Varr[(int64_t)k * na + (t - (W - 1))] = val;
     }
     if (tid == 0) taua[k] = tau;
+    __syncthreads();  // B1: u complete; column k read by everyone
+    for (int t = tid; t < m; t += blockDim.x) {
+      const int row = k + W + t;
+      R[row * (row + 1) / 2 + k] = (t == 0) ? beta : 0.0;
+    }
     if (tau == 0.0) {
       __syncthreads();
       continue;
@@ -207,29 +198,27 @@ __global__ __launch_bounds__(1024) void rr_arrow_kernel(const double* __restrict
       acc += __shfl_xor(acc, 2, 64);
       if (ri < nT && sl == 0) p[ri] = tau * acc;
     }
-    __syncthreads();
+    __syncthreads();  // B2: p complete
     double pp = 0.0;
-    for (int t = tid; t < nT; t += blockDim.x) pp += p[t] * u[t];
-    const double K = 0.5 * tau * rb_block_sum(pp, red);
-    for (int t = tid; t < nT; t += blockDim.x) p[t] -= K * u[t];  // w
-    __syncthreads();
+    for (int t = lane; t < nT; t += 64) pp += p[t] * u[t];
+    const double K = 0.5 * tau * rb_wave_sum(pp);  // every wave, same order: same K
     {
       const int ri = tid >> 2, sl = tid & 3;
       if (ri < nT) {
         const int gi = o + ri;
         double* rowp = R + gi * (gi + 1) / 2 + o;
-        const double ui = u[ri], wi = p[ri];
+        const double ui = u[ri], wi = p[ri] - K * u[ri];
         int j = sl;
         for (; j + 4 <= ri; j += 8) {
-          const double r0 = rowp[j] - (ui * p[j] + wi * u[j]);
-          const double r1 = rowp[j + 4] - (ui * p[j + 4] + wi * u[j + 4]);
+          const double r0 = rowp[j] - (ui * (p[j] - K * u[j]) + wi * u[j]);
+          const double r1 = rowp[j + 4] - (ui * (p[j + 4] - K * u[j + 4]) + wi * u[j + 4]);
           rowp[j] = r0;
           rowp[j + 4] = r1;
         }
-        for (; j <= ri; j += 4) rowp[j] -= ui * p[j] + wi * u[j];
+        for (; j <= ri; j += 4) rowp[j] -= ui * (p[j] - K * u[j]) + wi * u[j];
       }
     }
-    __syncthreads();
+    __syncthreads();  // B3: step done
   }
   for (int e = tid; e < na * (W + 1); e += blockDim.x) {
     const int a = e / (W + 1), kd = e % (W + 1);
