@@ -979,6 +979,13 @@ struct Eig {
         --cycle;
         continue;
       }
+      for (int j = 0; j < keep; ++j)  // a non-finite Ritz pair cannot recover: stop with details
+        if (!std::isfinite(wh[j]) || (j < d && !std::isfinite(res2[j])))
+          throw StatusFail{N2V2R_ERR_NO_CONVERGENCE,
+                           "non-finite Ritz pair " + std::to_string(j) + " at cycle " +
+                               std::to_string(cycle) + " (c " + std::to_string(c) + ", b " +
+                               std::to_string(b) + (dense_rr ? ", dense" : ", banded") +
+                               " Rayleigh-Ritz, theta " + std::to_string(wh[j]) + ")"};
       maxres = 0;
       conv = 0;
       const double th1 = std::max(wh[0], 1e-300);

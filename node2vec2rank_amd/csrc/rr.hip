@@ -398,6 +398,14 @@ __global__ __launch_bounds__(256) void rr_backtransform_kernel(const double* __r
   }
 }
 
+// reciprocal to fp64 accuracy: v_rcp_f64 and two Newton steps (off the IEEE-division path)
+__device__ __forceinline__ double inv_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(r, fma(-x, r, 1.0), r);
+  r = fma(r, fma(-x, r, 1.0), r);
+  return r;
+}
+
 // ---- eigenpairs of the tridiagonal T on the GPU --------------------------------------------
 // rr_bisect_kernel: one workgroup per wanted eigenvalue (j-th largest, j < p).  Multisection
 // on the Gershgorin interval: each round the 256 threads evaluate the Sturm count (negative
@@ -448,7 +456,7 @@ __global__ __launch_bounds__(RR_BIS_THREADS) void rr_bisect_kernel(const double*
     if (fabs(q) < pivmin) q = -pivmin;
     neg += q < 0.0;
     for (int i = 1; i < c; ++i) {
-      q = (d[i] - x) - e2[i] / q;
+      q = (d[i] - x) - e2[i] * inv_nr(q);  // Newton reciprocal: shorter serial chain
       if (fabs(q) < pivmin) q = -pivmin;
       neg += q < 0.0;
     }
@@ -472,14 +480,6 @@ __global__ __launch_bounds__(RR_BIS_THREADS) void rr_bisect_kernel(const double*
     if (hi - lo <= 2.2e-16 * fmax(fabs(lo), fabs(hi))) break;
   }
   if (tid == 0) w[j] = 0.5 * (lo + hi);
-}
-
-// reciprocal to fp64 accuracy: v_rcp_f64 and two Newton steps (off the IEEE-division path)
-__device__ __forceinline__ double inv_nr(double x) {
-  double r = __builtin_amdgcn_rcp(x);
-  r = fma(r, fma(-x, r, 1.0), r);
-  r = fma(r, fma(-x, r, 1.0), r);
-  return r;
 }
 
 // rr_inviter_kernel: eigenvectors of T for the p wanted eigenvalues (descending).  One

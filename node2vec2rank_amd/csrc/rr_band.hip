@@ -286,7 +286,7 @@ __global__ __launch_bounds__(RB_CH_WAVES * 64) void rr_chase_kernel(
   const int na = kp > 0 ? kp + W : 0;
   const int j0 = kp / W;
   const int base1 = (kp + W) * W;
-  for (int e = tid; e < c * S; e += blockDim.x) L[e] = 0.0;
+  for (int e = tid; e < c * S + 2; e += blockDim.x) L[e] = 0.0;  // band + trash + zero slots
   for (int e = tid; e < c; e += blockDim.x) done[e] = 0;
   if (tid == 0) abort_flag = 0;
   __syncthreads();
@@ -377,18 +377,17 @@ __global__ __launch_bounds__(RB_CH_WAVES * 64) void rr_chase_kernel(
       {
         const bool rv = r < MR;
         const int d0 = R0 - C0 + r;
-        // branch-free window access: entries outside the window read / write the spare LDS
-        // slot `spare` (past the band) and are masked to zero, so the 16 loads issue together
-        const int spare = c * S;
+        // branch-free window access: entries outside the window read the zero slot `zslot`
+        // (never written) and write the trash slot `spare` (both past the band), so the 16
+        // loads issue together and need no masking
+        const int spare = c * S, zslot = c * S + 1;
         double O[W], D[W];
 #pragma unroll
         for (int t = 0; t < W; ++t) {
           const int hi = r > t ? r : t, lo = r > t ? t : r;
           const bool oko = rv && t < NC, okd = rv && t < MR;
-          const double ov = L[oko ? (R0 + r) * S + (d0 - t) : spare];
-          const double dv = L[okd ? (R0 + hi) * S + (hi - lo) : spare];
-          O[t] = oko ? ov : 0.0;
-          D[t] = okd ? dv : 0.0;
+          O[t] = L[oko ? (R0 + r) * S + (d0 - t) : zslot];
+          D[t] = L[okd ? (R0 + hi) * S + (hi - lo) : zslot];
         }
         // right-apply the previous reflector (acts on O's columns)
         const double tt = taup * dot8(O, vp);
