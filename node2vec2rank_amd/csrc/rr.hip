@@ -515,6 +515,79 @@ __global__ __launch_bounds__(64) void rr_inviter_kernel(const double* __restrict
   const double clus = clus_rel * fmax(tn, 1e-300);
   if (j0 > 0 && fabs(w[j0 - 1] - w[j0]) <= clus) return;  // not a cluster start (uniform)
   const double tiny = fmax(2.220446049250313e-16 * tn, 1e-300);
+  if (j0 + 1 >= p || fabs(w[j0] - w[j0 + 1]) > clus) {
+    // isolated eigenvalue: the twisted factorisation T - lam I = N_r Delta_r N_r^T (top-down
+    // LDL^T in lane 0 and bottom-up UDU^T in lane 1, in parallel), twist r = argmin |gamma_r|,
+    // z_r = 1 and two outward product recurrences: two serial chains of c steps instead of the
+    // pivoted LU and two inverse-iteration solves.  A non-finite z falls back to those below.
+    const double lam = w[j0];
+    if (lane == 0) {
+      double D = ds[0] - lam;
+      for (int i = 0; i < c - 1; ++i) {
+        if (fabs(D) < tiny) D = (D < 0 ? -tiny : tiny);
+        dgv[i] = D;
+        const double L = es[i] * inv_nr(D);
+        lm[i] = L;
+        D = fma(-L, es[i], ds[i + 1] - lam);
+      }
+      if (fabs(D) < tiny) D = (D < 0 ? -tiny : tiny);
+      dgv[c - 1] = D;
+    } else if (lane == 1) {
+      double Dt = ds[c - 1] - lam;
+      for (int i = c - 2; i >= 0; --i) {
+        if (fabs(Dt) < tiny) Dt = (Dt < 0 ? -tiny : tiny);
+        u2[i + 1] = Dt;
+        const double U = es[i] * inv_nr(Dt);
+        u1[i] = U;
+        Dt = fma(-U, es[i], ds[i] - lam);
+      }
+      if (fabs(Dt) < tiny) Dt = (Dt < 0 ? -tiny : tiny);
+      u2[0] = Dt;
+    }
+    __syncthreads();
+    double best = 1e308;
+    int br = 0;
+    for (int i = lane; i < c; i += 64) {
+      const double g = fabs(dgv[i] + u2[i] - (ds[i] - lam));
+      if (g < best) {
+        best = g;
+        br = i;
+      }
+    }
+    for (int o = 32; o >= 1; o >>= 1) {  // argmin, ties to the lower index
+      const double ob = __shfl_xor(best, o, 64);
+      const int orr = __shfl_xor(br, o, 64);
+      if (ob < best || (ob == best && orr < br)) {
+        best = ob;
+        br = orr;
+      }
+    }
+    if (lane == 0) {
+      double z = 1.0;
+      x[br] = 1.0;
+      for (int i = br - 1; i >= 0; --i) {
+        z = -lm[i] * z;
+        x[i] = z;
+      }
+    } else if (lane == 1) {
+      double z = 1.0;
+      for (int i = br; i < c - 1; ++i) {
+        z = -u1[i] * z;
+        x[i + 1] = z;
+      }
+    }
+    __syncthreads();
+    double s2 = 0.0;
+    for (int i = lane; i < c; i += 64) s2 += x[i] * x[i];
+    for (int o = 32; o >= 1; o >>= 1) s2 += __shfl_xor(s2, o, 64);
+    if (isfinite(s2) && s2 > 0.0) {  // uniform
+      const double inv = 1.0 / sqrt(s2);
+      double* yj = Y + (int64_t)j0 * c;
+      for (int i = lane; i < c; i += 64) yj[i] = x[i] * inv;
+      return;
+    }
+    __syncthreads();
+  }
   for (int j = j0; j < p && (j == j0 || fabs(w[j - 1] - w[j]) <= clus); ++j) {
     const double lam = w[j];
     for (int i = lane; i < c; i += 64) {
