@@ -346,7 +346,6 @@ __global__ __launch_bounds__(256) void ts_tn_lines_kernel(BlockList A, const flo
 // v = bitrev5(rl) of its half, and the wave writes its 64 fp64 partials as one contiguous run.
 // Chunks with the same rows run on one XCD (nchunks % 8 == 0, workgroup id = y * nchunks + x),
 // so each XCD's L2 fetches a Z chunk once for all of its column groups.
-#define TS_U 4
 #define TS_MAX_CHUNK 8192
 template <int MASK>
 __device__ __forceinline__ double xor_lanes_f64(double v) {
@@ -368,6 +367,7 @@ __device__ __forceinline__ void rs_step(double* v, int rl) {
   }
 }
 
+template <int TS_U>
 __global__ __launch_bounds__(256) void ts_tn_stream_kernel(BlockList A, const float* __restrict__ Bz,
                                                            int64_t n, int64_t rows_per_chunk,
                                                            double* __restrict__ partial,
@@ -446,6 +446,13 @@ static bool tn_stream_form() {
   }();
   return v != 0;
 }
+static int tn_stream_u() {  // row-steps of 32 rows per iteration (N2V2R_TN_U: 4 or 8)
+  static const int v = [] {
+    const char* s = getenv("N2V2R_TN_U");
+    return s ? atoi(s) : 4;
+  }();
+  return v;
+}
 static int64_t tn_stream_waves() {
   static const int64_t v = [] {
     const char* s = getenv("N2V2R_TN_WAVES");
@@ -475,8 +482,12 @@ extern "C" hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B,
     const int64_t elems = (int64_t)ca * cb;
     const int64_t nchunks = s_chunks, rows_per_chunk = s_rows;
     const dim3 grid((unsigned)nchunks, (unsigned)((A.count + 3) / 4));
-    hipLaunchKernelGGL(ts_tn_stream_kernel, grid, dim3(256), 0, stream, A, B.blk[0], n,
-                       rows_per_chunk, partial, cond);
+    if (tn_stream_u() == 8)
+      hipLaunchKernelGGL(ts_tn_stream_kernel<8>, grid, dim3(256), 0, stream, A, B.blk[0], n,
+                         rows_per_chunk, partial, cond);
+    else
+      hipLaunchKernelGGL(ts_tn_stream_kernel<4>, grid, dim3(256), 0, stream, A, B.blk[0], n,
+                         rows_per_chunk, partial, cond);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((elems + 3) / 4)), dim3(256), 0,
@@ -1074,6 +1085,7 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   return __hiloint2double(hi, lo);
 }
 
+template <int QB>
 __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float* Zin, float* Zout,
                                                         const double* __restrict__ G, int c,
                                                         int64_t n, const int* cond, int* flags,
@@ -1169,15 +1181,15 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
     }
   }
   int q = 0;
-  for (; q + 4 <= Q.count; q += 4) {  // 4 blocks x 2 rows (8 x 16-B loads) in flight per step
-    f32x4 a4[4][2];
+  for (; q + QB <= Q.count; q += QB) {  // QB blocks x 2 rows (2 QB x 16-B loads) in flight
+    f32x4 a4[QB][2];
 #pragma unroll
-    for (int b4 = 0; b4 < 4; ++b4)
+    for (int b4 = 0; b4 < QB; ++b4)
 #pragma unroll
       for (int u = 0; u < 2; ++u)
         a4[b4][u] = *reinterpret_cast<const f32x4*>(Q.blk[q + b4] + rw[u] * 8 + 4 * h);
 #pragma unroll
-    for (int b4 = 0; b4 < 4; ++b4) {
+    for (int b4 = 0; b4 < QB; ++b4) {
       const float* g = cf + ((q + b4) * 8 + 4 * h) * 8;
 #pragma unroll
       for (int m = 0; m < 4; ++m)
@@ -1232,8 +1244,18 @@ extern "C" hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zi
   const size_t lds = sizeof(double) * ((size_t)(c + 8) * 8 + 256) + sizeof(float) * ((size_t)c * 8 + 64) + 16;
   if (lds > 64 * 1024) return hipErrorInvalidValue;
   const unsigned grid = (unsigned)((n + 255) / 256);
-  hipLaunchKernelGGL(pip_fused_kernel, dim3(grid ? grid : 1), dim3(256), lds, stream, Q, Zin, Zout, G, c, n,
-                     cond, flags, any_flag, save, save_row0, save_rows, sticky, seed, row0);
+  static const int qb = [] {
+    const char* s = getenv("N2V2R_PIP_QB");
+    return s ? atoi(s) : 4;
+  }();
+  if (qb == 8)
+    hipLaunchKernelGGL(pip_fused_kernel<8>, dim3(grid ? grid : 1), dim3(256), lds, stream, Q, Zin,
+                       Zout, G, c, n, cond, flags, any_flag, save, save_row0, save_rows, sticky,
+                       seed, row0);
+  else
+    hipLaunchKernelGGL(pip_fused_kernel<4>, dim3(grid ? grid : 1), dim3(256), lds, stream, Q, Zin,
+                       Zout, G, c, n, cond, flags, any_flag, save, save_row0, save_rows, sticky,
+                       seed, row0);
   return hipGetLastError();
 }
 

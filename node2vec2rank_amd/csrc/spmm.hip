@@ -303,6 +303,11 @@ static void launch_spmm_b(const SpmmArgs& args, hipStream_t stream) {
   const double want_l = LPN * avg / 3.5;
   int rpw = 1;
   while (rpw < 8 && 64 / (rpw * 2) >= LPN && 64.0 / (rpw * 2) >= want_l) rpw *= 2;
+  static const int rpw_env = [] {  // N2V2R_SPMM_RPW: rows per wave override (tuning runs)
+    const char* s = getenv("N2V2R_SPMM_RPW");
+    return s ? atoi(s) : 0;
+  }();
+  if (rpw_env == 1 || rpw_env == 2 || rpw_env == 4 || rpw_env == 8) rpw = rpw_env;
   switch (rpw) {
     case 8: if constexpr (64 / 8 >= LPN) { launch_spmm_t<B, 8>(args, stream); break; } [[fallthrough]];
     case 4: if constexpr (64 / 4 >= LPN) { launch_spmm_t<B, 4>(args, stream); break; } [[fallthrough]];
