@@ -516,7 +516,7 @@ __global__ __launch_bounds__(256) void rr_band_back_kernel(const double* __restr
                                                            int bufd) {
   constexpr int W = RB_W;
   extern __shared__ double lds[];
-  const int sb = (c / W) | 1;
+  const int sb = ((c + W - 1) / W + 1) | 1;  // odd, and past the last window's reach (c + 7)
   const int ys = W * sb + 8;  // per-wave y image + spare slots
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int vec = blockIdx.x * RB_BT_VW + wave;
@@ -525,8 +525,9 @@ __global__ __launch_bounds__(256) void rr_band_back_kernel(const double* __restr
   const int spare = W * sb + (lane & 7);
   double* tau_s = lds + RB_BT_VW * ys;               // arrow reflector taus (RB_MAXNA)
   double* buf0 = tau_s + RB_MAXNA;                   // two reflector buffers of bufd doubles
+  for (int t = lane; t < ys; t += 64) y[t] = 0.0;  // zero padding past c
+  rb_cbar();
   for (int t = lane; t < c; t += 64) y[(t & 7) * sb + (t >> 3)] = vok ? Y[(int64_t)vec * c + t] : 0.0;
-  if (lane < 8) y[W * sb + lane] = 0.0;  // spare slots stay finite (masked products are 0)
   const int na = kp > 0 ? kp + W : 0, nref = kp > 0 ? na - W - 1 : 0;
   for (int k = tid; k < nref; k += 256) tau_s[k] = taua[k];
   const int nsw = c - 2;  // sweeps 0 .. c-3
@@ -573,22 +574,20 @@ __global__ __launch_bounds__(256) void rr_band_back_kernel(const double* __restr
       for (int ii = cnt - 1; ii >= 0; --ii) {
         const int i = lo + ii;
         const int nsteps = (c - (i + 1) + W - 1) / W;
-        const bool act = lane < nsteps && c - 1 - i >= 2;
+        const bool act = lane < nsteps;
         const int j = act ? lane : 0;
-        const int s = i + 1 + j * W;
-        const int m = (c - s) < W ? (c - s) : W;
         const double* rv = cur + ((int64_t)ii * jm + j) * 9;
-        const double tau = act ? rv[8] : 0.0;
+        const double tau = rv[8];
         double yv[W], vv[W];
         int ad[W];
 #pragma unroll
         for (int t = 0; t < W; ++t) {
-          // entry s + t = (i + 1 + t) + 8 j: its residue-major slot is a sweep-uniform base + j
+          // entry (i + 1 + t) + 8 j: its residue-major slot is a sweep-uniform base + j.  The last
+          // window may reach past c: those slots are zero padding and the reflector entries
+          // there are zero (written so by the chase), so no mask; inactive lanes use the spare
           const int it = i + 1 + t;
-          const bool ok = act && t < m;
-          ad[t] = ok ? (it & 7) * sb + (it >> 3) + j : spare;
-          const double rvt = rv[t];
-          vv[t] = ok ? rvt : 0.0;
+          ad[t] = act ? (it & 7) * sb + (it >> 3) + j : spare;
+          vv[t] = rv[t];
           yv[t] = y[ad[t]];
         }
         const double dot = tau * ((fma(vv[0], yv[0], vv[1] * yv[1]) + fma(vv[2], yv[2], vv[3] * yv[3])) +
@@ -679,7 +678,7 @@ extern "C" hipError_t n2v2r_launch_rr_band(const double* hband, int c, int kp, d
   if (kp > 0 && bufd < kp + RB_W) bufd = kp + RB_W;
   bufd = (bufd + 1) & ~1;
   if (bufd > 2 * 256 * RB_BT_PF) return hipErrorInvalidValue;
-  const size_t lbt = sizeof(double) * ((size_t)RB_BT_VW * (RB_W * ((c / RB_W) | 1) + 8) +
+  const size_t lbt = sizeof(double) * ((size_t)RB_BT_VW * (RB_W * (((c + RB_W - 1) / RB_W + 1) | 1) + 8) +
                                        RB_MAXNA + 2 * (size_t)bufd);
   hipLaunchKernelGGL(rr_band_back_kernel, dim3((unsigned)((p + RB_BT_VW - 1) / RB_BT_VW)),
                      dim3(64 * RB_BT_VW), lbt, stream, Y, c, p, refl, jm, kp, Varr, taua, S, ldS,
