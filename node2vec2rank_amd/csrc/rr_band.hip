@@ -286,7 +286,7 @@ __global__ __launch_bounds__(RB_CH_WAVES * 64) void rr_chase_kernel(
   const int na = kp > 0 ? kp + W : 0;
   const int j0 = kp / W;
   const int base1 = (kp + W) * W;
-  for (int e = tid; e < c * S + 2; e += blockDim.x) L[e] = 0.0;  // band + trash + zero slots
+  for (int e = tid; e < (c + W) * S + 2; e += blockDim.x) L[e] = 0.0;  // band, 8 zero padding rows, trash + zero slots
   for (int e = tid; e < c; e += blockDim.x) done[e] = 0;
   if (tid == 0) abort_flag = 0;
   __syncthreads();
@@ -349,10 +349,14 @@ __global__ __launch_bounds__(RB_CH_WAVES * 64) void rr_chase_kernel(
         if (r == 0) __hip_atomic_store(&done[i], RB_DONE_ALL, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
       }
+      // inactive groups run the step on the zero padding rows c .. c+7 (every value stays 0;
+      // nothing of theirs is recorded)
+      int C0e = C0;
       if (!act) {
-        R0 = 0;
+        R0 = c;
+        C0e = c - W;
         MR = 0;
-        NC = 0;
+        NC = W;
       }
       // the group's first sweep waits for the previous group's last sweep (another wave)
       if (act && g == 0 && i > 0) {
@@ -375,26 +379,24 @@ __global__ __launch_bounds__(RB_CH_WAVES * 64) void rr_chase_kernel(
       }
       rb_cbar();
       {
-        const bool rv = r < MR;
-        const int d0 = R0 - C0 + r;
-        // branch-free window access: entries outside the window read the zero slot `zslot`
-        // (never written) and write the trash slot `spare` (both past the band), so the 16
-        // loads issue together and need no masking
-        const int spare = c * S, zslot = c * S + 1;
+        // rows past c are the zero padding rows (no row masks); O columns t >= NC read the
+        // zero slot `zslot`, masked stores go to the trash slot `spare`.  Per-lane bases:
+        // O[t] at oB - t; D[t] at dB1 - t (t <= r, row R0 + r) or dB2 + t (S + 1) (t > r, row R0 + t)
+        const int spare = (c + W) * S, zslot = (c + W) * S + 1;
+        const int oB = (R0 + r) * S + (R0 - C0e) + r;
+        const int dB1 = (R0 + r) * S + r, dB2 = R0 * S - r;
         double O[W], D[W];
 #pragma unroll
         for (int t = 0; t < W; ++t) {
-          const int hi = r > t ? r : t, lo = r > t ? t : r;
-          const bool oko = rv && t < NC, okd = rv && t < MR;
-          O[t] = L[oko ? (R0 + r) * S + (d0 - t) : zslot];
-          D[t] = L[okd ? (R0 + hi) * S + (hi - lo) : zslot];
+          O[t] = L[t < NC ? oB - t : zslot];
+          D[t] = L[t <= r ? dB1 - t : dB2 + t * (S + 1)];
         }
         // right-apply the previous reflector (acts on O's columns)
         const double tt = taup * dot8(O, vp);
 #pragma unroll
         for (int t = 0; t < W; ++t) O[t] -= tt * vp[t];
         // reflector from O's first column
-        gs[64 + r] = rv ? O[0] : 0.0;
+        gs[64 + r] = O[0];
         rb_cbar();
         double x[W];
 #pragma unroll
@@ -406,7 +408,7 @@ __global__ __launch_bounds__(RB_CH_WAVES * 64) void rr_chase_kernel(
         double v2[W];
 #pragma unroll
         for (int t = 0; t < W; ++t) v2[t] = (t == 0) ? 1.0 : x[t] * scale2;
-        const double v2r = (r == 0) ? 1.0 : (rv ? O[0] * scale2 : 0.0);
+        const double v2r = (r == 0) ? 1.0 : O[0] * scale2;
         // one LDS round trip for both the transpose of v2r O (left-apply: u_q = sum_r v2_r
         // O[r][q]) and p = tau D v2 (two-sided update of D)
         const double pr = tau2 * dot8(D, v2);
@@ -430,14 +432,14 @@ __global__ __launch_bounds__(RB_CH_WAVES * 64) void rr_chase_kernel(
         for (int t = 0; t < W; ++t) O[t] -= tau2 * v2r * gs[64 + t];
         O[0] = (r == 0) ? beta2 : 0.0;
 #pragma unroll
-        for (int t = 0; t < W; ++t) L[(rv && t < NC) ? (R0 + r) * S + (d0 - t) : spare] = O[t];
+        for (int t = 0; t < W; ++t) L[t < NC ? oB - t : spare] = O[t];
         // two-sided update of D
         const double K = 0.5 * tau2 * ks;
         const double wr = pr - K * v2r;
 #pragma unroll
         for (int t = 0; t < W; ++t) {
           D[t] -= v2r * (ps[t] - K * v2[t]) + wr * v2[t];
-          L[(rv && t < MR && t <= r) ? (R0 + r) * S + (r - t) : spare] = D[t];
+          L[t <= r ? dB1 - t : spare] = D[t];
         }
         if (act) {
           // record the reflector for the back-transform
@@ -660,7 +662,7 @@ extern "C" hipError_t n2v2r_launch_rr_band(const double* hband, int c, int kp, d
     hipError_t er = hipGetLastError();
     if (er != hipSuccess) return er;
   }
-  const size_t lch = sizeof(double) * ((size_t)c * (2 * RB_W + 1) + 8);  // + the spare slot
+  const size_t lch = sizeof(double) * ((size_t)(c + RB_W) * (2 * RB_W + 1) + 8);  // + padding rows, spare slots
   hipLaunchKernelGGL(rr_chase_kernel, dim3(1), dim3(RB_CH_WAVES * 64), lch, stream, hband, c, kp,
                      AB, d, e, refl, jm, err);
   hipError_t er = hipGetLastError();
