@@ -657,7 +657,11 @@ extern "C" hipError_t n2v2r_launch_rr_band(const double* hband, int c, int kp, d
   if (kp > 0) {
     const int na = kp + RB_W;
     const size_t lds = sizeof(double) * ((size_t)na * (na + 1) / 2 + 2 * (size_t)na);
-    hipLaunchKernelGGL(rr_arrow_kernel, dim3(1), dim3(1024), lds, stream, theta, kp, hband, AB,
+    // 4 threads per row of the trailing matrix (nT <= na - 1 rows), whole waves, >= 256
+    int nthr = ((4 * na + 63) / 64) * 64;
+    if (nthr < 256) nthr = 256;
+    if (nthr > 1024) nthr = 1024;
+    hipLaunchKernelGGL(rr_arrow_kernel, dim3(1), dim3(nthr), lds, stream, theta, kp, hband, AB,
                        Varr, taua);
     hipError_t er = hipGetLastError();
     if (er != hipSuccess) return er;
