@@ -244,6 +244,8 @@ def main():
     # partitioned)
     b = int(eig.get("block", 0)) or (32 if cfg.get("dense") else 8)  # the solver's panel width
     X = np.random.default_rng(0).standard_normal((cfg["n"], b)).astype(np.float32)
+    col_blocks = (not cfg.get("dense")) and eng.spmm_col_blocks(b)
+    nloc_rows = float(eng.dist_info()[3])
     _, spmm_ms, spmm_bytes = eng.bench_spmm(0, X, reps=50, want_y=False)
     del X
     achieved = spmm_bytes / (spmm_ms * 1e-3) / 1e9
@@ -286,12 +288,18 @@ def main():
                    "parallelism": par},
         "roofline": {"bound": "hbm",
                      "kernel": ("dense_gemm_kernel<1> (A_k X, MFMA f32)" if cfg.get("dense")
-                                else ("spmm8_pipe_kernel<*> (b=8)" if b == 8
-                                      else f"spmm_csr_panel_kernel<{b},*>")),
+                                else ("spmm8_cb_kernel<*> + cb_reduce_kernel (b=8, XCD-local "
+                                      "column blocks)" if col_blocks
+                                      else ("spmm8_pipe_kernel<*> (b=8)" if b == 8
+                                            else f"spmm_csr_panel_kernel<{b},*>"))),
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "algo_bytes_per_launch": spmm_bytes, "avg_launch_ms": round(spmm_ms, 5),
                      "gathered_bytes_per_launch": gathered,
+                     # column blocks: 8 partial outputs written and re-read by the reduce
+                     # (HBM bytes beyond the algorithmic ones)
+                     "partial_bytes_per_launch": (2.0 * 8 * 4 * 8 * nloc_rows
+                                                  if col_blocks else 0.0),
                      "gather_GBps": (None if gathered is None else
                                      round(gathered / (spmm_ms * 1e-3) / 1e9, 1))},
         "eig": {k: (float(f"{v:.4g}") if isinstance(v, float) else v) for k, v in stats.items()},

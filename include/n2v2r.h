@@ -163,6 +163,13 @@ int n2v2r_synchronize(n2v2r_handle* h);
 int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, const float* X,
                      float* Y, double* avg_ms, double* algo_bytes);
 
+/* 1 when UASE (and n2v2r_bench_spmm) use the XCD-local column-block SpMM at panel width b on
+ * this handle's layers (b = 8 CSR panels above 16 MB: each layer split into 8 column blocks,
+ * workgroup i mod 8 on XCD i mod 8 gathers only from block i mod 8, fixed-order reduce of the
+ * 8 partials; env N2V2R_SPMM_CB=1/0 forces it), else 0.  Then bench_spmm times the block
+ * launch plus the reduce. */
+int n2v2r_spmm_col_blocks(const n2v2r_handle* h, int b);
+
 /* Rayleigh-Ritz stage alone (tests): top-p eigenpairs of a host symmetric c x c fp64 matrix H
  * (3 <= c <= 768) through UASE's own path, all on the GPU (Householder tridiagonalisation,
  * bisection + inverse iteration on the tridiagonal, compact-WY back-transform).  w: p eigenvalues, descending; S: c x p

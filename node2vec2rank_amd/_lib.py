@@ -35,7 +35,7 @@ EXPORTED = [
     "n2v2r_get_left_embedding", "n2v2r_get_singular_values", "n2v2r_set_embedding",
     "n2v2r_rank", "n2v2r_get_distances", "n2v2r_get_borda", "n2v2r_rank_timing",
     "n2v2r_pairwise_distances", "n2v2r_borda_columns", "n2v2r_column_sums",
-    "n2v2r_synchronize", "n2v2r_bench_spmm",
+    "n2v2r_synchronize", "n2v2r_bench_spmm", "n2v2r_spmm_col_blocks",
     "n2v2r_comm_unique_id", "n2v2r_create_rccl", "n2v2r_simgroup_create",
     "n2v2r_simgroup_destroy", "n2v2r_create_sim", "n2v2r_dist_info", "n2v2r_set_layer_csr_rows",
     "n2v2r_rr_top", "n2v2r_rr_band_top", "n2v2r_set_layer_dense", "n2v2r_project",
@@ -117,6 +117,7 @@ def load(path: str | None = None):
             "n2v2r_bench_spmm": (_i, [_vp, _i, _i, _i, _i, _p(np.float32), _vp,
                                       ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_double)]),
+            "n2v2r_spmm_col_blocks": (_i, [_vp, _i]),
             "n2v2r_rr_top": (_i, [_vp, _i, _p(np.float64), _i, _p(np.float64), _p(np.float32)]),
             "n2v2r_rr_band_top": (_i, [_vp, _i, _i, _p(np.float64), ctypes.c_int64, _vp, _i,
                                        _p(np.float64), _p(np.float32)]),
@@ -429,6 +430,13 @@ class Engine:
                                               int(reps), X, yp, ctypes.byref(ms),
                                               ctypes.byref(by)), "bench_spmm")
         return Y, ms.value, by.value
+
+    def spmm_col_blocks(self, b: int = 8) -> bool:
+        """True when the SpMM at panel width b runs the XCD-local column-block form."""
+        r = self.lib.n2v2r_spmm_col_blocks(self.h, int(b))
+        if r < 0 or r > 1:
+            self._check(r, "spmm_col_blocks")
+        return r == 1
 
     def project(self, W, on: str = "columns"):
         """W^T W (on="columns") or W W^T (on="rows") of a dense m x n matrix, fp32 on the GPU."""

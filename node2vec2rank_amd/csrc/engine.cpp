@@ -55,6 +55,14 @@ struct SpmmArgs {
   int sum;
   const float* colscale;
 };
+#define CB_NB 8
+struct SpmmCbArgs {  // spmm.hip: column block j of one layer, partial j at P + j * pstride
+  CsrDev A[CB_NB];
+  const float* X;
+  int64_t ldx;
+  float* P;
+  int64_t pstride;
+};
 #define DIST_MAX_COLS 256
 struct DistPlan {
   int n_cols;
@@ -66,6 +74,12 @@ struct DistPlan {
 extern "C" {
 hipError_t n2v2r_launch_spmm(const SpmmArgs& args, int B, hipStream_t stream);
 hipError_t n2v2r_launch_row_sums(const CsrDev& A, float* out, hipStream_t stream);
+hipError_t n2v2r_launch_spmm_cb(const SpmmCbArgs& a, hipStream_t stream);
+hipError_t n2v2r_launch_cb_reduce(const float* P, int nparts, int64_t pstride, int64_t n,
+                                  float* out, int64_t ldo, hipStream_t stream);
+hipError_t n2v2r_launch_cb_count(const CsrDev& A, int64_t cw, int32_t* cnt, hipStream_t stream);
+hipError_t n2v2r_launch_cb_fill(const CsrDev& A, int64_t cw, const int64_t* rp, int32_t* idx,
+                                float* dat, hipStream_t stream);
 hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n, double* partial,
                               size_t partial_elems, double* out, const int* cond,
                               hipStream_t stream);
@@ -226,7 +240,71 @@ struct LayerDev {
     return CsrDev{t_indptr.as<int64_t>(), t_indices.as<int32_t>(), t_data.as<float>(), n_rows,
                   t_nnz, t_unit ? 1 : 0};
   }
+  // column-block form of A and (directed) A^T for the XCD-local SpMM (built on first use)
+  struct ColBlocks {
+    DevBuf rp, idx, dat;   // [CB_NB][n_rows + 1] absolute row pointers; entries; values
+    CsrDev blk[CB_NB];
+    int64_t ncols = 0;     // column count the blocks were cut for
+    bool built = false;
+  };
+  ColBlocks cb, cb_t;
+  void drop_col_blocks() {
+    for (ColBlocks* c : {&cb, &cb_t}) {
+      c->rp.release();
+      c->idx.release();
+      c->dat.release();
+      c->built = false;
+    }
+  }
 };
+
+// Split a CSR into CB_NB column blocks of ceil(ncols / CB_NB) columns (spmm.hip, XCD-local
+// SpMM): per-row counts on the GPU, row-pointer scan on the host, scatter on the GPU (each
+// row's entries keep their order).  One-off per layer; not part of a fit's timed work.
+void build_col_blocks(const CsrDev& A, int64_t ncols, LayerDev::ColBlocks& out, hipStream_t st) {
+  const int64_t n = A.n_rows;
+  const int64_t cw = (ncols + CB_NB - 1) / CB_NB;
+  DevBuf cnt;
+  cnt.ensure(sizeof(int32_t) * CB_NB * std::max<int64_t>(n, 1), st);
+  HIPCHK(n2v2r_launch_cb_count(A, cw, cnt.as<int32_t>(), st));
+  std::vector<int32_t> hc((size_t)CB_NB * n);
+  if (n > 0)
+    HIPCHK(hipMemcpyAsync(hc.data(), cnt.p, sizeof(int32_t) * hc.size(), hipMemcpyDeviceToHost,
+                          st));
+  HIPCHK(hipStreamSynchronize(st));
+  std::vector<int64_t> rp((size_t)CB_NB * (n + 1));
+  int64_t pos = 0;
+  for (int j = 0; j < CB_NB; ++j) {
+    int64_t* r = rp.data() + (size_t)j * (n + 1);
+    for (int64_t i = 0; i < n; ++i) {
+      r[i] = pos;
+      pos += hc[(size_t)j * n + i];
+    }
+    r[n] = pos;
+  }
+  if (pos != A.nnz) throw StatusFail{N2V2R_ERR_HIP, "column-block split lost entries"};
+  out.rp.ensure(sizeof(int64_t) * rp.size(), st);
+  out.idx.ensure(sizeof(int32_t) * std::max<int64_t>(A.nnz, 1), st);
+  if (!A.unit) out.dat.ensure(sizeof(float) * std::max<int64_t>(A.nnz, 1), st);
+  HIPCHK(hipMemcpyAsync(out.rp.p, rp.data(), sizeof(int64_t) * rp.size(), hipMemcpyHostToDevice,
+                        st));
+  HIPCHK(n2v2r_launch_cb_fill(A, cw, out.rp.as<int64_t>(), out.idx.as<int32_t>(),
+                              A.unit ? nullptr : out.dat.as<float>(), st));
+  HIPCHK(hipStreamSynchronize(st));
+  for (int j = 0; j < CB_NB; ++j) {
+    const int64_t* r = rp.data() + (size_t)j * (n + 1);
+    out.blk[j] = CsrDev{out.rp.as<int64_t>() + (size_t)j * (n + 1), out.idx.as<int32_t>(),
+                        A.unit ? nullptr : out.dat.as<float>(), n, r[n] - r[0], A.unit};
+  }
+  out.ncols = ncols;
+  out.built = true;
+}
+
+void ensure_col_blocks(LayerDev& L, int64_t ncols, hipStream_t st) {
+  if (!L.cb.built || L.cb.ncols != ncols) build_col_blocks(L.csr(), ncols, L.cb, st);
+  if (!L.symmetric && (!L.cb_t.built || L.cb_t.ncols != ncols))
+    build_col_blocks(L.csr_t(), ncols, L.cb_t, st);
+}
 
 // ---- communicators ----------------------------------------------------------------------
 struct Comm {
@@ -353,6 +431,7 @@ struct EigWorkspace {
   DevBuf tri, refl, ytri, tscr;               // GPU Rayleigh-Ritz: [d|e|tau], reflectors, Y_T
   DevBuf hband, band, varr, taua, rrerr;      // banded RR: band columns, band matrix, arrow
   DevBuf fcoef;                               // fp32 [-C R^-1; R^-1] of the apply pass
+  DevBuf cbpart;                              // [K][CB_NB][npad][8] column-block partials
 };
 }  // namespace
 
@@ -540,6 +619,11 @@ double spmm_algo_bytes(int64_t nnz, bool unit, int64_t rows, int64_t panel_rows,
          4.0 * (double)(panel_rows + rows) * b;
 }
 
+// XCD-local column-block SpMM: b = 8 CSR panels beyond N2V2R_CB_MIN_MB (default 16 MB, where
+// a panel spans several XCD L2s); N2V2R_SPMM_CB=1 / 0 forces it on / off (tests, A/B runs).
+// Read on every call, so a test can switch it between fits.
+bool col_blocks_wanted(const n2v2r_handle* h, int b);
+
 // ---- the eigensolver ----------------------------------------------------------------------
 struct Eig {
   n2v2r_handle* h;
@@ -563,6 +647,7 @@ struct Eig {
   int kry0 = 0;             // index of the first Krylov block of the current cycle
   bool full_first = false;  // N2V2R_EIG_FULL_FIRST_PASS
   bool band_rr = false;     // banded Rayleigh-Ritz (b = 8, c <= 512), else dense
+  bool col_blocks = false;  // XCD-local column-block SpMM (b = 8, large panels)
 
   float* take() {
     if (freelist.empty()) {
@@ -636,6 +721,11 @@ struct Eig {
       t_spmm += now_ms() - t0;
       return;
     }
+    if (col_blocks) {
+      apply_M_cb(xg, Wout, ng);
+      t_spmm += now_ms() - t0;
+      return;
+    }
     SpmmArgs a{};
     a.K = K;
     a.sum = 0;
@@ -674,6 +764,48 @@ struct Eig {
     }
     launches += 2;
     t_spmm += now_ms() - t0;
+  }
+
+  // apply_M with the column-block SpMM (spmm.hip): per layer one launch per stage writing
+  // CB_NB partials, reduced in fixed (layer, block) order.
+  void apply_M_cb(const float* xg, float* Wout, int64_t ng) {
+    const int64_t pst = npad * 8;
+    float* part = h->ews.cbpart.as<float>();
+    for (int k = 0; k < K; ++k) {
+      LayerDev& L = *h->layers[k];
+      SpmmCbArgs a{};
+      for (int j = 0; j < CB_NB; ++j) a.A[j] = (L.symmetric ? L.cb : L.cb_t).blk[j];
+      a.X = xg;
+      a.ldx = 8;
+      a.P = part + (size_t)k * CB_NB * pst;
+      a.pstride = pst;
+      HIPCHK(n2v2r_launch_spmm_cb(a, st));
+      HIPCHK(n2v2r_launch_cb_reduce(a.P, CB_NB, pst, n, h->ews.zk[k]->as<float>(), 8, st));
+    }
+    for (int k = 0; k < K; ++k) {
+      LayerDev& L = *h->layers[k];
+      const float* zin = h->ews.zk[k]->as<float>();
+      if (h->comm) {
+        float* zgk = h->ews.zg.as<float>() + (size_t)k * ng * b;
+        h->gather_panel(h->ews.zk[k]->as<float>(), zgk, b);
+        zin = zgk;
+      }
+      SpmmCbArgs a{};
+      for (int j = 0; j < CB_NB; ++j) a.A[j] = L.cb.blk[j];
+      a.X = zin;
+      a.ldx = 8;
+      a.P = part + (size_t)k * CB_NB * pst;
+      a.pstride = pst;
+      HIPCHK(n2v2r_launch_spmm_cb(a, st));
+    }
+    HIPCHK(n2v2r_launch_cb_reduce(part, K * CB_NB, pst, n, Wout, 8, st));
+    for (int k = 0; k < K; ++k) {
+      const LayerDev& L = *h->layers[k];
+      algo_bytes += spmm_algo_bytes(L.nnz, L.unit, n, n, b) +
+                    spmm_algo_bytes(L.symmetric ? L.nnz : L.t_nnz,
+                                    L.symmetric ? L.unit : L.t_unit, n, n, b);
+    }
+    launches += 2 * K + K + 1;
   }
 
   // One fused BCGS + CholQR pass: G = [Q Z]^T Z -> R^{-1} -> Z <- [Q Z] [-C R^{-1}; R^{-1}],
@@ -818,6 +950,11 @@ struct Eig {
     if (h->comm) {
       h->gath.ensure(sizeof(float) * h->world * npad * b);
       h->ews.zg.ensure(sizeof(float) * (size_t)K * h->world * npad * b);
+    }
+    col_blocks = col_blocks_wanted(h, b);
+    if (col_blocks) {
+      for (auto& Lp : h->layers) ensure_col_blocks(*Lp, nglob, st);
+      h->ews.cbpart.ensure(sizeof(float) * (size_t)K * CB_NB * npad * 8);
     }
     // chunk partials: also the streaming Gram form at b = 8 (chunks of <= 8192 rows, rounded to
     // a multiple of 8, (c + b) x b fp64 each)
@@ -1071,6 +1208,18 @@ n2v2r_handle* new_handle(int device) {
 }  // namespace
 
 // ======================================================================================
+namespace {
+bool col_blocks_wanted(const n2v2r_handle* h, int b) {
+  if (b != 8 || h->dense_layers() || h->layers.empty()) return false;
+  const char* e = std::getenv("N2V2R_SPMM_CB");
+  if (e && e[0] == '1') return true;
+  if (e && e[0] == '0') return false;
+  const char* m = std::getenv("N2V2R_CB_MIN_MB");
+  const double min_mb = m ? atof(m) : 16.0;
+  return 4.0 * b * (double)h->n > min_mb * 1e6;
+}
+}  // namespace
+
 extern "C" {
 
 const char* n2v2r_version(void) { return "n2v2r-mi355x 0.2.0 (gfx950)"; }
@@ -1227,6 +1376,7 @@ int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const in
       }
     LayerDev& L = *h->layers[k];
     L.dense = false;
+    L.drop_col_blocks();
     L.n_rows = h->nloc;
     L.unit = upload_rows(h->stream, h->row0, h->nloc, indptr, indices, data, L.indptr, L.indices,
                          L.data, L.nnz);
@@ -1314,6 +1464,7 @@ int n2v2r_set_layer_csr_rows(n2v2r_handle* h, int k, int64_t n, int64_t row0, in
         return N2V2R_ERR_BAD_ARG;
       }
     LayerDev& L = *h->layers[k];
+    L.drop_col_blocks();
     L.n_rows = h->nloc;
     L.unit = upload_rows(h->stream, 0, n_rows, indptr, indices, data, L.indptr, L.indices, L.data,
                          L.nnz);
@@ -1824,6 +1975,11 @@ int n2v2r_rr_band_top(n2v2r_handle* h, int c, int kp, const double* hband, int64
   });
 }
 
+int n2v2r_spmm_col_blocks(const n2v2r_handle* h, int b) {
+  if (!h) return N2V2R_ERR_BAD_ARG;
+  return col_blocks_wanted(h, b) ? 1 : 0;
+}
+
 int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, const float* X,
                      float* Y, double* avg_ms, double* algo_bytes) {
   return guarded(h, [&]() -> int {
@@ -1854,6 +2010,46 @@ int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, con
       if (avg_ms) *avg_ms = (double)ms / reps;
       if (algo_bytes)
         *algo_bytes = 4.0 * (double)h->nloc * (double)h->n + 4.0 * (double)(h->n + h->nloc) * b;
+      if (Y)
+        HIPCHK(hipMemcpyAsync(Y, yd.p, sizeof(float) * h->nloc * b, hipMemcpyDeviceToHost,
+                              h->stream));
+      HIPCHK(hipStreamSynchronize(h->stream));
+      return N2V2R_OK;
+    }
+    if (col_blocks_wanted(h, b)) {
+      // column-block SpMM of one layer: the block launch + the fixed-order partial reduce,
+      // timed together (the same algorithmic bytes as the row kernel; the partials are extra)
+      LayerDev& Lm = *h->layers[k];
+      ensure_col_blocks(Lm, h->n, h->stream);
+      const int64_t pst = std::max<int64_t>(h->nloc, 1) * 8;
+      DevBuf part;
+      part.ensure(sizeof(float) * CB_NB * pst, h->stream);
+      SpmmCbArgs a{};
+      const LayerDev::ColBlocks& cbs = (transpose && !Lm.symmetric) ? Lm.cb_t : Lm.cb;
+      for (int j = 0; j < CB_NB; ++j) a.A[j] = cbs.blk[j];
+      a.X = xd.as<float>();
+      a.ldx = 8;
+      a.P = part.as<float>();
+      a.pstride = pst;
+      auto once = [&]() {
+        HIPCHK(n2v2r_launch_spmm_cb(a, h->stream));
+        HIPCHK(n2v2r_launch_cb_reduce(a.P, CB_NB, pst, h->nloc, yd.as<float>(), 8, h->stream));
+      };
+      once();  // warm-up
+      hipEvent_t e0, e1;
+      HIPCHK(hipEventCreate(&e0));
+      HIPCHK(hipEventCreate(&e1));
+      HIPCHK(hipEventRecord(e0, h->stream));
+      for (int r = 0; r < reps; ++r) once();
+      HIPCHK(hipEventRecord(e1, h->stream));
+      HIPCHK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+      if (avg_ms) *avg_ms = (double)ms / reps;
+      const CsrDev c0 = transpose ? Lm.csr_t() : Lm.csr();
+      if (algo_bytes) *algo_bytes = spmm_algo_bytes(c0.nnz, c0.unit != 0, h->nloc, h->n, b);
       if (Y)
         HIPCHK(hipMemcpyAsync(Y, yd.p, sizeof(float) * h->nloc * b, hipMemcpyDeviceToHost,
                               h->stream));

@@ -330,6 +330,152 @@ extern "C" hipError_t n2v2r_launch_spmm(const SpmmArgs& args, int B, hipStream_t
   return hipGetLastError();
 }
 
+// ---- XCD-local column blocks (b = 8, panels larger than the L2s) -------------------------
+// At N = 1M a b = 8 panel is 32 MB: it lives in the Infinity Cache, and every 32-B gather
+// pulls a whole line over the fabric, so the gathers run at Infinity-Cache line bandwidth.
+// The column-block form splits each layer's columns into CB_NB = 8 equal ranges and keeps one
+// CSR per range (same row order, entries of a row in their original order).  Workgroup i runs
+// on XCD i mod 8 (round-robin dispatch), so XCD j only gathers from panel rows of column block
+// j (N/8 x 32 B = 4 MB at N = 1M): the gathers hit that XCD's L2.  Each block writes its own
+// partial output (N x 8 fp32); cb_reduce sums the partials in fixed block order (then layer
+// order), so the result is deterministic.  Extra traffic: 2 x 8 x N x 32 B of partials per
+// layer launch.
+#define CB_NB 8
+
+struct SpmmCbArgs {
+  CsrDev A[CB_NB];   // column block j of one layer: absolute int64 row pointers
+  const float* X;    // gathered panel, global column index = panel row
+  int64_t ldx;
+  float* P;          // partial j at P + j * pstride, rows of 8 fp32
+  int64_t pstride;
+};
+
+template <int RPW>
+__global__ __launch_bounds__(256) void spmm8_cb_kernel(SpmmCbArgs a) {
+  constexpr int L = 64 / RPW;
+  const int lane = threadIdx.x & 63;
+  const int j = blockIdx.x & (CB_NB - 1);
+  const int64_t t = blockIdx.x / CB_NB;
+  const int64_t nwg = gridDim.x / CB_NB;
+  const CsrDev& A = a.A[j];
+  const int64_t n = A.n_rows;
+  const int li = lane % L;
+  float* __restrict__ P = a.P + (int64_t)j * a.pstride;
+  const int64_t nw = nwg * (blockDim.x / 64);
+  for (int64_t wid = t * (blockDim.x / 64) + (threadIdx.x >> 6); wid * RPW < n; wid += nw) {
+    const int64_t row = wid * RPW + lane / L;
+    const bool row_ok = row < n;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    spmm_row_accumulate<8, RPW>(A, a.X, a.ldx, row, row_ok, lane, acc);
+#pragma unroll
+    for (int m = 2; m < L; m <<= 1) {
+      acc.x += __shfl_xor(acc.x, m, 64);
+      acc.y += __shfl_xor(acc.y, m, 64);
+      acc.z += __shfl_xor(acc.z, m, 64);
+      acc.w += __shfl_xor(acc.w, m, 64);
+    }
+    if (row_ok && li < 2) *reinterpret_cast<f32x4*>(P + row * 8 + li * 4) = acc;
+  }
+}
+
+extern "C" hipError_t n2v2r_launch_spmm_cb(const SpmmCbArgs& a, hipStream_t stream) {
+  const int64_t n = a.A[0].n_rows;
+  double avg = (double)(a.A[0].nnz) / (double)(n > 0 ? n : 1);  // per block row
+  for (int j = 1; j < CB_NB; ++j) avg = avg > (double)a.A[j].nnz / (double)(n > 0 ? n : 1) ? avg : (double)a.A[j].nnz / (double)(n > 0 ? n : 1);
+  int rpw = 1;  // aim for ~3-4 gather steps of L/2 panel rows per row group
+  while (rpw < 16 && 64.0 / (rpw * 2) / 2.0 * 3.5 >= avg) rpw *= 2;
+  const int64_t waves = (n + rpw - 1) / rpw;
+  int64_t per = (waves + 3) / 4;  // workgroups per block
+  const int64_t cap = N2V2R_SPMM_WGS / CB_NB;
+  if (per > cap) per = cap;
+  if (per < 1) per = 1;
+  dim3 grid((unsigned)(per * CB_NB));
+  switch (rpw) {
+    case 16: hipLaunchKernelGGL((spmm8_cb_kernel<16>), grid, dim3(256), 0, stream, a); break;
+    case 8: hipLaunchKernelGGL((spmm8_cb_kernel<8>), grid, dim3(256), 0, stream, a); break;
+    case 4: hipLaunchKernelGGL((spmm8_cb_kernel<4>), grid, dim3(256), 0, stream, a); break;
+    case 2: hipLaunchKernelGGL((spmm8_cb_kernel<2>), grid, dim3(256), 0, stream, a); break;
+    default: hipLaunchKernelGGL((spmm8_cb_kernel<1>), grid, dim3(256), 0, stream, a); break;
+  }
+  return hipGetLastError();
+}
+
+// out[r] = colscale .* sum_{p < nparts} P[p][r] (rows of 8 fp32, fixed part order)
+__global__ __launch_bounds__(256) void cb_reduce_kernel(const float* __restrict__ P, int nparts,
+                                                        int64_t pstride, int64_t n,
+                                                        float* __restrict__ out, int64_t ldo) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one float4 each
+  if (i >= n * 2) return;
+  const int64_t r = i >> 1;
+  const int h = (int)(i & 1);
+  f32x4 s = *reinterpret_cast<const f32x4*>(P + r * 8 + h * 4);
+  for (int p = 1; p < nparts; ++p)
+    s += *reinterpret_cast<const f32x4*>(P + p * pstride + r * 8 + h * 4);
+  *reinterpret_cast<f32x4*>(out + r * ldo + h * 4) = s;
+}
+
+extern "C" hipError_t n2v2r_launch_cb_reduce(const float* P, int nparts, int64_t pstride,
+                                             int64_t n, float* out, int64_t ldo,
+                                             hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  const int64_t thr = n * 2;
+  hipLaunchKernelGGL(cb_reduce_kernel, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, stream,
+                     P, nparts, pstride, n, out, ldo);
+  return hipGetLastError();
+}
+
+// Column-block split, step 1: cnt[j * n + r] = entries of row r in column block j
+// (block j = columns [j * cw, (j + 1) * cw)).
+__global__ void cb_count_kernel(CsrDev A, int64_t cw, int32_t* __restrict__ cnt) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= A.n_rows) return;
+  int c[CB_NB] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t p = A.indptr[r]; p < A.indptr[r + 1]; ++p) {
+    const int jb = (int)(A.indices[p] / cw);
+#pragma unroll
+    for (int j = 0; j < CB_NB; ++j) c[j] += jb == j;
+  }
+#pragma unroll
+  for (int j = 0; j < CB_NB; ++j) cnt[(int64_t)j * A.n_rows + r] = c[j];
+}
+
+// step 2 (after the host scan): scatter each row's entries to rp[j][r] + running count,
+// keeping their order inside the row.
+__global__ void cb_fill_kernel(CsrDev A, int64_t cw, const int64_t* __restrict__ rp,
+                               int32_t* __restrict__ idx, float* __restrict__ dat) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= A.n_rows) return;
+  int64_t pos[CB_NB];
+#pragma unroll
+  for (int j = 0; j < CB_NB; ++j) pos[j] = rp[(int64_t)j * (A.n_rows + 1) + r];
+  for (int64_t p = A.indptr[r]; p < A.indptr[r + 1]; ++p) {
+    const int32_t col = A.indices[p];
+    const int jb = (int)(col / cw);
+    int64_t q = 0;
+#pragma unroll
+    for (int j = 0; j < CB_NB; ++j)
+      if (jb == j) q = pos[j]++;
+    idx[q] = col;
+    if (!A.unit) dat[q] = A.data[p];
+  }
+}
+
+extern "C" hipError_t n2v2r_launch_cb_count(const CsrDev& A, int64_t cw, int32_t* cnt,
+                                            hipStream_t stream) {
+  if (A.n_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(cb_count_kernel, dim3((unsigned)((A.n_rows + 255) / 256)), dim3(256), 0,
+                     stream, A, cw, cnt);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t n2v2r_launch_cb_fill(const CsrDev& A, int64_t cw, const int64_t* rp,
+                                           int32_t* idx, float* dat, hipStream_t stream) {
+  if (A.n_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(cb_fill_kernel, dim3((unsigned)((A.n_rows + 255) / 256)), dim3(256), 0,
+                     stream, A, cw, rp, idx, dat);
+  return hipGetLastError();
+}
+
 // Column sums of a CSR layer (DeDi, model.py:282-311): out[j] = sum_i A[i][j].  fp32
 // atomics would make the order run-dependent, so the engine calls this on A^T (row sums of
 // the transpose = column sums) when the layer is not symmetric.

@@ -126,6 +126,14 @@ def test_partitioned_matches_reference(engine, name, world):
                                    rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("name", ["er_cfg1", "directed_weighted"])
+def test_partitioned_column_blocks(engine, name, monkeypatch):
+    """Row partition + the XCD-local column-block SpMM (forced on): column blocks are cut over
+    the global column range of the gathered panel."""
+    monkeypatch.setenv("N2V2R_SPMM_CB", "1")
+    test_partitioned_matches_reference(engine, name, 2)
+
+
 def test_partitioned_er_large_rows_ingest(engine):
     """N=20k ER, d=16, 4 ranks, local-rows ingest (no global CSR handed to the engine)."""
     from node2vec2rank_amd import synthetic

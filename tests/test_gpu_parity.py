@@ -28,6 +28,26 @@ def test_spmm_matches_scipy(engine, name, b):
             assert ms > 0 and by > 0
 
 
+@pytest.mark.parametrize("name", ["er_cfg1", "directed_weighted", "demo"])
+def test_spmm_column_blocks_matches_scipy(engine, name, monkeypatch):
+    """The column-block SpMM (block launch + fixed-order reduce of the 8 partials), forced on."""
+    monkeypatch.setenv("N2V2R_SPMM_CB", "1")
+    fx = load_fixture(name)
+    layers = fixture_layers(fx)
+    engine.set_layers(layers)
+    assert engine.spmm_col_blocks(8) and not engine.spmm_col_blocks(16)
+    X = np.random.default_rng(5).standard_normal((layers[0].shape[0], 8)).astype(np.float32)
+    for k, A in enumerate(layers):
+        for tr in (False, True):
+            Y, ms, by = engine.bench_spmm(k, X, transpose=tr, reps=2)
+            M = A.T if tr else A
+            ref = M.astype(np.float64) @ X.astype(np.float64)
+            scale = np.abs(M).astype(np.float64) @ np.abs(X).astype(np.float64)
+            assert np.all(np.abs(Y - ref) <= 1e-5 * scale + 1e-6), (name, k, tr)
+    monkeypatch.setenv("N2V2R_SPMM_CB", "0")
+    assert not engine.spmm_col_blocks(8)
+
+
 @pytest.mark.parametrize("weighted", [False, True])
 def test_spmm_b8_long_rows_and_empty_rows(engine, weighted):
     """The B = 8 pipelined kernel: rows longer than 32 (the non-pipelined remainder), empty
@@ -287,6 +307,49 @@ def test_uase_residuals_er_20k(engine):
     np.testing.assert_allclose(X.T @ X, np.eye(d), atol=1e-5)
     _, s_ref, _ = orc.uase(layers, d, seed=42)
     np.testing.assert_allclose(s, s_ref, rtol=1e-5)
+
+
+@pytest.mark.parametrize("name", ["er_cfg1", "directed_weighted", "demo"])
+def test_uase_column_blocks_golden(engine, name, monkeypatch):
+    """The XCD-local column-block SpMM (forced on at fixture size; by default it runs for
+    panels > 16 MB) reproduces the reference embedding: symmetric, directed (A^T split) and
+    weighted layers."""
+    monkeypatch.setenv("N2V2R_SPMM_CB", "1")
+    fx = load_fixture(name)
+    layers = fixture_layers(fx)
+    d = int(fx["dims"].max())
+    engine.set_layers(layers)
+    engine.uase(d, seed=int(fx["seed"]), block=8)
+    np.testing.assert_allclose(engine.singular_values(), fx["sigma"], rtol=2e-5)
+    Ya = orc.align_signs(engine.embedding().astype(np.float64), fx["Y"])
+    env, _ = _envelope(layers, d, int(fx["seed"]))
+    err = np.abs(Ya - fx["Y"]).max() / np.abs(fx["Y"]).max()
+    assert err <= max(5e-4, 3 * env), (name, err, env)
+
+
+def test_uase_column_blocks_er_20k(engine, monkeypatch):
+    """Column-block SpMM vs the row SpMM on a 20k-node ER graph with a ragged column count
+    (20,003: the last block is short): same sigma within fp32 tolerance, true residuals, and
+    run-to-run bit-identical embeddings (fixed partial order)."""
+    from node2vec2rank_amd import synthetic
+    layers = synthetic.er_layers(20_003, 20, 2)
+    d = 32
+    engine.set_layers(layers)
+    monkeypatch.setenv("N2V2R_SPMM_CB", "0")
+    engine.uase(d, seed=42)
+    s_row = engine.singular_values().copy()
+    monkeypatch.setenv("N2V2R_SPMM_CB", "1")
+    st = engine.uase(d, seed=42)
+    assert st["converged"] == d
+    s = engine.singular_values()
+    Y1 = engine.embedding().copy()
+    np.testing.assert_allclose(s, s_row, rtol=1e-5)
+    X = engine.left_embedding().astype(np.float64) / np.sqrt(s)[None, :]
+    A = sp.hstack(layers).tocsr().astype(np.float64)
+    res = np.linalg.norm(A @ (A.T @ X) - X * (s ** 2)[None, :], axis=0) / s[0] ** 2
+    assert res.max() < 1e-5
+    engine.uase(d, seed=42)
+    assert np.array_equal(engine.embedding(), Y1)
 
 
 @pytest.mark.parametrize("block", [8, 16, 64])
