@@ -164,7 +164,7 @@ int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, con
                      float* Y, double* avg_ms, double* algo_bytes);
 
 /* 1 when UASE (and n2v2r_bench_spmm) use the XCD-local column-block SpMM at panel width b on
- * this handle's layers (b = 8 CSR panels above 16 MB: each layer split into 8 column blocks,
+ * this handle's layers (b = 8 CSR panels of 8-160 MB: each layer split into 8 column blocks,
  * workgroup i mod 8 on XCD i mod 8 gathers only from block i mod 8, fixed-order reduce of the
  * 8 partials; env N2V2R_SPMM_CB=1/0 forces it), else 0.  Then bench_spmm times the block
  * launch plus the reduce. */

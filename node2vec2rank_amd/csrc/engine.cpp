@@ -619,8 +619,9 @@ double spmm_algo_bytes(int64_t nnz, bool unit, int64_t rows, int64_t panel_rows,
          4.0 * (double)(panel_rows + rows) * b;
 }
 
-// XCD-local column-block SpMM: b = 8 CSR panels beyond N2V2R_CB_MIN_MB (default 16 MB, where
-// a panel spans several XCD L2s); N2V2R_SPMM_CB=1 / 0 forces it on / off (tests, A/B runs).
+// XCD-local column-block SpMM: b = 8 CSR panels of (N2V2R_CB_MIN_MB, N2V2R_CB_MAX_MB] (default
+// 8-160 MB: several XCD L2s' worth, inside the Infinity Cache); N2V2R_SPMM_CB=1 / 0 forces it
+// on / off (tests, A/B runs).
 // Read on every call, so a test can switch it between fits.
 bool col_blocks_wanted(const n2v2r_handle* h, int b);
 
@@ -1214,9 +1215,15 @@ bool col_blocks_wanted(const n2v2r_handle* h, int b) {
   const char* e = std::getenv("N2V2R_SPMM_CB");
   if (e && e[0] == '1') return true;
   if (e && e[0] == '0') return false;
+  // measured (tools/cb_probe.py, one layer, HIP events): row kernel / column blocks =
+  // 0.56 at a 3.2 MB panel (N = 100k: the panel already fits one L2), 1.35 at 9.6 MB,
+  // 1.61 at 32 MB, 1.16 at 96 MB, 0.93 at 320 MB (beyond the Infinity Cache the gathers go
+  // to HBM either way and the partials only add traffic)
   const char* m = std::getenv("N2V2R_CB_MIN_MB");
-  const double min_mb = m ? atof(m) : 16.0;
-  return 4.0 * b * (double)h->n > min_mb * 1e6;
+  const char* x = std::getenv("N2V2R_CB_MAX_MB");
+  const double min_mb = m ? atof(m) : 8.0, max_mb = x ? atof(x) : 160.0;
+  const double panel = 4.0 * b * (double)h->n;
+  return panel > min_mb * 1e6 && panel <= max_mb * 1e6;
 }
 }  // namespace
 

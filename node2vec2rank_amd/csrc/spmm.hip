@@ -38,7 +38,9 @@ struct SpmmArgs {
 // lanes gather one panel row (one 16-B load each) and NPS = L / LPN panel rows are gathered
 // per step.  Short rows (ER / k-NN graphs: tens of nnz) then keep several rows' gathers in
 // flight per wave instead of leaving most lanes idle.
-template <int B, int RPW>
+// NT: the once-read index / value stream uses non-temporal loads (column blocks: keeps the
+// XCD's L2 for the panel block)
+template <int B, int RPW, bool NT = false>
 __device__ __forceinline__ void spmm_row_accumulate(const CsrDev& A, const float* __restrict__ X,
                                                     int64_t ldx, int64_t row, bool row_ok,
                                                     int lane, f32x4& acc) {
@@ -67,8 +69,13 @@ __device__ __forceinline__ void spmm_row_accumulate(const CsrDev& A, const float
     int colv = 0;
     float valv = 0.f;
     if (off + li < len) {
-      colv = A.indices[beg + off + li];
-      valv = A.unit ? 1.f : A.data[beg + off + li];  // unweighted layers: no value stream
+      if constexpr (NT) {
+        colv = __builtin_nontemporal_load(A.indices + beg + off + li);
+        valv = A.unit ? 1.f : __builtin_nontemporal_load(A.data + beg + off + li);
+      } else {
+        colv = A.indices[beg + off + li];
+        valv = A.unit ? 1.f : A.data[beg + off + li];  // unweighted layers: no value stream
+      }
     }
     int64_t rem = maxlen - off;
     const int nn = (int)(rem < L ? rem : L);
@@ -350,7 +357,7 @@ struct SpmmCbArgs {
   int64_t pstride;
 };
 
-template <int RPW>
+template <int RPW, bool NT>
 __global__ __launch_bounds__(256) void spmm8_cb_kernel(SpmmCbArgs a) {
   constexpr int L = 64 / RPW;
   const int lane = threadIdx.x & 63;
@@ -366,7 +373,7 @@ __global__ __launch_bounds__(256) void spmm8_cb_kernel(SpmmCbArgs a) {
     const int64_t row = wid * RPW + lane / L;
     const bool row_ok = row < n;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    spmm_row_accumulate<8, RPW>(A, a.X, a.ldx, row, row_ok, lane, acc);
+    spmm_row_accumulate<8, RPW, NT>(A, a.X, a.ldx, row, row_ok, lane, acc);
 #pragma unroll
     for (int m = 2; m < L; m <<= 1) {
       acc.x += __shfl_xor(acc.x, m, 64);
@@ -374,14 +381,28 @@ __global__ __launch_bounds__(256) void spmm8_cb_kernel(SpmmCbArgs a) {
       acc.z += __shfl_xor(acc.z, m, 64);
       acc.w += __shfl_xor(acc.w, m, 64);
     }
-    if (row_ok && li < 2) *reinterpret_cast<f32x4*>(P + row * 8 + li * 4) = acc;
+    if (row_ok && li < 2) {
+      if constexpr (NT) {
+        // write-through (sc1) store: the partial leaves the XCD's L2 instead of evicting the
+        // panel block (a partial is re-read only by cb_reduce, a later launch)
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(P, 0, 0x7FFFFFFF, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc), rsrc,
+                                               (int)(row * 32 + li * 16), 0, 16);
+      } else {
+        *reinterpret_cast<f32x4*>(P + row * 8 + li * 4) = acc;
+      }
+    }
   }
 }
 
 extern "C" hipError_t n2v2r_launch_spmm_cb(const SpmmCbArgs& a, hipStream_t stream) {
   const int64_t n = a.A[0].n_rows;
-  double avg = (double)(a.A[0].nnz) / (double)(n > 0 ? n : 1);  // per block row
-  for (int j = 1; j < CB_NB; ++j) avg = avg > (double)a.A[j].nnz / (double)(n > 0 ? n : 1) ? avg : (double)a.A[j].nnz / (double)(n > 0 ? n : 1);
+  double avg = 0.0;  // mean entries per block row, largest block
+  for (int j = 0; j < CB_NB; ++j) {
+    const double m = (double)a.A[j].nnz / (double)(n > 0 ? n : 1);
+    avg = m > avg ? m : avg;
+  }
   int rpw = 1;  // aim for ~3-4 gather steps of L/2 panel rows per row group
   while (rpw < 16 && 64.0 / (rpw * 2) / 2.0 * 3.5 >= avg) rpw *= 2;
   const int64_t waves = (n + rpw - 1) / rpw;
@@ -390,12 +411,26 @@ extern "C" hipError_t n2v2r_launch_spmm_cb(const SpmmCbArgs& a, hipStream_t stre
   if (per > cap) per = cap;
   if (per < 1) per = 1;
   dim3 grid((unsigned)(per * CB_NB));
+  static const int nt = [] {  // N2V2R_CB_NT=1: non-temporal index stream (A/B runs)
+    const char* s = getenv("N2V2R_CB_NT");
+    return s && s[0] == '1';
+  }();
+  if (nt) {
+    switch (rpw) {
+      case 16: hipLaunchKernelGGL((spmm8_cb_kernel<16, true>), grid, dim3(256), 0, stream, a); break;
+      case 8: hipLaunchKernelGGL((spmm8_cb_kernel<8, true>), grid, dim3(256), 0, stream, a); break;
+      case 4: hipLaunchKernelGGL((spmm8_cb_kernel<4, true>), grid, dim3(256), 0, stream, a); break;
+      case 2: hipLaunchKernelGGL((spmm8_cb_kernel<2, true>), grid, dim3(256), 0, stream, a); break;
+      default: hipLaunchKernelGGL((spmm8_cb_kernel<1, true>), grid, dim3(256), 0, stream, a); break;
+    }
+    return hipGetLastError();
+  }
   switch (rpw) {
-    case 16: hipLaunchKernelGGL((spmm8_cb_kernel<16>), grid, dim3(256), 0, stream, a); break;
-    case 8: hipLaunchKernelGGL((spmm8_cb_kernel<8>), grid, dim3(256), 0, stream, a); break;
-    case 4: hipLaunchKernelGGL((spmm8_cb_kernel<4>), grid, dim3(256), 0, stream, a); break;
-    case 2: hipLaunchKernelGGL((spmm8_cb_kernel<2>), grid, dim3(256), 0, stream, a); break;
-    default: hipLaunchKernelGGL((spmm8_cb_kernel<1>), grid, dim3(256), 0, stream, a); break;
+    case 16: hipLaunchKernelGGL((spmm8_cb_kernel<16, false>), grid, dim3(256), 0, stream, a); break;
+    case 8: hipLaunchKernelGGL((spmm8_cb_kernel<8, false>), grid, dim3(256), 0, stream, a); break;
+    case 4: hipLaunchKernelGGL((spmm8_cb_kernel<4, false>), grid, dim3(256), 0, stream, a); break;
+    case 2: hipLaunchKernelGGL((spmm8_cb_kernel<2, false>), grid, dim3(256), 0, stream, a); break;
+    default: hipLaunchKernelGGL((spmm8_cb_kernel<1, false>), grid, dim3(256), 0, stream, a); break;
   }
   return hipGetLastError();
 }

@@ -312,7 +312,7 @@ def test_uase_residuals_er_20k(engine):
 @pytest.mark.parametrize("name", ["er_cfg1", "directed_weighted", "demo"])
 def test_uase_column_blocks_golden(engine, name, monkeypatch):
     """The XCD-local column-block SpMM (forced on at fixture size; by default it runs for
-    panels > 16 MB) reproduces the reference embedding: symmetric, directed (A^T split) and
+    panels of 8-160 MB) reproduces the reference embedding: symmetric, directed (A^T split) and
     weighted layers."""
     monkeypatch.setenv("N2V2R_SPMM_CB", "1")
     fx = load_fixture(name)
