@@ -38,9 +38,7 @@ struct SpmmArgs {
 // lanes gather one panel row (one 16-B load each) and NPS = L / LPN panel rows are gathered
 // per step.  Short rows (ER / k-NN graphs: tens of nnz) then keep several rows' gathers in
 // flight per wave instead of leaving most lanes idle.
-// NT: the once-read index / value stream uses non-temporal loads (column blocks: keeps the
-// XCD's L2 for the panel block)
-template <int B, int RPW, bool NT = false>
+template <int B, int RPW>
 __device__ __forceinline__ void spmm_row_accumulate(const CsrDev& A, const float* __restrict__ X,
                                                     int64_t ldx, int64_t row, bool row_ok,
                                                     int lane, f32x4& acc) {
@@ -69,13 +67,8 @@ __device__ __forceinline__ void spmm_row_accumulate(const CsrDev& A, const float
     int colv = 0;
     float valv = 0.f;
     if (off + li < len) {
-      if constexpr (NT) {
-        colv = __builtin_nontemporal_load(A.indices + beg + off + li);
-        valv = A.unit ? 1.f : __builtin_nontemporal_load(A.data + beg + off + li);
-      } else {
-        colv = A.indices[beg + off + li];
-        valv = A.unit ? 1.f : A.data[beg + off + li];  // unweighted layers: no value stream
-      }
+      colv = A.indices[beg + off + li];
+      valv = A.unit ? 1.f : A.data[beg + off + li];  // unweighted layers: no value stream
     }
     int64_t rem = maxlen - off;
     const int nn = (int)(rem < L ? rem : L);
@@ -357,7 +350,60 @@ struct SpmmCbArgs {
   int64_t pstride;
 };
 
-template <int RPW, bool NT>
+// b = 8 row accumulation for the column blocks: block rows are short (N avg-deg / 8 entries),
+// so the index loads of two group-widths are issued together before the gathers (one
+// index -> gather latency per 2L entries instead of per L).  Same per-lane entry order as
+// spmm_row_accumulate<8, RPW>.
+template <int RPW>
+__device__ __forceinline__ void cb_row_accumulate(const CsrDev& A, const float* __restrict__ X,
+                                                  int64_t ldx, int64_t row, bool row_ok,
+                                                  int lane, f32x4& acc) {
+  constexpr int L = 64 / RPW;
+  constexpr int NPS = L / 2;  // panel rows per step (2 lanes per 32-B panel row)
+  const int g = lane / L;
+  const int li = lane % L;
+  const int sub = li & 1;
+  const int srcbase = g * L + (li >> 1);
+  int64_t beg = 0, end = 0;
+  if (row_ok) {
+    beg = A.indptr[row];
+    end = A.indptr[row + 1];
+  }
+  const int64_t len = end - beg;
+  int64_t maxlen = len;
+#pragma unroll
+  for (int m = L; m < 64; m <<= 1) {
+    const int64_t o = __shfl_xor(maxlen, m, 64);
+    maxlen = o > maxlen ? o : maxlen;
+  }
+  for (int64_t off = 0; off < maxlen; off += 2 * L) {
+    int cv[2] = {0, 0};
+    float vv[2] = {0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t p = off + u * L + li;
+      if (p < len) {
+        cv[u] = A.indices[beg + p];
+        vv[u] = A.unit ? 1.f : A.data[beg + p];
+      }
+    }
+    const int64_t rem = maxlen - off;
+    const int nn = (int)(rem < 2 * L ? rem : 2 * L);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (s * NPS >= nn) break;
+      const int u = s >> 1;  // L / NPS = 2 steps per group-width
+      const int c0 = __shfl(cv[u], srcbase + (s & 1) * NPS, 64);
+      const float v0 = __shfl(vv[u], srcbase + (s & 1) * NPS, 64);
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(X + (int64_t)c0 * ldx + sub * 4);
+      acc += v0 * x0;
+    }
+  }
+}
+
+// UNR: cb_row_accumulate (two group-widths of indices per gather round), else the generic
+// spmm_row_accumulate<8, RPW> (A/B: N2V2R_CB_UNR=0)
+template <int RPW, bool UNR>
 __global__ __launch_bounds__(256) void spmm8_cb_kernel(SpmmCbArgs a) {
   constexpr int L = 64 / RPW;
   const int lane = threadIdx.x & 63;
@@ -373,7 +419,10 @@ __global__ __launch_bounds__(256) void spmm8_cb_kernel(SpmmCbArgs a) {
     const int64_t row = wid * RPW + lane / L;
     const bool row_ok = row < n;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    spmm_row_accumulate<8, RPW, NT>(A, a.X, a.ldx, row, row_ok, lane, acc);
+    if constexpr (UNR)
+      cb_row_accumulate<RPW>(A, a.X, a.ldx, row, row_ok, lane, acc);
+    else
+      spmm_row_accumulate<8, RPW>(A, a.X, a.ldx, row, row_ok, lane, acc);
 #pragma unroll
     for (int m = 2; m < L; m <<= 1) {
       acc.x += __shfl_xor(acc.x, m, 64);
@@ -381,18 +430,7 @@ __global__ __launch_bounds__(256) void spmm8_cb_kernel(SpmmCbArgs a) {
       acc.z += __shfl_xor(acc.z, m, 64);
       acc.w += __shfl_xor(acc.w, m, 64);
     }
-    if (row_ok && li < 2) {
-      if constexpr (NT) {
-        // write-through (sc1) store: the partial leaves the XCD's L2 instead of evicting the
-        // panel block (a partial is re-read only by cb_reduce, a later launch)
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(P, 0, 0x7FFFFFFF, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc), rsrc,
-                                               (int)(row * 32 + li * 16), 0, 16);
-      } else {
-        *reinterpret_cast<f32x4*>(P + row * 8 + li * 4) = acc;
-      }
-    }
+    if (row_ok && li < 2) *reinterpret_cast<f32x4*>(P + row * 8 + li * 4) = acc;
   }
 }
 
@@ -405,33 +443,40 @@ extern "C" hipError_t n2v2r_launch_spmm_cb(const SpmmCbArgs& a, hipStream_t stre
   }
   int rpw = 1;  // aim for ~3-4 gather steps of L/2 panel rows per row group
   while (rpw < 16 && 64.0 / (rpw * 2) / 2.0 * 3.5 >= avg) rpw *= 2;
+  static const int rpw_env = [] {  // N2V2R_CB_RPW / N2V2R_CB_WGS: tuning runs
+    const char* s = getenv("N2V2R_CB_RPW");
+    return s ? atoi(s) : 0;
+  }();
+  static const int wgs_env = [] {
+    const char* s = getenv("N2V2R_CB_WGS");
+    return s ? atoi(s) : 0;
+  }();
+  if (rpw_env == 1 || rpw_env == 2 || rpw_env == 4 || rpw_env == 8 || rpw_env == 16) rpw = rpw_env;
   const int64_t waves = (n + rpw - 1) / rpw;
   int64_t per = (waves + 3) / 4;  // workgroups per block
-  const int64_t cap = N2V2R_SPMM_WGS / CB_NB;
+  const int64_t cap = (wgs_env >= CB_NB ? wgs_env : N2V2R_SPMM_WGS) / CB_NB;
   if (per > cap) per = cap;
   if (per < 1) per = 1;
   dim3 grid((unsigned)(per * CB_NB));
-  static const int nt = [] {  // N2V2R_CB_NT=1: non-temporal index stream (A/B runs)
-    const char* s = getenv("N2V2R_CB_NT");
-    return s && s[0] == '1';
+  static const bool unr = [] {
+    const char* s = getenv("N2V2R_CB_UNR");
+    return !(s && s[0] == '0');
   }();
-  if (nt) {
-    switch (rpw) {
-      case 16: hipLaunchKernelGGL((spmm8_cb_kernel<16, true>), grid, dim3(256), 0, stream, a); break;
-      case 8: hipLaunchKernelGGL((spmm8_cb_kernel<8, true>), grid, dim3(256), 0, stream, a); break;
-      case 4: hipLaunchKernelGGL((spmm8_cb_kernel<4, true>), grid, dim3(256), 0, stream, a); break;
-      case 2: hipLaunchKernelGGL((spmm8_cb_kernel<2, true>), grid, dim3(256), 0, stream, a); break;
-      default: hipLaunchKernelGGL((spmm8_cb_kernel<1, true>), grid, dim3(256), 0, stream, a); break;
-    }
-    return hipGetLastError();
-  }
+#define CB_LAUNCH(R)                                                                         \
+  do {                                                                                       \
+    if (unr)                                                                                 \
+      hipLaunchKernelGGL((spmm8_cb_kernel<R, true>), grid, dim3(256), 0, stream, a);         \
+    else                                                                                     \
+      hipLaunchKernelGGL((spmm8_cb_kernel<R, false>), grid, dim3(256), 0, stream, a);        \
+  } while (0)
   switch (rpw) {
-    case 16: hipLaunchKernelGGL((spmm8_cb_kernel<16, false>), grid, dim3(256), 0, stream, a); break;
-    case 8: hipLaunchKernelGGL((spmm8_cb_kernel<8, false>), grid, dim3(256), 0, stream, a); break;
-    case 4: hipLaunchKernelGGL((spmm8_cb_kernel<4, false>), grid, dim3(256), 0, stream, a); break;
-    case 2: hipLaunchKernelGGL((spmm8_cb_kernel<2, false>), grid, dim3(256), 0, stream, a); break;
-    default: hipLaunchKernelGGL((spmm8_cb_kernel<1, false>), grid, dim3(256), 0, stream, a); break;
+    case 16: CB_LAUNCH(16); break;
+    case 8: CB_LAUNCH(8); break;
+    case 4: CB_LAUNCH(4); break;
+    case 2: CB_LAUNCH(2); break;
+    default: CB_LAUNCH(1); break;
   }
+#undef CB_LAUNCH
   return hipGetLastError();
 }
 
