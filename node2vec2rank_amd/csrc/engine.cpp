@@ -1100,6 +1100,17 @@ struct Eig {
         goto rayleigh_ritz;
       }
       if (test_redo && cycle == 0 && lazy) refilled = 1;  // tests: exercise the recovery
+      // a non-finite Ritz pair under the lazy (two-pass) orthogonalisation: redo the cycle's
+      // expansion with three passes from the kept (finite) basis before giving up below
+      if (lazy && !refilled)
+        for (int j = 0; j < keep; ++j)
+          if (!std::isfinite(wh[j]) || (j < d && !std::isfinite(res2[j]))) {
+            if (trace)
+              fprintf(stderr, "[n2v2r] non-finite Ritz pair %d, cycle %d expanded again\n", j,
+                      cycle);
+            refilled = 1;
+            break;
+          }
       if (refilled) {  // a second pass refilled a column: expand this cycle again, 3 passes
         if (trace) fprintf(stderr, "[n2v2r] rank-deficient block, cycle %d expanded again\n", cycle);
         for (int q = 0; q < pb; ++q) {
