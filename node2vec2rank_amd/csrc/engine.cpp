@@ -438,6 +438,9 @@ struct EigWorkspace {
 struct n2v2r_handle {
   int device = 0;
   hipStream_t stream = nullptr;
+  // side stream + events for the column-block SpMM's stage-1 reduce overlap
+  hipStream_t side = nullptr;
+  hipEvent_t cb_ev[2 * SPMM_MAX_LAYERS] = {};
   std::string err;
   int K = 0;
   int64_t n = 0;        // global nodes
@@ -772,6 +775,52 @@ struct Eig {
   void apply_M_cb(const float* xg, float* Wout, int64_t ng) {
     const int64_t pst = npad * 8;
     float* part = h->ews.cbpart.as<float>();
+    static const bool overlap = [] {  // measured: cfg4 fit 2240 -> 2221 ms; =0 disables
+      const char* e = std::getenv("N2V2R_CB_OVERLAP");
+      return !(e && e[0] == '0');
+    }();
+    if (overlap && !h->comm) {
+      // stage-1 reduce of layer k on the side stream, beside the block launch of layer k + 1
+      // (and the stage-2 launch of layer k - 1); the same kernels and order of sums
+      if (!h->side) {
+        HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+        for (hipEvent_t& e : h->cb_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      }
+      for (int k = 0; k < K; ++k) {
+        LayerDev& L = *h->layers[k];
+        SpmmCbArgs a{};
+        for (int j = 0; j < CB_NB; ++j) a.A[j] = (L.symmetric ? L.cb : L.cb_t).blk[j];
+        a.X = xg;
+        a.ldx = 8;
+        a.P = part + (size_t)k * CB_NB * pst;
+        a.pstride = pst;
+        HIPCHK(n2v2r_launch_spmm_cb(a, st));
+        HIPCHK(hipEventRecord(h->cb_ev[k], st));
+        HIPCHK(hipStreamWaitEvent(h->side, h->cb_ev[k], 0));
+        HIPCHK(n2v2r_launch_cb_reduce(a.P, CB_NB, pst, n, h->ews.zk[k]->as<float>(), 8, h->side));
+        HIPCHK(hipEventRecord(h->cb_ev[SPMM_MAX_LAYERS + k], h->side));
+      }
+      for (int k = 0; k < K; ++k) {
+        LayerDev& L = *h->layers[k];
+        HIPCHK(hipStreamWaitEvent(st, h->cb_ev[SPMM_MAX_LAYERS + k], 0));
+        SpmmCbArgs a{};
+        for (int j = 0; j < CB_NB; ++j) a.A[j] = L.cb.blk[j];
+        a.X = h->ews.zk[k]->as<float>();
+        a.ldx = 8;
+        a.P = part + (size_t)k * CB_NB * pst;
+        a.pstride = pst;
+        HIPCHK(n2v2r_launch_spmm_cb(a, st));
+      }
+      HIPCHK(n2v2r_launch_cb_reduce(part, K * CB_NB, pst, n, Wout, 8, st));
+      for (int k = 0; k < K; ++k) {
+        const LayerDev& L = *h->layers[k];
+        algo_bytes += spmm_algo_bytes(L.nnz, L.unit, n, n, b) +
+                      spmm_algo_bytes(L.symmetric ? L.nnz : L.t_nnz,
+                                      L.symmetric ? L.unit : L.t_unit, n, n, b);
+      }
+      launches += 2 * K + K + 1;
+      return;
+    }
     for (int k = 0; k < K; ++k) {
       LayerDev& L = *h->layers[k];
       SpmmCbArgs a{};
@@ -1329,6 +1378,9 @@ void n2v2r_destroy(n2v2r_handle* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   h->layers.clear();
   h->comm.reset();
+  for (hipEvent_t& e : h->cb_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->side) (void)hipStreamDestroy(h->side);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
