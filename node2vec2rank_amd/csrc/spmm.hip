@@ -451,7 +451,9 @@ extern "C" hipError_t n2v2r_launch_spmm_cb(const SpmmCbArgs& a, hipStream_t stre
     const char* s = getenv("N2V2R_CB_WGS");
     return s ? atoi(s) : 0;
   }();
-  if (rpw_env == 1 || rpw_env == 2 || rpw_env == 4 || rpw_env == 8 || rpw_env == 16) rpw = rpw_env;
+  if (rpw_env == 1 || rpw_env == 2 || rpw_env == 4 || rpw_env == 8 || rpw_env == 16 ||
+      rpw_env == 32)
+    rpw = rpw_env;
   const int64_t waves = (n + rpw - 1) / rpw;
   int64_t per = (waves + 3) / 4;  // workgroups per block
   const int64_t cap = (wgs_env >= CB_NB ? wgs_env : N2V2R_SPMM_WGS) / CB_NB;
@@ -470,6 +472,7 @@ extern "C" hipError_t n2v2r_launch_spmm_cb(const SpmmCbArgs& a, hipStream_t stre
       hipLaunchKernelGGL((spmm8_cb_kernel<R, false>), grid, dim3(256), 0, stream, a);        \
   } while (0)
   switch (rpw) {
+    case 32: CB_LAUNCH(32); break;
     case 16: CB_LAUNCH(16); break;
     case 8: CB_LAUNCH(8); break;
     case 4: CB_LAUNCH(4); break;
