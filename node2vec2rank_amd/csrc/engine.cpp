@@ -56,8 +56,17 @@ struct SpmmArgs {
   const float* colscale;
 };
 #define CB_NB 8
+struct CsrBlk {  // spmm.hip: one column block, int32 row pointers relative to base
+  const int32_t* rp;
+  const int32_t* indices;
+  const float* data;
+  int64_t base;
+  int64_t n_rows;
+  int64_t nnz;
+  int unit;
+};
 struct SpmmCbArgs {  // spmm.hip: column block j of one layer, partial j at P + j * pstride
-  CsrDev A[CB_NB];
+  CsrBlk A[CB_NB];
   const float* X;
   int64_t ldx;
   float* P;
@@ -242,10 +251,11 @@ struct LayerDev {
   }
   // column-block form of A and (directed) A^T for the XCD-local SpMM (built on first use)
   struct ColBlocks {
-    DevBuf rp, idx, dat;   // [CB_NB][n_rows + 1] absolute row pointers; entries; values
-    CsrDev blk[CB_NB];
+    DevBuf rp, idx, dat;   // [CB_NB][n_rows + 1] int32 row pointers (relative); entries; values
+    CsrBlk blk[CB_NB];
     int64_t ncols = 0;     // column count the blocks were cut for
     bool built = false;
+    bool usable = false;   // every block under 2^31 entries (int32 row pointers)
   };
   ColBlocks cb, cb_t;
   void drop_col_blocks() {
@@ -264,6 +274,9 @@ struct LayerDev {
 void build_col_blocks(const CsrDev& A, int64_t ncols, LayerDev::ColBlocks& out, hipStream_t st) {
   const int64_t n = A.n_rows;
   const int64_t cw = (ncols + CB_NB - 1) / CB_NB;
+  out.ncols = ncols;
+  out.built = true;
+  out.usable = false;
   DevBuf cnt;
   cnt.ensure(sizeof(int32_t) * CB_NB * std::max<int64_t>(n, 1), st);
   HIPCHK(n2v2r_launch_cb_count(A, cw, cnt.as<int32_t>(), st));
@@ -272,38 +285,50 @@ void build_col_blocks(const CsrDev& A, int64_t ncols, LayerDev::ColBlocks& out, 
     HIPCHK(hipMemcpyAsync(hc.data(), cnt.p, sizeof(int32_t) * hc.size(), hipMemcpyDeviceToHost,
                           st));
   HIPCHK(hipStreamSynchronize(st));
-  std::vector<int64_t> rp((size_t)CB_NB * (n + 1));
+  std::vector<int64_t> rp((size_t)CB_NB * (n + 1));  // absolute, for the scatter
+  std::vector<int32_t> rp32((size_t)CB_NB * (n + 1));  // relative to the block's base
   int64_t pos = 0;
+  int64_t base[CB_NB];
   for (int j = 0; j < CB_NB; ++j) {
     int64_t* r = rp.data() + (size_t)j * (n + 1);
+    int32_t* r32 = rp32.data() + (size_t)j * (n + 1);
+    base[j] = pos;
     for (int64_t i = 0; i < n; ++i) {
       r[i] = pos;
+      r32[i] = (int32_t)(pos - base[j]);
       pos += hc[(size_t)j * n + i];
     }
     r[n] = pos;
+    if (pos - base[j] > (int64_t)INT32_MAX) return;  // too large for int32: row kernel
+    r32[n] = (int32_t)(pos - base[j]);
   }
   if (pos != A.nnz) throw StatusFail{N2V2R_ERR_HIP, "column-block split lost entries"};
-  out.rp.ensure(sizeof(int64_t) * rp.size(), st);
+  DevBuf rp64;
+  rp64.ensure(sizeof(int64_t) * rp.size(), st);
+  out.rp.ensure(sizeof(int32_t) * rp32.size(), st);
   out.idx.ensure(sizeof(int32_t) * std::max<int64_t>(A.nnz, 1), st);
   if (!A.unit) out.dat.ensure(sizeof(float) * std::max<int64_t>(A.nnz, 1), st);
-  HIPCHK(hipMemcpyAsync(out.rp.p, rp.data(), sizeof(int64_t) * rp.size(), hipMemcpyHostToDevice,
+  HIPCHK(hipMemcpyAsync(rp64.p, rp.data(), sizeof(int64_t) * rp.size(), hipMemcpyHostToDevice,
                         st));
-  HIPCHK(n2v2r_launch_cb_fill(A, cw, out.rp.as<int64_t>(), out.idx.as<int32_t>(),
+  HIPCHK(hipMemcpyAsync(out.rp.p, rp32.data(), sizeof(int32_t) * rp32.size(),
+                        hipMemcpyHostToDevice, st));
+  HIPCHK(n2v2r_launch_cb_fill(A, cw, rp64.as<int64_t>(), out.idx.as<int32_t>(),
                               A.unit ? nullptr : out.dat.as<float>(), st));
   HIPCHK(hipStreamSynchronize(st));
   for (int j = 0; j < CB_NB; ++j) {
     const int64_t* r = rp.data() + (size_t)j * (n + 1);
-    out.blk[j] = CsrDev{out.rp.as<int64_t>() + (size_t)j * (n + 1), out.idx.as<int32_t>(),
-                        A.unit ? nullptr : out.dat.as<float>(), n, r[n] - r[0], A.unit};
+    out.blk[j] = CsrBlk{out.rp.as<int32_t>() + (size_t)j * (n + 1), out.idx.as<int32_t>(),
+                        A.unit ? nullptr : out.dat.as<float>(), base[j], n, r[n] - r[0], A.unit};
   }
-  out.ncols = ncols;
-  out.built = true;
+  out.usable = true;
 }
 
-void ensure_col_blocks(LayerDev& L, int64_t ncols, hipStream_t st) {
+// false when a block would exceed int32 row pointers (then the row kernel runs)
+bool ensure_col_blocks(LayerDev& L, int64_t ncols, hipStream_t st) {
   if (!L.cb.built || L.cb.ncols != ncols) build_col_blocks(L.csr(), ncols, L.cb, st);
   if (!L.symmetric && (!L.cb_t.built || L.cb_t.ncols != ncols))
     build_col_blocks(L.csr_t(), ncols, L.cb_t, st);
+  return L.cb.usable && (L.symmetric || L.cb_t.usable);
 }
 
 // ---- communicators ----------------------------------------------------------------------
@@ -1003,8 +1028,8 @@ struct Eig {
     }
     col_blocks = col_blocks_wanted(h, b);
     if (col_blocks) {
-      for (auto& Lp : h->layers) ensure_col_blocks(*Lp, nglob, st);
-      h->ews.cbpart.ensure(sizeof(float) * (size_t)K * CB_NB * npad * 8);
+      for (auto& Lp : h->layers) col_blocks = ensure_col_blocks(*Lp, nglob, st) && col_blocks;
+      if (col_blocks) h->ews.cbpart.ensure(sizeof(float) * (size_t)K * CB_NB * npad * 8);
     }
     // chunk partials: also the streaming Gram form at b = 8 (chunks of <= 8192 rows, rounded to
     // a multiple of 8, (c + b) x b fp64 each)
@@ -2086,11 +2111,10 @@ int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, con
       HIPCHK(hipStreamSynchronize(h->stream));
       return N2V2R_OK;
     }
-    if (col_blocks_wanted(h, b)) {
+    if (col_blocks_wanted(h, b) && ensure_col_blocks(*h->layers[k], h->n, h->stream)) {
       // column-block SpMM of one layer: the block launch + the fixed-order partial reduce,
       // timed together (the same algorithmic bytes as the row kernel; the partials are extra)
       LayerDev& Lm = *h->layers[k];
-      ensure_col_blocks(Lm, h->n, h->stream);
       const int64_t pst = std::max<int64_t>(h->nloc, 1) * 8;
       DevBuf part;
       part.ensure(sizeof(float) * CB_NB * pst, h->stream);

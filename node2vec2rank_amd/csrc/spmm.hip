@@ -342,8 +342,20 @@ extern "C" hipError_t n2v2r_launch_spmm(const SpmmArgs& args, int B, hipStream_t
 // layer launch.
 #define CB_NB 8
 
+// One column block: int32 row pointers relative to `base` (the block's first entry in the
+// shared index / value arrays; half the row-pointer bytes of int64).
+struct CsrBlk {
+  const int32_t* rp;      // n_rows + 1
+  const int32_t* indices; // shared by the 8 blocks of a layer
+  const float* data;      // shared (nullptr when unit)
+  int64_t base;
+  int64_t n_rows;
+  int64_t nnz;
+  int unit;
+};
+
 struct SpmmCbArgs {
-  CsrDev A[CB_NB];   // column block j of one layer: absolute int64 row pointers
+  CsrBlk A[CB_NB];   // column block j of one layer
   const float* X;    // gathered panel, global column index = panel row
   int64_t ldx;
   float* P;          // partial j at P + j * pstride, rows of 8 fp32
@@ -355,7 +367,7 @@ struct SpmmCbArgs {
 // index -> gather latency per 2L entries instead of per L).  Same per-lane entry order as
 // spmm_row_accumulate<8, RPW>.
 template <int RPW>
-__device__ __forceinline__ void cb_row_accumulate(const CsrDev& A, const float* __restrict__ X,
+__device__ __forceinline__ void cb_row_accumulate(const CsrBlk& A, const float* __restrict__ X,
                                                   int64_t ldx, int64_t row, bool row_ok,
                                                   int lane, f32x4& acc) {
   constexpr int L = 64 / RPW;
@@ -366,8 +378,8 @@ __device__ __forceinline__ void cb_row_accumulate(const CsrDev& A, const float* 
   const int srcbase = g * L + (li >> 1);
   int64_t beg = 0, end = 0;
   if (row_ok) {
-    beg = A.indptr[row];
-    end = A.indptr[row + 1];
+    beg = A.base + A.rp[row];
+    end = A.base + A.rp[row + 1];
   }
   const int64_t len = end - beg;
   int64_t maxlen = len;
@@ -401,16 +413,14 @@ __device__ __forceinline__ void cb_row_accumulate(const CsrDev& A, const float* 
   }
 }
 
-// UNR: cb_row_accumulate (two group-widths of indices per gather round), else the generic
-// spmm_row_accumulate<8, RPW> (A/B: N2V2R_CB_UNR=0)
-template <int RPW, bool UNR>
+template <int RPW>
 __global__ __launch_bounds__(256) void spmm8_cb_kernel(SpmmCbArgs a) {
   constexpr int L = 64 / RPW;
   const int lane = threadIdx.x & 63;
   const int j = blockIdx.x & (CB_NB - 1);
   const int64_t t = blockIdx.x / CB_NB;
   const int64_t nwg = gridDim.x / CB_NB;
-  const CsrDev& A = a.A[j];
+  const CsrBlk& A = a.A[j];
   const int64_t n = A.n_rows;
   const int li = lane % L;
   float* __restrict__ P = a.P + (int64_t)j * a.pstride;
@@ -419,10 +429,7 @@ __global__ __launch_bounds__(256) void spmm8_cb_kernel(SpmmCbArgs a) {
     const int64_t row = wid * RPW + lane / L;
     const bool row_ok = row < n;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (UNR)
-      cb_row_accumulate<RPW>(A, a.X, a.ldx, row, row_ok, lane, acc);
-    else
-      spmm_row_accumulate<8, RPW>(A, a.X, a.ldx, row, row_ok, lane, acc);
+    cb_row_accumulate<RPW>(A, a.X, a.ldx, row, row_ok, lane, acc);
 #pragma unroll
     for (int m = 2; m < L; m <<= 1) {
       acc.x += __shfl_xor(acc.x, m, 64);
@@ -460,17 +467,7 @@ extern "C" hipError_t n2v2r_launch_spmm_cb(const SpmmCbArgs& a, hipStream_t stre
   if (per > cap) per = cap;
   if (per < 1) per = 1;
   dim3 grid((unsigned)(per * CB_NB));
-  static const bool unr = [] {
-    const char* s = getenv("N2V2R_CB_UNR");
-    return !(s && s[0] == '0');
-  }();
-#define CB_LAUNCH(R)                                                                         \
-  do {                                                                                       \
-    if (unr)                                                                                 \
-      hipLaunchKernelGGL((spmm8_cb_kernel<R, true>), grid, dim3(256), 0, stream, a);         \
-    else                                                                                     \
-      hipLaunchKernelGGL((spmm8_cb_kernel<R, false>), grid, dim3(256), 0, stream, a);        \
-  } while (0)
+#define CB_LAUNCH(R) hipLaunchKernelGGL((spmm8_cb_kernel<R>), grid, dim3(256), 0, stream, a)
   switch (rpw) {
     case 32: CB_LAUNCH(32); break;
     case 16: CB_LAUNCH(16); break;
