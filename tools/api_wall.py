@@ -1,0 +1,60 @@
+"""PCIe-inclusive wall time of the drop-in API on one GPU.
+
+    python tools/api_wall.py [--config cfg2|cfg4] [--reps 3]
+
+Each rep builds a fresh ``N2V2R`` from host scipy CSR layers and times
+``fit_transform_rank()`` + ``aggregate_transform()`` end to end: host->HBM copy of the CSR
+layers, UASE, distances, Borda, the device->host copies and the DataFrame construction.
+``bench.py``'s ``value`` excludes the host->HBM copy (layers resident before the timed
+region); this is the rate a caller of the Python API sees.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+from node2vec2rank_amd import synthetic  # noqa: E402
+from node2vec2rank_amd.model import N2V2R  # noqa: E402
+
+CONFIGS = {
+    "cfg2": dict(n=100_000, avg_deg=20.0, dims=[64]),
+    "cfg4": dict(n=1_000_000, avg_deg=50.0, dims=[8, 16, 32, 64, 128]),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--reps", type=int, default=3)
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    layers = synthetic.er_layers(cfg["n"], cfg["avg_deg"], 2, seed_base=1000)
+    nodes = [f"n{i}" for i in range(cfg["n"])]
+    config = dict(embed_dimensions=cfg["dims"], distance_metrics=["cosine", "euclidean"],
+                  comp_strategy="sequential", seed=7, verbose=-1)
+    times = []
+    for rep in range(args.reps + 1):  # rep 0 warms the engine (module load, allocations)
+        t0 = time.perf_counter()
+        model = N2V2R(layers, nodes, config)
+        model.fit_transform_rank()
+        model.aggregate_transform()
+        t1 = time.perf_counter()
+        if rep:
+            times.append(t1 - t0)
+        del model
+    best = min(times)
+    print(json.dumps({"config": args.config, "nodes": cfg["n"], "reps": args.reps,
+                      "s_per_call": [round(t, 4) for t in times],
+                      "nodes_per_s_best": round(cfg["n"] / best, 1),
+                      "csr_bytes": int(sum(a.data.nbytes + a.indices.nbytes + a.indptr.nbytes
+                                           for a in layers))}))
+
+
+if __name__ == "__main__":
+    main()
