@@ -597,21 +597,46 @@ void host_transpose(int64_t n, int64_t nnz, const int64_t* ip, const int32_t* ix
 bool host_is_symmetric(int64_t n, const int64_t* ip, const int32_t* ix, const float* dv,
                        const std::vector<int64_t>& tp, const std::vector<int32_t>& tx,
                        const std::vector<float>& td) {
-  // A == A^T iff row r of A equals row r of A^T as (sorted col, value) multisets.
-  for (int64_t r = 0; r < n; ++r) {
-    const int64_t a0 = ip[r], a1 = ip[r + 1], b0 = tp[r], b1 = tp[r + 1];
-    if (a1 - a0 != b1 - b0) return false;
+  // A == A^T iff row r of A equals row r of A^T as (sorted col, value) multisets.  Transpose
+  // rows come out column-sorted; a column-sorted row of A (the Python side sorts) compares in
+  // place, an unsorted one through a sorted copy.  Rows are split over up to 16 host threads.
+  auto rows_match = [&](int64_t r0, int64_t r1) -> bool {
     std::vector<std::pair<int32_t, float>> ra, rb;
-    ra.reserve(a1 - a0);
-    rb.reserve(b1 - b0);
-    for (int64_t p = a0; p < a1; ++p) ra.emplace_back(ix[p], dv[p]);
-    for (int64_t p = b0; p < b1; ++p) rb.emplace_back(tx[p], td[p]);
-    bool sorted_a = true;
-    for (size_t i = 1; i < ra.size(); ++i)
-      if (ra[i].first < ra[i - 1].first) sorted_a = false;
-    if (!sorted_a) std::sort(ra.begin(), ra.end());
-    if (ra != rb) return false;  // transpose rows come out column-sorted already
-  }
+    for (int64_t r = r0; r < r1; ++r) {
+      const int64_t a0 = ip[r], a1 = ip[r + 1], b0 = tp[r], b1 = tp[r + 1];
+      if (a1 - a0 != b1 - b0) return false;
+      bool sorted_a = true;
+      for (int64_t p = a0 + 1; p < a1; ++p)
+        if (ix[p] < ix[p - 1]) sorted_a = false;
+      if (sorted_a) {
+        for (int64_t i = 0; i < a1 - a0; ++i)
+          if (ix[a0 + i] != tx[b0 + i] || !(dv[a0 + i] == td[b0 + i])) return false;
+        continue;
+      }
+      ra.clear();
+      rb.clear();
+      for (int64_t p = a0; p < a1; ++p) ra.emplace_back(ix[p], dv[p]);
+      for (int64_t p = b0; p < b1; ++p) rb.emplace_back(tx[p], td[p]);
+      std::sort(ra.begin(), ra.end());
+      if (ra != rb) return false;
+    }
+    return true;
+  };
+  const int64_t nnz = ip[n];
+  int nt = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+  if (nnz < (int64_t)1 << 20 || n < 4096) nt = 1;
+  if (nt == 1) return rows_match(0, n);
+  std::vector<char> ok(nt, 1);
+  std::vector<std::thread> pool;
+  const int64_t per = (n + nt - 1) / nt;
+  for (int t = 0; t < nt; ++t)
+    pool.emplace_back([&, t] {
+      const int64_t r0 = std::min<int64_t>(n, t * per), r1 = std::min<int64_t>(n, r0 + per);
+      ok[t] = rows_match(r0, r1) ? 1 : 0;
+    });
+  for (auto& th : pool) th.join();
+  for (char c : ok)
+    if (!c) return false;
   return true;
 }
 
