@@ -581,17 +581,68 @@ int guarded(n2v2r_handle* h, F&& f) {
 void host_transpose(int64_t n, int64_t nnz, const int64_t* ip, const int32_t* ix, const float* dv,
                     std::vector<int64_t>& tp, std::vector<int32_t>& tx, std::vector<float>& td) {
   tp.assign(n + 1, 0);
-  for (int64_t p = 0; p < nnz; ++p) tp[ix[p] + 1]++;
-  for (int64_t i = 0; i < n; ++i) tp[i + 1] += tp[i];
   tx.resize(nnz);
   td.resize(nnz);
-  std::vector<int64_t> cur(tp.begin(), tp.end() - 1);
-  for (int64_t r = 0; r < n; ++r)
-    for (int64_t p = ip[r]; p < ip[r + 1]; ++p) {
-      const int64_t q = cur[ix[p]]++;
-      tx[q] = (int32_t)r;
-      td[q] = dv[p];
+  // Counting sort.  Large layers: rows split into nt ordered chunks, per-chunk column counts,
+  // chunk t's entries of a column placed after chunks 0..t-1's, so every transpose row keeps
+  // ascending source-row order (the same output as the serial sort).
+  int nt = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+  while (nt > 1 && (double)nt * (double)n * 8.0 > 1024.0 * 1024 * 1024) --nt;
+  if (nnz < (int64_t)1 << 22 || n < 4096) nt = 1;
+  if (nt == 1) {
+    for (int64_t p = 0; p < nnz; ++p) tp[ix[p] + 1]++;
+    for (int64_t i = 0; i < n; ++i) tp[i + 1] += tp[i];
+    std::vector<int64_t> cur(tp.begin(), tp.end() - 1);
+    for (int64_t r = 0; r < n; ++r)
+      for (int64_t p = ip[r]; p < ip[r + 1]; ++p) {
+        const int64_t q = cur[ix[p]]++;
+        tx[q] = (int32_t)r;
+        td[q] = dv[p];
+      }
+    return;
+  }
+  const int64_t per = (n + nt - 1) / nt;
+  std::vector<int64_t> cnt((size_t)nt * n, 0);  // [chunk][column] counts, then cursors
+  auto run = [&](auto&& fn) {
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nt; ++t) pool.emplace_back([&, t] { fn(t); });
+    for (auto& th : pool) th.join();
+  };
+  run([&](int t) {
+    int64_t* c = cnt.data() + (size_t)t * n;
+    const int64_t r0 = std::min<int64_t>(n, t * per), r1 = std::min<int64_t>(n, r0 + per);
+    for (int64_t p = ip[r0]; p < ip[r1]; ++p) c[ix[p]]++;
+  });
+  run([&](int t) {  // column totals, for columns of slice t
+    const int64_t c0 = std::min<int64_t>(n, t * per), c1 = std::min<int64_t>(n, c0 + per);
+    for (int64_t col = c0; col < c1; ++col) {
+      int64_t s = 0;
+      for (int u = 0; u < nt; ++u) s += cnt[(size_t)u * n + col];
+      tp[col + 1] = s;
     }
+  });
+  for (int64_t i = 0; i < n; ++i) tp[i + 1] += tp[i];
+  run([&](int t) {  // per-chunk start offsets, for columns of slice t
+    const int64_t c0 = std::min<int64_t>(n, t * per), c1 = std::min<int64_t>(n, c0 + per);
+    for (int64_t col = c0; col < c1; ++col) {
+      int64_t s = tp[col];
+      for (int u = 0; u < nt; ++u) {
+        const int64_t k = cnt[(size_t)u * n + col];
+        cnt[(size_t)u * n + col] = s;
+        s += k;
+      }
+    }
+  });
+  run([&](int t) {
+    int64_t* cur = cnt.data() + (size_t)t * n;
+    const int64_t r0 = std::min<int64_t>(n, t * per), r1 = std::min<int64_t>(n, r0 + per);
+    for (int64_t r = r0; r < r1; ++r)
+      for (int64_t p = ip[r]; p < ip[r + 1]; ++p) {
+        const int64_t q = cur[ix[p]]++;
+        tx[q] = (int32_t)r;
+        td[q] = dv[p];
+      }
+  });
 }
 
 bool host_is_symmetric(int64_t n, const int64_t* ip, const int32_t* ix, const float* dv,
