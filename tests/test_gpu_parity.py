@@ -48,6 +48,28 @@ def test_spmm_column_blocks_matches_scipy(engine, name, monkeypatch):
     assert not engine.spmm_col_blocks(8)
 
 
+@pytest.mark.parametrize("symmetrise", [False, True])
+def test_spmm_large_directed_host_transpose(engine, symmetrise):
+    """Layers large enough (>= 2^22 entries) for the multi-threaded host transpose and symmetry
+    check at ingest: A^T x through the stored transpose (or A itself when detected symmetric)
+    matches scipy; an asymmetric layer wrongly detected symmetric would fail here."""
+    n = 300_000
+    rng = np.random.default_rng(11)
+    A = sp.random(n, n, density=16.0 / n, format="csr", dtype=np.float32, random_state=rng)
+    A.data = rng.integers(1, 5, A.nnz).astype(np.float32)
+    if symmetrise:
+        A = (A + A.T).tocsr()
+    assert A.nnz >= 1 << 22
+    engine.set_layers([A])
+    X = rng.standard_normal((n, 8)).astype(np.float32)
+    for tr in (False, True):
+        Y, _, _ = engine.bench_spmm(0, X, transpose=tr, reps=1)
+        M = A.T if tr else A
+        ref = M.astype(np.float64) @ X.astype(np.float64)
+        scale = np.abs(M).astype(np.float64) @ np.abs(X).astype(np.float64)
+        assert np.all(np.abs(Y - ref) <= 1e-5 * scale + 1e-6), (symmetrise, tr)
+
+
 @pytest.mark.parametrize("weighted", [False, True])
 def test_spmm_b8_long_rows_and_empty_rows(engine, weighted):
     """The B = 8 pipelined kernel: rows longer than 32 (the non-pipelined remainder), empty
