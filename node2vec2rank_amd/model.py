@@ -83,6 +83,14 @@ class N2V2R:
         self._cols = None
 
     # ------------------------------------------------------------------------------------
+    def _node_index(self):
+        """``pd.Index`` of the node labels, built once per label list (building it from a
+        Python list is the slowest host step of a 1M-node call; every output frame shares it)."""
+        if getattr(self, "_index_src", None) is not self.node_names:
+            self._index = pd.Index(self.node_names)
+            self._index_src = self.node_names
+        return self._index
+
     def _load_layers(self):
         if not self._layers_loaded:
             self._engine.set_layers([_as_layer(g) for g in self.graphs])
@@ -115,7 +123,7 @@ class N2V2R:
         out = {}
         for c, key in enumerate(keys):
             D = self._engine.distances(c)
-            out[key] = pd.DataFrame(D, index=self.node_names, columns=cols)
+            out[key] = pd.DataFrame(D, index=self._node_index(), columns=cols)
         return out
 
     def fit_transform_rank(self):
@@ -167,7 +175,7 @@ class N2V2R:
             out = {}
             for c, key in enumerate(self._keys):
                 b = self._engine.borda(c)
-                out[key] = pd.DataFrame(b, index=self.node_names, columns=['borda_ranks'])
+                out[key] = pd.DataFrame(b, index=self._node_index(), columns=['borda_ranks'])
             self.pairwise_aggregate_ranks = out
             if self.config["verbose"] == 1:
                 print(f"\tFinished aggregation in {round(time.time() - start, 2)} seconds")
