@@ -578,6 +578,30 @@ int guarded(n2v2r_handle* h, F&& f) {
 }
 
 // ---- host CSR helpers -------------------------------------------------------------------
+// every column index in [0, n); large layers are checked in up to 16 host threads
+bool host_indices_in_range(int64_t nnz, const int32_t* ix, int64_t n) {
+  auto ok = [&](int64_t p0, int64_t p1) {
+    bool good = true;
+    for (int64_t p = p0; p < p1; ++p) good &= (ix[p] >= 0) & ((int64_t)ix[p] < n);
+    return good;
+  };
+  int nt = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+  if (nnz < (int64_t)1 << 22) nt = 1;
+  if (nt == 1) return ok(0, nnz);
+  std::vector<char> res(nt, 1);
+  std::vector<std::thread> pool;
+  const int64_t per = (nnz + nt - 1) / nt;
+  for (int t = 0; t < nt; ++t)
+    pool.emplace_back([&, t] {
+      const int64_t p0 = std::min<int64_t>(nnz, t * per);
+      res[t] = ok(p0, std::min<int64_t>(nnz, p0 + per)) ? 1 : 0;
+    });
+  for (auto& th : pool) th.join();
+  for (char c : res)
+    if (!c) return false;
+  return true;
+}
+
 void host_transpose(int64_t n, int64_t nnz, const int64_t* ip, const int32_t* ix, const float* dv,
                     std::vector<int64_t>& tp, std::vector<int32_t>& tx, std::vector<float>& td) {
   tp.assign(n + 1, 0);
@@ -1535,11 +1559,10 @@ int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const in
         h->set_err("layer %d: indptr not monotone", k);
         return N2V2R_ERR_BAD_ARG;
       }
-    for (int64_t p = 0; p < nnz; ++p)
-      if (indices[p] < 0 || indices[p] >= n) {
-        h->set_err("layer %d: column index out of range", k);
-        return N2V2R_ERR_BAD_ARG;
-      }
+    if (!host_indices_in_range(nnz, indices, n)) {
+      h->set_err("layer %d: column index out of range", k);
+      return N2V2R_ERR_BAD_ARG;
+    }
     for (int j = 0; j < h->K; ++j)
       if (j != k && h->layers[j]->loaded && h->layers[j]->dense) {
         h->err = "layers must be all CSR or all dense";

@@ -48,6 +48,22 @@ def test_spmm_column_blocks_matches_scipy(engine, name, monkeypatch):
     assert not engine.spmm_col_blocks(8)
 
 
+@pytest.mark.parametrize("n,deg", [(1000, 4), (300_000, 16)])
+@pytest.mark.parametrize("bad", [-1, "n"])
+def test_set_layer_csr_rejects_out_of_range_columns(engine, n, deg, bad):
+    """A column index outside [0, n) is refused at ingest (small layers: serial check; >= 2^22
+    entries: the multi-threaded check), with the error text of the C-ABI."""
+    nnz = n * deg
+    indptr = np.arange(0, nnz + 1, deg, dtype=np.int64)
+    indices = np.tile(np.arange(deg, dtype=np.int32), n)
+    indices[nnz - 3] = -1 if bad == -1 else n
+    data = np.ones(nnz, dtype=np.float32)
+    engine._check(engine.lib.n2v2r_set_num_layers(engine.h, 1, n), "set_num_layers")
+    st = engine.lib.n2v2r_set_layer_csr(engine.h, 0, n, nnz, indptr, indices, data, 1)
+    with pytest.raises(Exception, match="out of range"):
+        engine._check(st, "layer 0")
+
+
 @pytest.mark.parametrize("symmetrise", [False, True])
 def test_spmm_large_directed_host_transpose(engine, symmetrise):
     """Layers large enough (>= 2^22 entries) for the multi-threaded host transpose and symmetry
