@@ -36,7 +36,8 @@ typedef enum {
   N2V2R_ERR_HIP = 4,                /* -> RuntimeError */
   N2V2R_ERR_OUT_OF_MEMORY = 5,      /* -> MemoryError */
   N2V2R_ERR_NOT_READY = 6,          /* -> ValueError("No n2v2r embeddings found"), model.py:199 */
-  N2V2R_ERR_UNSUPPORTED_AGG = 7     /* -> NotImplementedError, model.py:182-183 */
+  N2V2R_ERR_UNSUPPORTED_AGG = 7,    /* -> NotImplementedError, model.py:182-183 */
+  N2V2R_ERR_INTERNAL = 8            /* -> RuntimeError (host-side failure, e.g. a thread) */
 } n2v2r_status;
 
 /* comp_strategy (model.py:59-84) */

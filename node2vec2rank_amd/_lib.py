@@ -23,6 +23,7 @@ ERR_HIP = 4
 ERR_OUT_OF_MEMORY = 5
 ERR_NOT_READY = 6
 ERR_UNSUPPORTED_AGG = 7
+ERR_INTERNAL = 8
 
 STRATEGY = {"sequential": 0, "one_vs_before": 1, "one_vs_rest": 2}
 METRIC = {"cosine": 0, "euclidean": 1, "correlation": 2}

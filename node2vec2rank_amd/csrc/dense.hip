@@ -1441,3 +1441,24 @@ extern "C" hipError_t n2v2r_launch_colmax_sign(const unsigned long long* best, i
                      best, ncols_padded, U, ldu, d, row0, n, sign);
   return hipGetLastError();
 }
+
+// ----------------------------------------------------------------------------- debug
+// N2V2R_DEBUG_FINITE: *flag = 1 if any of `count` fp32 (f64 == 0) or fp64 values is not finite
+// (plain vector stores from the offending lanes; the host zeroes the flag and reads it back).
+__global__ void nonfinite_kernel(const void* __restrict__ p, int64_t count, int f64,
+                                 int* __restrict__ flag) {
+  bool bad = false;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < count;
+       e += (int64_t)gridDim.x * blockDim.x)
+    bad |= f64 ? !isfinite(static_cast<const double*>(p)[e]) : !isfinite(static_cast<const float*>(p)[e]);
+  if (bad) flag[0] = 1;
+}
+
+extern "C" hipError_t n2v2r_launch_nonfinite(const void* p, int64_t count, int f64, int* flag,
+                                             hipStream_t stream) {
+  if (count <= 0) return hipSuccess;
+  int64_t nb = (count + 255) / 256;
+  if (nb > 1024) nb = 1024;
+  hipLaunchKernelGGL(nonfinite_kernel, dim3((unsigned)nb), dim3(256), 0, stream, p, count, f64, flag);
+  return hipGetLastError();
+}

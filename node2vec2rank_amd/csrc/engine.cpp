@@ -38,6 +38,8 @@
 #include <numeric>
 #include <string>
 #include <thread>
+#include <exception>
+#include <system_error>
 #include <vector>
 
 #include "../../include/n2v2r.h"
@@ -162,6 +164,8 @@ hipError_t n2v2r_launch_rr_tri_eig(const double* d, const double* e, int c, int 
 hipError_t n2v2r_launch_rr_backtransform(const double* V, const double* tau, int c,
                                          const double* Y, int p, float* S, int lds,
                                          hipStream_t stream);
+hipError_t n2v2r_launch_nonfinite(const void* p, int64_t count, int f64, int* flag,
+                                  hipStream_t stream);
 }
 
 namespace {
@@ -184,6 +188,25 @@ struct StatusFail {
 double now_ms() {
   using namespace std::chrono;
   return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
+}
+
+// Debug switches (off by default; diagnostics only, never on the bench path):
+//   N2V2R_POISON=1        new allocations and, at every fit, the eigensolver's scratch are
+//                         filled with 0xFF bytes (NaN) instead of zeros: a read of anything a
+//                         kernel did not write this fit turns into a non-finite value;
+//   N2V2R_DEBUG_FINITE=1  the eigensolver checks every stage's output for non-finite values
+//                         and stops at the first stage that produced one, naming it.
+bool env_flag(const char* name) {
+  const char* e = std::getenv(name);
+  return e && *e && *e != '0';
+}
+bool debug_poison() {
+  static const bool v = env_flag("N2V2R_POISON");
+  return v;
+}
+bool debug_finite() {
+  static const bool v = env_flag("N2V2R_DEBUG_FINITE");
+  return v;
 }
 
 // Device allocation owned by the handle (zero-filled on allocation: padded rows stay zero).
@@ -211,10 +234,11 @@ struct DevBuf {
       throw StatusFail{N2V2R_ERR_OUT_OF_MEMORY,
                        "hipMalloc of " + std::to_string(b) + " bytes failed"};
     }
+    const int fill = debug_poison() ? 0xFF : 0;
     if (st) {
-      e = hipMemsetAsync(p, 0, b, st);
+      e = hipMemsetAsync(p, fill, b, st);
     } else {
-      e = hipMemset(p, 0, b);
+      e = hipMemset(p, fill, b);
       if (e == hipSuccess) e = hipDeviceSynchronize();
     }
     if (e != hipSuccess) throw HipFail{e, "hipMemset"};
@@ -457,6 +481,7 @@ struct EigWorkspace {
   DevBuf hband, band, varr, taua, rrerr;      // banded RR: band columns, band matrix, arrow
   DevBuf fcoef;                               // fp32 [-C R^-1; R^-1] of the apply pass
   DevBuf cbpart;                              // [K][CB_NB][npad][8] column-block partials
+  DevBuf dbgflag;                             // N2V2R_DEBUG_FINITE result flag
 };
 }  // namespace
 
@@ -574,10 +599,39 @@ int guarded(n2v2r_handle* h, F&& f) {
   } catch (const std::bad_alloc&) {
     h->err = "host allocation failed";
     return N2V2R_ERR_OUT_OF_MEMORY;
+  } catch (const std::exception& ex) {  // e.g. std::system_error from a host thread
+    h->err = std::string("host error: ") + ex.what();
+    return N2V2R_ERR_INTERNAL;
   }
 }
 
 // ---- host CSR helpers -------------------------------------------------------------------
+int host_threads() {
+  return (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+}
+
+// run fn(0) .. fn(nt - 1), one host thread each.  A thread that cannot be created leaves its
+// chunk (and the later ones) to the calling thread; every started thread is joined before
+// returning or rethrowing, so no joinable std::thread is ever destroyed.
+template <class F>
+void parallel_chunks(int nt, F&& fn) {
+  std::vector<std::thread> pool;
+  pool.reserve(nt);
+  int t = 0;
+  try {
+    for (; t < nt; ++t) pool.emplace_back([&fn, t] { fn(t); });
+  } catch (const std::system_error&) {
+  }
+  std::exception_ptr err;
+  try {
+    for (; t < nt; ++t) fn(t);
+  } catch (...) {
+    err = std::current_exception();
+  }
+  for (auto& th : pool) th.join();
+  if (err) std::rethrow_exception(err);
+}
+
 // every column index in [0, n); large layers are checked in up to 16 host threads
 bool host_indices_in_range(int64_t nnz, const int32_t* ix, int64_t n) {
   auto ok = [&](int64_t p0, int64_t p1) {
@@ -585,18 +639,15 @@ bool host_indices_in_range(int64_t nnz, const int32_t* ix, int64_t n) {
     for (int64_t p = p0; p < p1; ++p) good &= (ix[p] >= 0) & ((int64_t)ix[p] < n);
     return good;
   };
-  int nt = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+  int nt = host_threads();
   if (nnz < (int64_t)1 << 22) nt = 1;
   if (nt == 1) return ok(0, nnz);
   std::vector<char> res(nt, 1);
-  std::vector<std::thread> pool;
   const int64_t per = (nnz + nt - 1) / nt;
-  for (int t = 0; t < nt; ++t)
-    pool.emplace_back([&, t] {
-      const int64_t p0 = std::min<int64_t>(nnz, t * per);
-      res[t] = ok(p0, std::min<int64_t>(nnz, p0 + per)) ? 1 : 0;
-    });
-  for (auto& th : pool) th.join();
+  parallel_chunks(nt, [&](int t) {
+    const int64_t p0 = std::min<int64_t>(nnz, t * per);
+    res[t] = ok(p0, std::min<int64_t>(nnz, p0 + per)) ? 1 : 0;
+  });
   for (char c : res)
     if (!c) return false;
   return true;
@@ -610,7 +661,7 @@ void host_transpose(int64_t n, int64_t nnz, const int64_t* ip, const int32_t* ix
   // Counting sort.  Large layers: rows split into nt ordered chunks, per-chunk column counts,
   // chunk t's entries of a column placed after chunks 0..t-1's, so every transpose row keeps
   // ascending source-row order (the same output as the serial sort).
-  int nt = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+  int nt = host_threads();
   while (nt > 1 && (double)nt * (double)n * 8.0 > 1024.0 * 1024 * 1024) --nt;
   if (nnz < (int64_t)1 << 22 || n < 4096) nt = 1;
   if (nt == 1) {
@@ -627,11 +678,7 @@ void host_transpose(int64_t n, int64_t nnz, const int64_t* ip, const int32_t* ix
   }
   const int64_t per = (n + nt - 1) / nt;
   std::vector<int64_t> cnt((size_t)nt * n, 0);  // [chunk][column] counts, then cursors
-  auto run = [&](auto&& fn) {
-    std::vector<std::thread> pool;
-    for (int t = 0; t < nt; ++t) pool.emplace_back([&, t] { fn(t); });
-    for (auto& th : pool) th.join();
-  };
+  auto run = [&](auto&& fn) { parallel_chunks(nt, fn); };
   run([&](int t) {
     int64_t* c = cnt.data() + (size_t)t * n;
     const int64_t r0 = std::min<int64_t>(n, t * per), r1 = std::min<int64_t>(n, r0 + per);
@@ -698,18 +745,15 @@ bool host_is_symmetric(int64_t n, const int64_t* ip, const int32_t* ix, const fl
     return true;
   };
   const int64_t nnz = ip[n];
-  int nt = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+  int nt = host_threads();
   if (nnz < (int64_t)1 << 20 || n < 4096) nt = 1;
   if (nt == 1) return rows_match(0, n);
   std::vector<char> ok(nt, 1);
-  std::vector<std::thread> pool;
   const int64_t per = (n + nt - 1) / nt;
-  for (int t = 0; t < nt; ++t)
-    pool.emplace_back([&, t] {
-      const int64_t r0 = std::min<int64_t>(n, t * per), r1 = std::min<int64_t>(n, r0 + per);
-      ok[t] = rows_match(r0, r1) ? 1 : 0;
-    });
-  for (auto& th : pool) th.join();
+  parallel_chunks(nt, [&](int t) {
+    const int64_t r0 = std::min<int64_t>(n, t * per), r1 = std::min<int64_t>(n, r0 + per);
+    ok[t] = rows_match(r0, r1) ? 1 : 0;
+  });
   for (char c : ok)
     if (!c) return false;
   return true;
@@ -777,6 +821,36 @@ struct Eig {
   bool full_first = false;  // N2V2R_EIG_FULL_FIRST_PASS
   bool band_rr = false;     // banded Rayleigh-Ritz (b = 8, c <= 512), else dense
   bool col_blocks = false;  // XCD-local column-block SpMM (b = 8, large panels)
+
+  // N2V2R_DEBUG_FINITE: stop at the first stage whose output holds a non-finite value
+  int dbg_cycle = 0, dbg_apps = 0;
+  void dbg(const void* p, int64_t count, bool f64, const char* what) {
+    if (!debug_finite() || !p || count <= 0) return;
+    int* flag = h->ews.dbgflag.as<int>();
+    HIPCHK(hipMemsetAsync(flag, 0, sizeof(int), st));
+    HIPCHK(n2v2r_launch_nonfinite(p, count, f64 ? 1 : 0, flag, st));
+    int bad = 0;
+    HIPCHK(hipMemcpyAsync(&bad, flag, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (bad) {
+      const std::string msg = std::string("non-finite values first seen in ") + what +
+                              " (cycle " + std::to_string(dbg_cycle) + ", block application " +
+                              std::to_string(dbg_apps) + ", b " + std::to_string(b) + ")";
+      fprintf(stderr, "[n2v2r] %s\n", msg.c_str());
+      throw StatusFail{N2V2R_ERR_INTERNAL, msg};
+    }
+  }
+  // N2V2R_POISON: NaN-fill the scratch a fit must write before it reads it
+  void poison_scratch() {
+    if (!debug_poison()) return;
+    EigWorkspace& w = h->ews;
+    for (DevBuf* d : {&w.rinv, &w.flg, &w.anyflag, &w.gsmall, &w.csmall, &w.tri, &w.refl,
+                      &w.ytri, &w.tscr, &w.hband, &w.band, &w.varr, &w.taua, &w.rrerr, &w.fcoef,
+                      &w.cbpart, &h->partial, &h->theta, &h->resid})
+      if (d->p) HIPCHK(hipMemsetAsync(d->p, 0xFF, d->bytes, st));
+    for (auto& d : w.pool) HIPCHK(hipMemsetAsync(d->p, 0xFF, d->bytes, st));
+    for (auto& d : w.zk) HIPCHK(hipMemsetAsync(d->p, 0xFF, d->bytes, st));
+  }
 
   float* take() {
     if (freelist.empty()) {
@@ -1064,8 +1138,11 @@ struct Eig {
                        ? h->ews.hband.as<double>() + band_off((int)basis.size() - 1)
                        : nullptr;
     orthonormalize(z, basis, w_from, &loc, save, lazy);  // reads W_from, writes z: no copy
+    dbg(z, n * b, false, "orthonormalised Krylov block");
     float* w = take();
     apply_M(z, w);
+    dbg(w, n * b, false, "SpMM image M q");
+    ++dbg_apps;
     qs.push_back(z);
     ws.push_back(w);
   }
@@ -1160,6 +1237,8 @@ struct Eig {
       h->ews.rrerr.ensure(sizeof(int) * 4);
     }
 
+    h->ews.dbgflag.ensure(sizeof(int) * 4);
+    poison_scratch();
     std::vector<double> wh(keep);
     std::vector<double> res2(keep);
 
@@ -1168,8 +1247,10 @@ struct Eig {
     HIPCHK(n2v2r_launch_fill_normal(q0, b, n, seed, nullptr, nullptr, (uint64_t)row0 * b, st));
     Q.assign(1, q0);
     orthonormalize(q0, {});
+    dbg(q0, n * b, false, "orthonormalised start block");
     W.assign(1, take());
     apply_M(Q[0], W[0]);
+    dbg(W[0], n * b, false, "SpMM image of the start block");
     int apps = 1;
     int cycle = 0;
     double maxres = 0;
@@ -1184,6 +1265,7 @@ struct Eig {
     }();
     double t_rr = 0;
     for (;; ++cycle) {
+      dbg_cycle = cycle;
       const int q_start = (int)Q.size();
       if (lazy) HIPCHK(hipMemsetAsync(h->ews.anyflag.as<int>() + 3, 0, sizeof(int), st));
       while ((int)Q.size() < nb_max) {
@@ -1221,14 +1303,21 @@ struct Eig {
                                     h->ews.rrerr.as<int>(), st));
       } else {
         tn(blocks(Q, 0, nq), blocks(W, 0, nq), h->ews.gsmall.as<double>(), nullptr);
+        dbg(h->ews.gsmall.p, (int64_t)c * c, true, "projected matrix H = Q^T W");
         HIPCHK(n2v2r_launch_rr_tridiag(h->ews.gsmall.as<double>(), c, trid, trid + c_max,
                                        trid + 2 * c_max, h->ews.refl.as<double>(), st));
+        dbg(trid, c, true, "tridiagonal diagonal");
+        dbg(trid + c_max, c - 1, true, "tridiagonal off-diagonal");
         HIPCHK(n2v2r_launch_rr_tri_eig(trid, trid + c_max, c, keep, h->theta.as<double>(),
                                        h->ews.ytri.as<double>(), h->ews.tscr.as<double>(), st));
+        dbg(h->theta.p, keep, true, "tridiagonal eigenvalues (bisection)");
+        dbg(h->ews.ytri.p, (int64_t)c * keep, true, "tridiagonal eigenvectors");
         HIPCHK(n2v2r_launch_rr_backtransform(h->ews.refl.as<double>(), trid + 2 * c_max, c,
                                              h->ews.ytri.as<double>(), keep,
                                              h->ews.csmall.as<float>(), keep, st));
       }
+      dbg(h->theta.p, keep, true, "Ritz values");
+      dbg(h->ews.csmall.p, (int64_t)c * keep, false, "Ritz coefficients S");
       t_rr += now_ms() - tr0;
       }
       // Ritz vectors X = Q S, MX = W S (keep columns, pb blocks)
@@ -1249,6 +1338,10 @@ struct Eig {
                                   nullptr, nullptr, 0, st));
         HIPCHK(n2v2r_launch_ts_nn(blocks(W, 0, nq), g, keep, nt * b, omx, one(nullptr), 1.f, 0.f,
                                   n, nullptr, nullptr, 0, st));
+      }
+      for (int q = 0; q < pb; ++q) {
+        dbg(X[q], n * b, false, "Ritz vectors X = Q S");
+        dbg(MX[q], n * b, false, "Ritz images MX = W S");
       }
       HIPCHK(n2v2r_launch_resid(blocks(X, 0, pb), blocks(MX, 0, pb), h->theta.as<double>(), n,
                                 h->partial.as<double>(), h->partial_elems, h->resid.as<double>(),
@@ -1274,14 +1367,18 @@ struct Eig {
         goto rayleigh_ritz;
       }
       if (test_redo && cycle == 0 && lazy) refilled = 1;  // tests: exercise the recovery
-      // a non-finite Ritz pair under the lazy (two-pass) orthogonalisation: redo the cycle's
-      // expansion with three passes from the kept (finite) basis before giving up below
+      // a non-finite Ritz pair under the lazy (two-pass) orthogonalisation: diagnostic
+      // fallback only (no known cause remains; N2V2R_DEBUG_FINITE=1 names the first stage that
+      // produces one).  Always reported on stderr, then the cycle's expansion is redone with
+      // three passes from the kept (finite) basis before giving up below.
       if (lazy && !refilled)
         for (int j = 0; j < keep; ++j)
           if (!std::isfinite(wh[j]) || (j < d && !std::isfinite(res2[j]))) {
-            if (trace)
-              fprintf(stderr, "[n2v2r] non-finite Ritz pair %d, cycle %d expanded again\n", j,
-                      cycle);
+            fprintf(stderr,
+                    "[n2v2r] WARNING: non-finite Ritz pair %d at cycle %d (c %d, b %d, %s "
+                    "Rayleigh-Ritz); cycle expanded again with three passes.  Rerun with "
+                    "N2V2R_DEBUG_FINITE=1 to locate the stage.\n",
+                    j, cycle, c, b, dense_rr ? "dense" : "banded");
             refilled = 1;
             break;
           }
@@ -1652,12 +1749,22 @@ int n2v2r_set_layer_csr_rows(n2v2r_handle* h, int k, int64_t n, int64_t row0, in
                  (long long)h->row0, (long long)(h->row0 + h->nloc));
       return N2V2R_ERR_BAD_ARG;
     }
-    for (int64_t p = 0; p < nnz; ++p)
-      if (indices[p] < 0 || indices[p] >= n) {
-        h->set_err("layer %d: column index out of range", k);
+    for (int64_t r = 0; r < n_rows; ++r)  // a non-monotone block would hand the SpMM bad spans
+      if (indptr[r + 1] < indptr[r]) {
+        h->set_err("layer %d: indptr not monotone", k);
+        return N2V2R_ERR_BAD_ARG;
+      }
+    if (!host_indices_in_range(nnz, indices, n)) {
+      h->set_err("layer %d: column index out of range", k);
+      return N2V2R_ERR_BAD_ARG;
+    }
+    for (int j = 0; j < h->K; ++j)
+      if (j != k && h->layers[j]->loaded && h->layers[j]->dense) {
+        h->err = "layers must be all CSR or all dense";
         return N2V2R_ERR_BAD_ARG;
       }
     LayerDev& L = *h->layers[k];
+    L.dense = false;
     L.drop_col_blocks();
     L.n_rows = h->nloc;
     L.unit = upload_rows(h->stream, 0, n_rows, indptr, indices, data, L.indptr, L.indices, L.data,
@@ -2149,6 +2256,7 @@ int n2v2r_rr_band_top(n2v2r_handle* h, int c, int kp, const double* hband, int64
     y.ensure(sizeof(double) * c * p);
     s.ensure(sizeof(float) * c * p);
     er.ensure(sizeof(int));
+    HIPCHK(hipMemsetAsync(er.p, 0, sizeof(int), h->stream));  // the chase only sets it on failure
     HIPCHK(hipMemcpyAsync(hb.p, hband, sizeof(double) * hband_len, hipMemcpyHostToDevice,
                           h->stream));
     if (kp > 0)

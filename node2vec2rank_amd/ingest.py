@@ -193,7 +193,8 @@ class DataLoader:
             self.interest_nodes = cols
         print(f"\tThere are {len(self.interest_nodes)} common nodes and resulting networks will "
               f"have size {len(self.interest_nodes)} by {len(self.interest_nodes)}")
-        top = int(self.config.get("top_percent_keep", 100))
+        # passed through unchanged, as dataloader.py:74 does (a fractional percentage moves the cut)
+        top = self.config.get("top_percent_keep", 100)
         out = [transform(L, threshold=self.config.get("threshold"), top_percent_keep=top,
                          binarize=bool(self.config.get("binarize")),
                          absolute=bool(self.config.get("absolute")),

@@ -2,7 +2,7 @@
 
 Run in the survey container only (needs /root/reference; never on the GPU box):
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_ingest_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_ingest_golden.py [case ...]
 
 Imports the reference's ``node2vec2rank/dataloader.py`` unchanged and loads the files in
 ``tests/golden/ingest_inputs/`` (the reference's own ``input/`` fixtures, copied as data, plus
@@ -45,6 +45,13 @@ CASES = {
                                   binarize=True),
     "named_edges_thresh": dict(graph_filenames=["test1_named.edgelist", "test2_named.edgelist"],
                                separator=" ", is_edge_list=True, threshold=3.0),
+    # fractional percentages go to np.percentile unchanged (dataloader.py:74)
+    # (37.5 and 62.5 keep more edges of dups.edgelist than 37 and 62 would)
+    "dup_edges_top37p5": dict(graph_filenames=["dups.edgelist", "dups2.edgelist"], separator=" ",
+                              is_edge_list=True, top_percent_keep=37.5),
+    "dup_edges_top62p5_bin": dict(graph_filenames=["dups.edgelist", "dups2.edgelist"],
+                                  separator=" ", is_edge_list=True, top_percent_keep=62.5,
+                                  binarize=True),
     "bip_columns_abs_top30": dict(graph_filenames=["bip1.csv", "bip2.csv"], separator=",",
                                   is_edge_list=False, absolute=True, top_percent_keep=30,
                                   project_unipartite_on="columns"),
@@ -71,7 +78,10 @@ def main():
         return out
 
     dlmod.match_networks = recording_match
+    only = set(sys.argv[1:])  # optional case names: regenerate just those
     for name, case in CASES.items():
+        if only and name not in only:
+            continue
         cfg = dict(BASE, **case)
         cfg_out = {k: v for k, v in cfg.items() if k != "data_dir"}
         try:

@@ -64,6 +64,25 @@ def test_set_layer_csr_rejects_out_of_range_columns(engine, n, deg, bad):
         engine._check(st, "layer 0")
 
 
+@pytest.mark.parametrize("n,deg", [(1000, 4), (300_000, 16)])
+@pytest.mark.parametrize("fault", ["non_monotone", -1, "n"])
+def test_set_layer_csr_rows_rejects_malformed_blocks(engine, n, deg, fault):
+    """The rank-local ingest refuses a non-monotone indptr and out-of-range columns (either
+    would hand the SpMM row spans / gathers outside its buffers)."""
+    nnz = n * deg
+    indptr = np.arange(0, nnz + 1, deg, dtype=np.int64)
+    indices = np.tile(np.arange(deg, dtype=np.int32), n)
+    if fault == "non_monotone":
+        indptr[n // 2] = indptr[n // 2 + 1] + 1
+    else:
+        indices[nnz - 3] = -1 if fault == -1 else n
+    data = np.ones(nnz, dtype=np.float32)
+    engine._check(engine.lib.n2v2r_set_num_layers(engine.h, 1, n), "set_num_layers")
+    st = engine.lib.n2v2r_set_layer_csr_rows(engine.h, 0, n, 0, n, nnz, indptr, indices, data)
+    with pytest.raises(ValueError, match="monotone" if fault == "non_monotone" else "out of range"):
+        engine._check(st, "layer 0 rows")
+
+
 @pytest.mark.parametrize("symmetrise", [False, True])
 def test_spmm_large_directed_host_transpose(engine, symmetrise):
     """Layers large enough (>= 2^22 entries) for the multi-threaded host transpose and symmetry
