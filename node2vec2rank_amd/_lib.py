@@ -40,6 +40,7 @@ EXPORTED = [
     "n2v2r_comm_unique_id", "n2v2r_create_rccl", "n2v2r_simgroup_create",
     "n2v2r_simgroup_destroy", "n2v2r_create_sim", "n2v2r_dist_info", "n2v2r_set_layer_csr_rows",
     "n2v2r_rr_top", "n2v2r_rr_band_top", "n2v2r_set_layer_dense", "n2v2r_project",
+    "n2v2r_probe_spmm_stage2",
 ]
 UNIQUE_ID_BYTES = 128
 
@@ -119,6 +120,7 @@ def load(path: str | None = None):
                                       ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_double)]),
             "n2v2r_spmm_col_blocks": (_i, [_vp, _i]),
+            "n2v2r_probe_spmm_stage2": (_i, [_vp, _i, _i, ctypes.POINTER(ctypes.c_double)]),
             "n2v2r_rr_top": (_i, [_vp, _i, _p(np.float64), _i, _p(np.float64), _p(np.float32)]),
             "n2v2r_rr_band_top": (_i, [_vp, _i, _i, _p(np.float64), ctypes.c_int64, _vp, _i,
                                        _p(np.float64), _p(np.float32)]),
@@ -431,6 +433,14 @@ class Engine:
                                               int(reps), X, yp, ctypes.byref(ms),
                                               ctypes.byref(by)), "bench_spmm")
         return Y, ms.value, by.value
+
+    def probe_spmm_stage2(self, mode: int, reps: int = 50) -> float:
+        """Diagnostic: average ms of the b = 8 second SpMM stage (0 summed, 1 per layer,
+        2 per layer split over the XCDs) on the loaded layers."""
+        ms = ctypes.c_double(0)
+        self._check(self.lib.n2v2r_probe_spmm_stage2(self.h, int(mode), int(reps),
+                                                      ctypes.byref(ms)), "probe_spmm_stage2")
+        return ms.value
 
     def spmm_col_blocks(self, b: int = 8) -> bool:
         """True when the SpMM at panel width b runs the XCD-local column-block form."""

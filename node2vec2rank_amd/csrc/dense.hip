@@ -367,17 +367,45 @@ __device__ __forceinline__ void rs_step(double* v, int rl) {
   }
 }
 
-template <int TS_U>
+// ZSum (count > 0): the right-hand side Z is not stored yet; it is the sum of `count` per-layer
+// SpMM outputs (the XCD-split second stage), summed here in fixed order.  A's last block is Z
+// itself: the wave that owns it uses the sums as its A rows and stores them to `out` (the
+// block Z will live in), so the pass that follows reads a materialised Z.
+struct ZSum {
+  const float* p[8];
+  int count;
+  float* out;
+};
+
+template <bool SUM>
+__device__ __forceinline__ void zrow_load(const float* __restrict__ Bz, const ZSum& zs, int64_t rr,
+                                          f32x4& z0, f32x4& z1) {
+  if (!SUM) {
+    z0 = *reinterpret_cast<const f32x4*>(Bz + rr * 8);
+    z1 = *reinterpret_cast<const f32x4*>(Bz + rr * 8 + 4);
+    return;
+  }
+  z0 = *reinterpret_cast<const f32x4*>(zs.p[0] + rr * 8);
+  z1 = *reinterpret_cast<const f32x4*>(zs.p[0] + rr * 8 + 4);
+  for (int i = 1; i < zs.count; ++i) {
+    z0 += *reinterpret_cast<const f32x4*>(zs.p[i] + rr * 8);
+    z1 += *reinterpret_cast<const f32x4*>(zs.p[i] + rr * 8 + 4);
+  }
+}
+
+template <int TS_U, bool SUM>
 __global__ __launch_bounds__(256) void ts_tn_stream_kernel(BlockList A, const float* __restrict__ Bz,
                                                            int64_t n, int64_t rows_per_chunk,
                                                            double* __restrict__ partial,
-                                                           const int* cond) {
+                                                           const int* cond, ZSum zs) {
   if (cond && *cond == 0) return;
   const int lane = threadIdx.x & 63;
   const int blk = (int)blockIdx.y * 4 + (threadIdx.x >> 6);
   if (blk >= A.count) return;  // wave-uniform; no block barrier below
   const int h = lane >> 5, rl = lane & 31;
-  const float* ab = A.blk[blk] + 4 * h;
+  // SUM: the last block is Z (= the sums): this wave takes its A rows from them and stores them
+  const bool zblk = SUM && blk == A.count - 1;
+  const float* ab = (zblk ? A.blk[0] : A.blk[blk]) + 4 * h;
   const int64_t c0 = (int64_t)blockIdx.x * rows_per_chunk;
   int64_t c1 = c0 + rows_per_chunk;
   if (c1 > n) c1 = n;
@@ -392,9 +420,16 @@ __global__ __launch_bounds__(256) void ts_tn_stream_kernel(BlockList A, const fl
 #pragma unroll
     for (int u = 0; u < TS_U; ++u) {
       const int64_t rr = r + 32 * u + rl;
-      a[u] = *reinterpret_cast<const f32x4*>(ab + rr * 8);
-      z0[u] = *reinterpret_cast<const f32x4*>(Bz + rr * 8);
-      z1[u] = *reinterpret_cast<const f32x4*>(Bz + rr * 8 + 4);
+      if (!zblk) a[u] = *reinterpret_cast<const f32x4*>(ab + rr * 8);
+      zrow_load<SUM>(Bz, zs, rr, z0[u], z1[u]);
+    }
+    if (zblk) {
+#pragma unroll
+      for (int u = 0; u < TS_U; ++u) {
+        const int64_t rr = r + 32 * u + rl;
+        a[u] = h ? z1[u] : z0[u];
+        *reinterpret_cast<f32x4*>(zs.out + rr * 8 + 4 * h) = a[u];
+      }
     }
 #pragma unroll
     for (int u = 0; u < TS_U; ++u)
@@ -409,9 +444,14 @@ __global__ __launch_bounds__(256) void ts_tn_stream_kernel(BlockList A, const fl
   for (; r < c1; r += 32) {
     const int64_t rr = r + rl;
     if (rr < c1) {
-      const f32x4 a1 = *reinterpret_cast<const f32x4*>(ab + rr * 8);
-      const f32x4 y0 = *reinterpret_cast<const f32x4*>(Bz + rr * 8);
-      const f32x4 y1 = *reinterpret_cast<const f32x4*>(Bz + rr * 8 + 4);
+      f32x4 y0, y1, a1;
+      zrow_load<SUM>(Bz, zs, rr, y0, y1);
+      if (zblk) {
+        a1 = h ? y1 : y0;
+        *reinterpret_cast<f32x4*>(zs.out + rr * 8 + 4 * h) = a1;
+      } else {
+        a1 = *reinterpret_cast<const f32x4*>(ab + rr * 8);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -461,9 +501,9 @@ static int64_t tn_stream_waves() {
   return v;
 }
 
-extern "C" hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n,
-                                         double* partial, size_t partial_elems, double* out,
-                                         const int* cond, hipStream_t stream) {
+static hipError_t launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n,
+                               double* partial, size_t partial_elems, double* out,
+                               const int* cond, const ZSum* zs, hipStream_t stream) {
   const int ca = A.count * A.width, cb = B.count * B.width;
   int64_t s_chunks = 0, s_rows = 0;
   if (B.count == 1 && B.width == 8 && A.width == 8 && tn_stream_form()) {
@@ -482,18 +522,23 @@ extern "C" hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B,
     const int64_t elems = (int64_t)ca * cb;
     const int64_t nchunks = s_chunks, rows_per_chunk = s_rows;
     const dim3 grid((unsigned)nchunks, (unsigned)((A.count + 3) / 4));
-    if (tn_stream_u() == 8)
-      hipLaunchKernelGGL(ts_tn_stream_kernel<8>, grid, dim3(256), 0, stream, A, B.blk[0], n,
-                         rows_per_chunk, partial, cond);
+    const ZSum none{};
+    if (zs && zs->count > 0)
+      hipLaunchKernelGGL((ts_tn_stream_kernel<4, true>), grid, dim3(256), 0, stream, A, B.blk[0],
+                         n, rows_per_chunk, partial, cond, *zs);
+    else if (tn_stream_u() == 8)
+      hipLaunchKernelGGL((ts_tn_stream_kernel<8, false>), grid, dim3(256), 0, stream, A, B.blk[0],
+                         n, rows_per_chunk, partial, cond, none);
     else
-      hipLaunchKernelGGL(ts_tn_stream_kernel<4>, grid, dim3(256), 0, stream, A, B.blk[0], n,
-                         rows_per_chunk, partial, cond);
+      hipLaunchKernelGGL((ts_tn_stream_kernel<4, false>), grid, dim3(256), 0, stream, A, B.blk[0],
+                         n, rows_per_chunk, partial, cond, none);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((elems + 3) / 4)), dim3(256), 0,
                        stream, partial, (int)nchunks, elems, out, cond);
     return hipGetLastError();
   }
+  if (zs && zs->count > 0) return hipErrorNotSupported;  // the Z sums: streaming form only
   if (B.count == 1 && B.width == 8 && A.width == 8) {
     // line form: ~2048 waves, >= 64 rows per chunk, partials within the buffer
     const int64_t elems = (int64_t)ca * cb;
@@ -571,6 +616,51 @@ extern "C" hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B,
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((elems + 3) / 4)), dim3(256), 0,
                      stream, partial, (int)nchunks, elems, out, cond);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n,
+                                         double* partial, size_t partial_elems, double* out,
+                                         const int* cond, hipStream_t stream) {
+  return launch_ts_tn(A, B, n, partial, partial_elems, out, cond, nullptr, stream);
+}
+
+// G = [Q Z]^T Z with Z = sum of `count` partial panels, stored to zout (= A's last block and
+// B's only block) on the way; hipErrorNotSupported when the streaming form does not apply
+// (the caller then sums the partials itself)
+extern "C" hipError_t n2v2r_launch_ts_tn_zsum(const BlockList& A, int64_t n, const float* const* parts,
+                                              int count, float* zout, double* partial,
+                                              size_t partial_elems, double* out, hipStream_t stream) {
+  if (count < 1 || count > 8 || A.count < 1 || A.blk[A.count - 1] != zout) return hipErrorInvalidValue;
+  ZSum zs{};
+  for (int i = 0; i < count; ++i) zs.p[i] = parts[i];
+  zs.count = count;
+  zs.out = zout;
+  BlockList B{};
+  B.count = 1;
+  B.width = A.width;
+  B.blk[0] = zout;
+  return launch_ts_tn(A, B, n, partial, partial_elems, out, nullptr, &zs, stream);
+}
+
+// out = sum of `count` partial panels (fixed order), n x 8 fp32
+__global__ void zsum_kernel(ZSum zs, int64_t n) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one half row (16 B)
+  if (e >= n * 2) return;
+  f32x4 v = *reinterpret_cast<const f32x4*>(zs.p[0] + e * 4);
+  for (int i = 1; i < zs.count; ++i) v += *reinterpret_cast<const f32x4*>(zs.p[i] + e * 4);
+  *reinterpret_cast<f32x4*>(zs.out + e * 4) = v;
+}
+
+extern "C" hipError_t n2v2r_launch_zsum(const float* const* parts, int count, float* zout, int64_t n,
+                                        hipStream_t stream) {
+  if (count < 1 || count > 8) return hipErrorInvalidValue;
+  ZSum zs{};
+  for (int i = 0; i < count; ++i) zs.p[i] = parts[i];
+  zs.count = count;
+  zs.out = zout;
+  const int64_t th = n * 2;
+  hipLaunchKernelGGL(zsum_kernel, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, stream, zs, n);
   return hipGetLastError();
 }
 

@@ -56,6 +56,7 @@ struct SpmmArgs {
   int K;
   int sum;
   const float* colscale;
+  int split;
 };
 #define CB_NB 8
 struct CsrBlk {  // spmm.hip: one column block, int32 row pointers relative to base
@@ -166,6 +167,11 @@ hipError_t n2v2r_launch_rr_backtransform(const double* V, const double* tau, int
                                          hipStream_t stream);
 hipError_t n2v2r_launch_nonfinite(const void* p, int64_t count, int f64, int* flag,
                                   hipStream_t stream);
+hipError_t n2v2r_launch_ts_tn_zsum(const BlockList& A, int64_t n, const float* const* parts,
+                                   int count, float* zout, double* partial, size_t partial_elems,
+                                   double* out, hipStream_t stream);
+hipError_t n2v2r_launch_zsum(const float* const* parts, int count, float* zout, int64_t n,
+                             hipStream_t stream);
 }
 
 namespace {
@@ -482,6 +488,7 @@ struct EigWorkspace {
   DevBuf fcoef;                               // fp32 [-C R^-1; R^-1] of the apply pass
   DevBuf cbpart;                              // [K][CB_NB][npad][8] column-block partials
   DevBuf dbgflag;                             // N2V2R_DEBUG_FINITE result flag
+  DevBuf s2part;                              // [K][npad][8] XCD-split second-stage outputs
 };
 }  // namespace
 
@@ -797,6 +804,17 @@ double spmm_algo_bytes(int64_t nnz, bool unit, int64_t rows, int64_t panel_rows,
 // Read on every call, so a test can switch it between fits.
 bool col_blocks_wanted(const n2v2r_handle* h, int b);
 
+// XCD-split second SpMM stage: b = 8 CSR layers on one GPU whose K stage-2 panels together
+// exceed an XCD's 4 MB L2 (cfg2: 33.5 -> 24 us per stage; at N = 30k, where both panels fit,
+// 4 % slower).  N2V2R_SPMM_SPLIT=1 / 0 forces it on / off.
+bool split2_wanted(const n2v2r_handle* h, int b) {
+  const char* e = std::getenv("N2V2R_SPMM_SPLIT");  // read per fit (tests flip it)
+  const int force = e ? (e[0] == '0' ? 0 : 1) : -1;
+  if (b != 8 || h->comm || h->dense_layers() || h->K < 2 || h->K > 8) return false;
+  if (force >= 0) return force == 1;
+  return (double)h->K * (double)h->n * 32.0 > 4.0 * 1024 * 1024;
+}
+
 // ---- the eigensolver ----------------------------------------------------------------------
 struct Eig {
   n2v2r_handle* h;
@@ -821,6 +839,11 @@ struct Eig {
   bool full_first = false;  // N2V2R_EIG_FULL_FIRST_PASS
   bool band_rr = false;     // banded Rayleigh-Ritz (b = 8, c <= 512), else dense
   bool col_blocks = false;  // XCD-local column-block SpMM (b = 8, large panels)
+  // XCD-split second SpMM stage (b = 8, one GPU): A_k Z_k lands in per-layer partials on the
+  // XCDs of layer k; the image W = sum_k of them is stored by the next Gram pass that reads it
+  // (the local first pass of the next expansion), or by materialize() before any other use
+  bool split2 = false;
+  float* pending = nullptr;  // the W block whose value still sits in the partials
 
   // N2V2R_DEBUG_FINITE: stop at the first stage whose output holds a non-finite value
   int dbg_cycle = 0, dbg_apps = 0;
@@ -884,6 +907,16 @@ struct Eig {
     L.width = b;
     L.blk[0] = p;
     return L;
+  }
+
+  float* s2part(int k) const { return h->ews.s2part.as<float>() + (size_t)k * npad * 8; }
+  // store the pending image W = sum_k partial_k (fixed layer order)
+  void materialize() {
+    if (!pending) return;
+    const float* parts[8];
+    for (int k = 0; k < K; ++k) parts[k] = s2part(k);
+    HIPCHK(n2v2r_launch_zsum(parts, K, pending, n, st));
+    pending = nullptr;
   }
 
   // TN over local rows, summed over ranks
@@ -958,6 +991,13 @@ struct Eig {
       }
     }
     s.Y[0] = Wout;
+    if (split2) {
+      materialize();  // (a previous image is always consumed by now; kept for safety)
+      s.sum = 0;
+      s.split = 1;
+      for (int k = 0; k < K; ++k) s.Y[k] = s2part(k);
+      pending = Wout;
+    }
     HIPCHK(n2v2r_launch_spmm(s, b, st));
     for (int k = 0; k < K; ++k) {
       const LayerDev& L = *h->layers[k];
@@ -1068,7 +1108,24 @@ struct Eig {
     std::vector<float*> qz(basis);
     qz.push_back(const_cast<float*>(zin));
     const BlockList L = blocks(qz, 0, nq + 1);
-    tn(L, one(zin), h->ews.gsmall.as<double>(), cond);
+    bool done = false;
+    if (pending && zin == pending && !cond && !h->comm) {
+      // the Gram pass that first reads the pending image also stores it
+      const float* parts[8];
+      for (int k = 0; k < K; ++k) parts[k] = s2part(k);
+      const hipError_t e = n2v2r_launch_ts_tn_zsum(L, n, parts, K, pending, h->partial.as<double>(),
+                                                   h->partial_elems, h->ews.gsmall.as<double>(), st);
+      if (e == hipSuccess) {
+        pending = nullptr;
+        done = true;
+      } else if (e != hipErrorNotSupported) {
+        throw HipFail{e, "n2v2r_launch_ts_tn_zsum"};
+      }
+    }
+    if (!done) {
+      if (zin == pending) materialize();
+      tn(L, one(zin), h->ews.gsmall.as<double>(), cond);
+    }
     if (b == 8 && nq * b <= 512 && pip_fused()) {
       // b = 8: the Cholesky step runs inside the apply launch (every workgroup factors G)
       HIPCHK(n2v2r_launch_pip_fused(blocks(qz, 0, nq), zin, Z, h->ews.gsmall.as<double>(), nq * b,
@@ -1141,6 +1198,7 @@ struct Eig {
     dbg(z, n * b, false, "orthonormalised Krylov block");
     float* w = take();
     apply_M(z, w);
+    if (debug_finite()) materialize();
     dbg(w, n * b, false, "SpMM image M q");
     ++dbg_apps;
     qs.push_back(z);
@@ -1208,6 +1266,9 @@ struct Eig {
       for (auto& Lp : h->layers) col_blocks = ensure_col_blocks(*Lp, nglob, st) && col_blocks;
       if (col_blocks) h->ews.cbpart.ensure(sizeof(float) * (size_t)K * CB_NB * npad * 8);
     }
+    split2 = split2_wanted(h, b) && !col_blocks;
+    pending = nullptr;
+    if (split2) h->ews.s2part.ensure(sizeof(float) * (size_t)K * npad * 8);
     // chunk partials: also the streaming Gram form at b = 8 (chunks of <= 8192 rows, rounded to
     // a multiple of 8, (c + b) x b fp64 each)
     h->partial_elems = std::max<size_t>(4096ull * 1024ull, (size_t)c_max * c_max * 8);
@@ -1250,6 +1311,7 @@ struct Eig {
     dbg(q0, n * b, false, "orthonormalised start block");
     W.assign(1, take());
     apply_M(Q[0], W[0]);
+    if (debug_finite()) materialize();
     dbg(W[0], n * b, false, "SpMM image of the start block");
     int apps = 1;
     int cycle = 0;
@@ -1289,6 +1351,7 @@ struct Eig {
       //   dense: H = Q^T W (fp64, all-reduced) -> Householder tridiagonal -> bisection +
       //     inverse iteration on T -> compact-WY back-transform.
       double* trid = h->ews.tri.as<double>();
+      materialize();  // W.back() (every other W block was stored by its expansion's Gram pass)
       const double tr0 = now_ms();
       if (!dense_rr) {
         const std::vector<float*> loc = local_of(Q);
@@ -1447,6 +1510,7 @@ struct Eig {
       W.insert(W.end(), EW.begin(), EW.end());
       kry0 = pb;
     }
+    materialize();
     // U = first d columns of X (row stride ldu); theta
     theta_out.assign(wh.begin(), wh.begin() + d);
     for (int q = 0; q * b < d; ++q) {
@@ -2280,6 +2344,45 @@ int n2v2r_rr_band_top(n2v2r_handle* h, int c, int kp, const double* hband, int64
 int n2v2r_spmm_col_blocks(const n2v2r_handle* h, int b) {
   if (!h) return N2V2R_ERR_BAD_ARG;
   return col_blocks_wanted(h, b) ? 1 : 0;
+}
+
+int n2v2r_probe_spmm_stage2(n2v2r_handle* h, int mode, int reps, double* avg_ms) {
+  return guarded(h, [&]() -> int {
+    if (h->K < 1 || h->K > 8 || h->comm || h->dense_layers() || reps < 1 || !avg_ms ||
+        mode < 0 || mode > 2)
+      return N2V2R_ERR_BAD_ARG;
+    for (auto& L : h->layers)
+      if (!L->loaded) return N2V2R_ERR_BAD_ARG;
+    const int64_t n = h->n;
+    DevBuf z, y;
+    z.ensure(sizeof(float) * n * 8 * h->K, h->stream);
+    y.ensure(sizeof(float) * n * 8 * h->K, h->stream);
+    HIPCHK(n2v2r_launch_fill_normal(z.as<float>(), 8, n * h->K, 7, nullptr, nullptr, 0, h->stream));
+    SpmmArgs s{};
+    s.K = h->K;
+    s.sum = mode == 0 ? 1 : 0;
+    s.split = mode == 2 ? 1 : 0;
+    s.ldx = s.ldy = 8;
+    for (int k = 0; k < h->K; ++k) {
+      s.A[k] = h->layers[k]->csr();
+      s.X[k] = z.as<float>() + (size_t)k * n * 8;
+      s.Y[k] = y.as<float>() + (size_t)(mode == 0 ? 0 : k) * n * 8;
+    }
+    HIPCHK(n2v2r_launch_spmm(s, 8, h->stream));
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, h->stream));
+    for (int r = 0; r < reps; ++r) HIPCHK(n2v2r_launch_spmm(s, 8, h->stream));
+    HIPCHK(hipEventRecord(e1, h->stream));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    *avg_ms = (double)ms / reps;
+    return N2V2R_OK;
+  });
 }
 
 int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, const float* X,

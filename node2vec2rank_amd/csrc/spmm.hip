@@ -32,7 +32,20 @@ struct SpmmArgs {
   int K;                 // layers in this launch
   int sum;               // 1: Y[0] = sum_k A_k X_k ; 0: Y[k] = A_k X_k (grid.y = k)
   const float* colscale; // optional per-column scale of the output (nullptr = none)
+  int split;             // (b = 8, sum = 0, K <= 8) Y[k] = A_k X_k with grid.y = 1 and the
+                         // layers split over the XCDs: workgroup i runs layer (i mod 8) K / 8,
+                         // so each XCD's L2 holds one layer's panel
 };
+
+// XCD-split task space: the layer of this workgroup and its index / count among the
+// workgroups of that layer (grid.x a multiple of 8; workgroup i runs on XCD i mod 8)
+__device__ __forceinline__ void split_slot(int K, int& k, int64_t& wg, int64_t& nwg) {
+  const int xcd = blockIdx.x & 7;
+  k = (xcd * K) >> 3;
+  const int x0 = (k * 8 + K - 1) / K, x1 = ((k + 1) * 8 + K - 1) / K;
+  wg = (int64_t)(blockIdx.x >> 3) * (x1 - x0) + (xcd - x0);
+  nwg = (int64_t)(gridDim.x >> 3) * (x1 - x0);
+}
 
 // RPW rows per wave: each row owns a group of L = 64 / RPW lanes; inside the group LPN = B / 4
 // lanes gather one panel row (one 16-B load each) and NPS = L / LPN panel rows are gathered
@@ -147,11 +160,13 @@ __global__ __launch_bounds__(256) void spmm8_pipe_kernel(SpmmArgs args) {
   const int g = lane / L, li = lane % L, sub = li & 1;
   const int srcbase = g * L + (li >> 1);
   const int K = args.sum ? args.K : 1;
-  const int kfix = args.sum ? 0 : (int)blockIdx.y;
+  int kfix = args.sum ? 0 : (int)blockIdx.y;
+  int64_t wg = blockIdx.x, nwg = gridDim.x;
+  if (args.split) split_slot(args.K, kfix, wg, nwg);
   const int64_t n = args.A[kfix].n_rows;
   const int64_t ngroups = (n + RPW - 1) / RPW;
-  const int64_t gstride = (int64_t)gridDim.x * (blockDim.x / 64);
-  int64_t grp = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const int64_t gstride = nwg * (blockDim.x / 64);
+  int64_t grp = wg * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (grp >= ngroups) return;
   int k = 0;
   // current task
@@ -265,6 +280,88 @@ __global__ __launch_bounds__(256) void spmm8_pipe_kernel(SpmmArgs args) {
   }
 }
 
+// B = 8, one lane per entry: lane li of a row's L-lane group takes entries li, li + L, ... and
+// gathers the whole 32-B panel row itself (two 16-B loads), so a wave-instruction serves 64
+// entries (the two-lanes-per-row form serves 32) and no index / value shuffles are needed.
+// Two group-widths per step keep 4 loads per lane in flight; entries past the row end read
+// panel row 0 and multiply by 0 (clamped addresses: the loads issue as one batch).  The L
+// partial sums of a row are folded by an xor butterfly.
+template <int RPW>
+__global__ __launch_bounds__(256) void spmm8_lane_kernel(SpmmArgs args) {
+  constexpr int L = 64 / RPW;
+  const int lane = threadIdx.x & 63;
+  const int g = lane / L, li = lane % L;
+  const int K = args.sum ? args.K : 1;
+  const int kfix = args.sum ? 0 : (int)blockIdx.y;
+  const int64_t n = args.A[kfix].n_rows;
+  const int64_t ngroups = (n + RPW - 1) / RPW;
+  const int64_t gstride = (int64_t)gridDim.x * (blockDim.x / 64);
+  for (int64_t grp = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); grp < ngroups;
+       grp += gstride) {
+    const int64_t row = grp * RPW + g;
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < K; ++k) {
+      const CsrDev& A = args.A[kfix + k];
+      const float* X = args.X[kfix + k];
+      int64_t beg = 0, len = 0;
+      if (row < n) {
+        beg = A.indptr[row];
+        len = A.indptr[row + 1] - beg;
+      }
+      int64_t maxlen = len;
+#pragma unroll
+      for (int m = L; m < 64; m <<= 1) {
+        const int64_t o = __shfl_xor(maxlen, m, 64);
+        maxlen = o > maxlen ? o : maxlen;
+      }
+      for (int64_t off = 0; off < maxlen; off += 2 * L) {
+        const bool in0 = off + li < len, in1 = off + L + li < len;
+        const int c0 = in0 ? A.indices[beg + off + li] : 0;
+        const int c1 = in1 ? A.indices[beg + off + L + li] : 0;
+        float v0 = in0 ? 1.f : 0.f, v1 = in1 ? 1.f : 0.f;
+        if (!A.unit) {
+          v0 = in0 ? A.data[beg + off + li] : 0.f;
+          v1 = in1 ? A.data[beg + off + L + li] : 0.f;
+        }
+        const float* x0 = X + (int64_t)c0 * args.ldx;
+        const float* x1 = X + (int64_t)c1 * args.ldx;
+        const f32x4 x00 = *reinterpret_cast<const f32x4*>(x0);
+        const f32x4 x01 = *reinterpret_cast<const f32x4*>(x0 + 4);
+        const f32x4 x10 = *reinterpret_cast<const f32x4*>(x1);
+        const f32x4 x11 = *reinterpret_cast<const f32x4*>(x1 + 4);
+        a0 += v0 * x00;
+        a1 += v0 * x01;
+        a0 += v1 * x10;
+        a1 += v1 * x11;
+      }
+    }
+#pragma unroll
+    for (int m = 1; m < L; m <<= 1) {
+      a0.x += __shfl_xor(a0.x, m, 64);
+      a0.y += __shfl_xor(a0.y, m, 64);
+      a0.z += __shfl_xor(a0.z, m, 64);
+      a0.w += __shfl_xor(a0.w, m, 64);
+      a1.x += __shfl_xor(a1.x, m, 64);
+      a1.y += __shfl_xor(a1.y, m, 64);
+      a1.z += __shfl_xor(a1.z, m, 64);
+      a1.w += __shfl_xor(a1.w, m, 64);
+    }
+    if (row < n && li < 2) {
+      f32x4 o = li ? a1 : a0;
+      if (args.colscale) o *= *reinterpret_cast<const f32x4*>(args.colscale + li * 4);
+      *reinterpret_cast<f32x4*>(args.Y[kfix] + row * args.ldy + li * 4) = o;
+    }
+  }
+}
+
+static int spmm8_form() {  // N2V2R_SPMM8=lane: the one-lane-per-entry kernel (A/B runs)
+  static const int v = [] {
+    const char* s = getenv("N2V2R_SPMM8");
+    return (s && s[0] == 'l') ? 1 : 0;
+  }();
+  return v;
+}
+
 // B = 8 uses the pipelined kernel unless N2V2R_SPMM_PIPE=0 (A/B runs)
 static bool spmm8_pipelined() {
   static const bool v = [] {
@@ -282,6 +379,13 @@ static void launch_spmm_t(const SpmmArgs& args, hipStream_t stream) {
   const int64_t cap = (int64_t)N2V2R_SPMM_WGS / (args.sum ? 1 : args.K);
   if (wgs > cap) wgs = cap;
   dim3 grid((unsigned)wgs, args.sum ? 1 : args.K);
+  if (args.split) grid = dim3((unsigned)N2V2R_SPMM_WGS, 1);
+  if constexpr (B == 8) {
+    if (spmm8_form() == 1) {
+      hipLaunchKernelGGL((spmm8_lane_kernel<RPW>), grid, dim3(256), 0, stream, args);
+      return;
+    }
+  }
   if constexpr (B == 8 && RPW >= 2) {
     if (spmm8_pipelined()) {
       hipLaunchKernelGGL((spmm8_pipe_kernel<RPW>), grid, dim3(256), 0, stream, args);
@@ -316,7 +420,12 @@ static void launch_spmm_b(const SpmmArgs& args, hipStream_t stream) {
   }
 }
 
-extern "C" hipError_t n2v2r_launch_spmm(const SpmmArgs& args, int B, hipStream_t stream) {
+extern "C" hipError_t n2v2r_launch_spmm(const SpmmArgs& args_in, int B, hipStream_t stream) {
+  if (args_in.split && (B != 8 || args_in.sum || args_in.K > 8)) return hipErrorInvalidValue;
+  SpmmArgs args = args_in;
+  // the XCD split lives in the pipelined kernel; other b = 8 forms (A/B switches) write the
+  // same per-layer outputs with grid.y = layer
+  if (args.split && (!spmm8_pipelined() || spmm8_form() != 0)) args.split = 0;
   if (B == 8)
     launch_spmm_b<8>(args, stream);
   else if (B == 16)

@@ -409,6 +409,31 @@ def test_uase_column_blocks_er_20k(engine, monkeypatch):
     assert np.array_equal(engine.embedding(), Y1)
 
 
+@pytest.mark.parametrize("layers_k", [2, 3])
+def test_uase_split_stage2(engine, monkeypatch, layers_k):
+    """XCD-split second SpMM stage (per-layer partials, W stored by the next Gram pass) vs the
+    summed stage: same sigma within fp32 tolerance, true residuals, bit-identical reruns."""
+    from node2vec2rank_amd import synthetic
+    layers = synthetic.er_layers(20_003, 16, layers_k)
+    d = 24
+    engine.set_layers(layers)
+    monkeypatch.setenv("N2V2R_SPMM_SPLIT", "0")
+    engine.uase(d, seed=7)
+    s_sum = engine.singular_values().copy()
+    monkeypatch.setenv("N2V2R_SPMM_SPLIT", "1")
+    st = engine.uase(d, seed=7)
+    assert st["converged"] == d
+    s = engine.singular_values()
+    Y1 = engine.embedding().copy()
+    np.testing.assert_allclose(s, s_sum, rtol=1e-5)
+    X = engine.left_embedding().astype(np.float64) / np.sqrt(s)[None, :]
+    A = sp.hstack(layers).tocsr().astype(np.float64)
+    res = np.linalg.norm(A @ (A.T @ X) - X * (s ** 2)[None, :], axis=0) / s[0] ** 2
+    assert res.max() < 1e-5
+    engine.uase(d, seed=7)
+    assert np.array_equal(engine.embedding(), Y1)
+
+
 @pytest.mark.parametrize("block", [8, 16, 64])
 @pytest.mark.parametrize("name", ["er_cfg1", "directed_weighted", "demo"])
 def test_uase_block_widths(engine, name, block):
