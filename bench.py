@@ -54,6 +54,12 @@ CONFIGS = {
 CPU_SAMPLE = {"cfg1": 1000, "cfg2": 50_000, "cfg3": 2_000, "cfg4": 20_000, "cfg5": 20_000}
 METRICS = ["cosine", "euclidean"]
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# Scattered-line ceiling of the vector memory path: MI355X_MICROARCH.md's indexed-row gather
+# (1,152-B rows from an L2-resident table) runs 66-73 GB/s per CU = one 128-B line per ~4.4
+# cycles per CU, i.e. 256 CUs x 2.4 GHz / 4.4 = ~140 G lines/s.  A b = 8 SpMM touches one line
+# per stored entry (its 32-B panel row), whatever the locality (tools/spmm_locality.py: ER vs
+# a 256-wide band graph, 14.5 vs 12.6 us per 2M entries), so this, not HBM, bounds it.
+GATHER_LINE_PEAK_GLPS = 256 * 2.4 / 4.4
 
 
 def _dist_env():
@@ -253,6 +259,9 @@ def main():
     # HBM bytes, reported beside the roofline
     gathered = (None if cfg.get("dense") else
                 4.0 * b * float(nnz[0]) / max(1, world if mode == "partitioned" else 1))
+    lines_per_launch = (None if gathered is None else
+                        float(nnz[0]) / max(1, world if mode == "partitioned" else 1)
+                        * max(1, (4 * b) // 128))
     ms_dist, ms_borda = eng.rank_timing()
 
     traffic = None
@@ -301,7 +310,17 @@ def main():
                      "partial_bytes_per_launch": (2.0 * 8 * 4 * 8 * nloc_rows
                                                   if col_blocks else 0.0),
                      "gather_GBps": (None if gathered is None else
-                                     round(gathered / (spmm_ms * 1e-3) / 1e9, 1))},
+                                     round(gathered / (spmm_ms * 1e-3) / 1e9, 1)),
+                     # the bound that applies: 128-B lines touched by the panel-row gathers
+                     # (one per stored entry while a panel row fits one line)
+                     "gather_lines_per_launch": (None if gathered is None else
+                                                 lines_per_launch),
+                     "gather_line_rate_Glps": (None if gathered is None else
+                                               round(lines_per_launch / (spmm_ms * 1e-3) / 1e9, 1)),
+                     "gather_line_peak_Glps": round(GATHER_LINE_PEAK_GLPS, 1),
+                     "gather_line_frac": (None if gathered is None else
+                                          round(lines_per_launch / (spmm_ms * 1e-3) / 1e9
+                                                / GATHER_LINE_PEAK_GLPS, 4))},
         "eig": {k: (float(f"{v:.4g}") if isinstance(v, float) else v) for k, v in stats.items()},
         "eig_options": eig,
         "rank_ms": {"distances": round(ms_dist, 3), "borda": round(ms_borda, 3)},

@@ -163,8 +163,9 @@ int n2v2r_synchronize(n2v2r_handle* h);
  * 4 (N + n_loc) b.  Y may be NULL. */
 /* Diagnostic: time the b = 8 second SpMM stage W = sum_k A_k Z_k on the loaded layers with
  * random panels; mode 0 = one summed output (the solver's form), 1 = one output per layer
- * (grid.y = layer), 2 = one output per layer with the layers split over the XCDs.  Returns
- * the average launch time in ms. */
+ * (grid.y = layer), 2 = one output per layer with the layers split over the XCDs; 3 and 4 =
+ * modes 1 and 2 with one panel shared by all layers (the first stage's form).  Returns the
+ * average launch time in ms. */
 int n2v2r_probe_spmm_stage2(n2v2r_handle* h, int mode, int reps, double* avg_ms);
 int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, const float* X,
                      float* Y, double* avg_ms, double* algo_bytes);

@@ -172,6 +172,18 @@ hipError_t n2v2r_launch_ts_tn_zsum(const BlockList& A, int64_t n, const float* c
                                    double* out, hipStream_t stream);
 hipError_t n2v2r_launch_zsum(const float* const* parts, int count, float* zout, int64_t n,
                              hipStream_t stream);
+hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp, double* theta, double* scr,
+                                 size_t scr_elems, double* Y, float* S, int ldS, int p, int* err,
+                                 hipStream_t stream);
+size_t n2v2r_rr_sturm_scratch(int c, int p);
+}
+
+// Rayleigh-Ritz at b = 8: the band Sturm / inverse-iteration form (rr_sturm.hip) unless
+// N2V2R_RR=band (the reducing arrow -> chase path, also the fallback when a Sturm vector fails
+// its residual check).  Read per fit.
+static bool rr_sturm_enabled() {
+  const char* e = std::getenv("N2V2R_RR");
+  return !(e && e[0] == 'b');
 }
 
 namespace {
@@ -489,6 +501,7 @@ struct EigWorkspace {
   DevBuf cbpart;                              // [K][CB_NB][npad][8] column-block partials
   DevBuf dbgflag;                             // N2V2R_DEBUG_FINITE result flag
   DevBuf s2part;                              // [K][npad][8] XCD-split second-stage outputs
+  DevBuf sturm;                               // Sturm Rayleigh-Ritz: assembled arrow + band
 };
 }  // namespace
 
@@ -844,6 +857,7 @@ struct Eig {
   // (the local first pass of the next expansion), or by materialize() before any other use
   bool split2 = false;
   float* pending = nullptr;  // the W block whose value still sits in the partials
+  int stats_rr_fallbacks = 0;  // Sturm Rayleigh-Ritz cycles redone by the reducing path
 
   // N2V2R_DEBUG_FINITE: stop at the first stage whose output holds a non-finite value
   int dbg_cycle = 0, dbg_apps = 0;
@@ -968,6 +982,7 @@ struct Eig {
     a.ldx = b;
     a.ldy = b;
     a.colscale = nullptr;
+    a.split = split2 ? 1 : 0;  // first stage split over the XCDs too (24.2 -> 23.4 us at cfg2)
     for (int k = 0; k < K; ++k) {
       a.A[k] = h->layers[k]->csr_t();
       a.X[k] = xg;
@@ -1296,7 +1311,9 @@ struct Eig {
       h->ews.varr.ensure(sizeof(double) * (size_t)(keep + b) * (keep + b));
       h->ews.taua.ensure(sizeof(double) * (size_t)(keep + b));
       h->ews.rrerr.ensure(sizeof(int) * 4);
+      h->ews.sturm.ensure(sizeof(double) * n2v2r_rr_sturm_scratch(c_max, keep));
     }
+    const bool sturm = band_rr && rr_sturm_enabled();
 
     h->ews.dbgflag.ensure(sizeof(int) * 4);
     poison_scratch();
@@ -1341,6 +1358,7 @@ struct Eig {
         MX[q] = take();
       }
       bool dense_rr = !band_rr;
+      bool sturm_now = sturm;  // this cycle's banded form (the reducing one after a failure)
       int rr_err = 0;
     rayleigh_ritz:
       {
@@ -1358,12 +1376,20 @@ struct Eig {
         tn(blocks(loc, 0, (int)loc.size()), one(W.back()),
            h->ews.hband.as<double>() + band_off(nq - 1), nullptr);
         HIPCHK(hipMemsetAsync(h->ews.rrerr.as<int>(), 0, sizeof(int), st));
-        HIPCHK(n2v2r_launch_rr_band(h->ews.hband.as<double>(), c, kry0 * b, h->theta.as<double>(),
-                                    h->ews.band.as<double>(), h->ews.varr.as<double>(),
-                                    h->ews.taua.as<double>(), trid, trid + c_max,
-                                    h->ews.refl.as<double>(), h->ews.ytri.as<double>(),
-                                    h->ews.csmall.as<float>(), keep, keep,
-                                    h->ews.rrerr.as<int>(), st));
+        if (sturm_now) {
+          HIPCHK(n2v2r_launch_rr_sturm(h->ews.hband.as<double>(), c, kry0 * b,
+                                       h->theta.as<double>(), h->ews.sturm.as<double>(),
+                                       h->ews.sturm.bytes / sizeof(double),
+                                       h->ews.ytri.as<double>(), h->ews.csmall.as<float>(), keep,
+                                       keep, h->ews.rrerr.as<int>(), st));
+        } else {
+          HIPCHK(n2v2r_launch_rr_band(h->ews.hband.as<double>(), c, kry0 * b, h->theta.as<double>(),
+                                      h->ews.band.as<double>(), h->ews.varr.as<double>(),
+                                      h->ews.taua.as<double>(), trid, trid + c_max,
+                                      h->ews.refl.as<double>(), h->ews.ytri.as<double>(),
+                                      h->ews.csmall.as<float>(), keep, keep,
+                                      h->ews.rrerr.as<int>(), st));
+        }
       } else {
         tn(blocks(Q, 0, nq), blocks(W, 0, nq), h->ews.gsmall.as<double>(), nullptr);
         dbg(h->ews.gsmall.p, (int64_t)c * c, true, "projected matrix H = Q^T W");
@@ -1423,6 +1449,17 @@ struct Eig {
                               hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
       t_ortho += now_ms() - to0;
+      if (rr_err && !dense_rr && sturm_now) {  // a Sturm vector failed its residual check
+        if (trace) fprintf(stderr, "[n2v2r] Sturm Rayleigh-Ritz failed, reducing fallback\n");
+        // the kept Ritz values the reducing path reads: the copy the Sturm assembly made
+        if (kry0 > 0)
+          HIPCHK(hipMemcpyAsync(h->theta.as<double>(), h->ews.sturm.as<double>() + 4,
+                                sizeof(double) * kry0 * b, hipMemcpyDeviceToDevice, st));
+        sturm_now = false;
+        rr_err = 0;
+        ++stats_rr_fallbacks;
+        goto rayleigh_ritz;
+      }
       if (rr_err && !dense_rr) {  // the bulge chase gave up (should not happen): dense RR
         if (trace) fprintf(stderr, "[n2v2r] banded Rayleigh-Ritz failed, dense fallback\n");
         dense_rr = true;
@@ -2327,6 +2364,20 @@ int n2v2r_rr_band_top(n2v2r_handle* h, int c, int kp, const double* hband, int64
       HIPCHK(hipMemcpyAsync(th.p, theta_prev, sizeof(double) * kp, hipMemcpyHostToDevice,
                             h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));  // pageable sources: complete before the kernels
+    if (rr_sturm_enabled()) {  // the solver's default form (N2V2R_RR=band: the reducing one)
+      DevBuf scr;
+      scr.ensure(sizeof(double) * n2v2r_rr_sturm_scratch(c, p));
+      HIPCHK(n2v2r_launch_rr_sturm(hb.as<double>(), c, kp, th.as<double>(), scr.as<double>(),
+                                   scr.bytes / sizeof(double), y.as<double>(), s.as<float>(), p,
+                                   p, er.as<int>(), h->stream));
+      int e = 0;
+      HIPCHK(hipMemcpyAsync(&e, er.p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+      HIPCHK(hipMemcpyAsync(w, th.p, sizeof(double) * p, hipMemcpyDeviceToHost, h->stream));
+      HIPCHK(hipMemcpyAsync(S, s.p, sizeof(float) * c * p, hipMemcpyDeviceToHost, h->stream));
+      HIPCHK(hipStreamSynchronize(h->stream));
+      if (e) throw StatusFail{N2V2R_ERR_NO_CONVERGENCE, "Sturm Rayleigh-Ritz: residual check failed"};
+      return N2V2R_OK;
+    }
     HIPCHK(n2v2r_launch_rr_band(hb.as<double>(), c, kp, th.as<double>(), ab.as<double>(),
                                 va.as<double>(), ta.as<double>(), tri.as<double>(),
                                 tri.as<double>() + c, rf.as<double>(), y.as<double>(),
@@ -2349,7 +2400,7 @@ int n2v2r_spmm_col_blocks(const n2v2r_handle* h, int b) {
 int n2v2r_probe_spmm_stage2(n2v2r_handle* h, int mode, int reps, double* avg_ms) {
   return guarded(h, [&]() -> int {
     if (h->K < 1 || h->K > 8 || h->comm || h->dense_layers() || reps < 1 || !avg_ms ||
-        mode < 0 || mode > 2)
+        mode < 0 || mode > 4)
       return N2V2R_ERR_BAD_ARG;
     for (auto& L : h->layers)
       if (!L->loaded) return N2V2R_ERR_BAD_ARG;
@@ -2361,11 +2412,11 @@ int n2v2r_probe_spmm_stage2(n2v2r_handle* h, int mode, int reps, double* avg_ms)
     SpmmArgs s{};
     s.K = h->K;
     s.sum = mode == 0 ? 1 : 0;
-    s.split = mode == 2 ? 1 : 0;
+    s.split = (mode == 2 || mode == 4) ? 1 : 0;
     s.ldx = s.ldy = 8;
     for (int k = 0; k < h->K; ++k) {
       s.A[k] = h->layers[k]->csr();
-      s.X[k] = z.as<float>() + (size_t)k * n * 8;
+      s.X[k] = z.as<float>() + (size_t)(mode >= 3 ? 0 : k) * n * 8;  // 3, 4: one shared panel
       s.Y[k] = y.as<float>() + (size_t)(mode == 0 ? 0 : k) * n * 8;
     }
     HIPCHK(n2v2r_launch_spmm(s, 8, h->stream));

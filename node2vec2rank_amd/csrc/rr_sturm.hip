@@ -1,0 +1,529 @@
+// Rayleigh-Ritz of the block Krylov-Schur cycle WITHOUT reducing the projected matrix: the top-p
+// eigenpairs of H = Q^T M Q come straight from its arrow + band structure (gfx950, wave64).
+//
+// H, in the basis order [X (kp kept Ritz vectors) | E | Z_2 ... ] (8-wide blocks):
+//   * diag(Theta) on X, coupled only to E:   H[i][kp + q] = G0[i][q]        (i < kp, q < 8)
+//   * the Krylov part (rows kp .. c-1) is symmetric banded with half-bandwidth 8 (block
+//     tridiagonal, upper-triangular couplings R_j) -- the same entries rr_chase_kernel reads.
+// Eigenvalues: Sturm counts nu(x) = #eig(H) < x by symmetric Gaussian elimination of H - x I in
+// natural order, no pivoting: the kp X rows first (each a scalar pivot theta_i - x whose rank-1
+// Schur update lands in the 8 x 8 E block), then the band, one row per step with a 9 x 9 window
+// kept in registers (unrolled by 9 so the window shift is register renaming).  Pivots smaller
+// than eps ||H|| are replaced by -eps ||H|| (dstebz's rule, at the matrix's own noise level).
+// One workgroup per wanted eigenvalue runs a 256-point multisection, like rr_bisect_kernel.
+// Eigenvectors: inverse iteration on the same structure, one 64-thread workgroup per cluster
+// start (its members in order): the X rows eliminated exactly (their Schur complement is an
+// 8 x 8 update of the E block), then the same symmetric elimination of the band as the Sturm
+// count (L D L^T, guarded pivots, no interchanges), kept in LDS with the right-hand side and
+// the iterate, so lane 0's serial factor / solve chains never wait on global memory; two
+// solves, classical Gram-Schmidt against the earlier members of a cluster (as
+// rr_inviter_kernel).  Every vector's residual ||(H - lambda) y|| is checked; a failure (e.g.
+// element growth of the unpivoted factor) sets *err and the caller runs the reducing path
+// (arrow -> band -> bulge chase) instead.
+// Work per Sturm count O(kp b^2 + c b^2), per eigenvector O(c b^2): the O(c^2 b) bulge chase
+// (a serial chain of ~2c steps) and its back-transform are gone.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "common.h"
+
+#define RS_W 8
+#define RS_MAXC 512
+#define RS_BIS_THREADS 256
+#define RS_HDR 4  // scratch header: glo, ghi, tn, (unused)
+#define RS_LD 10  // band row stride in the scratch (9 entries + 1 pad: 16-B aligned rows)
+
+namespace {
+
+__device__ __forceinline__ double rs_rcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(r, fma(-x, r, 1.0), r);
+  r = fma(r, fma(-x, r, 1.0), r);
+  return r;
+}
+
+// |x| >= tiny, sign kept (zero -> -tiny, counted negative: dstebz's convention)
+__device__ __forceinline__ double rs_guard(double d, double tiny) {
+  return fabs(d) < tiny ? (d > 0.0 ? tiny : -tiny) : d;
+}
+
+}  // namespace
+
+// ---- assembly -----------------------------------------------------------------------------
+// scratch (fp64): [glo, ghi, tn, 0 | Xd (kp) | Xg (kp x 8) | Lb ((c - kp + 9) x RS_LD)] with
+// Lb[(r - kp) * RS_LD + t] = H[r][r - 8 + t] (t = 8: the diagonal; columns < kp stored as 0;
+// the 9 rows past c are zero: the eliminations read them but never pivot on them).
+__device__ __forceinline__ double rs_band_entry(const double* __restrict__ hband, int c, int kp,
+                                                int i, int col) {
+  // H[i][col] for kp <= col <= i < c, i - col <= 8 (the band part); zero outside the band
+  constexpr int W = RS_W;
+  if (col < kp || i - col > W || col > i) return 0.0;
+  const int j0 = kp / W;
+  const int base1 = (kp + W) * W;
+  const int j = i / W, r = i % W;
+  if (j == j0) {  // the E block: rows kp .. kp+7 of G0 = [X E]^T W_E
+    const double* G = hband;
+    const int cc = col - kp;
+    return 0.5 * (G[(kp + r) * W + cc] + G[(kp + cc) * W + r]);
+  }
+  const double* G = hband + base1 + (j - j0 - 1) * 2 * W * W;
+  if (col >= j * W) {
+    const int cc = col - j * W;
+    return 0.5 * (G[(W + r) * W + cc] + G[(W + cc) * W + r]);
+  }
+  const int cc = col - (j - 1) * W;  // R_j upper triangular: r <= cc
+  return (r <= cc) ? G[cc * W + r] : 0.0;
+}
+
+__global__ __launch_bounds__(256) void rr_sturm_prep_kernel(const double* __restrict__ hband,
+                                                            int c, int kp,
+                                                            const double* __restrict__ theta,
+                                                            double* __restrict__ scr) {
+  constexpr int W = RS_W;
+  __shared__ double red[3][256];
+  const int tid = threadIdx.x;
+  const int nb = c - kp;
+  double* Xd = scr + RS_HDR;
+  double* Xg = Xd + kp;
+  double* Lb = Xg + (size_t)kp * W;
+  for (int e = tid; e < (nb + 9) * RS_LD; e += 256) {
+    const int rr = e / RS_LD, t = e % RS_LD;
+    const int i = kp + rr, col = i - W + t;
+    Lb[e] = (rr < nb && t <= W) ? rs_band_entry(hband, c, kp, i, col) : 0.0;
+  }
+  for (int e = tid; e < kp * W; e += 256) Xg[e] = hband[e];
+  for (int e = tid; e < kp; e += 256) Xd[e] = theta[e];
+  // Gershgorin bounds and ||H||_inf
+  double lo = 1e300, hi = -1e300, tn = 0.0;
+  for (int i = tid; i < c; i += 256) {
+    double ctr, rad = 0.0;
+    if (i < kp) {
+      ctr = theta[i];
+      for (int q = 0; q < W; ++q) rad += fabs(hband[i * W + q]);
+    } else {
+      ctr = rs_band_entry(hband, c, kp, i, i);
+      for (int d = 1; d <= W; ++d) {
+        if (i - d >= kp) rad += fabs(rs_band_entry(hband, c, kp, i, i - d));
+        if (i + d < c) rad += fabs(rs_band_entry(hband, c, kp, i + d, i));
+      }
+      if (i < kp + W)
+        for (int a = 0; a < kp; ++a) rad += fabs(hband[a * W + (i - kp)]);
+    }
+    lo = fmin(lo, ctr - rad);
+    hi = fmax(hi, ctr + rad);
+    tn = fmax(tn, fabs(ctr) + rad);
+  }
+  red[0][tid] = lo;
+  red[1][tid] = hi;
+  red[2][tid] = tn;
+  __syncthreads();
+  for (int s = 128; s >= 1; s >>= 1) {
+    if (tid < s) {
+      red[0][tid] = fmin(red[0][tid], red[0][tid + s]);
+      red[1][tid] = fmax(red[1][tid], red[1][tid + s]);
+      red[2][tid] = fmax(red[2][tid], red[2][tid + s]);
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    scr[0] = red[0][0];
+    scr[1] = red[1][0];
+    scr[2] = red[2][0];
+    scr[3] = 0.0;
+  }
+}
+
+// ---- symmetric elimination (Sturm counts and the L D L^T of inverse iteration) -------------
+// The window: rows/columns k .. k+8 of the current Schur complement, lower triangle only, 45
+// values in registers.  Logical index i sits at physical slot (i + S) % 9 at step S of a 9-step
+// block, so the shift after a step is register renaming; WV(a, b) maps a physical pair onto the
+// lower triangle (a symmetric store: only 45 registers are ever live).
+#define WV(a, b) w[((a) > (b)) ? (a) : (b)][((a) > (b)) ? (b) : (a)]
+
+// One elimination step at band row k: pivot, multipliers t_i = w_i0 / d (returned in t[1..8]
+// when KEEP), rank-1 update of the trailing 8 x 8, then band row k + 9 enters as logical row 8
+// of the next step (rows past c are zero rows of the padded scratch).
+template <int S, bool KEEP>
+__device__ __forceinline__ double rs_step(double (&w)[9][9], int k, int kp,
+                                          const double* __restrict__ Lb, double x, double tiny,
+                                          double* t) {
+  constexpr int P0 = S % 9;
+  const double d = rs_guard(WV(P0, P0), tiny);
+  const double rd = rs_rcp(d);
+  double tt[9];
+#pragma unroll
+  for (int i = 1; i < 9; ++i) tt[i] = WV((i + S) % 9, P0) * rd;
+#pragma unroll
+  for (int i = 1; i < 9; ++i)
+#pragma unroll
+    for (int j = 1; j <= i; ++j) WV((i + S) % 9, (j + S) % 9) -= tt[i] * WV((j + S) % 9, P0);
+  if (KEEP)
+#pragma unroll
+    for (int i = 1; i < 9; ++i) t[i] = tt[i];
+  const double* src = Lb + (int64_t)(k + 9 - kp) * RS_LD;
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    const double v = src[j];
+    WV(P0, (j + S + 1) % 9) = (j == 8) ? v - x : v;
+  }
+  return d;
+}
+
+// the window for rows kp .. kp+8 of H - x I
+__device__ __forceinline__ void rs_window_init(double (&w)[9][9], int kp,
+                                               const double* __restrict__ Lb, double x) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i)
+#pragma unroll
+    for (int j = 0; j <= i; ++j) {
+      double v = Lb[(int64_t)i * RS_LD + 8 - (i - j)];
+      if (i == j) v -= x;
+      w[i][j] = v;
+    }
+  (void)kp;
+}
+
+// nu(x) = number of eigenvalues of H below x
+__device__ int rs_count(double x, int c, int kp, const double* __restrict__ Xd,
+                        const double* __restrict__ Xg, const double* __restrict__ Lb,
+                        double tiny) {
+  double w[9][9];
+  rs_window_init(w, kp, Lb, x);
+  int neg = 0;
+  // the X rows: pivot theta_a - x, rank-1 update of the E block (logical rows 0..7)
+  for (int a = 0; a < kp; ++a) {
+    const double d = rs_guard(Xd[a] - x, tiny);
+    neg += d < 0.0;
+    const double rd = rs_rcp(d);
+    double g[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) g[q] = Xg[a * 8 + q];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const double gi = g[i] * rd;
+#pragma unroll
+      for (int j = 0; j <= i; ++j) w[i][j] -= gi * g[j];
+    }
+  }
+#define RS_CSTEP(S_)                                                            \
+  if (k + S_ >= c) break;                                                      \
+  neg += rs_step<S_, false>(w, k + S_, kp, Lb, x, tiny, nullptr) < 0.0;
+  for (int k = kp; k < c; k += 9) {
+    RS_CSTEP(0) RS_CSTEP(1) RS_CSTEP(2) RS_CSTEP(3) RS_CSTEP(4) RS_CSTEP(5) RS_CSTEP(6)
+    RS_CSTEP(7) RS_CSTEP(8)
+  }
+#undef RS_CSTEP
+  return neg;
+}
+
+// One workgroup per wanted eigenvalue j (j-th largest), 256-point multisection.  Round 0 for
+// a kept index (j < kp) is anchored on the previous Ritz value theta_j, a lower bound by
+// interlacing (diag(Theta) is a principal submatrix of H): half the points at theta_j + tn
+// 10^(-16 + 16 t / 128) (log-spaced: a converged pair brackets to a width of a third of its
+// shift), half uniform on the Gershgorin interval; the two brackets are intersected.  Later
+// rounds are uniform, until ~8 eps relative width.
+__global__ __launch_bounds__(RS_BIS_THREADS) void rr_sturm_bisect_kernel(const double* __restrict__ scr,
+                                                                        int c, int kp, int p,
+                                                                        double* __restrict__ w) {
+  extern __shared__ __attribute__((aligned(16))) double sl[];
+  __shared__ int cnt[RS_BIS_THREADS];
+  __shared__ double xs[RS_BIS_THREADS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nb = c - kp;
+  const int total = kp + kp * RS_W + (nb + 9) * RS_LD;
+  for (int e = tid; e < total; e += RS_BIS_THREADS) sl[e] = scr[RS_HDR + e];
+  __syncthreads();
+  const double* Xd = sl;
+  const double* Xg = sl + kp;
+  const double* Lb = Xg + kp * RS_W;
+  const double tn = fmax(scr[2], 1e-300);
+  const double tiny = 2.220446049250313e-16 * tn;
+  double lo = scr[0] - 1e-14 * tn - 1e-300, hi = scr[1] + 1e-14 * tn + 1e-300;
+  const int jw = (int)blockIdx.x;
+  const int a = c - 1 - jw;  // ascending index of the wanted eigenvalue
+  constexpr int HALF = RS_BIS_THREADS / 2;
+  for (int round = 0; round < 8; ++round) {
+    const bool anchored = round == 0 && jw < kp;
+    double x;
+    if (anchored) {
+      x = (tid < HALF) ? Xd[jw] + tn * exp10(-16.0 + 16.0 * (double)tid / HALF)
+                       : lo + (hi - lo) * (double)(tid - HALF + 1) / (double)(HALF + 1);
+    } else {
+      x = lo + (hi - lo) * (double)(tid + 1) / (double)(RS_BIS_THREADS + 1);
+    }
+    const int neg = rs_count(x, c, kp, Xd, Xg, Lb, tiny);
+    __syncthreads();
+    cnt[tid] = neg;
+    xs[tid] = x;
+    __syncthreads();
+    // lambda_a in (x_{t-1}, x_t] for the first t with nu(x_t) > a, per increasing point set
+    // (a count perturbed by rounding cannot send the bracket backwards: the first such t)
+    const int s0 = (anchored && tid >= HALF) ? HALF : 0;
+    int first = RS_BIS_THREADS;
+    if (cnt[tid] > a && (tid == s0 || cnt[tid - 1] <= a)) first = tid;
+    if (anchored) {
+      // first hit in each half: lanes of waves 0-1 (half A) and 2-3 (half B) reduced apart
+      for (int o = 32; o >= 1; o >>= 1) first = min(first, __shfl_xor(first, o, 64));
+      __syncthreads();
+      if (lane == 0) cnt[wave] = first;
+      __syncthreads();
+      const int fa = min(cnt[0], cnt[1]), fb = min(cnt[2], cnt[3]);
+      // half A: points are theta_j + offsets (a miss: lambda above the last one)
+      double alo = (fa == 0) ? lo : ((fa >= HALF) ? xs[HALF - 1] : xs[fa - 1]);
+      double ahi = (fa >= HALF) ? hi : xs[fa];
+      if (fa == 0) alo = fmax(lo, Xd[jw] - 1e-14 * tn);  // lambda_j >= theta_j (interlacing)
+      const double blo = (fb == HALF) ? lo : xs[fb - 1];
+      const double bhi = (fb >= RS_BIS_THREADS) ? hi : xs[fb];
+      const double nlo = fmax(alo, (fb >= RS_BIS_THREADS) ? xs[RS_BIS_THREADS - 1] : blo);
+      const double nhi = fmin(ahi, bhi);
+      if (nlo < nhi) {
+        lo = nlo;
+        hi = nhi;
+      }
+    } else {
+      for (int o = 32; o >= 1; o >>= 1) first = min(first, __shfl_xor(first, o, 64));
+      __syncthreads();
+      if (lane == 0) cnt[wave] = first;
+      __syncthreads();
+      first = min(min(cnt[0], cnt[1]), min(cnt[2], cnt[3]));
+      const double step = (hi - lo) / (double)(RS_BIS_THREADS + 1);
+      const double nlo = lo + step * first;
+      const double nhi = (first < RS_BIS_THREADS) ? lo + step * (first + 1) : hi;
+      lo = nlo;
+      hi = nhi;
+    }
+    if (hi - lo <= 8.0 * 2.220446049250313e-16 * fmax(fabs(lo), fabs(hi)) + 1e-300) break;
+    __syncthreads();
+  }
+  if (tid == 0) w[blockIdx.x] = 0.5 * (lo + hi);
+}
+
+// ---- eigenvectors -------------------------------------------------------------------------
+// One 64-thread workgroup per cluster start (gap to eigenvalue j-1 above clus); its members in
+// order.  Everything the serial chains touch lives in LDS: the assembled matrix, the factor
+// (pivots d_k and multipliers t_k,1..8, nb x 9), the right-hand side f and the iterate y.  Lane
+// 0 runs the factorization and the two triangular solves (serial in k); the Gram-Schmidt,
+// norms and the residual check are lane-parallel.  Per member, with D_a = 1 / (theta_a - lambda)
+// (guarded): the E block takes -sum_a D_a g_a g_a^T, the band is eliminated as in the Sturm
+// count; solve: f_E -= G^T D f_X; L z = f_B; y_B = L^{-T} D^{-1} z; y_X = D (f_X - G y_E).
+__device__ void rs_factor_lane(int c, int kp, const double* Xd, const double* Xg,
+                               const double* Lb, double lam, double tiny, double* F) {
+  double w[9][9];
+  rs_window_init(w, kp, Lb, lam);
+  for (int a = 0; a < kp; ++a) {
+    const double rd = rs_rcp(rs_guard(Xd[a] - lam, tiny));
+    double g[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) g[q] = Xg[a * 8 + q];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const double gi = g[i] * rd;
+#pragma unroll
+      for (int jj = 0; jj <= i; ++jj) w[i][jj] -= gi * g[jj];
+    }
+  }
+  double t[9];
+#define RS_FSTEP(S_)                                                                   \
+  if (k + S_ >= c) break;                                                             \
+  {                                                                                   \
+    const double d = rs_step<S_, true>(w, k + S_, kp, Lb, lam, tiny, t);               \
+    double* fk = F + (k + S_ - kp) * 9;                                               \
+    fk[0] = d;                                                                        \
+    _Pragma("unroll") for (int i = 1; i < 9; ++i) fk[i] = t[i];                       \
+  }
+  for (int k = kp; k < c; k += 9) {
+    RS_FSTEP(0) RS_FSTEP(1) RS_FSTEP(2) RS_FSTEP(3) RS_FSTEP(4) RS_FSTEP(5) RS_FSTEP(6)
+    RS_FSTEP(7) RS_FSTEP(8)
+  }
+#undef RS_FSTEP
+}
+
+// y = (H - lam)^{-1} f with the factor F (f's band part is overwritten by z)
+__device__ void rs_solve_lane(int c, int kp, const double* Xd, const double* Xg, double lam,
+                              double tiny, const double* F, double* f, double* y) {
+  const int nb = c - kp;
+  double fe[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int a = 0; a < kp; ++a) {
+    const double s = f[a] * rs_rcp(rs_guard(Xd[a] - lam, tiny));
+#pragma unroll
+    for (int q = 0; q < 8; ++q) fe[q] += Xg[a * 8 + q] * s;
+  }
+  double r[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) r[q] = (q < nb) ? f[kp + q] - fe[q] : 0.0;
+#pragma unroll 4
+  for (int k = 0; k < nb; ++k) {
+    const double zk = r[0];
+    f[kp + k] = zk;
+    const double* fk = F + k * 9;
+    const double nf = (k + 8 < nb) ? f[kp + k + 8] : 0.0;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) r[q] = r[q + 1] - fk[q + 1] * zk;
+    r[7] = nf - fk[8] * zk;
+  }
+  double yw[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // y_{k+1} .. y_{k+8}
+#pragma unroll 4
+  for (int k = nb - 1; k >= 0; --k) {
+    const double* fk = F + k * 9;
+    double v = f[kp + k] * rs_rcp(fk[0]);
+#pragma unroll
+    for (int i = 1; i < 9; ++i) v -= fk[i] * yw[i - 1];
+#pragma unroll
+    for (int q = 7; q > 0; --q) yw[q] = yw[q - 1];
+    yw[0] = v;
+    y[kp + k] = v;
+  }
+  double ye[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) ye[q] = (q < nb) ? y[kp + q] : 0.0;
+  for (int a = 0; a < kp; ++a) {
+    double acc = f[a];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc -= Xg[a * 8 + q] * ye[q];
+    y[a] = acc * rs_rcp(rs_guard(Xd[a] - lam, tiny));
+  }
+}
+
+__device__ __forceinline__ double rs_wave_sum(double v) {
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __restrict__ scr, int c,
+                                                              int kp, int p,
+                                                              const double* __restrict__ w,
+                                                              double clus_rel,
+                                                              double* __restrict__ Y,
+                                                              float* __restrict__ S, int ldS,
+                                                              int* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) double il[];
+  const int lane = threadIdx.x;
+  const int j0 = blockIdx.x;
+  const double tn = fmax(scr[2], 1e-300);
+  const double clus = clus_rel * tn;
+  if (j0 > 0 && fabs(w[j0 - 1] - w[j0]) <= clus) return;  // not a cluster start (uniform)
+  const double tiny = 2.220446049250313e-16 * tn;
+  const int nb = c - kp;
+  const int total = kp + kp * RS_W + (nb + 9) * RS_LD;
+  for (int e = lane; e < total; e += 64) il[e] = scr[RS_HDR + e];
+  const double* Xd = il;
+  const double* Xg = il + kp;
+  const double* Lb = Xg + kp * RS_W;
+  double* F = il + ((total + 1) & ~1);
+  double* f = F + nb * 9;
+  double* y = f + c;
+  __shared__ double proj;
+  __syncthreads();
+  for (int j = j0; j < p && (j == j0 || fabs(w[j - 1] - w[j]) <= clus); ++j) {
+    const double lam = w[j];
+    if (lane == 0) rs_factor_lane(c, kp, Xd, Xg, Lb, lam, tiny, F);
+    for (int i = lane; i < c; i += 64) {
+      const uint64_t hsh = splitmix64(0x9E3779B97F4A7C15ull ^ ((uint64_t)j << 32) ^ (uint64_t)i);
+      f[i] = (double)(hsh >> 11) * (1.0 / 9007199254740992.0) - 0.5;
+    }
+    __syncthreads();
+    bool ok = true;
+    for (int it = 0; it < 2 && ok; ++it) {
+      if (lane == 0) rs_solve_lane(c, kp, Xd, Xg, lam, tiny, F, f, y);
+      __syncthreads();
+      // classical Gram-Schmidt against the cluster's earlier members (Y columns j0 .. j-1)
+      for (int q = j0; q < j; ++q) {
+        double dq = 0.0;
+        for (int i = lane; i < c; i += 64) dq += Y[(int64_t)i * p + q] * y[i];
+        dq = rs_wave_sum(dq);
+        for (int i = lane; i < c; i += 64) y[i] -= dq * Y[(int64_t)i * p + q];
+        __syncthreads();
+      }
+      double s2 = 0.0;
+      for (int i = lane; i < c; i += 64) s2 += y[i] * y[i];
+      s2 = rs_wave_sum(s2);
+      ok = s2 > 0.0 && isfinite(s2);
+      const double inv = ok ? 1.0 / sqrt(s2) : 0.0;
+      for (int i = lane; i < c; i += 64) {
+        const double v = y[i] * inv;
+        y[i] = v;
+        f[i] = v;
+      }
+      __syncthreads();
+    }
+    // residual r = (H - lam) y: X rows, then the band rows (+ the X couplings of the E rows)
+    double r2 = 0.0;
+    for (int i = lane; i < c; i += 64) {
+      double v;
+      if (i < kp) {
+        v = (Xd[i] - lam) * y[i];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v += Xg[i * 8 + q] * y[kp + q];
+      } else {
+        const int rr = i - kp;
+        v = -lam * y[i];
+        for (int d = -8; d <= 8; ++d) {
+          const int col = rr + d;
+          if (col < 0 || col >= nb) continue;
+          const double h = d <= 0 ? Lb[rr * RS_LD + 8 + d] : Lb[col * RS_LD + 8 - d];
+          v += h * y[kp + col];
+        }
+        if (rr < 8)
+          for (int aa = 0; aa < kp; ++aa) v += Xg[aa * 8 + rr] * y[aa];
+      }
+      r2 += v * v;
+    }
+    r2 = rs_wave_sum(r2);
+    if (lane == 0 && (!ok || !(sqrt(r2) <= 1e-8 * tn) || !isfinite(r2))) err[0] = 1;
+    for (int i = lane; i < c; i += 64) {
+      Y[(int64_t)i * p + j] = y[i];
+      S[(int64_t)i * ldS + j] = (float)y[i];
+    }
+    __syncthreads();
+    (void)proj;
+  }
+}
+
+static size_t rs_asm_elems(int c, int kp) {  // header + Xd + Xg + padded band rows
+  return (size_t)RS_HDR + (size_t)kp * (1 + RS_W) + (size_t)(c - kp + 9) * RS_LD;
+}
+
+// scratch doubles for any kp <= c - 8: the assembly (at most RS_HDR + RS_LD (c + 9))
+extern "C" size_t n2v2r_rr_sturm_scratch(int c, int p) {
+  (void)p;
+  return ((size_t)RS_HDR + (size_t)RS_LD * (c + 9) + 7) & ~(size_t)7;
+}
+
+static size_t rs_inviter_lds(int c, int kp) {  // assembly + factor + f + y
+  const size_t total = (size_t)kp * (1 + RS_W) + (size_t)(c - kp + 9) * RS_LD;
+  return sizeof(double) * (((total + 1) & ~(size_t)1) + (size_t)(c - kp) * 9 + 2 * (size_t)c);
+}
+
+extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
+                                           double* theta, double* scr, size_t scr_elems,
+                                           double* Y, float* S, int ldS, int p, int* err,
+                                           hipStream_t stream) {
+  if (c < 9 || c > RS_MAXC || c % RS_W || kp % RS_W || kp + RS_W > c || p < 1 || p > c ||
+      ldS < p)
+    return hipErrorInvalidValue;
+  if (rs_asm_elems(c, kp) > scr_elems) return hipErrorInvalidValue;  // inside the scratch
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)rr_sturm_bisect_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
+    (void)hipFuncSetAttribute((const void*)rr_sturm_inviter_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
+    attr = true;
+  }
+  const size_t asm_d = rs_asm_elems(c, kp);
+  const size_t lbis = sizeof(double) * (asm_d - RS_HDR);
+  const size_t linv = rs_inviter_lds(c, kp);
+  if (lbis > 150 * 1024 || linv > 150 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rr_sturm_prep_kernel, dim3(1), dim3(256), 0, stream, hband, c, kp, theta, scr);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  // theta holds the kept Ritz values (kp) until the prep kernel has copied them
+  hipLaunchKernelGGL(rr_sturm_bisect_kernel, dim3((unsigned)p), dim3(RS_BIS_THREADS), lbis, stream,
+                     scr, c, kp, p, theta);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(rr_sturm_inviter_kernel, dim3((unsigned)p), dim3(64), linv, stream, scr, c,
+                     kp, p, theta, 1e-9, Y, S, ldS, err);
+  return hipGetLastError();
+}

@@ -515,9 +515,13 @@ def _band_problem(c, kp, seed, cluster=False, decoupled=0):
     (40, 0, 12, False, 0), (256, 0, 80, False, 0), (256, 80, 80, False, 0),
     (256, 80, 80, True, 30), (384, 160, 160, False, 0), (512, 184, 184, True, 100),
     (96, 80, 80, False, 0)])
-def test_rayleigh_ritz_band_stage(engine, c, kp, p, cluster, decoupled):
-    """Banded Rayleigh-Ritz (arrow reduction, bulge chasing, bisection, band inverse
-    iteration, arrow back-transform) vs numpy eigh of the same structured matrix."""
+@pytest.mark.parametrize("method", ["sturm", "band"])
+def test_rayleigh_ritz_band_stage(engine, monkeypatch, c, kp, p, cluster, decoupled, method):
+    """Banded Rayleigh-Ritz vs numpy eigh of the same structured matrix, both forms: "sturm"
+    (Sturm-count multisection + inverse iteration on the unreduced arrow + band matrix, the
+    default) and "band" (arrow reduction, bulge chasing, bisection, tridiagonal inverse
+    iteration, back-transform)."""
+    monkeypatch.setenv("N2V2R_RR", method)
     H, hband, theta = _band_problem(c, kp, seed=c + kp, cluster=cluster, decoupled=decoupled)
     w, S = engine.rr_band_top(hband, c, kp, theta, p)
     ref = np.sort(np.linalg.eigvalsh(H))[::-1][:p]

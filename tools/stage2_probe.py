@@ -12,6 +12,7 @@ deg = float(sys.argv[2]) if len(sys.argv) > 2 else 20.0
 eng = _lib.Engine(0)
 eng.set_layers(synthetic.er_layers(n, deg, 2))
 for rep in range(2):
-    t = [eng.probe_spmm_stage2(m, reps=100) * 1e3 for m in (0, 1, 2)]
-    print(f"n {n} deg {deg}: summed {t[0]:.2f} us  per-layer {t[1]:.2f} us  xcd-split {t[2]:.2f} us",
-          flush=True)
+    t = [eng.probe_spmm_stage2(m, reps=100) * 1e3 for m in (0, 1, 2, 3, 4)]
+    print(f"n {n} deg {deg}: stage 2 summed {t[0]:.2f} us  per-layer {t[1]:.2f} us  "
+          f"xcd-split {t[2]:.2f} us | shared panel (stage 1): per-layer {t[3]:.2f} us  "
+          f"xcd-split {t[4]:.2f} us", flush=True)
