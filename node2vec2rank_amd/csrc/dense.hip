@@ -578,6 +578,7 @@ static hipError_t launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024);
       (void)hipFuncSetAttribute((const void*)ts_tn_narrow_kernel<16, true>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024);
+      (void)hipGetLastError();  // a refused attribute must not surface at a later launch
       attr = true;
     }
     const bool flush = rows_per_chunk / 4 > TN_FLUSH;  // rows per wave beyond one fp32 span

@@ -783,6 +783,7 @@ extern "C" hipError_t n2v2r_launch_rr_tridiag(double* A, int c, double* d, doubl
                               hipFuncAttributeMaxDynamicSharedMemorySize, cap);
     (void)hipFuncSetAttribute((const void*)rr_tridiag_kernel<12, 512, false>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+    (void)hipGetLastError();  // a refused attribute must not surface at a later launch
     attr_set = true;
   }
   const dim3 g(1);

@@ -651,6 +651,7 @@ extern "C" hipError_t n2v2r_launch_rr_band(const double* hband, int c, int kp, d
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 46 * 1024);
     (void)hipFuncSetAttribute((const void*)rr_band_back_kernel,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 2048);
+    (void)hipGetLastError();  // a refused attribute must not surface at a later launch
     attr = true;
   }
   const int jm = n2v2r_rr_band_jm(c);

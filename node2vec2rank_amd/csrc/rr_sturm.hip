@@ -30,7 +30,7 @@
 
 #define RS_W 8
 #define RS_MAXC 512
-#define RS_BIS_THREADS 256
+#define RS_BIS_THREADS 512  // points per multisection round (2 waves per SIMD)
 #define RS_HDR 4  // scratch header: glo, ghi, tn, (unused)
 #define RS_LD 10  // band row stride in the scratch (9 entries + 1 pad: 16-B aligned rows)
 
@@ -222,8 +222,9 @@ __device__ int rs_count(double x, int c, int kp, const double* __restrict__ Xd,
 // interlacing (diag(Theta) is a principal submatrix of H): half the points at theta_j + tn
 // 10^(-16 + 16 t / 128) (log-spaced: a converged pair brackets to a width of a third of its
 // shift), half uniform on the Gershgorin interval; the two brackets are intersected.  Later
-// rounds are uniform, until ~8 eps relative width.
-__global__ __launch_bounds__(RS_BIS_THREADS) void rr_sturm_bisect_kernel(const double* __restrict__ scr,
+// rounds are uniform, until the bracket is below 1e-11 ||H|| (the Rayleigh quotient of the
+// inverse-iteration vector refines the value).
+__global__ __launch_bounds__(RS_BIS_THREADS, RS_BIS_THREADS / 256) void rr_sturm_bisect_kernel(const double* __restrict__ scr,
                                                                         int c, int kp, int p,
                                                                         double* __restrict__ w) {
   extern __shared__ __attribute__((aligned(16))) double sl[];
@@ -268,7 +269,12 @@ __global__ __launch_bounds__(RS_BIS_THREADS) void rr_sturm_bisect_kernel(const d
       __syncthreads();
       if (lane == 0) cnt[wave] = first;
       __syncthreads();
-      const int fa = min(cnt[0], cnt[1]), fb = min(cnt[2], cnt[3]);
+      int fa = RS_BIS_THREADS, fb = RS_BIS_THREADS;
+#pragma unroll
+      for (int v = 0; v < RS_BIS_THREADS / 64; ++v) {
+        if (v < RS_BIS_THREADS / 128) fa = min(fa, cnt[v]);
+        else fb = min(fb, cnt[v]);
+      }
       // half A: points are theta_j + offsets (a miss: lambda above the last one)
       double alo = (fa == 0) ? lo : ((fa >= HALF) ? xs[HALF - 1] : xs[fa - 1]);
       double ahi = (fa >= HALF) ? hi : xs[fa];
@@ -286,14 +292,17 @@ __global__ __launch_bounds__(RS_BIS_THREADS) void rr_sturm_bisect_kernel(const d
       __syncthreads();
       if (lane == 0) cnt[wave] = first;
       __syncthreads();
-      first = min(min(cnt[0], cnt[1]), min(cnt[2], cnt[3]));
+#pragma unroll
+      for (int v = 0; v < RS_BIS_THREADS / 64; ++v) first = min(first, cnt[v]);
       const double step = (hi - lo) / (double)(RS_BIS_THREADS + 1);
       const double nlo = lo + step * first;
       const double nhi = (first < RS_BIS_THREADS) ? lo + step * (first + 1) : hi;
       lo = nlo;
       hi = nhi;
     }
-    if (hi - lo <= 8.0 * 2.220446049250313e-16 * fmax(fabs(lo), fabs(hi)) + 1e-300) break;
+    // 1e-11 ||H||: two orders below the cluster threshold; the inverse iteration's Rayleigh
+    // quotient then gives the eigenvalue to fp64 accuracy
+    if (hi - lo <= fmax(1e-11 * tn, 8.0 * 2.220446049250313e-16 * fmax(fabs(lo), fabs(hi)))) break;
     __syncthreads();
   }
   if (tid == 0) w[blockIdx.x] = 0.5 * (lo + hi);
@@ -307,22 +316,16 @@ __global__ __launch_bounds__(RS_BIS_THREADS) void rr_sturm_bisect_kernel(const d
 // norms and the residual check are lane-parallel.  Per member, with D_a = 1 / (theta_a - lambda)
 // (guarded): the E block takes -sum_a D_a g_a g_a^T, the band is eliminated as in the Sturm
 // count; solve: f_E -= G^T D f_X; L z = f_B; y_B = L^{-T} D^{-1} z; y_X = D (f_X - G y_E).
-__device__ void rs_factor_lane(int c, int kp, const double* Xd, const double* Xg,
-                               const double* Lb, double lam, double tiny, double* F) {
+// lane 0: band elimination of B' = band - lam I - Sch (Sch: the X rows' 8 x 8 Schur complement
+// on the E block, formed lane-parallel beforehand); pivots and multipliers to F (nb x 9)
+__device__ void rs_factor_lane(int c, int kp, const double* Lb, const double* sch, double lam,
+                               double tiny, double* F) {
   double w[9][9];
   rs_window_init(w, kp, Lb, lam);
-  for (int a = 0; a < kp; ++a) {
-    const double rd = rs_rcp(rs_guard(Xd[a] - lam, tiny));
-    double g[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) g[q] = Xg[a * 8 + q];
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const double gi = g[i] * rd;
-#pragma unroll
-      for (int jj = 0; jj <= i; ++jj) w[i][jj] -= gi * g[jj];
-    }
-  }
+    for (int jj = 0; jj <= i; ++jj) w[i][jj] -= sch[i * 8 + jj];
   double t[9];
 #define RS_FSTEP(S_)                                                                   \
   if (k + S_ >= c) break;                                                             \
@@ -339,16 +342,10 @@ __device__ void rs_factor_lane(int c, int kp, const double* Xd, const double* Xg
 #undef RS_FSTEP
 }
 
-// y = (H - lam)^{-1} f with the factor F (f's band part is overwritten by z)
-__device__ void rs_solve_lane(int c, int kp, const double* Xd, const double* Xg, double lam,
-                              double tiny, const double* F, double* f, double* y) {
+// lane 0: z = L^{-1} (f_B - fe) in place of f_B, then y_B = L^{-T} D^{-1} z
+__device__ void rs_band_solve_lane(int c, int kp, const double* F, const double* fe, double* f,
+                                   double* y) {
   const int nb = c - kp;
-  double fe[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int a = 0; a < kp; ++a) {
-    const double s = f[a] * rs_rcp(rs_guard(Xd[a] - lam, tiny));
-#pragma unroll
-    for (int q = 0; q < 8; ++q) fe[q] += Xg[a * 8 + q] * s;
-  }
   double r[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) r[q] = (q < nb) ? f[kp + q] - fe[q] : 0.0;
@@ -374,15 +371,6 @@ __device__ void rs_solve_lane(int c, int kp, const double* Xd, const double* Xg,
     yw[0] = v;
     y[kp + k] = v;
   }
-  double ye[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) ye[q] = (q < nb) ? y[kp + q] : 0.0;
-  for (int a = 0; a < kp; ++a) {
-    double acc = f[a];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) acc -= Xg[a * 8 + q] * ye[q];
-    y[a] = acc * rs_rcp(rs_guard(Xd[a] - lam, tiny));
-  }
 }
 
 __device__ __forceinline__ double rs_wave_sum(double v) {
@@ -390,10 +378,32 @@ __device__ __forceinline__ double rs_wave_sum(double v) {
   return v;
 }
 
+// y = (H - lam)^{-1} f: the X rows lane-parallel (dX = 1 / (theta - lam)), the band by lane 0
+__device__ void rs_solve(int c, int kp, const double* Xg, const double* dX, const double* F,
+                         double* fe, double* f, double* y) {
+  const int lane = threadIdx.x;
+  if (lane < 8) {  // f_E -= G^T D f_X
+    double acc = 0.0;
+    for (int a = 0; a < kp; ++a) acc += Xg[a * 8 + lane] * (f[a] * dX[a]);
+    fe[lane] = acc;
+  }
+  __syncthreads();
+  if (lane == 0) rs_band_solve_lane(c, kp, F, fe, f, y);
+  __syncthreads();
+  for (int a = lane; a < kp; a += 64) {  // y_X = D (f_X - G y_E)
+    double acc = f[a];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc -= Xg[a * 8 + q] * y[kp + q];
+    y[a] = acc * dX[a];
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __restrict__ scr, int c,
                                                               int kp, int p,
                                                               const double* __restrict__ w,
                                                               double clus_rel,
+                                                              double* __restrict__ wout,
                                                               double* __restrict__ Y,
                                                               float* __restrict__ S, int ldS,
                                                               int* __restrict__ err) {
@@ -413,20 +423,30 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
   double* F = il + ((total + 1) & ~1);
   double* f = F + nb * 9;
   double* y = f + c;
-  __shared__ double proj;
+  double* dX = y + c;       // [kp] 1 / (theta_a - lam)
+  double* sch = dX + kp;    // [64] the X rows' Schur complement on the E block
+  double* fe = sch + 64;    // [8]
   __syncthreads();
   for (int j = j0; j < p && (j == j0 || fabs(w[j - 1] - w[j]) <= clus); ++j) {
     const double lam = w[j];
-    if (lane == 0) rs_factor_lane(c, kp, Xd, Xg, Lb, lam, tiny, F);
+    for (int a = lane; a < kp; a += 64) dX[a] = rs_rcp(rs_guard(Xd[a] - lam, tiny));
+    __syncthreads();
+    {
+      const int i = lane >> 3, jj = lane & 7;
+      double acc = 0.0;
+      for (int a = 0; a < kp; ++a) acc += Xg[a * 8 + i] * Xg[a * 8 + jj] * dX[a];
+      sch[lane] = acc;
+    }
     for (int i = lane; i < c; i += 64) {
       const uint64_t hsh = splitmix64(0x9E3779B97F4A7C15ull ^ ((uint64_t)j << 32) ^ (uint64_t)i);
       f[i] = (double)(hsh >> 11) * (1.0 / 9007199254740992.0) - 0.5;
     }
     __syncthreads();
+    if (lane == 0) rs_factor_lane(c, kp, Lb, sch, lam, tiny, F);
+    __syncthreads();
     bool ok = true;
     for (int it = 0; it < 2 && ok; ++it) {
-      if (lane == 0) rs_solve_lane(c, kp, Xd, Xg, lam, tiny, F, f, y);
-      __syncthreads();
+      rs_solve(c, kp, Xg, dX, F, fe, f, y);
       // classical Gram-Schmidt against the cluster's earlier members (Y columns j0 .. j-1)
       for (int q = j0; q < j; ++q) {
         double dq = 0.0;
@@ -447,8 +467,9 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
       }
       __syncthreads();
     }
-    // residual r = (H - lam) y: X rows, then the band rows (+ the X couplings of the E rows)
-    double r2 = 0.0;
+    // r = (H - lam) y: X rows, then the band rows (+ the X couplings of the E rows); the
+    // Rayleigh quotient lam + y.r refines the eigenvalue, ||(H - rq) y||^2 = r.r - (y.r)^2
+    double r2 = 0.0, yr = 0.0;
     for (int i = lane; i < c; i += 64) {
       double v;
       if (i < kp) {
@@ -468,15 +489,20 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
           for (int aa = 0; aa < kp; ++aa) v += Xg[aa * 8 + rr] * y[aa];
       }
       r2 += v * v;
+      yr += v * y[i];
     }
     r2 = rs_wave_sum(r2);
-    if (lane == 0 && (!ok || !(sqrt(r2) <= 1e-8 * tn) || !isfinite(r2))) err[0] = 1;
+    yr = rs_wave_sum(yr);
+    const double res2 = fmax(r2 - yr * yr, 0.0);
+    if (lane == 0) {
+      wout[j] = lam + yr;
+      if (!ok || !(sqrt(res2) <= 1e-8 * tn) || !isfinite(r2)) err[0] = 1;
+    }
     for (int i = lane; i < c; i += 64) {
       Y[(int64_t)i * p + j] = y[i];
       S[(int64_t)i * ldS + j] = (float)y[i];
     }
     __syncthreads();
-    (void)proj;
   }
 }
 
@@ -484,15 +510,17 @@ static size_t rs_asm_elems(int c, int kp) {  // header + Xd + Xg + padded band r
   return (size_t)RS_HDR + (size_t)kp * (1 + RS_W) + (size_t)(c - kp + 9) * RS_LD;
 }
 
-// scratch doubles for any kp <= c - 8: the assembly (at most RS_HDR + RS_LD (c + 9))
+// scratch doubles for any kp <= c - 8: the assembly (at most RS_HDR + RS_LD (c + 9)) and the
+// bisection values (c)
 extern "C" size_t n2v2r_rr_sturm_scratch(int c, int p) {
   (void)p;
-  return ((size_t)RS_HDR + (size_t)RS_LD * (c + 9) + 7) & ~(size_t)7;
+  return (((size_t)RS_HDR + (size_t)RS_LD * (c + 9) + 7) & ~(size_t)7) + (size_t)c;
 }
 
 static size_t rs_inviter_lds(int c, int kp) {  // assembly + factor + f + y
   const size_t total = (size_t)kp * (1 + RS_W) + (size_t)(c - kp + 9) * RS_LD;
-  return sizeof(double) * (((total + 1) & ~(size_t)1) + (size_t)(c - kp) * 9 + 2 * (size_t)c);
+  return sizeof(double) * (((total + 1) & ~(size_t)1) + (size_t)(c - kp) * 9 + 2 * (size_t)c +
+                           (size_t)kp + 64 + 8);
 }
 
 extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
@@ -502,13 +530,18 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
   if (c < 9 || c > RS_MAXC || c % RS_W || kp % RS_W || kp + RS_W > c || p < 1 || p > c ||
       ldS < p)
     return hipErrorInvalidValue;
-  if (rs_asm_elems(c, kp) > scr_elems) return hipErrorInvalidValue;  // inside the scratch
+  const size_t wbis_off = (rs_asm_elems(c, kp) + 7) & ~(size_t)7;
+  if (wbis_off + (size_t)p > scr_elems) return hipErrorInvalidValue;  // inside the scratch
+  double* wbis = scr + wbis_off;
   static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)rr_sturm_bisect_kernel,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
-    (void)hipFuncSetAttribute((const void*)rr_sturm_inviter_kernel,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
+  if (!attr) {  // room for the dynamic LDS checked below (the static arrays stay under 10 KB)
+    hipError_t a1 = hipFuncSetAttribute((const void*)rr_sturm_bisect_kernel,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    hipError_t a2 = hipFuncSetAttribute((const void*)rr_sturm_inviter_kernel,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    (void)hipGetLastError();  // a refused attribute must not surface as a later launch error
+    if (a1 != hipSuccess) return a1;
+    if (a2 != hipSuccess) return a2;
     attr = true;
   }
   const size_t asm_d = rs_asm_elems(c, kp);
@@ -518,12 +551,13 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
   hipLaunchKernelGGL(rr_sturm_prep_kernel, dim3(1), dim3(256), 0, stream, hband, c, kp, theta, scr);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  // theta holds the kept Ritz values (kp) until the prep kernel has copied them
+  // theta holds the kept Ritz values (kp) until the prep kernel has copied them; the
+  // bisection writes wbis, the inverse iteration the refined values into theta
   hipLaunchKernelGGL(rr_sturm_bisect_kernel, dim3((unsigned)p), dim3(RS_BIS_THREADS), lbis, stream,
-                     scr, c, kp, p, theta);
+                     scr, c, kp, p, wbis);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(rr_sturm_inviter_kernel, dim3((unsigned)p), dim3(64), linv, stream, scr, c,
-                     kp, p, theta, 1e-9, Y, S, ldS, err);
+                     kp, p, wbis, 1e-9, theta, Y, S, ldS, err);
   return hipGetLastError();
 }
