@@ -1176,7 +1176,7 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   return __hiloint2double(hi, lo);
 }
 
-template <int QB>
+template <int QB, int NU>
 __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float* Zin, float* Zout,
                                                         const double* __restrict__ G, int c,
                                                         int64_t n, const int* cond, int* flags,
@@ -1253,17 +1253,17 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
     }
   }
   __syncthreads();
-  // rows: wave w owns rows 64 w .. 64 w + 63 of the workgroup's 256, lane = (row offset
-  // ro = lane >> 1, column half h = lane & 1) over two 32-row halves u, so one load
+  // rows: wave w owns rows 32 NU w .. 32 NU (w + 1) - 1 of the workgroup's 128 NU, lane =
+  // (row offset ro = lane >> 1, column half h = lane & 1) over NU 32-row parts u, so one load
   // instruction reads 32 consecutive 32-B rows of a block (1 KB contiguous)
   const int lane = tid & 63, h = lane & 1, ro = lane >> 1;
-  const int64_t rbase = (int64_t)blockIdx.x * 256 + (tid >> 6) * 64 + ro;
+  const int64_t rbase = (int64_t)blockIdx.x * (128 * NU) + (tid >> 6) * (32 * NU) + ro;
   if (rbase >= n) return;
-  const bool ok1 = rbase + 32 < n;
+  const bool ok1 = NU > 1 && rbase + 32 < n;
   const int64_t rw[2] = {rbase, ok1 ? rbase + 32 : rbase};
   float acc[2][8];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < NU; ++u) {
     const f32x4 z = *reinterpret_cast<const f32x4*>(Zin + rw[u] * 8 + 4 * h);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -1272,12 +1272,12 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
     }
   }
   int q = 0;
-  for (; q + QB <= Q.count; q += QB) {  // QB blocks x 2 rows (2 QB x 16-B loads) in flight
+  for (; q + QB <= Q.count; q += QB) {  // QB blocks x NU rows (QB NU x 16-B loads) in flight
     f32x4 a4[QB][2];
 #pragma unroll
     for (int b4 = 0; b4 < QB; ++b4)
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < NU; ++u)
         a4[b4][u] = *reinterpret_cast<const f32x4*>(Q.blk[q + b4] + rw[u] * 8 + 4 * h);
 #pragma unroll
     for (int b4 = 0; b4 < QB; ++b4) {
@@ -1287,28 +1287,28 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float gv = g[m * 8 + j];
-          acc[0][j] -= a4[b4][0][m] * gv;
-          acc[1][j] -= a4[b4][1][m] * gv;
+#pragma unroll
+          for (int u = 0; u < NU; ++u) acc[u][j] -= a4[b4][u][m] * gv;
         }
     }
   }
   for (; q < Q.count; ++q) {
     f32x4 a4[2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) a4[u] = *reinterpret_cast<const f32x4*>(Q.blk[q] + rw[u] * 8 + 4 * h);
+    for (int u = 0; u < NU; ++u) a4[u] = *reinterpret_cast<const f32x4*>(Q.blk[q] + rw[u] * 8 + 4 * h);
     const float* g = cf + (q * 8 + 4 * h) * 8;
 #pragma unroll
     for (int m = 0; m < 4; ++m)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float gv = g[m * 8 + j];
-        acc[0][j] -= a4[0][m] * gv;
-        acc[1][j] -= a4[1][m] * gv;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) acc[u][j] -= a4[u][m] * gv;
       }
   }
   const int bad = badw[0];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < NU; ++u) {
     // the two column halves of a row sit in adjacent lanes: fold them (quad_perm [1,0,3,2])
 #pragma unroll
     for (int j = 0; j < 8; ++j)
@@ -1334,19 +1334,25 @@ extern "C" hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zi
   if (Q.width != 8 || c != Q.count * 8) return hipErrorInvalidValue;
   const size_t lds = sizeof(double) * ((size_t)(c + 8) * 8 + 256) + sizeof(float) * ((size_t)c * 8 + 64) + 16;
   if (lds > 64 * 1024) return hipErrorInvalidValue;
-  const unsigned grid = (unsigned)((n + 255) / 256);
   static const int qb = [] {
     const char* s = getenv("N2V2R_PIP_QB");
     return s ? atoi(s) : 4;
   }();
-  if (qb == 8)
-    hipLaunchKernelGGL(pip_fused_kernel<8>, dim3(grid ? grid : 1), dim3(256), lds, stream, Q, Zin,
-                       Zout, G, c, n, cond, flags, any_flag, save, save_row0, save_rows, sticky,
-                       seed, row0);
-  else
-    hipLaunchKernelGGL(pip_fused_kernel<4>, dim3(grid ? grid : 1), dim3(256), lds, stream, Q, Zin,
-                       Zout, G, c, n, cond, flags, any_flag, save, save_row0, save_rows, sticky,
-                       seed, row0);
+  static const int rows = [] {  // rows per workgroup: 128 (32 per wave) or 256 (64 per wave)
+    const char* s = getenv("N2V2R_PIP_ROWS");
+    return (s && atoi(s) == 256) ? 256 : 128;
+  }();
+  const unsigned grid = (unsigned)((n + rows - 1) / rows);
+#define PIP_LAUNCH(QB_, NU_)                                                                   \
+  hipLaunchKernelGGL((pip_fused_kernel<QB_, NU_>), dim3(grid ? grid : 1), dim3(256), lds, stream, Q, \
+                     Zin, Zout, G, c, n, cond, flags, any_flag, save, save_row0, save_rows, sticky,  \
+                     seed, row0)
+  if (rows == 256) {
+    if (qb == 8) PIP_LAUNCH(8, 2); else PIP_LAUNCH(4, 2);
+  } else {
+    if (qb == 4) PIP_LAUNCH(4, 1); else PIP_LAUNCH(8, 1);
+  }
+#undef PIP_LAUNCH
   return hipGetLastError();
 }
 
