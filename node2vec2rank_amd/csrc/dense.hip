@@ -377,6 +377,10 @@ struct ZSum {
   float* out;
 };
 
+__device__ __forceinline__ void zsum_store(const ZSum& zs, int64_t off, const f32x4& v) {
+  *reinterpret_cast<f32x4*>(zs.out + off) = v;
+}
+
 template <bool SUM>
 __device__ __forceinline__ void zrow_load(const float* __restrict__ Bz, const ZSum& zs, int64_t rr,
                                           f32x4& z0, f32x4& z1) {
@@ -428,7 +432,7 @@ __global__ __launch_bounds__(256) void ts_tn_stream_kernel(BlockList A, const fl
       for (int u = 0; u < TS_U; ++u) {
         const int64_t rr = r + 32 * u + rl;
         a[u] = h ? z1[u] : z0[u];
-        *reinterpret_cast<f32x4*>(zs.out + rr * 8 + 4 * h) = a[u];
+        zsum_store(zs, rr * 8 + 4 * h, a[u]);
       }
     }
 #pragma unroll
@@ -448,7 +452,7 @@ __global__ __launch_bounds__(256) void ts_tn_stream_kernel(BlockList A, const fl
       zrow_load<SUM>(Bz, zs, rr, y0, y1);
       if (zblk) {
         a1 = h ? y1 : y0;
-        *reinterpret_cast<f32x4*>(zs.out + rr * 8 + 4 * h) = a1;
+        zsum_store(zs, rr * 8 + 4 * h, a1);
       } else {
         a1 = *reinterpret_cast<const f32x4*>(ab + rr * 8);
       }

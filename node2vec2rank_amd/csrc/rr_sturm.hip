@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -33,6 +34,7 @@
 #define RS_BIS_THREADS 512  // points per multisection round (2 waves per SIMD)
 #define RS_HDR 4  // scratch header: glo, ghi, tn, (unused)
 #define RS_LD 10  // band row stride in the scratch (9 entries + 1 pad: 16-B aligned rows)
+#define RS_PADR 10  // zero rows past c (the elimination reads up to row c + 9)
 
 namespace {
 
@@ -51,9 +53,9 @@ __device__ __forceinline__ double rs_guard(double d, double tiny) {
 }  // namespace
 
 // ---- assembly -----------------------------------------------------------------------------
-// scratch (fp64): [glo, ghi, tn, 0 | Xd (kp) | Xg (kp x 8) | Lb ((c - kp + 9) x RS_LD)] with
+// scratch (fp64): [glo, ghi, tn, 0 | Xd (kp) | Xg (kp x 8) | Lb ((c - kp + RS_PADR) x RS_LD)] with
 // Lb[(r - kp) * RS_LD + t] = H[r][r - 8 + t] (t = 8: the diagonal; columns < kp stored as 0;
-// the 9 rows past c are zero: the eliminations read them but never pivot on them).
+// the RS_PADR rows past c are zero: the eliminations read them but never pivot on them).
 __device__ __forceinline__ double rs_band_entry(const double* __restrict__ hband, int c, int kp,
                                                 int i, int col) {
   // H[i][col] for kp <= col <= i < c, i - col <= 8 (the band part); zero outside the band
@@ -87,7 +89,7 @@ __global__ __launch_bounds__(256) void rr_sturm_prep_kernel(const double* __rest
   double* Xd = scr + RS_HDR;
   double* Xg = Xd + kp;
   double* Lb = Xg + (size_t)kp * W;
-  for (int e = tid; e < (nb + 9) * RS_LD; e += 256) {
+  for (int e = tid; e < (nb + RS_PADR) * RS_LD; e += 256) {
     const int rr = e / RS_LD, t = e % RS_LD;
     const int i = kp + rr, col = i - W + t;
     Lb[e] = (rr < nb && t <= W) ? rs_band_entry(hband, c, kp, i, col) : 0.0;
@@ -142,15 +144,20 @@ __global__ __launch_bounds__(256) void rr_sturm_prep_kernel(const double* __rest
 #define WV(a, b) w[((a) > (b)) ? (a) : (b)][((a) > (b)) ? (b) : (a)]
 
 // One elimination step at band row k: pivot, multipliers t_i = w_i0 / d (returned in t[1..8]
-// when KEEP), rank-1 update of the trailing 8 x 8, then band row k + 9 enters as logical row 8
-// of the next step (rows past c are zero rows of the padded scratch).
+// when KEEP), rank-1 update of the trailing 8 x 8, then band row k + 9 (held in nr, loaded one
+// step earlier) enters as logical row 8 of the next step and row k + 10 is loaded into nr, so a
+// row's LDS latency hides behind a whole step (rows past c are zero rows of the padded scratch).
+// The pivot reciprocal takes one Newton step (~2^-50 relative: far inside the count's backward
+// error) for the counts, two for the factor of inverse iteration.
 template <int S, bool KEEP>
-__device__ __forceinline__ double rs_step(double (&w)[9][9], int k, int kp,
+__device__ __forceinline__ double rs_step(double (&w)[9][9], double (&nr)[9], int k, int kp,
                                           const double* __restrict__ Lb, double x, double tiny,
                                           double* t) {
   constexpr int P0 = S % 9;
   const double d = rs_guard(WV(P0, P0), tiny);
-  const double rd = rs_rcp(d);
+  double rd = __builtin_amdgcn_rcp(d);
+  rd = fma(rd, fma(-d, rd, 1.0), rd);
+  if (KEEP) rd = fma(rd, fma(-d, rd, 1.0), rd);
   double tt[9];
 #pragma unroll
   for (int i = 1; i < 9; ++i) tt[i] = WV((i + S) % 9, P0) * rd;
@@ -161,17 +168,16 @@ __device__ __forceinline__ double rs_step(double (&w)[9][9], int k, int kp,
   if (KEEP)
 #pragma unroll
     for (int i = 1; i < 9; ++i) t[i] = tt[i];
-  const double* src = Lb + (int64_t)(k + 9 - kp) * RS_LD;
 #pragma unroll
-  for (int j = 0; j < 9; ++j) {
-    const double v = src[j];
-    WV(P0, (j + S + 1) % 9) = (j == 8) ? v - x : v;
-  }
+  for (int j = 0; j < 9; ++j) WV(P0, (j + S + 1) % 9) = (j == 8) ? nr[j] - x : nr[j];
+  const double* src = Lb + (int64_t)(k + 10 - kp) * RS_LD;
+#pragma unroll
+  for (int j = 0; j < 9; ++j) nr[j] = src[j];
   return d;
 }
 
-// the window for rows kp .. kp+8 of H - x I
-__device__ __forceinline__ void rs_window_init(double (&w)[9][9], int kp,
+// the window for rows kp .. kp+8 of H - x I, and band row kp + 9 in nr
+__device__ __forceinline__ void rs_window_init(double (&w)[9][9], double (&nr)[9], int kp,
                                                const double* __restrict__ Lb, double x) {
 #pragma unroll
   for (int i = 0; i < 9; ++i)
@@ -181,6 +187,8 @@ __device__ __forceinline__ void rs_window_init(double (&w)[9][9], int kp,
       if (i == j) v -= x;
       w[i][j] = v;
     }
+#pragma unroll
+  for (int j = 0; j < 9; ++j) nr[j] = Lb[(int64_t)9 * RS_LD + j];
   (void)kp;
 }
 
@@ -188,8 +196,8 @@ __device__ __forceinline__ void rs_window_init(double (&w)[9][9], int kp,
 __device__ int rs_count(double x, int c, int kp, const double* __restrict__ Xd,
                         const double* __restrict__ Xg, const double* __restrict__ Lb,
                         double tiny) {
-  double w[9][9];
-  rs_window_init(w, kp, Lb, x);
+  double w[9][9], nr[9];
+  rs_window_init(w, nr, kp, Lb, x);
   int neg = 0;
   // the X rows: pivot theta_a - x, rank-1 update of the E block (logical rows 0..7)
   for (int a = 0; a < kp; ++a) {
@@ -208,7 +216,7 @@ __device__ int rs_count(double x, int c, int kp, const double* __restrict__ Xd,
   }
 #define RS_CSTEP(S_)                                                            \
   if (k + S_ >= c) break;                                                      \
-  neg += rs_step<S_, false>(w, k + S_, kp, Lb, x, tiny, nullptr) < 0.0;
+  neg += rs_step<S_, false>(w, nr, k + S_, kp, Lb, x, tiny, nullptr) < 0.0;
   for (int k = kp; k < c; k += 9) {
     RS_CSTEP(0) RS_CSTEP(1) RS_CSTEP(2) RS_CSTEP(3) RS_CSTEP(4) RS_CSTEP(5) RS_CSTEP(6)
     RS_CSTEP(7) RS_CSTEP(8)
@@ -232,7 +240,7 @@ __global__ __launch_bounds__(RS_BIS_THREADS, RS_BIS_THREADS / 256) void rr_sturm
   __shared__ double xs[RS_BIS_THREADS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nb = c - kp;
-  const int total = kp + kp * RS_W + (nb + 9) * RS_LD;
+  const int total = kp + kp * RS_W + (nb + RS_PADR) * RS_LD;
   for (int e = tid; e < total; e += RS_BIS_THREADS) sl[e] = scr[RS_HDR + e];
   __syncthreads();
   const double* Xd = sl;
@@ -308,6 +316,123 @@ __global__ __launch_bounds__(RS_BIS_THREADS, RS_BIS_THREADS / 256) void rr_sturm
   if (tid == 0) w[blockIdx.x] = 0.5 * (lo + hi);
 }
 
+// ---- global multisection (all CUs) ---------------------------------------------------------
+// Round 0: T = p * M points uniform on the Gershgorin interval, one count per thread over all
+// p * (M / 256) workgroups.  Round r >= 1: eigenvalue j (j-th largest, ascending index
+// a = c-1-j) gets its own M points inside its bracket from round r-1 (M / 256 workgroups, each
+// re-deriving the bracket from the previous counts); its workgroup 0 records the bracket so
+// the next round can rebuild the point set.  Counts are used through "the first point whose
+// count exceeds a" (a rounding-perturbed count cannot move a bracket backwards); with no such
+// point the eigenvalue lies above the last point.  rr_msect_finish_kernel turns the last round's
+// counts into w[j] (bracket midpoints; rounds until the bracket is below 1e-10 ||H||).
+struct RsMsect {
+  int* cnt[2];     // [p * M] counts of the previous / current round
+  double* brk[2];  // [p][2] brackets (round >= 1)
+};
+
+__device__ __forceinline__ double rs_pt(double lo, double hi, int k, int npts) {
+  return lo + (hi - lo) * (double)(k + 1) / (double)(npts + 1);
+}
+
+// bracket of ascending index a from `npts` counts at rs_pt(lo, hi, k, npts): (x_{k-1}, x_k] for
+// the first k with cnt > a, (x_{npts-1}, hi] if none (whole workgroup; the same in every thread)
+__device__ __forceinline__ int rs_block_min(int v, int* red) {
+  for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[wave] = v;
+  __syncthreads();
+  v = 0x7fffffff;
+  for (int w = 0; w < nw; ++w) v = min(v, red[w]);
+  __syncthreads();
+  return v;
+}
+
+__device__ void rs_bracket(const int* __restrict__ cnt, int npts, int a, double& lo, double& hi,
+                           int* red) {
+  // two levels, every load of a level in flight together: the first of blockDim.x segments
+  // whose last count exceeds a, then the first such point inside it
+  const int nt = blockDim.x, t = threadIdx.x;
+  const int seg = (npts + nt - 1) / nt;
+  int sfirst = nt;
+  {
+    const int last = min(t * seg + seg - 1, npts - 1);
+    if (t * seg < npts && cnt[last] > a) sfirst = t;
+  }
+  sfirst = rs_block_min(sfirst, red);
+  int first = npts;
+  if (sfirst < nt) {
+    const int k0 = sfirst * seg;
+    for (int k = k0 + t; k < min(k0 + seg, npts); k += nt)
+      if (cnt[k] > a && (k == 0 || cnt[k - 1] <= a)) first = min(first, k);
+    first = rs_block_min(first, red);
+    if (first >= npts) first = k0;  // a rounding wobble inside the segment: its start
+  }
+  // no point above the eigenvalue: it lies in the top sub-interval (x_{npts-1}, hi]
+  const double nlo = first > 0 ? rs_pt(lo, hi, first - 1, npts) : lo;
+  const double nhi = first < npts ? rs_pt(lo, hi, first, npts) : hi;
+  lo = nlo;
+  hi = nhi;
+}
+
+#define RS_MS_THREADS 512  // counts per workgroup per round (2 waves per SIMD)
+__global__ __launch_bounds__(RS_MS_THREADS, RS_MS_THREADS / 256) void rr_msect_kernel(
+    const double* __restrict__ scr, int c, int kp, int p, int M, int round, RsMsect ms) {
+  extern __shared__ __attribute__((aligned(16))) double sl[];
+  __shared__ int red[RS_MS_THREADS / 64];
+  const int tid = threadIdx.x;
+  const int nb = c - kp;
+  const int total = kp + kp * RS_W + (nb + RS_PADR) * RS_LD;
+  for (int e = tid; e < total; e += RS_MS_THREADS) sl[e] = scr[RS_HDR + e];
+  const double* Xd = sl;
+  const double* Xg = sl + kp;
+  const double* Lb = Xg + kp * RS_W;
+  const double tn = fmax(scr[2], 1e-300);
+  const double tiny = 2.220446049250313e-16 * tn;
+  const double glo = scr[0] - 1e-14 * tn - 1e-300, ghi = scr[1] + 1e-14 * tn + 1e-300;
+  const int m = M / RS_MS_THREADS;
+  const int j = blockIdx.x / m, part = blockIdx.x % m;
+  const int cur = round & 1, prev = cur ^ 1;
+  double x;
+  int slot;
+  if (round == 0) {
+    slot = blockIdx.x * RS_MS_THREADS + tid;
+    x = rs_pt(glo, ghi, slot, p * M);
+    __syncthreads();
+  } else {
+    double lo, hi;
+    if (round == 1) {
+      lo = glo;
+      hi = ghi;
+      __syncthreads();
+      rs_bracket(ms.cnt[prev], p * M, c - 1 - j, lo, hi, red);
+    } else {
+      lo = ms.brk[prev][2 * j];
+      hi = ms.brk[prev][2 * j + 1];
+      __syncthreads();
+      rs_bracket(ms.cnt[prev] + (size_t)j * M, M, c - 1 - j, lo, hi, red);
+    }
+    if (part == 0 && tid == 0) {
+      ms.brk[cur][2 * j] = lo;
+      ms.brk[cur][2 * j + 1] = hi;
+    }
+    const int k = part * RS_MS_THREADS + tid;
+    slot = j * M + k;
+    x = rs_pt(lo, hi, k, M);
+  }
+  ms.cnt[cur][slot] = rs_count(x, c, kp, Xd, Xg, Lb, tiny);
+}
+
+__global__ __launch_bounds__(256) void rr_msect_finish_kernel(int c, int p, int M, int last,
+                                                              RsMsect ms, double* __restrict__ w) {
+  __shared__ int red[4];
+  const int j = blockIdx.x;
+  const int cur = last & 1;
+  double lo = ms.brk[cur][2 * j], hi = ms.brk[cur][2 * j + 1];
+  rs_bracket(ms.cnt[cur] + (size_t)j * M, M, c - 1 - j, lo, hi, red);
+  if (threadIdx.x == 0) w[j] = 0.5 * (lo + hi);
+}
+
 // ---- eigenvectors -------------------------------------------------------------------------
 // One 64-thread workgroup per cluster start (gap to eigenvalue j-1 above clus); its members in
 // order.  Everything the serial chains touch lives in LDS: the assembled matrix, the factor
@@ -320,8 +445,8 @@ __global__ __launch_bounds__(RS_BIS_THREADS, RS_BIS_THREADS / 256) void rr_sturm
 // on the E block, formed lane-parallel beforehand); pivots and multipliers to F (nb x 9)
 __device__ void rs_factor_lane(int c, int kp, const double* Lb, const double* sch, double lam,
                                double tiny, double* F) {
-  double w[9][9];
-  rs_window_init(w, kp, Lb, lam);
+  double w[9][9], nr[9];
+  rs_window_init(w, nr, kp, Lb, lam);
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -330,7 +455,7 @@ __device__ void rs_factor_lane(int c, int kp, const double* Lb, const double* sc
 #define RS_FSTEP(S_)                                                                   \
   if (k + S_ >= c) break;                                                             \
   {                                                                                   \
-    const double d = rs_step<S_, true>(w, k + S_, kp, Lb, lam, tiny, t);               \
+    const double d = rs_step<S_, true>(w, nr, k + S_, kp, Lb, lam, tiny, t);           \
     double* fk = F + (k + S_ - kp) * 9;                                               \
     fk[0] = d;                                                                        \
     _Pragma("unroll") for (int i = 1; i < 9; ++i) fk[i] = t[i];                       \
@@ -415,7 +540,7 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
   if (j0 > 0 && fabs(w[j0 - 1] - w[j0]) <= clus) return;  // not a cluster start (uniform)
   const double tiny = 2.220446049250313e-16 * tn;
   const int nb = c - kp;
-  const int total = kp + kp * RS_W + (nb + 9) * RS_LD;
+  const int total = kp + kp * RS_W + (nb + RS_PADR) * RS_LD;
   for (int e = lane; e < total; e += 64) il[e] = scr[RS_HDR + e];
   const double* Xd = il;
   const double* Xg = il + kp;
@@ -507,18 +632,25 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
 }
 
 static size_t rs_asm_elems(int c, int kp) {  // header + Xd + Xg + padded band rows
-  return (size_t)RS_HDR + (size_t)kp * (1 + RS_W) + (size_t)(c - kp + 9) * RS_LD;
+  return (size_t)RS_HDR + (size_t)kp * (1 + RS_W) + (size_t)(c - kp + RS_PADR) * RS_LD;
 }
 
-// scratch doubles for any kp <= c - 8: the assembly (at most RS_HDR + RS_LD (c + 9)) and the
-// bisection values (c)
+// scratch doubles for any kp <= c - 8: the assembly (at most RS_HDR + RS_LD (c + RS_PADR)), the
+// bisection values (c), the multisection brackets (2 x p x 2) and counts (2 x p x M ints)
+static int rs_msect_m(int p) {  // points per eigenvalue per round: RS_MS_THREADS x workgroups
+  int m = 256 / (p > 0 ? p : 1);
+  m = m < 1 ? 1 : (m > 4 ? 4 : m);
+  return RS_MS_THREADS * m;
+}
+
 extern "C" size_t n2v2r_rr_sturm_scratch(int c, int p) {
-  (void)p;
-  return (((size_t)RS_HDR + (size_t)RS_LD * (c + 9) + 7) & ~(size_t)7) + (size_t)c;
+  const size_t M = (size_t)rs_msect_m(p);
+  return (((size_t)RS_HDR + (size_t)RS_LD * (c + RS_PADR) + 7) & ~(size_t)7) + (size_t)c +
+         4 * (size_t)p + (2 * (size_t)p * M + 1) / 2 + 8;
 }
 
 static size_t rs_inviter_lds(int c, int kp) {  // assembly + factor + f + y
-  const size_t total = (size_t)kp * (1 + RS_W) + (size_t)(c - kp + 9) * RS_LD;
+  const size_t total = (size_t)kp * (1 + RS_W) + (size_t)(c - kp + RS_PADR) * RS_LD;
   return sizeof(double) * (((total + 1) & ~(size_t)1) + (size_t)(c - kp) * 9 + 2 * (size_t)c +
                            (size_t)kp + 64 + 8);
 }
@@ -531,14 +663,25 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
       ldS < p)
     return hipErrorInvalidValue;
   const size_t wbis_off = (rs_asm_elems(c, kp) + 7) & ~(size_t)7;
-  if (wbis_off + (size_t)p > scr_elems) return hipErrorInvalidValue;  // inside the scratch
+  const int M = rs_msect_m(p);
+  const size_t brk_off = wbis_off + (size_t)c, cnt_off = brk_off + 4 * (size_t)p;
+  if (cnt_off + ((2 * (size_t)p * M + 1) / 2) > scr_elems || p > c)
+    return hipErrorInvalidValue;  // every region inside the scratch
   double* wbis = scr + wbis_off;
+  RsMsect ms;
+  ms.brk[0] = scr + brk_off;
+  ms.brk[1] = ms.brk[0] + 2 * p;
+  ms.cnt[0] = reinterpret_cast<int*>(scr + cnt_off);
+  ms.cnt[1] = ms.cnt[0] + (size_t)p * M;
   static bool attr = false;
   if (!attr) {  // room for the dynamic LDS checked below (the static arrays stay under 10 KB)
     hipError_t a1 = hipFuncSetAttribute((const void*)rr_sturm_bisect_kernel,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     hipError_t a2 = hipFuncSetAttribute((const void*)rr_sturm_inviter_kernel,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    hipError_t a3 = hipFuncSetAttribute((const void*)rr_msect_kernel,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    if (a2 == hipSuccess) a2 = a3;
     (void)hipGetLastError();  // a refused attribute must not surface as a later launch error
     if (a1 != hipSuccess) return a1;
     if (a2 != hipSuccess) return a2;
@@ -553,8 +696,28 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
   if (e != hipSuccess) return e;
   // theta holds the kept Ritz values (kp) until the prep kernel has copied them; the
   // bisection writes wbis, the inverse iteration the refined values into theta
-  hipLaunchKernelGGL(rr_sturm_bisect_kernel, dim3((unsigned)p), dim3(RS_BIS_THREADS), lbis, stream,
-                     scr, c, kp, p, wbis);
+  static const bool per_wg = [] {  // N2V2R_RR_MSECT=wg: one multisection per workgroup (A/B)
+    const char* v = getenv("N2V2R_RR_MSECT");
+    return v && v[0] == 'w';
+  }();
+  if (per_wg) {
+    hipLaunchKernelGGL(rr_sturm_bisect_kernel, dim3((unsigned)p), dim3(RS_BIS_THREADS), lbis, stream,
+                       scr, c, kp, p, wbis);
+  } else {
+    const size_t lms = sizeof(double) * (asm_d - RS_HDR);
+    const unsigned grid = (unsigned)(p * (M / RS_MS_THREADS));
+    // rounds until the bracket is below 1e-10 ||H|| (3 at p = 80, M = 768; 4 at p = 160)
+    int rounds = 1;
+    for (double wdt = 2.0 / ((double)p * M + 1.0); wdt > 1e-10; wdt /= (double)(M + 1)) ++rounds;
+    for (int r = 0; r < rounds; ++r) {
+      hipLaunchKernelGGL(rr_msect_kernel, dim3(grid), dim3(RS_MS_THREADS), lms, stream, scr, c, kp,
+                         p, M, r, ms);
+      e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(rr_msect_finish_kernel, dim3((unsigned)p), dim3(256), 0, stream, c, p, M,
+                       rounds - 1, ms, wbis);
+  }
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(rr_sturm_inviter_kernel, dim3((unsigned)p), dim3(64), linv, stream, scr, c,
