@@ -1342,9 +1342,11 @@ extern "C" hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zi
     const char* s = getenv("N2V2R_PIP_QB");
     return s ? atoi(s) : 4;
   }();
-  static const int rows = [] {  // rows per workgroup: 128 (32 per wave) or 256 (64 per wave)
+  // rows per workgroup: 256 (64 per wave); N2V2R_PIP_ROWS=128 halves them (cfg2 flat, cfg4
+  // +20 %: every workgroup stages the (c + 8) x 8 fp64 Gram, 33 KB at c = 512)
+  static const int rows = [] {
     const char* s = getenv("N2V2R_PIP_ROWS");
-    return (s && atoi(s) == 256) ? 256 : 128;
+    return (s && atoi(s) == 128) ? 128 : 256;
   }();
   const unsigned grid = (unsigned)((n + rows - 1) / rows);
 #define PIP_LAUNCH(QB_, NU_)                                                                   \
