@@ -79,6 +79,8 @@ typedef struct {
   int64_t spmm_launches;     /* SpMM kernel launches (for roofline accounting) */
   double spmm_algo_bytes;    /* sum over launches of the SURVEY 8(d) algorithmic bytes */
   int stagnated;             /* 1: stopped at the fp32 residual floor (flat 8 cycles, <= 100x tol) */
+  int rr_fallbacks;          /* Rayleigh-Ritz cycles whose Sturm/inverse-iteration vectors failed
+                                the residual check and were redone by the reducing path */
 } n2v2r_eig_stats;
 
 /* lifecycle */

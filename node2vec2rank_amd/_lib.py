@@ -62,7 +62,8 @@ class EigStats(ctypes.Structure):
                 ("max_residual", ctypes.c_double), ("ms_total", ctypes.c_double),
                 ("ms_spmm", ctypes.c_double), ("ms_ortho", ctypes.c_double),
                 ("ms_rr_host", ctypes.c_double), ("spmm_launches", ctypes.c_int64),
-                ("spmm_algo_bytes", ctypes.c_double), ("stagnated", ctypes.c_int)]
+                ("spmm_algo_bytes", ctypes.c_double), ("stagnated", ctypes.c_int),
+                ("rr_fallbacks", ctypes.c_int)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -1569,6 +1569,7 @@ struct Eig {
       stats->spmm_launches = launches;
       stats->spmm_algo_bytes = algo_bytes;
       stats->stagnated = stagnated;
+      stats->rr_fallbacks = stats_rr_fallbacks;
     }
     return (conv == d || stagnated) ? N2V2R_OK : N2V2R_ERR_NO_CONVERGENCE;
   }

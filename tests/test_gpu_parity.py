@@ -355,6 +355,7 @@ def test_uase_residuals_er_20k(engine):
     engine.set_layers(layers)
     st = engine.uase(d, seed=42)
     assert st["converged"] == d
+    assert st["rr_fallbacks"] == 0, st   # every Sturm Rayleigh-Ritz vector passed its check
     s = engine.singular_values()
     X = engine.left_embedding().astype(np.float64) / np.sqrt(s)[None, :]   # U
     A = sp.hstack(layers).tocsr().astype(np.float64)
