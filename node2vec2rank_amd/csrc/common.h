@@ -57,3 +57,17 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
   return x ^ (x >> 31);
 }
+
+// Copy `total` doubles global -> LDS with NT threads, U loads in flight per thread before the
+// first LDS write (a plain strided copy loop waits out one memory round trip per NT entries).
+template <int NT, int U>
+__device__ __forceinline__ void stage_to_lds(double* __restrict__ dst,
+                                             const double* __restrict__ src, int total, int tid) {
+  for (int e0 = tid; e0 < total; e0 += NT * U) {
+    double t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) t[u] = src[min(e0 + NT * u, total - 1)];  // clamped: no branches
+#pragma unroll
+    for (int u = 0; u < U; ++u) dst[min(e0 + NT * u, total - 1)] = t[u];  // same value again
+  }
+}

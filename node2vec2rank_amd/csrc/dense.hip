@@ -141,6 +141,62 @@ __global__ __launch_bounds__(256) void reduce_chunks_kernel(const double* __rest
   if (lane == 0) out[e] = s;
 }
 
+// Same sum, coalesced: lane = element (64 consecutive elements per workgroup, one 512-B run of
+// every chunk's partial per wave-load), the 16 waves take chunks w, w + 16, ... with 4
+// independent accumulators each, then fold the 16 wave sums in fixed order through LDS
+// (deterministic).  The form above touches one 128-B line per lane (lanes stride the chunks),
+// which made the reduce of a 144-chunk Gram ~5 us.
+__global__ __launch_bounds__(1024) void reduce_cols_kernel(const double* __restrict__ partial,
+                                                           int nchunks, int64_t elems,
+                                                           double* __restrict__ out,
+                                                           const int* cond) {
+  if (cond && *cond == 0) return;
+  __shared__ double red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  double s = 0.0;
+  if (e < elems) {
+    const double* p = partial + e;
+    // batches of 16 loads per lane, all issued before the first add (one memory round trip
+    // per batch instead of one per 4 loads); fixed summation order
+    for (int c0 = w; c0 < nchunks; c0 += 16 * 16) {
+      double v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int c = c0 + 16 * u;
+        v[u] = c < nchunks ? p[(int64_t)c * elems] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += v[u];
+    }
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && e < elems) {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][lane];
+    out[e] = t;
+  }
+}
+
+// out[e] = sum_c partial[c][e] for the Gram forms below (N2V2R_REDUCE=wave: the per-element
+// wave form, A/B)
+static hipError_t launch_reduce(const double* partial, int64_t nchunks, int64_t elems, double* out,
+                                const int* cond, hipStream_t stream) {
+  static const bool wave_form = [] {
+    const char* s = getenv("N2V2R_REDUCE");
+    return s && strcmp(s, "wave") == 0;
+  }();
+  if (wave_form)
+    hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((elems + 3) / 4)), dim3(256), 0,
+                       stream, partial, (int)nchunks, elems, out, cond);
+  else
+    hipLaunchKernelGGL(reduce_cols_kernel, dim3((unsigned)((elems + 63) / 64)), dim3(1024), 0,
+                       stream, partial, (int)nchunks, elems, out, cond);
+  return hipGetLastError();
+}
+
 // Narrow right-hand side (one JB = 8/16-wide block B, the Gram step of the orthogonalisation
 // G = [Q Z]^T Z): VALU form.  Lane owns 4 consecutive columns of A (one 16-B load per row,
 // a wave covers 256 columns = 1 KB of every row), the B row is wave-uniform (scalar loads,
@@ -497,6 +553,14 @@ static int tn_stream_u() {  // row-steps of 32 rows per iteration (N2V2R_TN_U: 4
   }();
   return v;
 }
+static int64_t tn_stream_min_rows() {  // rows per chunk at least this (N2V2R_TN_MINROWS)
+  static const int64_t v = [] {
+    const char* s = getenv("N2V2R_TN_MINROWS");
+    const int64_t r = s ? atoll(s) : 256;
+    return r < 32 ? (int64_t)32 : (r > TS_MAX_CHUNK ? (int64_t)TS_MAX_CHUNK : r);
+  }();
+  return v;
+}
 static int64_t tn_stream_waves() {
   static const int64_t v = [] {
     const char* s = getenv("N2V2R_TN_WAVES");
@@ -513,7 +577,8 @@ static hipError_t launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n
   if (B.count == 1 && B.width == 8 && A.width == 8 && tn_stream_form()) {
     // streaming form: ~tn_stream_waves() (4096) waves, chunks of <= TS_MAX_CHUNK rows, nchunks % 8 == 0
     s_chunks = (tn_stream_waves() + A.count - 1) / A.count;
-    const int64_t lo = (n + TS_MAX_CHUNK - 1) / TS_MAX_CHUNK, hi = (n + 255) / 256;
+    const int64_t lo = (n + TS_MAX_CHUNK - 1) / TS_MAX_CHUNK,
+                  hi = (n + tn_stream_min_rows() - 1) / tn_stream_min_rows();
     if (s_chunks > hi) s_chunks = hi;
     if (s_chunks < lo) s_chunks = lo;
     s_chunks = (s_chunks + 7) & ~(int64_t)7;
@@ -538,9 +603,7 @@ static hipError_t launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n
                          n, rows_per_chunk, partial, cond, none);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((elems + 3) / 4)), dim3(256), 0,
-                       stream, partial, (int)nchunks, elems, out, cond);
-    return hipGetLastError();
+    return launch_reduce(partial, nchunks, elems, out, cond, stream);
   }
   if (zs && zs->count > 0) return hipErrorNotSupported;  // the Z sums: streaming form only
   if (B.count == 1 && B.width == 8 && A.width == 8) {
@@ -560,9 +623,7 @@ static hipError_t launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n
                        rows_per_chunk, partial, cond);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((elems + 3) / 4)), dim3(256), 0,
-                       stream, partial, (int)nchunks, elems, out, cond);
-    return hipGetLastError();
+    return launch_reduce(partial, nchunks, elems, out, cond, stream);
   }
   if (B.count == 1 && (B.width == 8 || B.width == 16) && A.width % 4 == 0) {
     // narrow form: ~1024 workgroups of >= 256 rows, partials within the buffer
@@ -597,9 +658,7 @@ static hipError_t launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n
 #undef TN_NARROW
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((elems + 3) / 4)), dim3(256), 0,
-                       stream, partial, (int)nchunks, elems, out, cond);
-    return hipGetLastError();
+    return launch_reduce(partial, nchunks, elems, out, cond, stream);
   }
   const int nti = (ca + 31) / 32, ntj = (cb + 31) / 32;
   const int ntiles = nti * ntj;
@@ -619,9 +678,7 @@ static hipError_t launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n
                      partial, cond);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((elems + 3) / 4)), dim3(256), 0,
-                     stream, partial, (int)nchunks, elems, out, cond);
-  return hipGetLastError();
+  return launch_reduce(partial, nchunks, elems, out, cond, stream);
 }
 
 extern "C" hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n,
@@ -1027,7 +1084,13 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
     const int n2 = ((c + b) * b) / 2;
     const double2* src = reinterpret_cast<const double2*>(G);
     double2* dst = reinterpret_cast<double2*>(gstage);
-    for (int e = threadIdx.x; e < n2; e += blockDim.x) dst[e] = src[e];
+    for (int e0 = threadIdx.x; e0 < n2; e0 += blockDim.x * 4) {  // 4 loads in flight
+      double2 t[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) t[u] = src[min(e0 + (int)blockDim.x * u, n2 - 1)];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) dst[min(e0 + (int)blockDim.x * u, n2 - 1)] = t[u];
+    }
     if (threadIdx.x == 0 && ((c + b) * b) % 2) gstage[(c + b) * b - 1] = G[(c + b) * b - 1];
     __syncthreads();
     Gs = gstage;
@@ -1202,17 +1265,35 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
   float* rv = cf + c * 8;
   int* badw = reinterpret_cast<int*>(rv + 64);
   const int ne2 = (c + 8) * 4;  // double2 count
-  for (int e = tid; e < ne2; e += 256)
-    reinterpret_cast<double2*>(gd)[e] = reinterpret_cast<const double2*>(G)[e];
+  // all of a thread's G loads in flight before the first LDS write (a load -> wait -> write
+  // loop costs one L2 round trip per 256 entries: ~7 of them at c = 384)
+  for (int e0 = tid; e0 < ne2; e0 += 256 * 8) {
+    double2 t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)  // clamped, unconditional: the loads cannot sink into branches
+      t[u] = reinterpret_cast<const double2*>(G)[min(e0 + 256 * u, ne2 - 1)];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)  // past the end: the last entry again, with its own value
+      reinterpret_cast<double2*>(gd)[min(e0 + 256 * u, ne2 - 1)] = t[u];
+  }
   __syncthreads();
   if (save && lead)
     for (int e = tid; e < save_rows * 8; e += 256) save[e] = gd[save_row0 * 8 + e];
   for (int e = tid; e < c * 8; e += 256) cf[e] = (float)gd[e];
   {
     const int e = tid & 63, sl = tid >> 6, i = e >> 3, j = e & 7;
-    double acc = 0.0;
-    for (int k = sl; k < c; k += 4) acc += gd[k * 8 + i] * gd[k * 8 + j];
-    part[sl * 64 + e] = acc;
+    // 4 independent chains (k, k + 4, k + 8, k + 12): the LDS loads of the next steps issue
+    // while the fp64 adds of this one complete (one chain of c / 4 dependent adds was ~2 us)
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    int k = sl;
+    for (; k + 12 < c; k += 16) {
+      a0 += gd[k * 8 + i] * gd[k * 8 + j];
+      a1 += gd[(k + 4) * 8 + i] * gd[(k + 4) * 8 + j];
+      a2 += gd[(k + 8) * 8 + i] * gd[(k + 8) * 8 + j];
+      a3 += gd[(k + 12) * 8 + i] * gd[(k + 12) * 8 + j];
+    }
+    for (; k < c; k += 4) a0 += gd[k * 8 + i] * gd[k * 8 + j];
+    part[sl * 64 + e] = (a0 + a1) + (a2 + a3);
   }
   __syncthreads();
   if (tid < 64) {
@@ -1432,9 +1513,7 @@ extern "C" hipError_t n2v2r_launch_resid(const BlockList& X, const BlockList& MX
                      theta, n, rows, partial);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((ncols + 3) / 4)), dim3(256), 0, stream,
-                     partial, (int)nchunks, ncols, out, (const int*)nullptr);
-  return hipGetLastError();
+  return launch_reduce(partial, nchunks, ncols, out, nullptr, stream);
 }
 
 // Scale the columns of an N x W block: blk[r][j] *= s[j]
@@ -1563,5 +1642,30 @@ extern "C" hipError_t n2v2r_launch_nonfinite(const void* p, int64_t count, int f
   int64_t nb = (count + 255) / 256;
   if (nb > 1024) nb = 1024;
   hipLaunchKernelGGL(nonfinite_kernel, dim3((unsigned)nb), dim3(256), 0, stream, p, count, f64, flag);
+  return hipGetLastError();
+}
+
+// N2V2R_POISON: fill the LDS of every CU with 0xFF bytes (NaN as fp32 and fp64).  LDS is not
+// cleared between dispatches, so a later kernel that reads LDS it did not write (or multiplies
+// stale LDS by a zero weight) turns non-finite instead of silently using an earlier kernel's data.
+__global__ __launch_bounds__(256) void lds_poison_kernel(int words) {
+  extern __shared__ unsigned int lds_words[];
+  for (int e = threadIdx.x; e < words; e += 256) lds_words[e] = 0xFFFFFFFFu;
+  __syncthreads();
+  if (lds_words[(threadIdx.x * 37) % words] != 0xFFFFFFFFu) lds_words[0] = 0;  // keep the stores
+}
+
+extern "C" hipError_t n2v2r_launch_lds_poison(hipStream_t stream) {
+  static const size_t bytes = [] {
+    const size_t want = 160 * 1024;
+    if (hipFuncSetAttribute((const void*)lds_poison_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)want) == hipSuccess)
+      return want;
+    (void)hipGetLastError();
+    return (size_t)64 * 1024;
+  }();
+  // 4 workgroups per CU: every CU's whole LDS is written whichever CUs the dispatcher picks
+  hipLaunchKernelGGL(lds_poison_kernel, dim3(1024), dim3(256), bytes, stream,
+                     (int)(bytes / sizeof(unsigned int)));
   return hipGetLastError();
 }

@@ -165,6 +165,7 @@ hipError_t n2v2r_launch_rr_tri_eig(const double* d, const double* e, int c, int 
 hipError_t n2v2r_launch_rr_backtransform(const double* V, const double* tau, int c,
                                          const double* Y, int p, float* S, int lds,
                                          hipStream_t stream);
+hipError_t n2v2r_launch_lds_poison(hipStream_t stream);
 hipError_t n2v2r_launch_nonfinite(const void* p, int64_t count, int f64, int* flag,
                                   hipStream_t stream);
 hipError_t n2v2r_launch_ts_tn_zsum(const BlockList& A, int64_t n, const float* const* parts,
@@ -889,6 +890,11 @@ struct Eig {
     for (auto& d : w.zk) HIPCHK(hipMemsetAsync(d->p, 0xFF, d->bytes, st));
   }
 
+  // N2V2R_POISON: NaN bytes into every CU's LDS before the next launch
+  void lds_poison() {
+    if (debug_poison()) HIPCHK(n2v2r_launch_lds_poison(st));
+  }
+
   float* take() {
     if (freelist.empty()) {
       h->ews.pool.emplace_back(new DevBuf());
@@ -943,6 +949,7 @@ struct Eig {
   // W = M X = sum_k A_k (A_k^T X); X, W local, gathered panels for the column side
   void apply_M(const float* X, float* Wout) {
     const double t0 = now_ms();
+    lds_poison();
     const int64_t ng = (int64_t)h->world * npad;  // rows of a gathered panel
     const float* xg = X;
     if (h->comm) {
@@ -1171,6 +1178,7 @@ struct Eig {
                       const std::vector<float*>* local = nullptr, double* save = nullptr,
                       bool lazy = false) {
     const double t0 = now_ms();
+    lds_poison();
     int* flg = h->ews.flg.as<int>();
     int* any = h->ews.anyflag.as<int>();
     const bool loc = local && !full_first && local->size() < basis.size();
@@ -1371,11 +1379,13 @@ struct Eig {
       double* trid = h->ews.tri.as<double>();
       materialize();  // W.back() (every other W block was stored by its expansion's Gram pass)
       const double tr0 = now_ms();
+      lds_poison();
       if (!dense_rr) {
         const std::vector<float*> loc = local_of(Q);
         tn(blocks(loc, 0, (int)loc.size()), one(W.back()),
            h->ews.hband.as<double>() + band_off(nq - 1), nullptr);
         HIPCHK(hipMemsetAsync(h->ews.rrerr.as<int>(), 0, sizeof(int), st));
+        lds_poison();
         if (sturm_now) {
           HIPCHK(n2v2r_launch_rr_sturm(h->ews.hband.as<double>(), c, kry0 * b,
                                        h->theta.as<double>(), h->ews.sturm.as<double>(),
@@ -1393,14 +1403,17 @@ struct Eig {
       } else {
         tn(blocks(Q, 0, nq), blocks(W, 0, nq), h->ews.gsmall.as<double>(), nullptr);
         dbg(h->ews.gsmall.p, (int64_t)c * c, true, "projected matrix H = Q^T W");
+        lds_poison();
         HIPCHK(n2v2r_launch_rr_tridiag(h->ews.gsmall.as<double>(), c, trid, trid + c_max,
                                        trid + 2 * c_max, h->ews.refl.as<double>(), st));
         dbg(trid, c, true, "tridiagonal diagonal");
         dbg(trid + c_max, c - 1, true, "tridiagonal off-diagonal");
+        lds_poison();
         HIPCHK(n2v2r_launch_rr_tri_eig(trid, trid + c_max, c, keep, h->theta.as<double>(),
                                        h->ews.ytri.as<double>(), h->ews.tscr.as<double>(), st));
         dbg(h->theta.p, keep, true, "tridiagonal eigenvalues (bisection)");
         dbg(h->ews.ytri.p, (int64_t)c * keep, true, "tridiagonal eigenvectors");
+        lds_poison();
         HIPCHK(n2v2r_launch_rr_backtransform(h->ews.refl.as<double>(), trid + 2 * c_max, c,
                                              h->ews.ytri.as<double>(), keep,
                                              h->ews.csmall.as<float>(), keep, st));
@@ -1411,6 +1424,7 @@ struct Eig {
       }
       // Ritz vectors X = Q S, MX = W S (keep columns, pb blocks)
       const double to0 = now_ms();
+      lds_poison();
       const int per_launch = std::max(1, 128 / b);  // output blocks per ts_nn launch (<= 128 cols)
       for (int q0b = 0; q0b < pb; q0b += per_launch) {
         const int nt = std::min(per_launch, pb - q0b);

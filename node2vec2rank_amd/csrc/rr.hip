@@ -360,9 +360,13 @@ __global__ __launch_bounds__(256) void rr_backtransform_kernel(const double* __r
       }
     }
     __syncthreads();
-    if (wa < nb) {
+    {
+      // every row of U is written: rows a >= nb (the partial block, processed first) are
+      // zero, not stale LDS -- the update below multiplies them by a zero w_a[i], and
+      // 0 * (a NaN / Inf bit pattern left by an earlier kernel) is NaN
       double sacc = 0.0;
-      for (int bb = wa; bb < nb; ++bb) sacc += T[wa][bb] * WZ[bb][wj];
+      if (wa < nb)
+        for (int bb = wa; bb < nb; ++bb) sacc += T[wa][bb] * WZ[bb][wj];
       U[wa][wj] = sacc;
     }
     __syncthreads();
@@ -501,17 +505,16 @@ __global__ __launch_bounds__(64) void rr_inviter_kernel(const double* __restrict
   __shared__ double nrm_s;
   const int j0 = blockIdx.x;
   const int lane = threadIdx.x;
+  stage_to_lds<64, 16>(ds, d, c, lane);
+  stage_to_lds<64, 16>(es, e, c - 1, lane);
+  if (lane == 0) es[c - 1] = 0.0;
+  __syncthreads();
   double tn = 0.0;
   for (int i = lane; i < c; i += 64) {
-    const double r = (i > 0 ? fabs(e[i - 1]) : 0.0) + (i < c - 1 ? fabs(e[i]) : 0.0);
-    tn = fmax(tn, fabs(d[i]) + r);
+    const double r = (i > 0 ? fabs(es[i - 1]) : 0.0) + fabs(es[i]);
+    tn = fmax(tn, fabs(ds[i]) + r);
   }
   for (int o = 32; o >= 1; o >>= 1) tn = fmax(tn, __shfl_xor(tn, o, 64));
-  for (int i = lane; i < c; i += 64) {
-    ds[i] = d[i];
-    es[i] = i < c - 1 ? e[i] : 0.0;
-  }
-  __syncthreads();
   const double clus = clus_rel * fmax(tn, 1e-300);
   if (j0 > 0 && fabs(w[j0 - 1] - w[j0]) <= clus) return;  // not a cluster start (uniform)
   const double tiny = fmax(2.220446049250313e-16 * tn, 1e-300);

@@ -148,26 +148,31 @@ __global__ __launch_bounds__(256) void rr_sturm_prep_kernel(const double* __rest
 // step earlier) enters as logical row 8 of the next step and row k + 10 is loaded into nr, so a
 // row's LDS latency hides behind a whole step (rows past c are zero rows of the padded scratch).
 // The pivot reciprocal takes one Newton step (~2^-50 relative: far inside the count's backward
-// error) for the counts, two for the factor of inverse iteration.
+// error, and inside inverse iteration's); KEEP returns it in t[0] (the solves multiply by it).
+// The next pivot's update is issued first: it is the only result the next step waits for.
 template <int S, bool KEEP>
 __device__ __forceinline__ double rs_step(double (&w)[9][9], double (&nr)[9], int k, int kp,
                                           const double* __restrict__ Lb, double x, double tiny,
                                           double* t) {
   constexpr int P0 = S % 9;
+  constexpr int P1 = (S + 1) % 9;
   const double d = rs_guard(WV(P0, P0), tiny);
   double rd = __builtin_amdgcn_rcp(d);
   rd = fma(rd, fma(-d, rd, 1.0), rd);
-  if (KEEP) rd = fma(rd, fma(-d, rd, 1.0), rd);
   double tt[9];
+  tt[1] = WV(P1, P0) * rd;
+  WV(P1, P1) -= tt[1] * WV(P1, P0);
 #pragma unroll
-  for (int i = 1; i < 9; ++i) tt[i] = WV((i + S) % 9, P0) * rd;
+  for (int i = 2; i < 9; ++i) tt[i] = WV((i + S) % 9, P0) * rd;
 #pragma unroll
-  for (int i = 1; i < 9; ++i)
+  for (int i = 2; i < 9; ++i)
 #pragma unroll
     for (int j = 1; j <= i; ++j) WV((i + S) % 9, (j + S) % 9) -= tt[i] * WV((j + S) % 9, P0);
-  if (KEEP)
+  if (KEEP) {
+    t[0] = rd;
 #pragma unroll
     for (int i = 1; i < 9; ++i) t[i] = tt[i];
+  }
 #pragma unroll
   for (int j = 0; j < 9; ++j) WV(P0, (j + S + 1) % 9) = (j == 8) ? nr[j] - x : nr[j];
   const double* src = Lb + (int64_t)(k + 10 - kp) * RS_LD;
@@ -193,7 +198,7 @@ __device__ __forceinline__ void rs_window_init(double (&w)[9][9], double (&nr)[9
 }
 
 // nu(x) = number of eigenvalues of H below x
-__device__ int rs_count(double x, int c, int kp, const double* __restrict__ Xd,
+__device__ __forceinline__ int rs_count(double x, int c, int kp, const double* __restrict__ Xd,
                         const double* __restrict__ Xg, const double* __restrict__ Lb,
                         double tiny) {
   double w[9][9], nr[9];
@@ -214,10 +219,19 @@ __device__ int rs_count(double x, int c, int kp, const double* __restrict__ Xd,
       for (int j = 0; j <= i; ++j) w[i][j] -= gi * g[j];
     }
   }
+  // whole groups of 9 steps without exit tests (one basic block: the next step's pivot chain
+  // overlaps this step's trailing updates), then the tail
+#define RS_CSTEP(S_) neg += rs_step<S_, false>(w, nr, k + S_, kp, Lb, x, tiny, nullptr) < 0.0;
+  int k = kp;
+  for (; k + 9 <= c; k += 9) {
+    RS_CSTEP(0) RS_CSTEP(1) RS_CSTEP(2) RS_CSTEP(3) RS_CSTEP(4) RS_CSTEP(5) RS_CSTEP(6)
+    RS_CSTEP(7) RS_CSTEP(8)
+  }
+#undef RS_CSTEP
 #define RS_CSTEP(S_)                                                            \
   if (k + S_ >= c) break;                                                      \
   neg += rs_step<S_, false>(w, nr, k + S_, kp, Lb, x, tiny, nullptr) < 0.0;
-  for (int k = kp; k < c; k += 9) {
+  for (; k < c; k += 9) {
     RS_CSTEP(0) RS_CSTEP(1) RS_CSTEP(2) RS_CSTEP(3) RS_CSTEP(4) RS_CSTEP(5) RS_CSTEP(6)
     RS_CSTEP(7) RS_CSTEP(8)
   }
@@ -241,7 +255,7 @@ __global__ __launch_bounds__(RS_BIS_THREADS, RS_BIS_THREADS / 256) void rr_sturm
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nb = c - kp;
   const int total = kp + kp * RS_W + (nb + RS_PADR) * RS_LD;
-  for (int e = tid; e < total; e += RS_BIS_THREADS) sl[e] = scr[RS_HDR + e];
+  stage_to_lds<RS_BIS_THREADS, 8>(sl, scr + RS_HDR, total, tid);
   __syncthreads();
   const double* Xd = sl;
   const double* Xg = sl + kp;
@@ -348,7 +362,7 @@ __device__ __forceinline__ int rs_block_min(int v, int* red) {
   return v;
 }
 
-__device__ void rs_bracket(const int* __restrict__ cnt, int npts, int a, double& lo, double& hi,
+__device__ __forceinline__ void rs_bracket(const int* __restrict__ cnt, int npts, int a, double& lo, double& hi,
                            int* red) {
   // two levels, every load of a level in flight together: the first of blockDim.x segments
   // whose last count exceeds a, then the first such point inside it
@@ -375,28 +389,32 @@ __device__ void rs_bracket(const int* __restrict__ cnt, int npts, int a, double&
   hi = nhi;
 }
 
-#define RS_MS_THREADS 512  // counts per workgroup per round (2 waves per SIMD)
-__global__ __launch_bounds__(RS_MS_THREADS, RS_MS_THREADS / 256) void rr_msect_kernel(
+// NT counts per workgroup per round: 256 (one wave per SIMD, M = 768 points per eigenvalue at
+// p = 80: the rounds are count-issue-bound, so half the points of the 512-thread form at the
+// same round count) or 512 (N2V2R_MSECT_THREADS=512, A/B)
+#define RS_MS_THREADS 512  // the largest form (scratch sizing)
+template <int NT>
+__global__ __launch_bounds__(NT, NT / 256) void rr_msect_kernel(
     const double* __restrict__ scr, int c, int kp, int p, int M, int round, RsMsect ms) {
   extern __shared__ __attribute__((aligned(16))) double sl[];
-  __shared__ int red[RS_MS_THREADS / 64];
+  __shared__ int red[NT / 64];
   const int tid = threadIdx.x;
   const int nb = c - kp;
   const int total = kp + kp * RS_W + (nb + RS_PADR) * RS_LD;
-  for (int e = tid; e < total; e += RS_MS_THREADS) sl[e] = scr[RS_HDR + e];
+  stage_to_lds<NT, 8>(sl, scr + RS_HDR, total, tid);
   const double* Xd = sl;
   const double* Xg = sl + kp;
   const double* Lb = Xg + kp * RS_W;
   const double tn = fmax(scr[2], 1e-300);
   const double tiny = 2.220446049250313e-16 * tn;
   const double glo = scr[0] - 1e-14 * tn - 1e-300, ghi = scr[1] + 1e-14 * tn + 1e-300;
-  const int m = M / RS_MS_THREADS;
+  const int m = M / NT;
   const int j = blockIdx.x / m, part = blockIdx.x % m;
   const int cur = round & 1, prev = cur ^ 1;
   double x;
   int slot;
   if (round == 0) {
-    slot = blockIdx.x * RS_MS_THREADS + tid;
+    slot = blockIdx.x * NT + tid;
     x = rs_pt(glo, ghi, slot, p * M);
     __syncthreads();
   } else {
@@ -416,7 +434,7 @@ __global__ __launch_bounds__(RS_MS_THREADS, RS_MS_THREADS / 256) void rr_msect_k
       ms.brk[cur][2 * j] = lo;
       ms.brk[cur][2 * j + 1] = hi;
     }
-    const int k = part * RS_MS_THREADS + tid;
+    const int k = part * NT + tid;
     slot = j * M + k;
     x = rs_pt(lo, hi, k, M);
   }
@@ -443,7 +461,7 @@ __global__ __launch_bounds__(256) void rr_msect_finish_kernel(int c, int p, int 
 // count; solve: f_E -= G^T D f_X; L z = f_B; y_B = L^{-T} D^{-1} z; y_X = D (f_X - G y_E).
 // lane 0: band elimination of B' = band - lam I - Sch (Sch: the X rows' 8 x 8 Schur complement
 // on the E block, formed lane-parallel beforehand); pivots and multipliers to F (nb x 9)
-__device__ void rs_factor_lane(int c, int kp, const double* Lb, const double* sch, double lam,
+__device__ __forceinline__ void rs_factor_lane(int c, int kp, const double* Lb, const double* sch, double lam,
                                double tiny, double* F) {
   double w[9][9], nr[9];
   rs_window_init(w, nr, kp, Lb, lam);
@@ -452,51 +470,121 @@ __device__ void rs_factor_lane(int c, int kp, const double* Lb, const double* sc
 #pragma unroll
     for (int jj = 0; jj <= i; ++jj) w[i][jj] -= sch[i * 8 + jj];
   double t[9];
+  // F row k: the pivot reciprocal 1 / d_k, then the multipliers t_k,1..8
+#define RS_FSTEP(S_)                                                                   \
+  {                                                                                   \
+    (void)rs_step<S_, true>(w, nr, k + S_, kp, Lb, lam, tiny, t);                      \
+    double* fk = F + (k + S_ - kp) * 9;                                               \
+    _Pragma("unroll") for (int i = 0; i < 9; ++i) fk[i] = t[i];                       \
+  }
+  int k = kp;
+  for (; k + 9 <= c; k += 9) {  // whole groups: one basic block (see rs_count)
+    RS_FSTEP(0) RS_FSTEP(1) RS_FSTEP(2) RS_FSTEP(3) RS_FSTEP(4) RS_FSTEP(5) RS_FSTEP(6)
+    RS_FSTEP(7) RS_FSTEP(8)
+  }
+#undef RS_FSTEP
 #define RS_FSTEP(S_)                                                                   \
   if (k + S_ >= c) break;                                                             \
   {                                                                                   \
-    const double d = rs_step<S_, true>(w, nr, k + S_, kp, Lb, lam, tiny, t);           \
+    (void)rs_step<S_, true>(w, nr, k + S_, kp, Lb, lam, tiny, t);                      \
     double* fk = F + (k + S_ - kp) * 9;                                               \
-    fk[0] = d;                                                                        \
-    _Pragma("unroll") for (int i = 1; i < 9; ++i) fk[i] = t[i];                       \
+    _Pragma("unroll") for (int i = 0; i < 9; ++i) fk[i] = t[i];                       \
   }
-  for (int k = kp; k < c; k += 9) {
+  for (; k < c; k += 9) {
     RS_FSTEP(0) RS_FSTEP(1) RS_FSTEP(2) RS_FSTEP(3) RS_FSTEP(4) RS_FSTEP(5) RS_FSTEP(6)
     RS_FSTEP(7) RS_FSTEP(8)
   }
 #undef RS_FSTEP
 }
 
-// lane 0: z = L^{-1} (f_B - fe) in place of f_B, then y_B = L^{-T} D^{-1} z
-__device__ void rs_band_solve_lane(int c, int kp, const double* F, const double* fe, double* f,
+// lane 0: z = L^{-1} (f_B - fe) in place of f_B, then y_B = L^{-T} D^{-1} z.  The serial chain
+// is one FMA per row; the coefficients of the next 4 rows are loaded from LDS while the
+// current 4 are processed (a row's loads otherwise stall the chain for an LDS round trip).
+#define RS_SG 4
+__device__ __forceinline__ void rs_band_solve_lane(int c, int kp, const double* F, const double* fe, double* f,
                                    double* y) {
   const int nb = c - kp;
   double r[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) r[q] = (q < nb) ? f[kp + q] - fe[q] : 0.0;
-#pragma unroll 4
-  for (int k = 0; k < nb; ++k) {
-    const double zk = r[0];
-    f[kp + k] = zk;
-    const double* fk = F + k * 9;
-    const double nf = (k + 8 < nb) ? f[kp + k + 8] : 0.0;
+  // forward: row k needs F[k][1..8] and f[kp + k + 8] (rows past nb: zero padding in F is
+  // not there, so the indices are clamped and the values masked)
+  double ca[RS_SG][8], na[RS_SG];
 #pragma unroll
-    for (int q = 0; q < 7; ++q) r[q] = r[q + 1] - fk[q + 1] * zk;
-    r[7] = nf - fk[8] * zk;
+  for (int u = 0; u < RS_SG; ++u) {
+    const int kk = min(u, nb - 1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ca[u][i] = F[kk * 9 + 1 + i];
+    na[u] = (u + 8 < nb) ? f[kp + u + 8] : 0.0;
   }
+  for (int k0 = 0; k0 < nb; k0 += RS_SG) {
+    double cb[RS_SG][8], nbv[RS_SG];
+#pragma unroll
+    for (int u = 0; u < RS_SG; ++u) {
+      const int kk = min(k0 + RS_SG + u, nb - 1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) cb[u][i] = F[kk * 9 + 1 + i];
+      nbv[u] = (k0 + RS_SG + u + 8 < nb) ? f[kp + k0 + RS_SG + u + 8] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < RS_SG; ++u) {
+      if (k0 + u >= nb) break;
+      const double zk = r[0];
+      f[kp + k0 + u] = zk;
+#pragma unroll
+      for (int q = 0; q < 7; ++q) r[q] = r[q + 1] - ca[u][q] * zk;
+      r[7] = na[u] - ca[u][7] * zk;
+    }
+#pragma unroll
+    for (int u = 0; u < RS_SG; ++u) {
+      na[u] = nbv[u];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ca[u][i] = cb[u][i];
+    }
+  }
+  // backward: y_k = z_k / d_k - sum_i t_k,i y_{k+i}; the terms with y_{k+2..k+8} are summed
+  // before y_{k+1} arrives, so the chain is one FMA per row
   double yw[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // y_{k+1} .. y_{k+8}
-#pragma unroll 4
-  for (int k = nb - 1; k >= 0; --k) {
-    const double* fk = F + k * 9;
-    double v = f[kp + k] * rs_rcp(fk[0]);
+  double ba[RS_SG][9], za[RS_SG];
+  const int top = nb - 1;
 #pragma unroll
-    for (int i = 1; i < 9; ++i) v -= fk[i] * yw[i - 1];
+  for (int u = 0; u < RS_SG; ++u) {
+    const int kk = max(top - u, 0);
 #pragma unroll
-    for (int q = 7; q > 0; --q) yw[q] = yw[q - 1];
-    yw[0] = v;
-    y[kp + k] = v;
+    for (int i = 0; i < 9; ++i) ba[u][i] = F[kk * 9 + i];
+    za[u] = f[kp + kk];
+  }
+  for (int k0 = top; k0 >= 0; k0 -= RS_SG) {
+    double bb[RS_SG][9], zb[RS_SG];
+#pragma unroll
+    for (int u = 0; u < RS_SG; ++u) {
+      const int kk = max(k0 - RS_SG - u, 0);
+#pragma unroll
+      for (int i = 0; i < 9; ++i) bb[u][i] = F[kk * 9 + i];
+      zb[u] = f[kp + kk];
+    }
+#pragma unroll
+    for (int u = 0; u < RS_SG; ++u) {
+      const int k = k0 - u;
+      if (k < 0) break;
+      double sacc = za[u] * ba[u][0];
+#pragma unroll
+      for (int i = 8; i >= 2; --i) sacc -= ba[u][i] * yw[i - 1];
+      const double v = sacc - ba[u][1] * yw[0];
+#pragma unroll
+      for (int q = 7; q > 0; --q) yw[q] = yw[q - 1];
+      yw[0] = v;
+      y[kp + k] = v;
+    }
+#pragma unroll
+    for (int u = 0; u < RS_SG; ++u) {
+      za[u] = zb[u];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) ba[u][i] = bb[u][i];
+    }
   }
 }
+#undef RS_SG
 
 __device__ __forceinline__ double rs_wave_sum(double v) {
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -504,7 +592,7 @@ __device__ __forceinline__ double rs_wave_sum(double v) {
 }
 
 // y = (H - lam)^{-1} f: the X rows lane-parallel (dX = 1 / (theta - lam)), the band by lane 0
-__device__ void rs_solve(int c, int kp, const double* Xg, const double* dX, const double* F,
+__device__ __forceinline__ void rs_solve(int c, int kp, const double* Xg, const double* dX, const double* F,
                          double* fe, double* f, double* y) {
   const int lane = threadIdx.x;
   if (lane < 8) {  // f_E -= G^T D f_X
@@ -531,7 +619,7 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
                                                               double* __restrict__ wout,
                                                               double* __restrict__ Y,
                                                               float* __restrict__ S, int ldS,
-                                                              int* __restrict__ err) {
+                                                              int* __restrict__ err, int inv_stop) {
   extern __shared__ __attribute__((aligned(16))) double il[];
   const int lane = threadIdx.x;
   const int j0 = blockIdx.x;
@@ -541,7 +629,7 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
   const double tiny = 2.220446049250313e-16 * tn;
   const int nb = c - kp;
   const int total = kp + kp * RS_W + (nb + RS_PADR) * RS_LD;
-  for (int e = lane; e < total; e += 64) il[e] = scr[RS_HDR + e];
+  stage_to_lds<64, 16>(il, scr + RS_HDR, total, lane);
   const double* Xd = il;
   const double* Xg = il + kp;
   const double* Lb = Xg + kp * RS_W;
@@ -552,8 +640,10 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
   double* sch = dX + kp;    // [64] the X rows' Schur complement on the E block
   double* fe = sch + 64;    // [8]
   __syncthreads();
+  const int stop = inv_stop;
   for (int j = j0; j < p && (j == j0 || fabs(w[j - 1] - w[j]) <= clus); ++j) {
     const double lam = w[j];
+    if (stop == 1) { if (lane == 0) err[0] = 1; return; }
     for (int a = lane; a < kp; a += 64) dX[a] = rs_rcp(rs_guard(Xd[a] - lam, tiny));
     __syncthreads();
     {
@@ -567,11 +657,14 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
       f[i] = (double)(hsh >> 11) * (1.0 / 9007199254740992.0) - 0.5;
     }
     __syncthreads();
+    if (stop == 2) { if (lane == 0) err[0] = 1; return; }
     if (lane == 0) rs_factor_lane(c, kp, Lb, sch, lam, tiny, F);
     __syncthreads();
+    if (stop == 3) { if (lane == 0) err[0] = 1; return; }
     bool ok = true;
     for (int it = 0; it < 2 && ok; ++it) {
       rs_solve(c, kp, Xg, dX, F, fe, f, y);
+      if (stop == 4) { if (lane == 0) err[0] = 1; return; }
       // classical Gram-Schmidt against the cluster's earlier members (Y columns j0 .. j-1)
       for (int q = j0; q < j; ++q) {
         double dq = 0.0;
@@ -592,6 +685,7 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
       }
       __syncthreads();
     }
+    if (stop == 5) { if (lane == 0) err[0] = 1; return; }
     // r = (H - lam) y: X rows, then the band rows (+ the X couplings of the E rows); the
     // Rayleigh quotient lam + y.r refines the eigenvalue, ||(H - rq) y||^2 = r.r - (y.r)^2
     double r2 = 0.0, yr = 0.0;
@@ -637,10 +731,19 @@ static size_t rs_asm_elems(int c, int kp) {  // header + Xd + Xg + padded band r
 
 // scratch doubles for any kp <= c - 8: the assembly (at most RS_HDR + RS_LD (c + RS_PADR)), the
 // bisection values (c), the multisection brackets (2 x p x 2) and counts (2 x p x M ints)
-static int rs_msect_m(int p) {  // points per eigenvalue per round: RS_MS_THREADS x workgroups
+static int rs_msect_threads() {  // N2V2R_MSECT_THREADS=512: the two-waves-per-SIMD form (A/B)
+  static const int v = [] {
+    const char* e = getenv("N2V2R_MSECT_THREADS");
+    return (e && atoi(e) == 512) ? 512 : 256;
+  }();
+  return v;
+}
+
+// points per eigenvalue per round: nt x workgroups (about one workgroup per CU)
+static int rs_msect_m(int p, int nt = RS_MS_THREADS) {
   int m = 256 / (p > 0 ? p : 1);
   m = m < 1 ? 1 : (m > 4 ? 4 : m);
-  return RS_MS_THREADS * m;
+  return nt * m;
 }
 
 extern "C" size_t n2v2r_rr_sturm_scratch(int c, int p) {
@@ -663,7 +766,8 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
       ldS < p)
     return hipErrorInvalidValue;
   const size_t wbis_off = (rs_asm_elems(c, kp) + 7) & ~(size_t)7;
-  const int M = rs_msect_m(p);
+  const int nt_ms = rs_msect_threads();
+  const int M = rs_msect_m(p, nt_ms);
   const size_t brk_off = wbis_off + (size_t)c, cnt_off = brk_off + 4 * (size_t)p;
   if (cnt_off + ((2 * (size_t)p * M + 1) / 2) > scr_elems || p > c)
     return hipErrorInvalidValue;  // every region inside the scratch
@@ -679,8 +783,11 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     hipError_t a2 = hipFuncSetAttribute((const void*)rr_sturm_inviter_kernel,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-    hipError_t a3 = hipFuncSetAttribute((const void*)rr_msect_kernel,
+    hipError_t a3 = hipFuncSetAttribute((const void*)rr_msect_kernel<256>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    hipError_t a4 = hipFuncSetAttribute((const void*)rr_msect_kernel<512>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    if (a3 == hipSuccess) a3 = a4;
     if (a2 == hipSuccess) a2 = a3;
     (void)hipGetLastError();  // a refused attribute must not surface as a later launch error
     if (a1 != hipSuccess) return a1;
@@ -705,13 +812,17 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
                        scr, c, kp, p, wbis);
   } else {
     const size_t lms = sizeof(double) * (asm_d - RS_HDR);
-    const unsigned grid = (unsigned)(p * (M / RS_MS_THREADS));
-    // rounds until the bracket is below 1e-10 ||H|| (3 at p = 80, M = 768; 4 at p = 160)
+    const unsigned grid = (unsigned)(p * (M / nt_ms));
+    // rounds until the bracket is below 1e-10 ||H|| (3 at p = 80, M = 768; 4 at p = 160, M = 256)
     int rounds = 1;
     for (double wdt = 2.0 / ((double)p * M + 1.0); wdt > 1e-10; wdt /= (double)(M + 1)) ++rounds;
     for (int r = 0; r < rounds; ++r) {
-      hipLaunchKernelGGL(rr_msect_kernel, dim3(grid), dim3(RS_MS_THREADS), lms, stream, scr, c, kp,
-                         p, M, r, ms);
+      if (nt_ms == 256)
+        hipLaunchKernelGGL(rr_msect_kernel<256>, dim3(grid), dim3(256), lms, stream, scr, c, kp, p,
+                           M, r, ms);
+      else
+        hipLaunchKernelGGL(rr_msect_kernel<512>, dim3(grid), dim3(512), lms, stream, scr, c, kp, p,
+                           M, r, ms);
       e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
@@ -720,7 +831,11 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
   }
   e = hipGetLastError();
   if (e != hipSuccess) return e;
+  static const int inv_stop = [] {  // N2V2R_INVITER_STOP=k: timing probe, phases after k skipped
+    const char* v = getenv("N2V2R_INVITER_STOP");
+    return v ? atoi(v) : 0;
+  }();
   hipLaunchKernelGGL(rr_sturm_inviter_kernel, dim3((unsigned)p), dim3(64), linv, stream, scr, c,
-                     kp, p, wbis, 1e-9, theta, Y, S, ldS, err);
+                     kp, p, wbis, 1e-9, theta, Y, S, ldS, err, inv_stop);
   return hipGetLastError();
 }
