@@ -175,7 +175,7 @@ hipError_t n2v2r_launch_zsum(const float* const* parts, int count, float* zout, 
                              hipStream_t stream);
 hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp, double* theta, double* scr,
                                  size_t scr_elems, double* Y, float* S, int ldS, int p, int* err,
-                                 hipStream_t stream);
+                                 hipStream_t stream, hipEvent_t before_vectors);
 size_t n2v2r_rr_sturm_scratch(int c, int p);
 }
 
@@ -185,6 +185,14 @@ size_t n2v2r_rr_sturm_scratch(int c, int p);
 static bool rr_sturm_enabled() {
   const char* e = std::getenv("N2V2R_RR");
   return !(e && e[0] == 'b');
+}
+
+// N2V2R_RESTART_OVERLAP=1: the thick-restart expansion issued on a second stream beside the
+// inverse iteration (A/B switch, off by default: cfg2 39.85 vs 39.46 ms per step although the
+// trace shows the expansion inside the inverse iteration's span).  Read per fit.
+static bool restart_overlap_enabled() {
+  const char* e = std::getenv("N2V2R_RESTART_OVERLAP");
+  return e && e[0] == '1';
 }
 
 namespace {
@@ -503,6 +511,9 @@ struct EigWorkspace {
   DevBuf dbgflag;                             // N2V2R_DEBUG_FINITE result flag
   DevBuf s2part;                              // [K][npad][8] XCD-split second-stage outputs
   DevBuf sturm;                               // Sturm Rayleigh-Ritz: assembled arrow + band
+  // the restart expansion run beside the Rayleigh-Ritz stage (spec stream): its own Gram
+  // partials, Gram and flags, so it shares no scratch with the stage
+  DevBuf spec_partial, spec_gsmall, spec_flg, spec_any;
 };
 }  // namespace
 
@@ -512,6 +523,25 @@ struct n2v2r_handle {
   // side stream + events for the column-block SpMM's stage-1 reduce overlap
   hipStream_t side = nullptr;
   hipEvent_t cb_ev[2 * SPMM_MAX_LAYERS] = {};
+  // stream + events of the restart expansion overlapped with the Rayleigh-Ritz stage
+  hipStream_t spec = nullptr;
+  hipEvent_t spec_ev[2] = {};
+  // pinned host staging of the per-cycle read-back (residuals, Ritz values, flags): the copies
+  // are asynchronous and one stream synchronisation ends the cycle (pageable targets made each
+  // copy a host round trip of its own)
+  void* pin = nullptr;
+  size_t pin_bytes = 0;
+  void ensure_pin(size_t bytes) {
+    if (pin_bytes >= bytes) return;
+    if (pin) (void)hipHostFree(pin);
+    pin = nullptr;
+    pin_bytes = 0;
+    if (hipHostMalloc(&pin, bytes, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      throw std::bad_alloc();
+    }
+    pin_bytes = bytes;
+  }
   std::string err;
   int K = 0;
   int64_t n = 0;        // global nodes
@@ -859,6 +889,13 @@ struct Eig {
   bool split2 = false;
   float* pending = nullptr;  // the W block whose value still sits in the partials
   int stats_rr_fallbacks = 0;  // Sturm Rayleigh-Ritz cycles redone by the reducing path
+  // Gram scratch of the orthogonalisation passes (the workspace's own, or the spec set while
+  // the restart expansion is issued on the spec stream)
+  double* part_p = nullptr;
+  size_t part_n = 0;
+  double* gsm_p = nullptr;
+  int* flg_p = nullptr;
+  int* any_p = nullptr;
 
   // N2V2R_DEBUG_FINITE: stop at the first stage whose output holds a non-finite value
   int dbg_cycle = 0, dbg_apps = 0;
@@ -884,7 +921,8 @@ struct Eig {
     EigWorkspace& w = h->ews;
     for (DevBuf* d : {&w.rinv, &w.flg, &w.anyflag, &w.gsmall, &w.csmall, &w.tri, &w.refl,
                       &w.ytri, &w.tscr, &w.hband, &w.band, &w.varr, &w.taua, &w.rrerr, &w.fcoef,
-                      &w.cbpart, &h->partial, &h->theta, &h->resid})
+                      &w.cbpart, &h->partial, &h->theta, &h->resid, &w.spec_partial,
+                      &w.spec_gsmall, &w.spec_flg, &w.spec_any})
       if (d->p) HIPCHK(hipMemsetAsync(d->p, 0xFF, d->bytes, st));
     for (auto& d : w.pool) HIPCHK(hipMemsetAsync(d->p, 0xFF, d->bytes, st));
     for (auto& d : w.zk) HIPCHK(hipMemsetAsync(d->p, 0xFF, d->bytes, st));
@@ -941,7 +979,7 @@ struct Eig {
 
   // TN over local rows, summed over ranks
   void tn(const BlockList& A, const BlockList& B, double* out, const int* cond) {
-    HIPCHK(n2v2r_launch_ts_tn(A, B, n, h->partial.as<double>(), h->partial_elems, out, cond, st));
+    HIPCHK(n2v2r_launch_ts_tn(A, B, n, part_p, part_n, out, cond, st));
     if (h->comm)
       h->allreduce_f64(out, (size_t)A.count * A.width * B.count * B.width);
   }
@@ -1135,8 +1173,8 @@ struct Eig {
       // the Gram pass that first reads the pending image also stores it
       const float* parts[8];
       for (int k = 0; k < K; ++k) parts[k] = s2part(k);
-      const hipError_t e = n2v2r_launch_ts_tn_zsum(L, n, parts, K, pending, h->partial.as<double>(),
-                                                   h->partial_elems, h->ews.gsmall.as<double>(), st);
+      const hipError_t e = n2v2r_launch_ts_tn_zsum(L, n, parts, K, pending, part_p, part_n, gsm_p,
+                                                   st);
       if (e == hipSuccess) {
         pending = nullptr;
         done = true;
@@ -1146,16 +1184,16 @@ struct Eig {
     }
     if (!done) {
       if (zin == pending) materialize();
-      tn(L, one(zin), h->ews.gsmall.as<double>(), cond);
+      tn(L, one(zin), gsm_p, cond);
     }
     if (b == 8 && nq * b <= 512 && pip_fused()) {
       // b = 8: the Cholesky step runs inside the apply launch (every workgroup factors G)
-      HIPCHK(n2v2r_launch_pip_fused(blocks(qz, 0, nq), zin, Z, h->ews.gsmall.as<double>(), nq * b,
+      HIPCHK(n2v2r_launch_pip_fused(blocks(qz, 0, nq), zin, Z, gsm_p, nq * b,
                                     n, cond, flags_out, any_out, save, save_row0, save_rows,
                                     sticky, seed ^ (0xABCDull + ++fill_counter), row0, st));
       return;
     }
-    HIPCHK(n2v2r_launch_pip_chol(h->ews.gsmall.as<double>(), nq * b, b, h->ews.rinv.as<double>(),
+    HIPCHK(n2v2r_launch_pip_chol(gsm_p, nq * b, b, h->ews.rinv.as<double>(),
                                  flags_out, any_out, cond, save, save_row0, save_rows,
                                  h->ews.fcoef.as<float>(), sticky, st));
     // rank-deficient columns (flags_out) are refilled with random values by the same launch
@@ -1179,8 +1217,8 @@ struct Eig {
                       bool lazy = false) {
     const double t0 = now_ms();
     lds_poison();
-    int* flg = h->ews.flg.as<int>();
-    int* any = h->ews.anyflag.as<int>();
+    int* flg = flg_p;
+    int* any = any_p;
     const bool loc = local && !full_first && local->size() < basis.size();
     const std::vector<float*>& first = loc ? *local : basis;
     const int nsave = (save && local) ? (int)local->size() : 0;
@@ -1231,6 +1269,8 @@ struct Eig {
   int run(int d_, const n2v2r_eig_opts& o, std::vector<double>& theta_out, float* Uout,
           int ldu) {
     d = d_;
+    // a previous fit that ended in an exception may have left a restart expansion in flight
+    if (h->spec) HIPCHK(hipStreamSynchronize(h->spec));
     seed = o.seed ? o.seed : 0x5EEDull;
     full_first = (o.solver_flags & N2V2R_EIG_FULL_FIRST_PASS) != 0;
     kry0 = 0;
@@ -1322,6 +1362,25 @@ struct Eig {
       h->ews.sturm.ensure(sizeof(double) * n2v2r_rr_sturm_scratch(c_max, keep));
     }
     const bool sturm = band_rr && rr_sturm_enabled();
+    part_p = h->partial.as<double>();
+    part_n = h->partial_elems;
+    gsm_p = h->ews.gsmall.as<double>();
+    flg_p = h->ews.flg.as<int>();
+    any_p = h->ews.anyflag.as<int>();
+    // the restart expansion (orth(W_last) against the old basis, then its SpMM) needs nothing
+    // from the Rayleigh-Ritz stage: issue it on the spec stream beside the stage (one GPU,
+    // banded Rayleigh-Ritz; N2V2R_RESTART_OVERLAP=0 keeps it in line)
+    const bool spec_ok = band_rr && !h->comm && restart_overlap_enabled();
+    if (spec_ok) {
+      h->ews.spec_partial.ensure(sizeof(double) * h->partial_elems);
+      h->ews.spec_gsmall.ensure(sizeof(double) * (size_t)c_max * c_max);
+      h->ews.spec_flg.ensure(sizeof(int) * 256);
+      h->ews.spec_any.ensure(sizeof(int) * 4);
+      if (!h->spec) {
+        HIPCHK(hipStreamCreateWithFlags(&h->spec, hipStreamNonBlocking));
+        for (hipEvent_t& e : h->spec_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      }
+    }
 
     h->ews.dbgflag.ensure(sizeof(int) * 4);
     poison_scratch();
@@ -1368,6 +1427,9 @@ struct Eig {
       bool dense_rr = !band_rr;
       bool sturm_now = sturm;  // this cycle's banded form (the reducing one after a failure)
       int rr_err = 0;
+      bool spec_live = false;  // the restart expansion is in flight on the spec stream
+      std::vector<float*> specE, specEW;
+      float* spec_pending = nullptr;
     rayleigh_ritz:
       {
       // Rayleigh-Ritz, all on the GPU, into the fp32 Ritz coefficients S (c x keep, ld keep)
@@ -1387,11 +1449,37 @@ struct Eig {
         HIPCHK(hipMemsetAsync(h->ews.rrerr.as<int>(), 0, sizeof(int), st));
         lds_poison();
         if (sturm_now) {
+          const bool spec_fork = spec_ok && !spec_live;
           HIPCHK(n2v2r_launch_rr_sturm(h->ews.hband.as<double>(), c, kry0 * b,
                                        h->theta.as<double>(), h->ews.sturm.as<double>(),
                                        h->ews.sturm.bytes / sizeof(double),
                                        h->ews.ytri.as<double>(), h->ews.csmall.as<float>(), keep,
-                                       keep, h->ews.rrerr.as<int>(), st));
+                                       keep, h->ews.rrerr.as<int>(), st,
+                                       spec_fork ? h->spec_ev[0] : nullptr));
+          if (spec_fork) {
+            // fork: the spec stream starts when the inverse iteration does (an 80-wave kernel
+            // of serial chains that leaves the CUs free; beside the all-CU multisection the
+            // expansion only delayed it).  The expansion's own scratch (Gram partials, Gram,
+            // flags; its SpMM panels are not used by the stage) and its pending split image
+            // are kept apart until the join at the restart.
+            HIPCHK(hipStreamWaitEvent(h->spec, h->spec_ev[0], 0));
+            const hipStream_t st0 = st;
+            st = h->spec;
+            part_p = h->ews.spec_partial.as<double>();
+            gsm_p = h->ews.spec_gsmall.as<double>();
+            flg_p = h->ews.spec_flg.as<int>();
+            any_p = h->ews.spec_any.as<int>();
+            expand_one(W.back(), Q, specE, specEW);
+            spec_pending = pending;
+            pending = nullptr;
+            HIPCHK(hipEventRecord(h->spec_ev[1], st));
+            st = st0;
+            part_p = h->partial.as<double>();
+            gsm_p = h->ews.gsmall.as<double>();
+            flg_p = h->ews.flg.as<int>();
+            any_p = h->ews.anyflag.as<int>();
+            spec_live = true;
+          }
         } else {
           HIPCHK(n2v2r_launch_rr_band(h->ews.hband.as<double>(), c, kry0 * b, h->theta.as<double>(),
                                       h->ews.band.as<double>(), h->ews.varr.as<double>(),
@@ -1450,18 +1538,27 @@ struct Eig {
                                 h->partial.as<double>(), h->partial_elems, h->resid.as<double>(),
                                 st));
       h->allreduce_f64(h->resid.as<double>(), keep);
-      HIPCHK(hipMemcpyAsync(res2.data(), h->resid.as<double>(), sizeof(double) * keep,
+      h->ensure_pin(sizeof(double) * 2 * (size_t)keep + 4 * sizeof(int));
+      double* pres = static_cast<double*>(h->pin);
+      double* pth = pres + keep;
+      int* pflag = reinterpret_cast<int*>(pth + keep);
+      pflag[0] = 0;
+      pflag[1] = 0;
+      HIPCHK(hipMemcpyAsync(pres, h->resid.as<double>(), sizeof(double) * keep,
                             hipMemcpyDeviceToHost, st));
-      HIPCHK(hipMemcpyAsync(wh.data(), h->theta.as<double>(), sizeof(double) * keep,
+      HIPCHK(hipMemcpyAsync(pth, h->theta.as<double>(), sizeof(double) * keep,
                             hipMemcpyDeviceToHost, st));
       if (!dense_rr)
-        HIPCHK(hipMemcpyAsync(&rr_err, h->ews.rrerr.as<int>(), sizeof(int),
-                              hipMemcpyDeviceToHost, st));
-      int refilled = 0;
+        HIPCHK(hipMemcpyAsync(pflag, h->ews.rrerr.as<int>(), sizeof(int), hipMemcpyDeviceToHost,
+                              st));
       if (lazy)
-        HIPCHK(hipMemcpyAsync(&refilled, h->ews.anyflag.as<int>() + 3, sizeof(int),
+        HIPCHK(hipMemcpyAsync(pflag + 1, h->ews.anyflag.as<int>() + 3, sizeof(int),
                               hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
+      std::copy(pres, pres + keep, res2.begin());
+      std::copy(pth, pth + keep, wh.begin());
+      if (!dense_rr) rr_err = pflag[0];
+      int refilled = lazy ? pflag[1] : 0;
       t_ortho += now_ms() - to0;
       if (rr_err && !dense_rr && sturm_now) {  // a Sturm vector failed its residual check
         if (trace) fprintf(stderr, "[n2v2r] Sturm Rayleigh-Ritz failed, reducing fallback\n");
@@ -1496,8 +1593,15 @@ struct Eig {
             refilled = 1;
             break;
           }
+      if (spec_live) {
+        // join: the main stream waits for the expansion before any of its blocks (or the
+        // buffers it wrote) is used or given back
+        HIPCHK(hipStreamWaitEvent(st, h->spec_ev[1], 0));
+      }
       if (refilled) {  // a second pass refilled a column: expand this cycle again, 3 passes
         if (trace) fprintf(stderr, "[n2v2r] rank-deficient block, cycle %d expanded again\n", cycle);
+        for (float* p : specE) give(p);
+        for (float* p : specEW) give(p);
         for (int q = 0; q < pb; ++q) {
           give(X[q]);
           give(MX[q]);
@@ -1548,10 +1652,20 @@ struct Eig {
           }
         }
       }
-      if (done) break;
+      if (done) {
+        for (float* p : specE) give(p);
+        for (float* p : specEW) give(p);
+        break;
+      }
       // restart: [X | orth(W_last) against the old basis] (thick restart)
       std::vector<float*> E, EW;
-      expand_one(W.back(), Q, E, EW);
+      if (spec_live) {
+        E = specE;
+        EW = specEW;
+        pending = spec_pending;
+      } else {
+        expand_one(W.back(), Q, E, EW);
+      }
       ++apps;
       for (float* p : Q) give(p);
       for (float* p : W) give(p);
@@ -1719,6 +1833,10 @@ void n2v2r_destroy(n2v2r_handle* h) {
   for (hipEvent_t& e : h->cb_ev)
     if (e) (void)hipEventDestroy(e);
   if (h->side) (void)hipStreamDestroy(h->side);
+  for (hipEvent_t e : h->spec_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->spec) (void)hipStreamDestroy(h->spec);
+  if (h->pin) (void)hipHostFree(h->pin);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -2384,7 +2502,7 @@ int n2v2r_rr_band_top(n2v2r_handle* h, int c, int kp, const double* hband, int64
       scr.ensure(sizeof(double) * n2v2r_rr_sturm_scratch(c, p));
       HIPCHK(n2v2r_launch_rr_sturm(hb.as<double>(), c, kp, th.as<double>(), scr.as<double>(),
                                    scr.bytes / sizeof(double), y.as<double>(), s.as<float>(), p,
-                                   p, er.as<int>(), h->stream));
+                                   p, er.as<int>(), h->stream, nullptr));
       int e = 0;
       HIPCHK(hipMemcpyAsync(&e, er.p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
       HIPCHK(hipMemcpyAsync(w, th.p, sizeof(double) * p, hipMemcpyDeviceToHost, h->stream));

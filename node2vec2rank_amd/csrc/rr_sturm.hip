@@ -661,7 +661,43 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
     if (lane == 0) rs_factor_lane(c, kp, Lb, sch, lam, tiny, F);
     __syncthreads();
     if (stop == 3) { if (lane == 0) err[0] = 1; return; }
-    bool ok = true;
+    // r = (H - lam) y: X rows, then the band rows (+ the X couplings of the E rows); the
+    // Rayleigh quotient lam + y.r refines the eigenvalue, ||(H - rq) y||^2 = r.r - (y.r)^2
+    double r2 = 0.0, yr = 0.0;
+    auto residual = [&]() {
+      r2 = 0.0;
+      yr = 0.0;
+      for (int i = lane; i < c; i += 64) {
+        double v;
+        if (i < kp) {
+          v = (Xd[i] - lam) * y[i];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v += Xg[i * 8 + q] * y[kp + q];
+        } else {
+          const int rr = i - kp;
+          v = -lam * y[i];
+          for (int d = -8; d <= 8; ++d) {
+            const int col = rr + d;
+            if (col < 0 || col >= nb) continue;
+            const double h = d <= 0 ? Lb[rr * RS_LD + 8 + d] : Lb[col * RS_LD + 8 - d];
+            v += h * y[kp + col];
+          }
+          if (rr < 8)
+            for (int aa = 0; aa < kp; ++aa) v += Xg[aa * 8 + rr] * y[aa];
+        }
+        r2 += v * v;
+        yr += v * y[i];
+      }
+      r2 = rs_wave_sum(r2);
+      yr = rs_wave_sum(yr);
+    };
+    // an isolated eigenvalue whose first iterate already has a residual below 1e-7 of its gap
+    // to the neighbouring wanted values (so its components along them are below 1e-7: fp32
+    // orthogonality of the Ritz coefficients) skips the second solve
+    double gap = 0.0;
+    if (j == j0 && j + 1 < p && j > 0) gap = fmin(w[j - 1] - lam, lam - w[j + 1]);
+    else if (j == j0 && j == 0 && p > 1) gap = lam - w[1];
+    bool ok = true, done = false;
     for (int it = 0; it < 2 && ok; ++it) {
       rs_solve(c, kp, Xg, dX, F, fe, f, y);
       if (stop == 4) { if (lane == 0) err[0] = 1; return; }
@@ -684,34 +720,16 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
         f[i] = v;
       }
       __syncthreads();
+      if (it == 0 && ok && gap > 0.0) {
+        residual();
+        if (sqrt(fmax(r2 - yr * yr, 0.0)) <= 1e-7 * gap) {  // uniform (wave sums)
+          done = true;
+          break;
+        }
+      }
     }
     if (stop == 5) { if (lane == 0) err[0] = 1; return; }
-    // r = (H - lam) y: X rows, then the band rows (+ the X couplings of the E rows); the
-    // Rayleigh quotient lam + y.r refines the eigenvalue, ||(H - rq) y||^2 = r.r - (y.r)^2
-    double r2 = 0.0, yr = 0.0;
-    for (int i = lane; i < c; i += 64) {
-      double v;
-      if (i < kp) {
-        v = (Xd[i] - lam) * y[i];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) v += Xg[i * 8 + q] * y[kp + q];
-      } else {
-        const int rr = i - kp;
-        v = -lam * y[i];
-        for (int d = -8; d <= 8; ++d) {
-          const int col = rr + d;
-          if (col < 0 || col >= nb) continue;
-          const double h = d <= 0 ? Lb[rr * RS_LD + 8 + d] : Lb[col * RS_LD + 8 - d];
-          v += h * y[kp + col];
-        }
-        if (rr < 8)
-          for (int aa = 0; aa < kp; ++aa) v += Xg[aa * 8 + rr] * y[aa];
-      }
-      r2 += v * v;
-      yr += v * y[i];
-    }
-    r2 = rs_wave_sum(r2);
-    yr = rs_wave_sum(yr);
+    if (!done) residual();
     const double res2 = fmax(r2 - yr * yr, 0.0);
     if (lane == 0) {
       wout[j] = lam + yr;
@@ -761,7 +779,7 @@ static size_t rs_inviter_lds(int c, int kp) {  // assembly + factor + f + y
 extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
                                            double* theta, double* scr, size_t scr_elems,
                                            double* Y, float* S, int ldS, int p, int* err,
-                                           hipStream_t stream) {
+                                           hipStream_t stream, hipEvent_t before_vectors) {
   if (c < 9 || c > RS_MAXC || c % RS_W || kp % RS_W || kp + RS_W > c || p < 1 || p > c ||
       ldS < p)
     return hipErrorInvalidValue;
@@ -831,6 +849,10 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
   }
   e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (before_vectors) {  // the caller may start other work beside the inverse iteration
+    e = hipEventRecord(before_vectors, stream);
+    if (e != hipSuccess) return e;
+  }
   static const int inv_stop = [] {  // N2V2R_INVITER_STOP=k: timing probe, phases after k skipped
     const char* v = getenv("N2V2R_INVITER_STOP");
     return v ? atoi(v) : 0;
