@@ -845,6 +845,153 @@ __global__ __launch_bounds__(256) void ts_nn_kernel(BlockList A, Coef F, int cb,
   }
 }
 
+// Ritz vectors and their images in one launch: O0 = A0 F, O1 = A1 F (X = Q S, MX = W S) with the
+// whole coefficient matrix F (ca x cb, cb <= 32 NT) staged in LDS ONCE per workgroup (one
+// workgroup per CU, 147 KB at ca = 384, NT = 3), then every wave walks 32-row tiles with no
+// block barrier: the next 64-deep k chunk of its A rows is loaded while the MFMAs of the
+// current one run (ts_nn_kernel re-stages F per chunk between two barriers).  Same MFMA form
+// and k permutation as ts_nn_kernel.
+#define RZ_T 512  // 8 waves (2 per SIMD: one hides the other's LDS / HBM waits), one F copy
+template <int NT>
+__global__ __launch_bounds__(RZ_T) void ritz_nn_kernel(BlockList A0, BlockList A1, const float* G,
+                                                      int ldg, int cb, OutBlockList O0,
+                                                      OutBlockList O1, int64_t n) {
+  extern __shared__ __attribute__((aligned(16))) float rf[];  // [ca][NT * 32]
+  constexpr int LDF = NT * 32;
+  const int ca = A0.count * A0.width;
+  {
+    // float4 staging, 8 loads in flight per thread (ldg and cb are multiples of 4: checked by
+    // the launcher); columns cb .. LDF-1 zero
+    constexpr int R4 = LDF / 4;
+    const int tot = ca * R4;
+    for (int e0 = threadIdx.x; e0 < tot; e0 += RZ_T * 8) {
+      f32x4 t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = min(e0 + RZ_T * u, tot - 1);
+        const int k = e / R4, j = (e % R4) * 4;
+        t[u] = j < cb ? *reinterpret_cast<const f32x4*>(G + (int64_t)k * ldg + j)
+                      : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = min(e0 + RZ_T * u, tot - 1);
+        *reinterpret_cast<f32x4*>(rf + (e / R4) * LDF + (e % R4) * 4) = t[u];
+      }
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int i = lane & 31, h = lane >> 5;
+  const int64_t ntile = (n + 31) / 32;
+  // wave index made provably uniform (readfirstlane): the tile, the pass and so the block
+  // pointers A.blk[k / 8] are then scalar values (scalar loads), not per-lane loads whose
+  // waits would serialise the k chunk's data loads
+  const int64_t wave0 =
+      (int64_t)blockIdx.x * (RZ_T / 64) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t nwaves = (int64_t)gridDim.x * (RZ_T / 64);
+  const int npass = O1.count > 0 ? 2 : 1;
+  // the B operands of one 8-deep k group: F[kb + 4h + m][t * 32 + i]
+  auto load_b = [&](int kb, float (&dst)[4][NT]) {
+    const float* fr = rf + (kb + 4 * h) * LDF + i;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) dst[m][t] = fr[m * LDF + t * 32];
+  };
+  for (int64_t tile = wave0; tile < ntile * npass; tile += nwaves) {
+    const int pass = (int)(tile / ntile);
+    const BlockList& A = pass ? A1 : A0;
+    const OutBlockList& O = pass ? O1 : O0;
+    const int64_t r0 = (tile % ntile) * 32;
+    const int64_t row = r0 + i;
+    const int64_t lrow = row < n ? row : n - 1;
+    f32x16 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x16{0.f};
+    f32x4 cur[8], nxt[8];
+#pragma unroll
+    for (int s8 = 0; s8 < 8; ++s8) {
+      const int kg = min(8 * s8, ca - 8);
+      cur[s8] = *reinterpret_cast<const f32x4*>(A.blk[kg / 8] + 4 * h + lrow * 8);
+    }
+    float bc[4][NT];
+    load_b(0, bc);
+    for (int k0 = 0; k0 < ca; k0 += 64) {
+      const int kn = min(64, ca - k0);
+      if (k0 + 64 < ca) {
+#pragma unroll
+        for (int s8 = 0; s8 < 8; ++s8) {
+          const int kg = min(k0 + 64 + 8 * s8, ca - 8);
+          nxt[s8] = *reinterpret_cast<const f32x4*>(A.blk[kg / 8] + 4 * h + lrow * 8);
+        }
+      }
+#pragma unroll
+      for (int s8 = 0; s8 < 8; ++s8) {
+        if (8 * s8 >= kn) break;
+        // the next group's LDS reads are issued before this group's 4 NT MFMAs (one wave per
+        // SIMD: nothing else would hide their latency); the sched barriers keep them there
+        float bn[4][NT];
+        load_b(min(k0 + 8 * s8 + 8, ca - 8), bn);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[s8][m], bc[m][t], acc[t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) bc[m][t] = bn[m][t];
+      }
+#pragma unroll
+      for (int s8 = 0; s8 < 8; ++s8) cur[s8] = nxt[s8];
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = t * 32 + i;
+      if (col >= cb) continue;
+      float* ob = O.blk[col / O.width] + (col % O.width);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int64_t rr = r0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (rr < n) ob[rr * (int64_t)O.width] = acc[t][q];
+      }
+    }
+  }
+}
+
+// X = Q S and MX = W S (O1.count == 0: X only); hipErrorNotSupported when the coefficients do
+// not fit one CU's LDS (the caller then uses n2v2r_launch_ts_nn per product)
+extern "C" hipError_t n2v2r_launch_ritz_nn(const BlockList& A0, const BlockList& A1, const float* G,
+                                           int ldg, int cb, const OutBlockList& O0,
+                                           const OutBlockList& O1, int64_t n, int grid,
+                                           hipStream_t stream) {
+  if (A0.width != 8 || O0.width < 1 || cb < 1 || cb > 96 || n < 1) return hipErrorInvalidValue;
+  if (ldg % 4 || cb % 4 || (reinterpret_cast<uintptr_t>(G) & 15)) return hipErrorNotSupported;
+  if (O1.count > 0 && (A1.count != A0.count || A1.width != 8 || O1.width != O0.width))
+    return hipErrorInvalidValue;
+  const int nt = (cb + 31) / 32;
+  const size_t lds = sizeof(float) * (size_t)A0.count * 8 * nt * 32;
+  if (lds > 150 * 1024) return hipErrorNotSupported;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)ritz_nn_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    (void)hipFuncSetAttribute((const void*)ritz_nn_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    (void)hipFuncSetAttribute((const void*)ritz_nn_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    (void)hipGetLastError();
+    attr = true;
+  }
+  const dim3 g((unsigned)(grid > 0 ? grid : 256));
+  switch (nt) {
+    case 1: hipLaunchKernelGGL(ritz_nn_kernel<1>, g, dim3(RZ_T), lds, stream, A0, A1, G, ldg, cb, O0, O1, n); break;
+    case 2: hipLaunchKernelGGL(ritz_nn_kernel<2>, g, dim3(RZ_T), lds, stream, A0, A1, G, ldg, cb, O0, O1, n); break;
+    default: hipLaunchKernelGGL(ritz_nn_kernel<3>, g, dim3(RZ_T), lds, stream, A0, A1, G, ldg, cb, O0, O1, n); break;
+  }
+  return hipGetLastError();
+}
+
 // Narrow outputs (cb <= 16, the Krylov block at b = 8/16): one thread per row, F staged in LDS
 // and read as broadcasts, A rows read as 16-B loads (consecutive lanes read consecutive rows of
 // a block: coalesced).  VALU FMAs; the pass is HBM-bound on A.

@@ -95,6 +95,9 @@ hipError_t n2v2r_launch_cb_fill(const CsrDev& A, int64_t cw, const int64_t* rp, 
 hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n, double* partial,
                               size_t partial_elems, double* out, const int* cond,
                               hipStream_t stream);
+hipError_t n2v2r_launch_ritz_nn(const BlockList& A0, const BlockList& A1, const float* G, int ldg,
+                                int cb, const OutBlockList& O0, const OutBlockList& O1, int64_t n,
+                                int grid, hipStream_t stream);
 hipError_t n2v2r_launch_ts_nn(const BlockList& A, const float* G, int ldg, int cb,
                               const OutBlockList& O, const BlockList& C, float alpha, float beta,
                               int64_t n, const int* cond, const int* flags, uint64_t seed,
@@ -185,6 +188,13 @@ size_t n2v2r_rr_sturm_scratch(int c, int p);
 static bool rr_sturm_enabled() {
   const char* e = std::getenv("N2V2R_RR");
   return !(e && e[0] == 'b');
+}
+
+// Ritz vectors and images by one launch with the coefficients staged once per CU
+// (ritz_nn_kernel) unless N2V2R_RITZ_NN=0.  Read per fit.
+static bool ritz_nn_enabled() {
+  const char* e = std::getenv("N2V2R_RITZ_NN");
+  return !(e && e[0] == '0');
 }
 
 // N2V2R_RESTART_OVERLAP=1: the thick-restart expansion issued on a second stream beside the
@@ -1514,7 +1524,23 @@ struct Eig {
       const double to0 = now_ms();
       lds_poison();
       const int per_launch = std::max(1, 128 / b);  // output blocks per ts_nn launch (<= 128 cols)
-      for (int q0b = 0; q0b < pb; q0b += per_launch) {
+      bool ritz_done = false;
+      if (b == 8 && keep <= 96 && ritz_nn_enabled()) {
+        // both products in one launch, the coefficients staged once per CU
+        OutBlockList ox{}, omx{};
+        ox.width = omx.width = b;
+        ox.count = omx.count = pb;
+        for (int t = 0; t < pb; ++t) {
+          ox.blk[t] = X[t];
+          omx.blk[t] = MX[t];
+        }
+        const hipError_t e = n2v2r_launch_ritz_nn(blocks(Q, 0, nq), blocks(W, 0, nq),
+                                                  h->ews.csmall.as<float>(), keep, keep, ox, omx,
+                                                  n, 0, st);
+        if (e == hipSuccess) ritz_done = true;
+        else if (e != hipErrorNotSupported) throw HipFail{e, "n2v2r_launch_ritz_nn"};
+      }
+      for (int q0b = 0; !ritz_done && q0b < pb; q0b += per_launch) {
         const int nt = std::min(per_launch, pb - q0b);
         OutBlockList ox{}, omx{};
         ox.width = omx.width = b;
