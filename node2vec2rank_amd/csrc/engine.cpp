@@ -46,18 +46,7 @@
 #include "common.h"
 
 // ---- kernel launchers (spmm.hip, dense.hip, rank.hip) ------------------------------------
-#define SPMM_MAX_LAYERS 8
-struct SpmmArgs {
-  CsrDev A[SPMM_MAX_LAYERS];
-  const float* X[SPMM_MAX_LAYERS];
-  float* Y[SPMM_MAX_LAYERS];
-  int64_t ldx;
-  int64_t ldy;
-  int K;
-  int sum;
-  const float* colscale;
-  int split;
-};
+#include "spmm_args.h"
 #define CB_NB 8
 struct CsrBlk {  // spmm.hip: one column block, int32 row pointers relative to base
   const int32_t* rp;

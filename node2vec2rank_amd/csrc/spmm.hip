@@ -18,24 +18,7 @@
 
 #include <cstdlib>
 
-#define SPMM_MAX_LAYERS 8
-#ifndef N2V2R_SPMM_WGS
-#define N2V2R_SPMM_WGS 2048  // workgroups per launch (8 per CU); rows are grid-strided
-#endif
-
-struct SpmmArgs {
-  CsrDev A[SPMM_MAX_LAYERS];
-  const float* X[SPMM_MAX_LAYERS];
-  float* Y[SPMM_MAX_LAYERS];
-  int64_t ldx;
-  int64_t ldy;
-  int K;                 // layers in this launch
-  int sum;               // 1: Y[0] = sum_k A_k X_k ; 0: Y[k] = A_k X_k (grid.y = k)
-  const float* colscale; // optional per-column scale of the output (nullptr = none)
-  int split;             // (b = 8, sum = 0, K <= 8) Y[k] = A_k X_k with grid.y = 1 and the
-                         // layers split over the XCDs: workgroup i runs layer (i mod 8) K / 8,
-                         // so each XCD's L2 holds one layer's panel
-};
+#include "spmm_args.h"
 
 // XCD-split task space: the layer of this workgroup and its index / count among the
 // workgroups of that layer (grid.x a multiple of 8; workgroup i runs on XCD i mod 8)
