@@ -573,6 +573,11 @@ extern "C" hipError_t n2v2r_launch_spmm_cb(const SpmmCbArgs& a, hipStream_t stre
 }
 
 // out[r] = colscale .* sum_{p < nparts} P[p][r] (rows of 8 fp32, fixed part order)
+// out row r = sum_p P[p] row r, p in order (the fixed order keeps results bit-identical to the
+// column-block partials' summation in every form).  NP > 0: all NP loads of a thread issued
+// before the first add (the runtime-count loop waited out one memory round trip per partial:
+// ~1.2 TB/s at N = 1M); NP = 0: any count.
+template <int NP>
 __global__ __launch_bounds__(256) void cb_reduce_kernel(const float* __restrict__ P, int nparts,
                                                         int64_t pstride, int64_t n,
                                                         float* __restrict__ out, int64_t ldo) {
@@ -580,9 +585,19 @@ __global__ __launch_bounds__(256) void cb_reduce_kernel(const float* __restrict_
   if (i >= n * 2) return;
   const int64_t r = i >> 1;
   const int h = (int)(i & 1);
-  f32x4 s = *reinterpret_cast<const f32x4*>(P + r * 8 + h * 4);
-  for (int p = 1; p < nparts; ++p)
-    s += *reinterpret_cast<const f32x4*>(P + p * pstride + r * 8 + h * 4);
+  const float* src = P + r * 8 + h * 4;
+  f32x4 s;
+  if constexpr (NP > 0) {
+    f32x4 v[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) v[p] = *reinterpret_cast<const f32x4*>(src + p * pstride);
+    s = v[0];
+#pragma unroll
+    for (int p = 1; p < NP; ++p) s += v[p];
+  } else {
+    s = *reinterpret_cast<const f32x4*>(src);
+    for (int p = 1; p < nparts; ++p) s += *reinterpret_cast<const f32x4*>(src + p * pstride);
+  }
   *reinterpret_cast<f32x4*>(out + r * ldo + h * 4) = s;
 }
 
@@ -591,8 +606,26 @@ extern "C" hipError_t n2v2r_launch_cb_reduce(const float* P, int nparts, int64_t
                                              hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   const int64_t thr = n * 2;
-  hipLaunchKernelGGL(cb_reduce_kernel, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, stream,
-                     P, nparts, pstride, n, out, ldo);
+  const dim3 g((unsigned)((thr + 255) / 256));
+  // the runtime-count loop by default: the stage-1 reduces run beside the next layer's block
+  // launch, where the unrolled form's burst of loads slowed that launch more than it saved
+  // (cfg4 2353 vs 2205 ms per step); unrolled for the stage-2 sum only: 2209 vs 2206.
+  // N2V2R_CB_REDUCE_UNROLL=1 / 2: always / stage-2 sums (K x 8 partials) only (A/B).
+  static const int unroll_mode = [] {
+    const char* e = getenv("N2V2R_CB_REDUCE_UNROLL");
+    return e ? atoi(e) : 0;
+  }();
+  const bool unrolled = unroll_mode == 1 || (unroll_mode == 2 && nparts >= 16);
+  if (!unrolled)
+    hipLaunchKernelGGL(cb_reduce_kernel<0>, g, dim3(256), 0, stream, P, nparts, pstride, n, out, ldo);
+  else if (nparts == 8)
+    hipLaunchKernelGGL(cb_reduce_kernel<8>, g, dim3(256), 0, stream, P, nparts, pstride, n, out, ldo);
+  else if (nparts == 16)
+    hipLaunchKernelGGL(cb_reduce_kernel<16>, g, dim3(256), 0, stream, P, nparts, pstride, n, out, ldo);
+  else if (nparts == 24)
+    hipLaunchKernelGGL(cb_reduce_kernel<24>, g, dim3(256), 0, stream, P, nparts, pstride, n, out, ldo);
+  else
+    hipLaunchKernelGGL(cb_reduce_kernel<0>, g, dim3(256), 0, stream, P, nparts, pstride, n, out, ldo);
   return hipGetLastError();
 }
 

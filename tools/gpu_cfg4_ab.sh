@@ -1,11 +1,13 @@
-# A/B of one cfg4 fit-and-rank under env settings: AB="ENV=V;ENV=V ENV=V ..." (space-separated
-# sets, ';'-joined assignments)
+# cfg4 A/B of one env switch: AB="VAR=a VAR=b" (each once, steps 2 warmup 1)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out/cfg4ab
-export TMPDIR=/tmp
-rm -f gpurun_out/cfg4ab/sweep.log
-for set in ${AB:-NONE=0}; do
-  echo "== $set" >> gpurun_out/cfg4ab/sweep.log
-  env ${set//;/ } timeout -k 10 200 python -u bench.py --config cfg4 --steps 1 --warmup 0 --no-cpu-baseline >> gpurun_out/cfg4ab/sweep.log 2>> gpurun_out/cfg4ab/err.log || { echo bench-fail; exit 1; }
+O=gpurun_out/cfg4ab
+mkdir -p $O
+for v in $AB; do
+  env $v timeout -k 10 400 python -u bench.py --config cfg4 --steps 2 --warmup 1 --no-cpu-baseline > $O/b.json 2> $O/b.err || { echo "fail $v"; tail -3 $O/b.err; exit 1; }
+  python3 -c "
+import json,sys
+d=json.loads(open('$O/b.json').read().strip().splitlines()[-1])
+print('%-34s %9.1f ms  apps %d' % (sys.argv[1], d['ms_per_step'], d['eig']['block_applications']))
+" "$v"
 done
