@@ -1445,7 +1445,7 @@ struct Eig {
         const std::vector<float*> loc = local_of(Q);
         tn(blocks(loc, 0, (int)loc.size()), one(W.back()),
            h->ews.hband.as<double>() + band_off(nq - 1), nullptr);
-        HIPCHK(hipMemsetAsync(h->ews.rrerr.as<int>(), 0, sizeof(int), st));
+        HIPCHK(hipMemsetAsync(h->ews.rrerr.as<int>(), 0, 4 * sizeof(int), st));
         lds_poison();
         if (sturm_now) {
           const bool spec_fork = spec_ok && !spec_live;
@@ -1553,26 +1553,28 @@ struct Eig {
                                 h->partial.as<double>(), h->partial_elems, h->resid.as<double>(),
                                 st));
       h->allreduce_f64(h->resid.as<double>(), keep);
-      h->ensure_pin(sizeof(double) * 2 * (size_t)keep + 4 * sizeof(int));
+      h->ensure_pin(sizeof(double) * 2 * (size_t)keep + 8 * sizeof(int));
       double* pres = static_cast<double*>(h->pin);
       double* pth = pres + keep;
       int* pflag = reinterpret_cast<int*>(pth + keep);
-      pflag[0] = 0;
-      pflag[1] = 0;
+      for (int q = 0; q < 4; ++q) pflag[q] = 0;
       HIPCHK(hipMemcpyAsync(pres, h->resid.as<double>(), sizeof(double) * keep,
                             hipMemcpyDeviceToHost, st));
       HIPCHK(hipMemcpyAsync(pth, h->theta.as<double>(), sizeof(double) * keep,
                             hipMemcpyDeviceToHost, st));
       if (!dense_rr)
-        HIPCHK(hipMemcpyAsync(pflag, h->ews.rrerr.as<int>(), sizeof(int), hipMemcpyDeviceToHost,
-                              st));
+        HIPCHK(hipMemcpyAsync(pflag + 2, h->ews.rrerr.as<int>(), 2 * sizeof(int),
+                              hipMemcpyDeviceToHost, st));
       if (lazy)
         HIPCHK(hipMemcpyAsync(pflag + 1, h->ews.anyflag.as<int>() + 3, sizeof(int),
                               hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
       std::copy(pres, pres + keep, res2.begin());
       std::copy(pth, pth + keep, wh.begin());
-      if (!dense_rr) rr_err = pflag[0];
+      if (!dense_rr) rr_err = pflag[2];
+      if (trace && !dense_rr && sturm_now)
+        fprintf(stderr, "[n2v2r] cycle %d: %d of %d Ritz vectors took a second solve\n", cycle,
+                pflag[3], keep);
       int refilled = lazy ? pflag[1] : 0;
       t_ortho += now_ms() - to0;
       if (rr_err && !dense_rr && sturm_now) {  // a Sturm vector failed its residual check
@@ -2504,8 +2506,8 @@ int n2v2r_rr_band_top(n2v2r_handle* h, int c, int kp, const double* hband, int64
     tri.ensure(sizeof(double) * 2 * c);
     y.ensure(sizeof(double) * c * p);
     s.ensure(sizeof(float) * c * p);
-    er.ensure(sizeof(int));
-    HIPCHK(hipMemsetAsync(er.p, 0, sizeof(int), h->stream));  // the chase only sets it on failure
+    er.ensure(4 * sizeof(int));
+    HIPCHK(hipMemsetAsync(er.p, 0, 4 * sizeof(int), h->stream));  // the chase only sets it on failure
     HIPCHK(hipMemcpyAsync(hb.p, hband, sizeof(double) * hband_len, hipMemcpyHostToDevice,
                           h->stream));
     if (kp > 0)

@@ -613,7 +613,7 @@ __device__ __forceinline__ void rs_solve(int c, int kp, const double* Xg, const 
 }
 
 __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __restrict__ scr, int c,
-                                                              int kp, int p,
+                                                              int kp, int p, int pw,
                                                               const double* __restrict__ w,
                                                               double clus_rel,
                                                               double* __restrict__ wout,
@@ -695,8 +695,8 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
     // to the neighbouring wanted values (so its components along them are below 1e-7: fp32
     // orthogonality of the Ritz coefficients) skips the second solve
     double gap = 0.0;
-    if (j == j0 && j + 1 < p && j > 0) gap = fmin(w[j - 1] - lam, lam - w[j + 1]);
-    else if (j == j0 && j == 0 && p > 1) gap = lam - w[1];
+    if (j == j0 && j + 1 < pw && j > 0) gap = fmin(w[j - 1] - lam, lam - w[j + 1]);
+    else if (j == j0 && j == 0 && pw > 1) gap = lam - w[1];
     bool ok = true, done = false;
     for (int it = 0; it < 2 && ok; ++it) {
       rs_solve(c, kp, Xg, dX, F, fe, f, y);
@@ -729,7 +729,10 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
       }
     }
     if (stop == 5) { if (lane == 0) err[0] = 1; return; }
-    if (!done) residual();
+    if (!done) {
+      residual();
+      if (lane == 0) atomicAdd(&err[1], 1);  // diagnostics: vectors that took the second solve
+    }
     const double res2 = fmax(r2 - yr * yr, 0.0);
     if (lane == 0) {
       wout[j] = lam + yr;
@@ -785,16 +788,17 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
     return hipErrorInvalidValue;
   const size_t wbis_off = (rs_asm_elems(c, kp) + 7) & ~(size_t)7;
   const int nt_ms = rs_msect_threads();
-  const int M = rs_msect_m(p, nt_ms);
-  const size_t brk_off = wbis_off + (size_t)c, cnt_off = brk_off + 4 * (size_t)p;
-  if (cnt_off + ((2 * (size_t)p * M + 1) / 2) > scr_elems || p > c)
+  const int pm = p;  // eigenvalues bracketed (the wanted ones)
+  const int M = rs_msect_m(pm, nt_ms);
+  const size_t brk_off = wbis_off + (size_t)c, cnt_off = brk_off + 4 * (size_t)pm;
+  if (cnt_off + ((2 * (size_t)pm * M + 1) / 2) > scr_elems || p > c)
     return hipErrorInvalidValue;  // every region inside the scratch
   double* wbis = scr + wbis_off;
   RsMsect ms;
   ms.brk[0] = scr + brk_off;
-  ms.brk[1] = ms.brk[0] + 2 * p;
+  ms.brk[1] = ms.brk[0] + 2 * pm;
   ms.cnt[0] = reinterpret_cast<int*>(scr + cnt_off);
-  ms.cnt[1] = ms.cnt[0] + (size_t)p * M;
+  ms.cnt[1] = ms.cnt[0] + (size_t)pm * M;
   static bool attr = false;
   if (!attr) {  // room for the dynamic LDS checked below (the static arrays stay under 10 KB)
     hipError_t a1 = hipFuncSetAttribute((const void*)rr_sturm_bisect_kernel,
@@ -826,25 +830,25 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
     return v && v[0] == 'w';
   }();
   if (per_wg) {
-    hipLaunchKernelGGL(rr_sturm_bisect_kernel, dim3((unsigned)p), dim3(RS_BIS_THREADS), lbis, stream,
-                       scr, c, kp, p, wbis);
+    hipLaunchKernelGGL(rr_sturm_bisect_kernel, dim3((unsigned)pm), dim3(RS_BIS_THREADS), lbis, stream,
+                       scr, c, kp, pm, wbis);
   } else {
     const size_t lms = sizeof(double) * (asm_d - RS_HDR);
-    const unsigned grid = (unsigned)(p * (M / nt_ms));
+    const unsigned grid = (unsigned)(pm * (M / nt_ms));
     // rounds until the bracket is below 1e-10 ||H|| (3 at p = 80, M = 768; 4 at p = 160, M = 256)
     int rounds = 1;
-    for (double wdt = 2.0 / ((double)p * M + 1.0); wdt > 1e-10; wdt /= (double)(M + 1)) ++rounds;
+    for (double wdt = 2.0 / ((double)pm * M + 1.0); wdt > 1e-10; wdt /= (double)(M + 1)) ++rounds;
     for (int r = 0; r < rounds; ++r) {
       if (nt_ms == 256)
-        hipLaunchKernelGGL(rr_msect_kernel<256>, dim3(grid), dim3(256), lms, stream, scr, c, kp, p,
+        hipLaunchKernelGGL(rr_msect_kernel<256>, dim3(grid), dim3(256), lms, stream, scr, c, kp, pm,
                            M, r, ms);
       else
-        hipLaunchKernelGGL(rr_msect_kernel<512>, dim3(grid), dim3(512), lms, stream, scr, c, kp, p,
+        hipLaunchKernelGGL(rr_msect_kernel<512>, dim3(grid), dim3(512), lms, stream, scr, c, kp, pm,
                            M, r, ms);
       e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(rr_msect_finish_kernel, dim3((unsigned)p), dim3(256), 0, stream, c, p, M,
+    hipLaunchKernelGGL(rr_msect_finish_kernel, dim3((unsigned)pm), dim3(256), 0, stream, c, pm, M,
                        rounds - 1, ms, wbis);
   }
   e = hipGetLastError();
@@ -858,6 +862,6 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
     return v ? atoi(v) : 0;
   }();
   hipLaunchKernelGGL(rr_sturm_inviter_kernel, dim3((unsigned)p), dim3(64), linv, stream, scr, c,
-                     kp, p, wbis, 1e-9, theta, Y, S, ldS, err, inv_stop);
+                     kp, p, pm, wbis, 1e-9, theta, Y, S, ldS, err, inv_stop);
   return hipGetLastError();
 }
