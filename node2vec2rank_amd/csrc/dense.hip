@@ -1396,7 +1396,7 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
                                                         int64_t n, const int* cond, int* flags,
                                                         int* any_flag, double* save, int save_row0,
                                                         int save_rows, int* sticky, uint64_t seed,
-                                                        int64_t row0) {
+                                                        int64_t row0, double* rsave) {
   const int tid = threadIdx.x;
   const bool lead = blockIdx.x == 0;
   if (cond && *cond == 0) {
@@ -1464,6 +1464,9 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
       const double rjc = __shfl(v, jj * 8 + j, 64);
       if (i > jj && j >= i) v -= rjr * rjc;
     }
+    // R (row-major, upper): Z - Q C = Z_out R; its columns' norms give the Krylov-Schur
+    // residual estimates of the lean-image solver mode
+    if (rsave && lead) rsave[tid] = v;
     // Gauss-Jordan on [R | I] from the last row up: x <- R^{-1}
     double x = (i == j) ? 1.0 : 0.0;
 #pragma unroll
@@ -1562,7 +1565,8 @@ extern "C" hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zi
                                              const double* G, int c, int64_t n, const int* cond,
                                              int* flags, int* any_flag, double* save,
                                              int save_row0, int save_rows, int* sticky,
-                                             uint64_t seed, int64_t row0, hipStream_t stream) {
+                                             uint64_t seed, int64_t row0, double* rsave,
+                                             hipStream_t stream) {
   if (Q.width != 8 || c != Q.count * 8) return hipErrorInvalidValue;
   const size_t lds = sizeof(double) * ((size_t)(c + 8) * 8 + 256) + sizeof(float) * ((size_t)c * 8 + 64) + 16;
   if (lds > 64 * 1024) return hipErrorInvalidValue;
@@ -1580,7 +1584,7 @@ extern "C" hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zi
 #define PIP_LAUNCH(QB_, NU_)                                                                   \
   hipLaunchKernelGGL((pip_fused_kernel<QB_, NU_>), dim3(grid ? grid : 1), dim3(256), lds, stream, Q, \
                      Zin, Zout, G, c, n, cond, flags, any_flag, save, save_row0, save_rows, sticky,  \
-                     seed, row0)
+                     seed, row0, rsave)
   if (rows == 256) {
     if (qb == 8) PIP_LAUNCH(8, 2); else PIP_LAUNCH(4, 2);
   } else {

@@ -110,7 +110,8 @@ static bool pip_fused() {
 hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zin, float* Zout,
                                   const double* G, int c, int64_t n, const int* cond, int* flags,
                                   int* any_flag, double* save, int save_row0, int save_rows,
-                                  int* sticky, uint64_t seed, int64_t row0, hipStream_t stream);
+                                  int* sticky, uint64_t seed, int64_t row0, double* rsave,
+                                  hipStream_t stream);
 hipError_t n2v2r_launch_pip_apply(const BlockList& QZ, const float* F, int c, int b,
                                   const OutBlockList& Z, int64_t n, const int* cond,
                                   const int* flags, uint64_t seed, int64_t row0,
@@ -183,6 +184,12 @@ static bool rr_sturm_enabled() {
 // (ritz_nn_kernel) unless N2V2R_RITZ_NN=0.  Read per fit.
 static bool ritz_nn_enabled() {
   const char* e = std::getenv("N2V2R_RITZ_NN");
+  return !(e && e[0] == '0');
+}
+
+// Lean images (banded Sturm Rayleigh-Ritz, one GPU) unless N2V2R_LEAN_W=0.  Read per fit.
+static bool lean_enabled() {
+  const char* e = std::getenv("N2V2R_LEAN_W");
   return !(e && e[0] == '0');
 }
 
@@ -513,6 +520,7 @@ struct EigWorkspace {
   // the restart expansion run beside the Rayleigh-Ritz stage (spec stream): its own Gram
   // partials, Gram and flags, so it shares no scratch with the stage
   DevBuf spec_partial, spec_gsmall, spec_flg, spec_any;
+  DevBuf rres;                                // lean images: R of the restart projection
 };
 }  // namespace
 
@@ -888,6 +896,13 @@ struct Eig {
   bool split2 = false;
   float* pending = nullptr;  // the W block whose value still sits in the partials
   int stats_rr_fallbacks = 0;  // Sturm Rayleigh-Ritz cycles redone by the reducing path
+  // Lean images: only the images a later step reads are kept (the cycle's input and the newest
+  // one), so the basis alone (<= 154 MB at cfg2) stays in the 256 MB Infinity Cache between its
+  // Gram and apply passes.  Residuals are the Krylov-Schur estimates ||R_E s_j|| (R_E: the
+  // triangular factor of the restart block's projection), and a fit is finished only after the
+  // true residuals of its d vectors (their images by SpMM) pass.
+  bool lean_off = false;  // set by the caller to rerun a fit without lean images
+  struct LeanRetry {};
   // Gram scratch of the orthogonalisation passes (the workspace's own, or the spec set while
   // the restart expansion is issued on the spec stream)
   double* part_p = nullptr;
@@ -942,7 +957,9 @@ struct Eig {
     freelist.pop_back();
     return p;
   }
-  void give(float* p) { freelist.push_back(p); }
+  void give(float* p) {
+    if (p) freelist.push_back(p);
+  }
 
   BlockList blocks(const std::vector<float*>& v, int from, int count) const {
     BlockList L{};
@@ -1160,7 +1177,8 @@ struct Eig {
   // refill deficient columns.  `cond` (device int, nullptr = always) skips the pass when zero.
   void pip_pass(float* Z, const std::vector<float*>& basis, const int* cond, int* flags_out,
                 int* any_out, const float* Zin = nullptr, double* save = nullptr,
-                int save_row0 = 0, int save_rows = 0, int* sticky = nullptr) {
+                int save_row0 = 0, int save_rows = 0, int* sticky = nullptr,
+                double* rsave = nullptr) {
     // Zin (default Z): the block to orthogonalise; the result is written to Z
     const float* zin = Zin ? Zin : Z;
     const int nq = (int)basis.size();
@@ -1189,9 +1207,11 @@ struct Eig {
       // b = 8: the Cholesky step runs inside the apply launch (every workgroup factors G)
       HIPCHK(n2v2r_launch_pip_fused(blocks(qz, 0, nq), zin, Z, gsm_p, nq * b,
                                     n, cond, flags_out, any_out, save, save_row0, save_rows,
-                                    sticky, seed ^ (0xABCDull + ++fill_counter), row0, st));
+                                    sticky, seed ^ (0xABCDull + ++fill_counter), row0, rsave,
+                                    st));
       return;
     }
+    if (rsave) throw StatusFail{N2V2R_ERR_INTERNAL, "R output needs the fused PIP pass"};
     HIPCHK(n2v2r_launch_pip_chol(gsm_p, nq * b, b, h->ews.rinv.as<double>(),
                                  flags_out, any_out, cond, save, save_row0, save_rows,
                                  h->ews.fcoef.as<float>(), sticky, st));
@@ -1211,9 +1231,10 @@ struct Eig {
   // lazy: no third pass; a refill in the second pass sets the cycle's sticky flag instead and
   // the cycle is expanded again with the third pass (rank deficiency after a local + full pass
   // is rare: it saves four launches per block).
+  // rsave_first: R of the first pass (lean images: its column norms are the residual estimates)
   void orthonormalize(float* Z, const std::vector<float*>& basis, const float* Zin = nullptr,
                       const std::vector<float*>* local = nullptr, double* save = nullptr,
-                      bool lazy = false) {
+                      bool lazy = false, double* rsave_first = nullptr) {
     const double t0 = now_ms();
     lds_poison();
     int* flg = flg_p;
@@ -1222,7 +1243,7 @@ struct Eig {
     const std::vector<float*>& first = loc ? *local : basis;
     const int nsave = (save && local) ? (int)local->size() : 0;
     pip_pass(Z, first, nullptr, flg, any, Zin, nsave ? save : nullptr,
-             ((int)first.size() - nsave) * b, nsave * b);
+             ((int)first.size() - nsave) * b, nsave * b, nullptr, rsave_first);
     pip_pass(Z, basis, nullptr, flg + 64, any + 1, nullptr, nullptr, 0, 0,
              lazy ? any + 3 : nullptr);
     if (!lazy) pip_pass(Z, basis, any + 1, flg + 128, any + 2);
@@ -1369,7 +1390,12 @@ struct Eig {
     // the restart expansion (orth(W_last) against the old basis, then its SpMM) needs nothing
     // from the Rayleigh-Ritz stage: issue it on the spec stream beside the stage (one GPU,
     // banded Rayleigh-Ritz; N2V2R_RESTART_OVERLAP=0 keeps it in line)
-    const bool spec_ok = band_rr && !h->comm && restart_overlap_enabled();
+    const bool lean =
+        b == 8 && pip_fused() && band_rr && sturm && !h->comm && !lean_off && lean_enabled();
+    if (lean) h->ews.rres.ensure(sizeof(double) * 64);
+    double est_scale = 1.0;  // lean: true / estimated residual seen at a failed final check
+    int lean_checks = 0;
+    const bool spec_ok = band_rr && !h->comm && !lean && restart_overlap_enabled();
     if (spec_ok) {
       h->ews.spec_partial.ensure(sizeof(double) * h->partial_elems);
       h->ews.spec_gsmall.ensure(sizeof(double) * (size_t)c_max * c_max);
@@ -1416,13 +1442,18 @@ struct Eig {
       while ((int)Q.size() < nb_max) {
         expand_one(W.back(), Q, Q, W, /*save_band=*/true, lazy);
         ++apps;
+        if (lean && (int)W.size() - 2 > q_start - 1) {  // consumed; the cycle's input stays
+          give(W[W.size() - 2]);
+          W[W.size() - 2] = nullptr;
+        }
       }
       const int nq = (int)Q.size();
       const int c = nq * b;
       for (int q = 0; q < pb; ++q) {
         X[q] = take();
-        MX[q] = take();
+        MX[q] = lean ? nullptr : take();
       }
+      float* E_lean = nullptr;  // lean: the restart block, built before the convergence test
       bool dense_rr = !band_rr;
       bool sturm_now = sturm;  // this cycle's banded form (the reducing one after a failure)
       int rr_err = 0;
@@ -1523,7 +1554,8 @@ struct Eig {
           ox.blk[t] = X[t];
           omx.blk[t] = MX[t];
         }
-        const hipError_t e = n2v2r_launch_ritz_nn(blocks(Q, 0, nq), blocks(W, 0, nq),
+        if (lean) omx.count = 0;  // X only
+        const hipError_t e = n2v2r_launch_ritz_nn(blocks(Q, 0, nq), lean ? one(nullptr) : blocks(W, 0, nq),
                                                   h->ews.csmall.as<float>(), keep, keep, ox, omx,
                                                   n, 0, st);
         if (e == hipSuccess) ritz_done = true;
@@ -1542,24 +1574,42 @@ struct Eig {
         const float* g = h->ews.csmall.as<float>() + q0b * b;
         HIPCHK(n2v2r_launch_ts_nn(blocks(Q, 0, nq), g, keep, nt * b, ox, one(nullptr), 1.f, 0.f, n,
                                   nullptr, nullptr, 0, st));
-        HIPCHK(n2v2r_launch_ts_nn(blocks(W, 0, nq), g, keep, nt * b, omx, one(nullptr), 1.f, 0.f,
-                                  n, nullptr, nullptr, 0, st));
+        if (!lean)
+          HIPCHK(n2v2r_launch_ts_nn(blocks(W, 0, nq), g, keep, nt * b, omx, one(nullptr), 1.f, 0.f,
+                                    n, nullptr, nullptr, 0, st));
       }
       for (int q = 0; q < pb; ++q) {
         dbg(X[q], n * b, false, "Ritz vectors X = Q S");
-        dbg(MX[q], n * b, false, "Ritz images MX = W S");
+        if (!lean) dbg(MX[q], n * b, false, "Ritz images MX = W S");
       }
-      HIPCHK(n2v2r_launch_resid(blocks(X, 0, pb), blocks(MX, 0, pb), h->theta.as<double>(), n,
-                                h->partial.as<double>(), h->partial_elems, h->resid.as<double>(),
-                                st));
-      h->allreduce_f64(h->resid.as<double>(), keep);
-      h->ensure_pin(sizeof(double) * 2 * (size_t)keep + 8 * sizeof(int));
+      if (lean) {
+        // the restart block now (it needs nothing from the Rayleigh-Ritz stage): its first,
+        // local pass leaves R with W_last - Q_loc C = Z_{m+1} R, Z_{m+1} orthonormal
+        E_lean = take();
+        const std::vector<float*> loc = local_of(Q);
+        orthonormalize(E_lean, Q, W.back(), &loc, nullptr, false, h->ews.rres.as<double>());
+      } else {
+        HIPCHK(n2v2r_launch_resid(blocks(X, 0, pb), blocks(MX, 0, pb), h->theta.as<double>(), n,
+                                  h->partial.as<double>(), h->partial_elems,
+                                  h->resid.as<double>(), st));
+        h->allreduce_f64(h->resid.as<double>(), keep);
+      }
+      h->ensure_pin(sizeof(double) * 2 * (size_t)keep + 8 * sizeof(int) + sizeof(double) * 64 +
+                    sizeof(float) * 8 * (size_t)keep);
       double* pres = static_cast<double*>(h->pin);
       double* pth = pres + keep;
       int* pflag = reinterpret_cast<int*>(pth + keep);
+      double* prr = reinterpret_cast<double*>(pflag + 8);   // lean: R (8 x 8)
+      float* psl = reinterpret_cast<float*>(prr + 64);      // lean: last 8 rows of S
       for (int q = 0; q < 4; ++q) pflag[q] = 0;
-      HIPCHK(hipMemcpyAsync(pres, h->resid.as<double>(), sizeof(double) * keep,
-                            hipMemcpyDeviceToHost, st));
+      if (lean) {
+        HIPCHK(hipMemcpyAsync(prr, h->ews.rres.p, sizeof(double) * 64, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(psl, h->ews.csmall.as<float>() + (size_t)(c - b) * keep,
+                              sizeof(float) * 8 * (size_t)keep, hipMemcpyDeviceToHost, st));
+      } else {
+        HIPCHK(hipMemcpyAsync(pres, h->resid.as<double>(), sizeof(double) * keep,
+                              hipMemcpyDeviceToHost, st));
+      }
       HIPCHK(hipMemcpyAsync(pth, h->theta.as<double>(), sizeof(double) * keep,
                             hipMemcpyDeviceToHost, st));
       if (!dense_rr)
@@ -1569,7 +1619,19 @@ struct Eig {
         HIPCHK(hipMemcpyAsync(pflag + 1, h->ews.anyflag.as<int>() + 3, sizeof(int),
                               hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
-      std::copy(pres, pres + keep, res2.begin());
+      if (lean) {  // ||M x_j - theta_j x_j||^2 = ||R s_j(last block)||^2 (Krylov-Schur), scaled
+        for (int j = 0; j < keep; ++j) {
+          double acc = 0.0;
+          for (int r = 0; r < 8; ++r) {
+            double v = 0.0;
+            for (int cc = r; cc < 8; ++cc) v += prr[r * 8 + cc] * (double)psl[cc * keep + j];
+            acc += v * v;
+          }
+          res2[j] = acc * est_scale * est_scale;
+        }
+      } else {
+        std::copy(pres, pres + keep, res2.begin());
+      }
       std::copy(pth, pth + keep, wh.begin());
       if (!dense_rr) rr_err = pflag[2];
       if (trace && !dense_rr && sturm_now)
@@ -1588,6 +1650,7 @@ struct Eig {
         ++stats_rr_fallbacks;
         goto rayleigh_ritz;
       }
+      if (rr_err && !dense_rr && lean) throw LeanRetry{};  // dense H needs every image
       if (rr_err && !dense_rr) {  // the bulge chase gave up (should not happen): dense RR
         if (trace) fprintf(stderr, "[n2v2r] banded Rayleigh-Ritz failed, dense fallback\n");
         dense_rr = true;
@@ -1619,6 +1682,7 @@ struct Eig {
         if (trace) fprintf(stderr, "[n2v2r] rank-deficient block, cycle %d expanded again\n", cycle);
         for (float* p : specE) give(p);
         for (float* p : specEW) give(p);
+        give(E_lean);
         for (int q = 0; q < pb; ++q) {
           give(X[q]);
           give(MX[q]);
@@ -1669,14 +1733,63 @@ struct Eig {
           }
         }
       }
+      if (lean && done) {
+        // lean images: the estimates say stop; the true residuals of the d wanted vectors
+        // (their images by SpMM) decide
+        ++lean_checks;
+        const int qd = (d + b - 1) / b;
+        std::vector<float*> MV(qd);
+        for (int q = 0; q < qd; ++q) {
+          MV[q] = take();
+          apply_M(X[q], MV[q]);
+          materialize();
+        }
+        HIPCHK(n2v2r_launch_resid(blocks(X, 0, qd), blocks(MV, 0, qd), h->theta.as<double>(), n,
+                                  h->partial.as<double>(), h->partial_elems,
+                                  h->resid.as<double>(), st));
+        HIPCHK(hipMemcpyAsync(pres, h->resid.as<double>(), sizeof(double) * qd * b,
+                              hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        for (float* p : MV) give(p);
+        double worst = 0.0, ratio = 1.0;
+        int tconv = 0;
+        for (int j = 0; j < d; ++j) {
+          const double r = std::sqrt(std::max(pres[j], 0.0)) / th1;
+          const double e = std::sqrt(std::max(res2[j], 0.0)) / th1;
+          worst = std::max(worst, r);
+          if (r <= tol) ++tconv;
+          if (e > 0.0) ratio = std::max(ratio, r / e);
+        }
+        if (trace)
+          fprintf(stderr, "[n2v2r] cycle %d: true max_res %.3e converged %d/%d (estimate %.3e)\n",
+                  cycle, worst, tconv, d, maxres);
+        maxres = worst;
+        conv = tconv;
+        stagnated = 0;
+        if (conv < d && cycle + 1 < max_restarts) {
+          // at the fp32 floor the true residual stops falling: finish within 100x tol
+          if (lean_checks >= 4 && worst <= 100.0 * tol) {
+            stagnated = 1;
+          } else {
+            done = false;
+            est_scale *= 1.25 * ratio;  // the estimates trail the true residual: demand more
+            hist_res.clear();
+          }
+        }
+      }
       if (done) {
         for (float* p : specE) give(p);
         for (float* p : specEW) give(p);
+        give(E_lean);
         break;
       }
       // restart: [X | orth(W_last) against the old basis] (thick restart)
       std::vector<float*> E, EW;
-      if (spec_live) {
+      if (lean) {
+        E.push_back(E_lean);
+        EW.push_back(take());
+        apply_M(E_lean, EW[0]);
+      } else if (spec_live) {
         E = specE;
         EW = specEW;
         pending = spec_pending;
@@ -2045,20 +2158,32 @@ int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_sta
     n2v2r_eig_opts o{};
     if (opts) o = *opts;
     if (stats) memset(stats, 0, sizeof(*stats));
-    Eig eig{};
-    eig.h = h;
-    eig.st = h->stream;
-    eig.n = h->nloc;
-    eig.npad = h->npad;
-    eig.row0 = h->row0;
-    eig.K = h->K;
-    eig.stats = stats;
     const int ldu = ((d + 63) / 64) * 64;  // a multiple of every block width
     h->U.ensure(sizeof(float) * h->npad * ldu);
     HIPCHK(hipMemsetAsync(h->U.p, 0, sizeof(float) * h->npad * ldu, h->stream));
     std::vector<double> theta;
-    const int st = eig.run(d, o, theta, h->U.as<float>(), ldu);
-    const int b = eig.b;
+    int st = 0, b = 0;
+    for (int attempt = 0;; ++attempt) {
+      Eig eig{};
+      eig.h = h;
+      eig.st = h->stream;
+      eig.n = h->nloc;
+      eig.npad = h->npad;
+      eig.row0 = h->row0;
+      eig.K = h->K;
+      eig.stats = stats;
+      eig.lean_off = attempt > 0;
+      try {
+        st = eig.run(d, o, theta, h->U.as<float>(), ldu);
+      } catch (const Eig::LeanRetry&) {
+        // lean images cannot take the dense Rayleigh-Ritz fallback: the fit again with images
+        fprintf(stderr, "[n2v2r] banded Rayleigh-Ritz failed under lean images; fit rerun\n");
+        HIPCHK(hipStreamSynchronize(h->stream));
+        continue;
+      }
+      b = eig.b;
+      break;
+    }
     // deterministic signs: largest-magnitude entry of every column of U positive
     h->keys.ensure(sizeof(unsigned long long) * 1024 * (size_t)ldu);
     h->best.ensure(sizeof(unsigned long long) * ldu);
