@@ -1396,7 +1396,8 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
                                                         int64_t n, const int* cond, int* flags,
                                                         int* any_flag, double* save, int save_row0,
                                                         int save_rows, int* sticky, uint64_t seed,
-                                                        int64_t row0, double* rsave) {
+                                                        int64_t row0, double* rsave, float skip_tol,
+                                                        int* skipped) {
   const int tid = threadIdx.x;
   const bool lead = blockIdx.x == 0;
   if (cond && *cond == 0) {
@@ -1424,6 +1425,56 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
       reinterpret_cast<double2*>(gd)[min(e0 + 256 * u, ne2 - 1)] = t[u];
   }
   __syncthreads();
+  // the basis blocks this pass applies: all, or (skip_tol > 0: selective reorthogonalisation of
+  // an in-place pass) those with max_ij |C_ij| / ||z_j|| > skip_tol; every workgroup decides
+  // alike from the same G.  Skipped blocks' C rows are zeroed so R factors the applied pass.
+  // (skip_tol < 0: the whole pass, all blocks or none, by |skip_tol|)
+  int* blist = badw + 4;  // compact list of applied blocks (<= 64)
+  const int nblk = c >> 3;
+  const bool skip_whole = skip_tol < 0.f;
+  skip_tol = fabsf(skip_tol);
+  if (tid < 64) {
+    bool on = tid < nblk;
+    if (on && skip_tol > 0.f) {
+      double cm = 0.0;
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const double g = gd[(tid * 8 + r) * 8 + j];
+          cm = fmax(cm, g * g / fmax(gd[(c + j) * 8 + j], 1e-300));
+        }
+      on = cm > (double)skip_tol * (double)skip_tol;
+    }
+    unsigned long long m = __ballot(on);
+    if (skip_whole && m) {
+      m = nblk == 64 ? ~0ull : ((1ull << nblk) - 1ull);
+      on = tid < nblk;
+    }
+    if (on) blist[__popcll(m & ((1ull << tid) - 1ull))] = tid;
+    if (tid == 0) {
+      badw[1] = (int)__popcll(m);
+      badw[2] = (int)(unsigned)(m & 0xFFFFFFFFull);
+      badw[3] = (int)(unsigned)(m >> 32);
+    }
+  }
+  __syncthreads();
+  const int napply = badw[1];
+  if (skip_tol > 0.f) {
+    if (napply == 0) {
+      if (lead && tid < 8) flags[tid] = 0;
+      if (lead && tid == 0) {
+        *any_flag = 0;
+        if (skipped) atomicAdd(skipped, 1);
+      }
+      return;
+    }
+    const unsigned long long m =
+        ((unsigned long long)(unsigned)badw[3] << 32) | (unsigned long long)(unsigned)badw[2];
+    for (int e = tid; e < c * 8; e += 256)
+      if (!((m >> (e >> 6)) & 1ull)) gd[e] = 0.0;
+    __syncthreads();
+  }
   if (save && lead)
     for (int e = tid; e < save_rows * 8; e += 256) save[e] = gd[save_row0 * 8 + e];
   for (int e = tid; e < c * 8; e += 256) cf[e] = (float)gd[e];
@@ -1507,16 +1558,19 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
     }
   }
   int q = 0;
-  for (; q + QB <= Q.count; q += QB) {  // QB blocks x NU rows (QB NU x 16-B loads) in flight
+  for (; q + QB <= napply; q += QB) {  // QB blocks x NU rows (QB NU x 16-B loads) in flight
     f32x4 a4[QB][2];
+    int bi[QB];
+#pragma unroll
+    for (int b4 = 0; b4 < QB; ++b4) bi[b4] = __builtin_amdgcn_readfirstlane(blist[q + b4]);
 #pragma unroll
     for (int b4 = 0; b4 < QB; ++b4)
 #pragma unroll
       for (int u = 0; u < NU; ++u)
-        a4[b4][u] = *reinterpret_cast<const f32x4*>(Q.blk[q + b4] + rw[u] * 8 + 4 * h);
+        a4[b4][u] = *reinterpret_cast<const f32x4*>(Q.blk[bi[b4]] + rw[u] * 8 + 4 * h);
 #pragma unroll
     for (int b4 = 0; b4 < QB; ++b4) {
-      const float* g = cf + ((q + b4) * 8 + 4 * h) * 8;
+      const float* g = cf + (bi[b4] * 8 + 4 * h) * 8;
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -1527,11 +1581,12 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
         }
     }
   }
-  for (; q < Q.count; ++q) {
+  for (; q < napply; ++q) {
     f32x4 a4[2];
+    const int bq = __builtin_amdgcn_readfirstlane(blist[q]);
 #pragma unroll
-    for (int u = 0; u < NU; ++u) a4[u] = *reinterpret_cast<const f32x4*>(Q.blk[q] + rw[u] * 8 + 4 * h);
-    const float* g = cf + (q * 8 + 4 * h) * 8;
+    for (int u = 0; u < NU; ++u) a4[u] = *reinterpret_cast<const f32x4*>(Q.blk[bq] + rw[u] * 8 + 4 * h);
+    const float* g = cf + (bq * 8 + 4 * h) * 8;
 #pragma unroll
     for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -1566,10 +1621,12 @@ extern "C" hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zi
                                              int* flags, int* any_flag, double* save,
                                              int save_row0, int save_rows, int* sticky,
                                              uint64_t seed, int64_t row0, double* rsave,
-                                             hipStream_t stream) {
+                                             float skip_tol, int* skipped, hipStream_t stream) {
   if (Q.width != 8 || c != Q.count * 8) return hipErrorInvalidValue;
-  const size_t lds = sizeof(double) * ((size_t)(c + 8) * 8 + 256) + sizeof(float) * ((size_t)c * 8 + 64) + 16;
-  if (lds > 64 * 1024) return hipErrorInvalidValue;
+  // a skipped block leaves Z in place; the band save reads G before the skipped rows are zeroed
+  if (skip_tol != 0.f && (Zin != Zout || save)) return hipErrorInvalidValue;
+  const size_t lds = sizeof(double) * ((size_t)(c + 8) * 8 + 256) + sizeof(float) * ((size_t)c * 8 + 64) + 16 + 256;
+  if (lds > 64 * 1024 || c > 512) return hipErrorInvalidValue;
   static const int qb = [] {
     const char* s = getenv("N2V2R_PIP_QB");
     return s ? atoi(s) : 4;
@@ -1584,7 +1641,7 @@ extern "C" hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zi
 #define PIP_LAUNCH(QB_, NU_)                                                                   \
   hipLaunchKernelGGL((pip_fused_kernel<QB_, NU_>), dim3(grid ? grid : 1), dim3(256), lds, stream, Q, \
                      Zin, Zout, G, c, n, cond, flags, any_flag, save, save_row0, save_rows, sticky,  \
-                     seed, row0, rsave)
+                     seed, row0, rsave, skip_tol, skipped)
   if (rows == 256) {
     if (qb == 8) PIP_LAUNCH(8, 2); else PIP_LAUNCH(4, 2);
   } else {

@@ -111,7 +111,7 @@ hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zin, float* Z
                                   const double* G, int c, int64_t n, const int* cond, int* flags,
                                   int* any_flag, double* save, int save_row0, int save_rows,
                                   int* sticky, uint64_t seed, int64_t row0, double* rsave,
-                                  hipStream_t stream);
+                                  float skip_tol, int* skipped, hipStream_t stream);
 hipError_t n2v2r_launch_pip_apply(const BlockList& QZ, const float* F, int c, int b,
                                   const OutBlockList& Z, int64_t n, const int* cond,
                                   const int* flags, uint64_t seed, int64_t row0,
@@ -521,6 +521,7 @@ struct EigWorkspace {
   // partials, Gram and flags, so it shares no scratch with the stage
   DevBuf spec_partial, spec_gsmall, spec_flg, spec_any;
   DevBuf rres;                                // lean images: R of the restart projection
+  DevBuf skipc;                               // full passes skipped (selective reorthogonalisation)
 };
 }  // namespace
 
@@ -902,6 +903,9 @@ struct Eig {
   // triangular factor of the restart block's projection), and a fit is finished only after the
   // true residuals of its d vectors (their images by SpMM) pass.
   bool lean_off = false;  // set by the caller to rerun a fit without lean images
+  // selective reorthogonalisation: a full pass after the local one is skipped (in the fused
+  // launch, by every workgroup alike) when max |Q^T z_j| <= reorth_tol ||z_j||
+  float reorth_tol = 0.f;
   struct LeanRetry {};
   // Gram scratch of the orthogonalisation passes (the workspace's own, or the spec set while
   // the restart expansion is issued on the spec stream)
@@ -1178,7 +1182,7 @@ struct Eig {
   void pip_pass(float* Z, const std::vector<float*>& basis, const int* cond, int* flags_out,
                 int* any_out, const float* Zin = nullptr, double* save = nullptr,
                 int save_row0 = 0, int save_rows = 0, int* sticky = nullptr,
-                double* rsave = nullptr) {
+                double* rsave = nullptr, float skip_tol = 0.f) {
     // Zin (default Z): the block to orthogonalise; the result is written to Z
     const float* zin = Zin ? Zin : Z;
     const int nq = (int)basis.size();
@@ -1208,10 +1212,12 @@ struct Eig {
       HIPCHK(n2v2r_launch_pip_fused(blocks(qz, 0, nq), zin, Z, gsm_p, nq * b,
                                     n, cond, flags_out, any_out, save, save_row0, save_rows,
                                     sticky, seed ^ (0xABCDull + ++fill_counter), row0, rsave,
+                                    skip_tol, skip_tol != 0.f ? h->ews.skipc.as<int>() : nullptr,
                                     st));
       return;
     }
     if (rsave) throw StatusFail{N2V2R_ERR_INTERNAL, "R output needs the fused PIP pass"};
+    // (skip_tol: the unfused pass always applies)
     HIPCHK(n2v2r_launch_pip_chol(gsm_p, nq * b, b, h->ews.rinv.as<double>(),
                                  flags_out, any_out, cond, save, save_row0, save_rows,
                                  h->ews.fcoef.as<float>(), sticky, st));
@@ -1245,7 +1251,7 @@ struct Eig {
     pip_pass(Z, first, nullptr, flg, any, Zin, nsave ? save : nullptr,
              ((int)first.size() - nsave) * b, nsave * b, nullptr, rsave_first);
     pip_pass(Z, basis, nullptr, flg + 64, any + 1, nullptr, nullptr, 0, 0,
-             lazy ? any + 3 : nullptr);
+             lazy ? any + 3 : nullptr, nullptr, loc ? reorth_tol : 0.f);
     if (!lazy) pip_pass(Z, basis, any + 1, flg + 128, any + 2);
     t_ortho += now_ms() - t0;
   }
@@ -1392,6 +1398,19 @@ struct Eig {
     // banded Rayleigh-Ritz; N2V2R_RESTART_OVERLAP=0 keeps it in line)
     const bool lean =
         b == 8 && pip_fused() && band_rr && sturm && !h->comm && !lean_off && lean_enabled();
+    {
+      // default: a tenth of the residual tolerance.  The residuals stall near the level of
+      // orthogonality left in the basis (~1.5x it in cfg2 sweeps: 2e-6 stalls at 3e-6); at
+      // 1e-7 .. 2.5e-7 cfg2 keeps its residuals and gains alike (most passes then touch only the
+      // few blocks, the kept Ritz vectors, that lost orthogonality).  N2V2R_REORTH_TOL=0: every
+      // block of every full pass.
+      const char* e = std::getenv("N2V2R_REORTH_TOL");
+      reorth_tol = e ? (float)std::atof(e) : (float)(0.1 * tol);
+      const char* m = std::getenv("N2V2R_REORTH_MODE");  // "whole": all blocks or none
+      if (m && m[0] == 'w') reorth_tol = -reorth_tol;
+    }
+    h->ews.skipc.ensure(sizeof(int) * 4);
+    HIPCHK(hipMemsetAsync(h->ews.skipc.p, 0, sizeof(int) * 4, st));
     if (lean) h->ews.rres.ensure(sizeof(double) * 64);
     double est_scale = 1.0;  // lean: true / estimated residual seen at a failed final check
     int lean_checks = 0;
@@ -1806,6 +1825,13 @@ struct Eig {
       kry0 = pb;
     }
     materialize();
+    if (trace && reorth_tol != 0.f) {
+      int sk = 0;
+      HIPCHK(hipMemcpyAsync(&sk, h->ews.skipc.p, sizeof(int), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      fprintf(stderr, "[n2v2r] %d full reorthogonalisation passes skipped (tol %.1e)\n", sk,
+              (double)reorth_tol);
+    }
     // U = first d columns of X (row stride ldu); theta
     theta_out.assign(wh.begin(), wh.begin() + d);
     for (int q = 0; q * b < d; ++q) {
