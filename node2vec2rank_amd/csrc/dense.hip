@@ -1433,25 +1433,29 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
   const int nblk = c >> 3;
   const bool skip_whole = skip_tol < 0.f;
   skip_tol = fabsf(skip_tol);
+  int* bflag = reinterpret_cast<int*>(part);  // per-block verdicts (part is free until C^T C)
+  if (skip_tol > 0.f) {
+    // wave w tests blocks w, w + 4, ...: lane = entry (r, j) of the block's 8 x 8 C rows
+    const int lane = tid & 63;
+    const double thr = (double)skip_tol * (double)skip_tol *
+                       fmax(gd[(c + (lane & 7)) * 8 + (lane & 7)], 1e-300);
+    for (int bk = tid >> 6; bk < nblk; bk += 4) {
+      const double g = gd[bk * 64 + lane];
+      const unsigned long long bm = __ballot(g * g > thr);
+      if (lane == 0) bflag[bk] = bm != 0ull;
+    }
+    __syncthreads();
+  }
   if (tid < 64) {
     bool on = tid < nblk;
-    if (on && skip_tol > 0.f) {
-      double cm = 0.0;
-#pragma unroll
-      for (int r = 0; r < 8; ++r)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const double g = gd[(tid * 8 + r) * 8 + j];
-          cm = fmax(cm, g * g / fmax(gd[(c + j) * 8 + j], 1e-300));
-        }
-      on = cm > (double)skip_tol * (double)skip_tol;
-    }
+    if (on && skip_tol > 0.f) on = bflag[tid] != 0;
     unsigned long long m = __ballot(on);
     if (skip_whole && m) {
       m = nblk == 64 ? ~0ull : ((1ull << nblk) - 1ull);
       on = tid < nblk;
     }
     if (on) blist[__popcll(m & ((1ull << tid) - 1ull))] = tid;
+    if (skipped && lead && on && skip_tol > 0.f) atomicAdd(skipped + 1 + tid, 1);  // histogram
     if (tid == 0) {
       badw[1] = (int)__popcll(m);
       badw[2] = (int)(unsigned)(m & 0xFFFFFFFFull);

@@ -1409,8 +1409,8 @@ struct Eig {
       const char* m = std::getenv("N2V2R_REORTH_MODE");  // "whole": all blocks or none
       if (m && m[0] == 'w') reorth_tol = -reorth_tol;
     }
-    h->ews.skipc.ensure(sizeof(int) * 4);
-    HIPCHK(hipMemsetAsync(h->ews.skipc.p, 0, sizeof(int) * 4, st));
+    h->ews.skipc.ensure(sizeof(int) * 68);
+    HIPCHK(hipMemsetAsync(h->ews.skipc.p, 0, sizeof(int) * 68, st));
     if (lean) h->ews.rres.ensure(sizeof(double) * 64);
     double est_scale = 1.0;  // lean: true / estimated residual seen at a failed final check
     int lean_checks = 0;
@@ -1826,11 +1826,13 @@ struct Eig {
     }
     materialize();
     if (trace && reorth_tol != 0.f) {
-      int sk = 0;
-      HIPCHK(hipMemcpyAsync(&sk, h->ews.skipc.p, sizeof(int), hipMemcpyDeviceToHost, st));
+      int sk[65] = {};
+      HIPCHK(hipMemcpyAsync(sk, h->ews.skipc.p, sizeof(int) * 65, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
-      fprintf(stderr, "[n2v2r] %d full reorthogonalisation passes skipped (tol %.1e)\n", sk,
-              (double)reorth_tol);
+      fprintf(stderr, "[n2v2r] %d full reorthogonalisation passes skipped (tol %.1e); applied "
+              "per basis block:", sk[0], (double)reorth_tol);
+      for (int q = 0; q < 64; ++q) fprintf(stderr, " %d", sk[1 + q]);
+      fprintf(stderr, "\n");
     }
     // U = first d columns of X (row stride ldu); theta
     theta_out.assign(wh.begin(), wh.begin() + d);
