@@ -1251,7 +1251,7 @@ struct Eig {
     pip_pass(Z, first, nullptr, flg, any, Zin, nsave ? save : nullptr,
              ((int)first.size() - nsave) * b, nsave * b, nullptr, rsave_first);
     pip_pass(Z, basis, nullptr, flg + 64, any + 1, nullptr, nullptr, 0, 0,
-             lazy ? any + 3 : nullptr, nullptr, loc ? reorth_tol : 0.f);
+             lazy ? any + 3 : nullptr, nullptr, reorth_tol);
     if (!lazy) pip_pass(Z, basis, any + 1, flg + 128, any + 2);
     t_ortho += now_ms() - t0;
   }

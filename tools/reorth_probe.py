@@ -19,11 +19,12 @@ cfg = bench.CONFIGS[cfg_name]
 eng = _lib.Engine(0)
 eng.set_layers(synthetic.er_layers(cfg["n"], cfg["avg_deg"], 2, seed_base=1000))
 d = cfg["d"]
+flags = int(os.environ.get("PROBE_FLAGS", "0"))
 base = None
 for t in tols:
     os.environ["N2V2R_REORTH_TOL"] = t
     try:
-        eng.uase(d, seed=42)  # warm
+        eng.uase(d, seed=42, solver_flags=flags)  # warm
     except _lib.ArpackNoConvergence as e:
         print(f"tol {t:>6s}: {e}", flush=True)
         continue
@@ -31,7 +32,7 @@ for t in tols:
     t0 = time.perf_counter()
     reps = 3
     for _ in range(reps):
-        st = eng.uase(d, seed=42)
+        st = eng.uase(d, seed=42, solver_flags=flags)
     eng.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / reps
     s = eng.singular_values().astype(np.float64)
