@@ -586,6 +586,108 @@ __device__ __forceinline__ void rs_band_solve_lane(int c, int kp, const double* 
 }
 #undef RS_SG
 
+// The same two solves with the chains spread over lanes q = lane & 7 (every lane runs them; lanes
+// 0..7 carry the values).  Forward (right-looking): lane q holds r_q, the pending right-hand
+// side of row k + q; per row z_k = r_0 is broadcast (readlane), the window shifts one lane
+// (DPP row_shl:1) and each lane applies its own multiplier t_{k,q+1}: one FMA per row on the
+// chain instead of lane 0's eight.  Backward (column form): lane j holds the partial sum of
+// row k - j, y_k = z_k / d_k - acc_0 is broadcast, and every pending row adds t y_k in one FMA.
+// Coefficients are read RS_PF rows ahead.  Same products as rs_band_solve_lane, summed in a
+// different order (rounding differs at the 1e-16 level).
+__device__ __forceinline__ double rs_dpp_shl1(double v) {  // lane l <- lane l + 1 (16-lane rows)
+  // (lanes at a row's end keep their own value: callers mask lane 7 and ignore lanes >= 8)
+  const int l = __double2loint(v), h = __double2hiint(v);
+  const int lo = __builtin_amdgcn_update_dpp(l, l, 0x101, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(h, h, 0x101, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double rs_lane0(double v) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), 0);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 0);
+  return __hiloint2double(hi, lo);
+}
+#define RS_PF 4
+__device__ __forceinline__ void rs_band_solve_par(int c, int kp, const double* F, const double* fe,
+                                                  double* f, double* y) {
+  const int nb = c - kp;
+  const int lane = threadIdx.x & 63, q = lane & 7;
+  // forward: r_q = f[kp + q] - fe[q]; at row k, lane q needs t_{k,q+1} = F[k][1 + q] and lane 7
+  // the entering right-hand side f[kp + k + 8]
+  double r = f[kp + q] - fe[q];
+  double tq[RS_PF], fv[RS_PF];
+#pragma unroll
+  for (int u = 0; u < RS_PF; ++u) {
+    tq[u] = F[min(u, nb - 1) * 9 + 1 + q];
+    fv[u] = f[kp + min(u + 8, nb - 1)];
+    if (u + 8 >= nb) fv[u] = 0.0;
+  }
+  for (int k0 = 0; k0 < nb; k0 += RS_PF) {
+    double tn[RS_PF], fn[RS_PF];
+#pragma unroll
+    for (int u = 0; u < RS_PF; ++u) {  // rows k0 + RS_PF + u, clamped (values past nb unused)
+      const int kk = k0 + RS_PF + u;
+      tn[u] = F[min(kk, nb - 1) * 9 + 1 + q];
+      fn[u] = (kk + 8 < nb) ? f[kp + kk + 8] : 0.0;
+    }
+    double zs = 0.0;  // lane u keeps z_{k0 + u}: one store per RS_PF rows, off the chain
+#pragma unroll
+    for (int u = 0; u < RS_PF; ++u) {
+      if (k0 + u >= nb) break;
+      const double zk = rs_lane0(r);
+      zs = (lane == u) ? zk : zs;
+      double nx = rs_dpp_shl1(r);
+      nx = (q == 7) ? fv[u] : nx;
+      r = fma(-tq[u], zk, nx);
+    }
+    if (lane < RS_PF && k0 + lane < nb) f[kp + k0 + lane] = zs;
+#pragma unroll
+    for (int u = 0; u < RS_PF; ++u) {
+      tq[u] = tn[u];
+      fv[u] = fn[u];
+    }
+  }
+  // backward: row k's solution y_k = z_k d_k^{-1} - sum_i t_{k,i} y_{k+i}; lane j holds that sum
+  // for row k - j; after y_k, lane j takes lane j + 1's sum plus t_{k-1-j, j+1} y_k
+  double acc = 0.0;
+  double zr[RS_PF], tb[RS_PF];
+  const int top = nb - 1;
+#pragma unroll
+  for (int u = 0; u < RS_PF; ++u) {
+    const int k = max(top - u, 0);
+    zr[u] = f[kp + k] * F[k * 9];
+    const int row = k - 1 - q;
+    tb[u] = row >= 0 ? F[row * 9 + q + 1] : 0.0;
+  }
+  for (int k0 = top; k0 >= 0; k0 -= RS_PF) {
+    double zn[RS_PF], tbn[RS_PF];
+#pragma unroll
+    for (int u = 0; u < RS_PF; ++u) {
+      const int k = max(k0 - RS_PF - u, 0);
+      zn[u] = f[kp + k] * F[k * 9];
+      const int row = k0 - RS_PF - u - 1 - q;
+      tbn[u] = row >= 0 ? F[row * 9 + q + 1] : 0.0;
+    }
+    double ys = 0.0;  // lane u keeps y_{k0 - u}
+#pragma unroll
+    for (int u = 0; u < RS_PF; ++u) {
+      const int k = k0 - u;
+      if (k < 0) break;
+      const double yk = zr[u] - rs_lane0(acc);
+      ys = (lane == u) ? yk : ys;
+      double sh = rs_dpp_shl1(acc);
+      sh = (q == 7) ? 0.0 : sh;
+      acc = fma(tb[u], yk, sh);
+    }
+    if (lane < RS_PF && k0 - lane >= 0) y[kp + k0 - lane] = ys;
+#pragma unroll
+    for (int u = 0; u < RS_PF; ++u) {
+      zr[u] = zn[u];
+      tb[u] = tbn[u];
+    }
+  }
+}
+#undef RS_PF
+
 __device__ __forceinline__ double rs_wave_sum(double v) {
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
@@ -593,7 +695,7 @@ __device__ __forceinline__ double rs_wave_sum(double v) {
 
 // y = (H - lam)^{-1} f: the X rows lane-parallel (dX = 1 / (theta - lam)), the band by lane 0
 __device__ __forceinline__ void rs_solve(int c, int kp, const double* Xg, const double* dX, const double* F,
-                         double* fe, double* f, double* y) {
+                         double* fe, double* f, double* y, bool par) {
   const int lane = threadIdx.x;
   if (lane < 8) {  // f_E -= G^T D f_X
     double acc = 0.0;
@@ -601,7 +703,8 @@ __device__ __forceinline__ void rs_solve(int c, int kp, const double* Xg, const 
     fe[lane] = acc;
   }
   __syncthreads();
-  if (lane == 0) rs_band_solve_lane(c, kp, F, fe, f, y);
+  if (par) rs_band_solve_par(c, kp, F, fe, f, y);
+  else if (lane == 0) rs_band_solve_lane(c, kp, F, fe, f, y);
   __syncthreads();
   for (int a = lane; a < kp; a += 64) {  // y_X = D (f_X - G y_E)
     double acc = f[a];
@@ -619,7 +722,8 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
                                                               double* __restrict__ wout,
                                                               double* __restrict__ Y,
                                                               float* __restrict__ S, int ldS,
-                                                              int* __restrict__ err, int inv_stop) {
+                                                              int* __restrict__ err, int inv_stop,
+                                                              bool inv_par) {
   extern __shared__ __attribute__((aligned(16))) double il[];
   const int lane = threadIdx.x;
   const int j0 = blockIdx.x;
@@ -699,7 +803,7 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
     else if (j == j0 && j == 0 && pw > 1) gap = lam - w[1];
     bool ok = true, done = false;
     for (int it = 0; it < 2 && ok; ++it) {
-      rs_solve(c, kp, Xg, dX, F, fe, f, y);
+      rs_solve(c, kp, Xg, dX, F, fe, f, y, inv_par);
       if (stop == 4) { if (lane == 0) err[0] = 1; return; }
       // classical Gram-Schmidt against the cluster's earlier members (Y columns j0 .. j-1)
       for (int q = j0; q < j; ++q) {
@@ -861,7 +965,11 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
     const char* v = getenv("N2V2R_INVITER_STOP");
     return v ? atoi(v) : 0;
   }();
+  static const bool inv_par = [] {  // N2V2R_INV_SOLVE=lane: lane 0 runs the band solves (A/B)
+    const char* v = getenv("N2V2R_INV_SOLVE");
+    return !(v && v[0] == 'l');
+  }();
   hipLaunchKernelGGL(rr_sturm_inviter_kernel, dim3((unsigned)p), dim3(64), linv, stream, scr, c,
-                     kp, p, pm, wbis, 1e-9, theta, Y, S, ldS, err, inv_stop);
+                     kp, p, pm, wbis, 1e-9, theta, Y, S, ldS, err, inv_stop, inv_par);
   return hipGetLastError();
 }
