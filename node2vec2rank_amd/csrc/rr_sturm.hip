@@ -606,84 +606,109 @@ __device__ __forceinline__ double rs_lane0(double v) {
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 0);
   return __hiloint2double(hi, lo);
 }
-#define RS_PF 4
+#define RS_PF 8
 __device__ __forceinline__ void rs_band_solve_par(int c, int kp, const double* F, const double* fe,
                                                   double* f, double* y) {
   const int nb = c - kp;
   const int lane = threadIdx.x & 63, q = lane & 7;
+  const bool last = q == 7;
   // forward: r_q = f[kp + q] - fe[q]; at row k, lane q needs t_{k,q+1} = F[k][1 + q] and lane 7
-  // the entering right-hand side f[kp + k + 8]
+  // the entering right-hand side f[kp + k + 8] (zero past the band: f is padded by 8 + RS_PF
+  // entries read as zero below).  Whole groups of RS_PF rows without exit tests; loads for the
+  // next group are issued before the current group's chain and are unconditional (clamped).
   double r = f[kp + q] - fe[q];
   double tq[RS_PF], fv[RS_PF];
+  auto fload = [&](int kk, double* t, double* v) {
 #pragma unroll
-  for (int u = 0; u < RS_PF; ++u) {
-    tq[u] = F[min(u, nb - 1) * 9 + 1 + q];
-    fv[u] = f[kp + min(u + 8, nb - 1)];
-    if (u + 8 >= nb) fv[u] = 0.0;
-  }
-  for (int k0 = 0; k0 < nb; k0 += RS_PF) {
-    double tn[RS_PF], fn[RS_PF];
-#pragma unroll
-    for (int u = 0; u < RS_PF; ++u) {  // rows k0 + RS_PF + u, clamped (values past nb unused)
-      const int kk = k0 + RS_PF + u;
-      tn[u] = F[min(kk, nb - 1) * 9 + 1 + q];
-      fn[u] = (kk + 8 < nb) ? f[kp + kk + 8] : 0.0;
+    for (int u = 0; u < RS_PF; ++u) {
+      const int k = kk + u;
+      t[u] = F[min(k, nb - 1) * 9 + 1 + q];
+      const double fx = f[kp + min(k + 8, nb - 1)];
+      v[u] = (k + 8 < nb) ? fx : 0.0;
     }
+  };
+  fload(0, tq, fv);
+  int k0 = 0;
+  for (; k0 + RS_PF <= nb; k0 += RS_PF) {
+    double tn[RS_PF], fn[RS_PF];
+    fload(k0 + RS_PF, tn, fn);
     double zs = 0.0;  // lane u keeps z_{k0 + u}: one store per RS_PF rows, off the chain
 #pragma unroll
     for (int u = 0; u < RS_PF; ++u) {
-      if (k0 + u >= nb) break;
       const double zk = rs_lane0(r);
       zs = (lane == u) ? zk : zs;
       double nx = rs_dpp_shl1(r);
-      nx = (q == 7) ? fv[u] : nx;
+      nx = last ? fv[u] : nx;
       r = fma(-tq[u], zk, nx);
     }
-    if (lane < RS_PF && k0 + lane < nb) f[kp + k0 + lane] = zs;
+    if (lane < RS_PF) f[kp + k0 + lane] = zs;
 #pragma unroll
     for (int u = 0; u < RS_PF; ++u) {
       tq[u] = tn[u];
       fv[u] = fn[u];
     }
   }
+  {
+    double zs = 0.0;
+#pragma unroll
+    for (int u = 0; u < RS_PF; ++u) {
+      if (k0 + u >= nb) break;
+      const double zk = rs_lane0(r);
+      zs = (lane == u) ? zk : zs;
+      double nx = rs_dpp_shl1(r);
+      nx = last ? fv[u] : nx;
+      r = fma(-tq[u], zk, nx);
+    }
+    if (lane < RS_PF && k0 + lane < nb) f[kp + k0 + lane] = zs;
+  }
   // backward: row k's solution y_k = z_k d_k^{-1} - sum_i t_{k,i} y_{k+i}; lane j holds that sum
   // for row k - j; after y_k, lane j takes lane j + 1's sum plus t_{k-1-j, j+1} y_k
   double acc = 0.0;
   double zr[RS_PF], tb[RS_PF];
   const int top = nb - 1;
-#pragma unroll
-  for (int u = 0; u < RS_PF; ++u) {
-    const int k = max(top - u, 0);
-    zr[u] = f[kp + k] * F[k * 9];
-    const int row = k - 1 - q;
-    tb[u] = row >= 0 ? F[row * 9 + q + 1] : 0.0;
-  }
-  for (int k0 = top; k0 >= 0; k0 -= RS_PF) {
-    double zn[RS_PF], tbn[RS_PF];
+  auto bload = [&](int kk, double* z, double* t) {
 #pragma unroll
     for (int u = 0; u < RS_PF; ++u) {
-      const int k = max(k0 - RS_PF - u, 0);
-      zn[u] = f[kp + k] * F[k * 9];
-      const int row = k0 - RS_PF - u - 1 - q;
-      tbn[u] = row >= 0 ? F[row * 9 + q + 1] : 0.0;
+      const int k = max(kk - u, 0);
+      z[u] = f[kp + k] * F[k * 9];
+      const int row = kk - u - 1 - q;
+      const double tx = F[max(row, 0) * 9 + q + 1];
+      t[u] = row >= 0 ? tx : 0.0;
     }
-    double ys = 0.0;  // lane u keeps y_{k0 - u}
+  };
+  bload(top, zr, tb);
+  int k1 = top;
+  for (; k1 - RS_PF + 1 >= 0; k1 -= RS_PF) {
+    double zn[RS_PF], tbn[RS_PF];
+    bload(k1 - RS_PF, zn, tbn);
+    double ys = 0.0;  // lane u keeps y_{k1 - u}
 #pragma unroll
     for (int u = 0; u < RS_PF; ++u) {
-      const int k = k0 - u;
-      if (k < 0) break;
       const double yk = zr[u] - rs_lane0(acc);
       ys = (lane == u) ? yk : ys;
       double sh = rs_dpp_shl1(acc);
-      sh = (q == 7) ? 0.0 : sh;
+      sh = last ? 0.0 : sh;
       acc = fma(tb[u], yk, sh);
     }
-    if (lane < RS_PF && k0 - lane >= 0) y[kp + k0 - lane] = ys;
+    if (lane < RS_PF) y[kp + k1 - lane] = ys;
 #pragma unroll
     for (int u = 0; u < RS_PF; ++u) {
       zr[u] = zn[u];
       tb[u] = tbn[u];
     }
+  }
+  {
+    double ys = 0.0;
+#pragma unroll
+    for (int u = 0; u < RS_PF; ++u) {
+      if (k1 - u < 0) break;
+      const double yk = zr[u] - rs_lane0(acc);
+      ys = (lane == u) ? yk : ys;
+      double sh = rs_dpp_shl1(acc);
+      sh = last ? 0.0 : sh;
+      acc = fma(tb[u], yk, sh);
+    }
+    if (lane < RS_PF && k1 - lane >= 0) y[kp + k1 - lane] = ys;
   }
 }
 #undef RS_PF
@@ -965,10 +990,9 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
     const char* v = getenv("N2V2R_INVITER_STOP");
     return v ? atoi(v) : 0;
   }();
-  static const bool inv_par = [] {  // N2V2R_INV_SOLVE=lane: lane 0 runs the band solves (A/B)
-    const char* v = getenv("N2V2R_INV_SOLVE");
-    return !(v && v[0] == 'l');
-  }();
+  // N2V2R_INV_SOLVE=lane: lane 0 runs the band solves (A/B; read per launch)
+  const char* inv_env = getenv("N2V2R_INV_SOLVE");
+  const bool inv_par = !(inv_env && inv_env[0] == 'l');
   hipLaunchKernelGGL(rr_sturm_inviter_kernel, dim3((unsigned)p), dim3(64), linv, stream, scr, c,
                      kp, p, pm, wbis, 1e-9, theta, Y, S, ldS, err, inv_stop, inv_par);
   return hipGetLastError();

@@ -435,6 +435,42 @@ def test_uase_split_stage2(engine, monkeypatch, layers_k):
     assert np.array_equal(engine.embedding(), Y1)
 
 
+@pytest.mark.parametrize("mode", ["lean", "lean_whole", "images_kept"])
+def test_uase_lean_images_selective_reorth(engine, monkeypatch, mode):
+    """Lean images (Krylov-Schur residual estimates, the true residuals checked before the fit
+    ends) and selective reorthogonalisation (full passes apply only the blocks above tol/10,
+    per block or the whole pass) vs the fit with every image kept and every block of every full
+    pass applied: same sigma within fp32 tolerance, true residuals and orthonormal U on the
+    host, the engine's reported residual matching the host's, bit-identical reruns."""
+    from node2vec2rank_amd import synthetic
+    layers = synthetic.er_layers(20_003, 16, 2)
+    d = 32
+    engine.set_layers(layers)
+    monkeypatch.setenv("N2V2R_LEAN_W", "0")
+    monkeypatch.setenv("N2V2R_REORTH_TOL", "0")
+    engine.uase(d, seed=11)
+    s_ref = engine.singular_values().copy()
+    monkeypatch.setenv("N2V2R_LEAN_W", "0" if mode == "images_kept" else "1")
+    monkeypatch.delenv("N2V2R_REORTH_TOL")
+    if mode == "lean_whole":
+        monkeypatch.setenv("N2V2R_REORTH_MODE", "whole")
+    st = engine.uase(d, seed=11)
+    assert st["converged"] == d and st["rr_fallbacks"] == 0, st
+    s = engine.singular_values()
+    Y1 = engine.embedding().copy()
+    np.testing.assert_allclose(s, s_ref, rtol=1e-5)
+    X = engine.left_embedding().astype(np.float64) / np.sqrt(s)[None, :]
+    A = sp.hstack(layers).tocsr().astype(np.float64)
+    res = np.linalg.norm(A @ (A.T @ X) - X * (s ** 2)[None, :], axis=0) / s[0] ** 2
+    assert res.max() < 1e-5
+    assert st["max_residual"] <= 1e-6
+    # the reported residual is a true one (fp32 products on the GPU vs fp64 here)
+    assert abs(st["max_residual"] - res.max()) < 0.5 * res.max() + 2e-7, (st["max_residual"], res.max())
+    np.testing.assert_allclose(X.T @ X, np.eye(d), atol=1e-5)
+    engine.uase(d, seed=11)
+    assert np.array_equal(engine.embedding(), Y1)
+
+
 @pytest.mark.parametrize("block", [8, 16, 64])
 @pytest.mark.parametrize("name", ["er_cfg1", "directed_weighted", "demo"])
 def test_uase_block_widths(engine, name, block):
@@ -516,13 +552,15 @@ def _band_problem(c, kp, seed, cluster=False, decoupled=0):
     (40, 0, 12, False, 0), (256, 0, 80, False, 0), (256, 80, 80, False, 0),
     (256, 80, 80, True, 30), (384, 160, 160, False, 0), (512, 184, 184, True, 100),
     (96, 80, 80, False, 0)])
-@pytest.mark.parametrize("method", ["sturm", "band"])
+@pytest.mark.parametrize("method", ["sturm", "sturm_lane0", "band"])
 def test_rayleigh_ritz_band_stage(engine, monkeypatch, c, kp, p, cluster, decoupled, method):
     """Banded Rayleigh-Ritz vs numpy eigh of the same structured matrix, both forms: "sturm"
     (Sturm-count multisection + inverse iteration on the unreduced arrow + band matrix, the
     default) and "band" (arrow reduction, bulge chasing, bisection, tridiagonal inverse
     iteration, back-transform)."""
-    monkeypatch.setenv("N2V2R_RR", method)
+    # sturm_lane0: the inverse iteration's band solves by lane 0 instead of 8 lanes
+    monkeypatch.setenv("N2V2R_INV_SOLVE", "lane" if method == "sturm_lane0" else "par")
+    monkeypatch.setenv("N2V2R_RR", "sturm" if method == "sturm_lane0" else method)
     H, hband, theta = _band_problem(c, kp, seed=c + kp, cluster=cluster, decoupled=decoupled)
     w, S = engine.rr_band_top(hband, c, kp, theta, p)
     ref = np.sort(np.linalg.eigvalsh(H))[::-1][:p]
