@@ -49,7 +49,10 @@ enum { N2V2R_SYM_DETECT = -1, N2V2R_SYM_NO = 0, N2V2R_SYM_YES = 1 };
 
 /* n2v2r_eig_opts.solver_flags */
 enum { N2V2R_EIG_FULL_FIRST_PASS = 1, N2V2R_EIG_DENSE_RR = 2,
-       N2V2R_EIG_TEST_REDO_CYCLE = 4 /* tests: re-expand the first cycle as after a refill */ };
+       N2V2R_EIG_TEST_REDO_CYCLE = 4 /* tests: re-expand the first cycle as after a refill */,
+       N2V2R_EIG_TEST_BAND_FAIL = 8 /* tests: every banded Rayleigh-Ritz result is treated as
+                                       failed, so the reducing, then the dense fallback runs
+                                       (and a lean-image fit reruns with images kept) */ };
 
 typedef struct n2v2r_handle n2v2r_handle;
 typedef struct n2v2r_simgroup n2v2r_simgroup;

@@ -1302,6 +1302,7 @@ struct Eig {
     kry0 = 0;
     bool lazy = true;
     const bool test_redo = (o.solver_flags & N2V2R_EIG_TEST_REDO_CYCLE) != 0;
+    const bool test_band_fail = (o.solver_flags & N2V2R_EIG_TEST_BAND_FAIL) != 0;
     const double tol = o.tol > 0 ? o.tol : 1e-6;
     const int max_restarts = o.max_restarts > 0 ? o.max_restarts : 2000;
     // default panel width: 8 for CSR layers (vector-applications grow with b); 32 for dense
@@ -1652,7 +1653,7 @@ struct Eig {
         std::copy(pres, pres + keep, res2.begin());
       }
       std::copy(pth, pth + keep, wh.begin());
-      if (!dense_rr) rr_err = pflag[2];
+      if (!dense_rr) rr_err = test_band_fail ? 1 : pflag[2];
       if (trace && !dense_rr && sturm_now)
         fprintf(stderr, "[n2v2r] cycle %d: %d of %d Ritz vectors took a second solve\n", cycle,
                 pflag[3], keep);

@@ -471,6 +471,27 @@ def test_uase_lean_images_selective_reorth(engine, monkeypatch, mode):
     assert np.array_equal(engine.embedding(), Y1)
 
 
+@pytest.mark.parametrize("lean", ["1", "0"])
+def test_uase_banded_rr_failure_fallbacks(engine, monkeypatch, lean):
+    """Every banded Rayleigh-Ritz result forced to fail (test flag 8): the Sturm stage falls
+    back to the reducing band path, that one to the dense Rayleigh-Ritz, and a lean-image fit
+    (which cannot form the dense H) reruns with every image kept.  The embedding still matches
+    the reference fixture."""
+    fx = load_fixture("er_cfg1")
+    layers = fixture_layers(fx)
+    d = int(fx["dims"].max())
+    engine.set_layers(layers)
+    monkeypatch.setenv("N2V2R_LEAN_W", lean)
+    st = engine.uase(d, seed=int(fx["seed"]), solver_flags=8)
+    assert st["converged"] == d
+    assert st["rr_fallbacks"] >= 1
+    np.testing.assert_allclose(engine.singular_values(), fx["sigma"], rtol=2e-5)
+    Ya = orc.align_signs(engine.embedding().astype(np.float64), fx["Y"])
+    env, _ = _envelope(layers, d, int(fx["seed"]))
+    err = np.abs(Ya - fx["Y"]).max() / np.abs(fx["Y"]).max()
+    assert err <= max(5e-4, 3 * env), err
+
+
 @pytest.mark.parametrize("block", [8, 16, 64])
 @pytest.mark.parametrize("name", ["er_cfg1", "directed_weighted", "demo"])
 def test_uase_block_widths(engine, name, block):
