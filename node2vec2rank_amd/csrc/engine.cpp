@@ -22,6 +22,7 @@
 // + an all-reduce, so every rank holds identical small matrices and runs the identical host
 // Rayleigh-Ritz.  Communicators: RCCL (one process per GPU) or an in-process thread group
 // (W ranks on one GPU, for testing the partitioned algorithm without W devices).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -168,7 +169,8 @@ hipError_t n2v2r_launch_zsum(const float* const* parts, int count, float* zout, 
                              hipStream_t stream);
 hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp, double* theta, double* scr,
                                  size_t scr_elems, double* Y, float* S, int ldS, int p, int* err,
-                                 hipStream_t stream, hipEvent_t before_vectors);
+                                 hipStream_t stream, hipEvent_t before_vectors,
+                                 hipStream_t vec_stream, hipEvent_t after_vectors);
 size_t n2v2r_rr_sturm_scratch(int c, int p);
 }
 
@@ -199,6 +201,28 @@ static bool lean_enabled() {
 static bool restart_overlap_enabled() {
   const char* e = std::getenv("N2V2R_RESTART_OVERLAP");
   return e && e[0] == '1';
+}
+
+// N2V2R_LEAN_OVERLAP=1 (A/B, off by default): under lean images the restart block (orth(W_last)
+// against the old basis) and its SpMM image are issued on a second stream beside the inverse
+// iteration of the Sturm Rayleigh-Ritz (they need nothing from it), the host joining the two
+// streams at the cycle end.  Measured cfg2 36.4-36.9 vs 35.8-36.0 ms per step: the trace under
+// rocprofv3 shows the expansion inside the inverse iteration's span (cycle ~140 us shorter), but
+// unprofiled every form with a second queue lost (GPU-side join +0.9 ms, host join +0.6-0.9 ms,
+// inverse iteration on a CU-masked stream of its own +2-3 ms).  Read per fit.
+static bool lean_overlap_enabled() {
+  const char* e = std::getenv("N2V2R_LEAN_OVERLAP");
+  return e && e[0] == '1';
+}
+
+// N2V2R_INV_CUS=k > 0: the inverse iteration runs on a stream of its own with k CUs and the
+// restart expansion on the other CUs (disjoint hipExtStreamCreateWithCUMask masks); 0: the same
+// on two plain streams; -1 (default): the inverse iteration stays on the main stream.  A/B only:
+// the main stream then waits for the inverse-iteration stream's event, and such a wait on
+// another queue cost ~150 us per cycle on MI355X (cfg2 +2 ms per fit).
+static int inv_cus_wanted() {
+  const char* e = std::getenv("N2V2R_INV_CUS");
+  return e ? std::atoi(e) : -1;
 }
 
 namespace {
@@ -534,6 +558,11 @@ struct n2v2r_handle {
   // stream + events of the restart expansion overlapped with the Rayleigh-Ritz stage
   hipStream_t spec = nullptr;
   hipEvent_t spec_ev[2] = {};
+  // lean-image restart overlap: the inverse iteration's stream and the expansion's stream, on
+  // disjoint CU masks (inv_cus CUs for the former; 0: plain streams)
+  hipStream_t inv_s = nullptr, spec_m = nullptr;
+  hipEvent_t inv_ev = nullptr;
+  int inv_cus = -1;
   // pinned host staging of the per-cycle read-back (residuals, Ritz values, flags): the copies
   // are asynchronous and one stream synchronisation ends the cycle (pageable targets made each
   // copy a host round trip of its own)
@@ -1292,11 +1321,38 @@ struct Eig {
     ws.push_back(w);
   }
 
+  // the lean-image restart overlap's streams: the inverse iteration on inv_cus CUs, the
+  // expansion on the others (hipExtStreamCreateWithCUMask); without masks two plain streams
+  void make_overlap_streams() {
+    const int want = inv_cus_wanted();
+    if (h->inv_s && h->inv_cus == want) return;
+    if (h->inv_s) HIPCHK(hipStreamDestroy(h->inv_s));
+    if (h->spec_m) HIPCHK(hipStreamDestroy(h->spec_m));
+    h->inv_s = h->spec_m = nullptr;
+    if (!h->inv_ev) HIPCHK(hipEventCreateWithFlags(&h->inv_ev, hipEventDisableTiming));
+    if (!h->spec_ev[0])
+      for (hipEvent_t& e : h->spec_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    int ncu = 0;
+    HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
+    if (want > 0 && want < ncu) {
+      std::vector<uint32_t> ma((ncu + 31) / 32, 0u), mb((ncu + 31) / 32, 0u);
+      for (int i = 0; i < ncu; ++i) (i < want ? ma : mb)[i / 32] |= 1u << (i % 32);
+      HIPCHK(hipExtStreamCreateWithCUMask(&h->inv_s, (uint32_t)ma.size(), ma.data()));
+      HIPCHK(hipExtStreamCreateWithCUMask(&h->spec_m, (uint32_t)mb.size(), mb.data()));
+    } else {
+      HIPCHK(hipStreamCreateWithFlags(&h->inv_s, hipStreamNonBlocking));
+      HIPCHK(hipStreamCreateWithFlags(&h->spec_m, hipStreamNonBlocking));
+    }
+    h->inv_cus = want;
+  }
+
   int run(int d_, const n2v2r_eig_opts& o, std::vector<double>& theta_out, float* Uout,
           int ldu) {
     d = d_;
     // a previous fit that ended in an exception may have left a restart expansion in flight
     if (h->spec) HIPCHK(hipStreamSynchronize(h->spec));
+    if (h->spec_m) HIPCHK(hipStreamSynchronize(h->spec_m));
+    if (h->inv_s) HIPCHK(hipStreamSynchronize(h->inv_s));
     seed = o.seed ? o.seed : 0x5EEDull;
     full_first = (o.solver_flags & N2V2R_EIG_FULL_FIRST_PASS) != 0;
     kry0 = 0;
@@ -1416,12 +1472,17 @@ struct Eig {
     double est_scale = 1.0;  // lean: true / estimated residual seen at a failed final check
     int lean_checks = 0;
     const bool spec_ok = band_rr && !h->comm && !lean && restart_overlap_enabled();
-    if (spec_ok) {
+    const bool lean_ovl = lean && lean_overlap_enabled();
+    // pinned read-back per cycle: residuals, Ritz values (keep each), flags, R (8 x 8), S's last rows
+    const size_t pin_bytes = sizeof(double) * 2 * (size_t)keep + 8 * sizeof(int) +
+                             sizeof(double) * 64 + sizeof(float) * 8 * (size_t)keep;
+    if (lean_ovl) make_overlap_streams();
+    if (spec_ok || lean_ovl) {
       h->ews.spec_partial.ensure(sizeof(double) * h->partial_elems);
       h->ews.spec_gsmall.ensure(sizeof(double) * (size_t)c_max * c_max);
       h->ews.spec_flg.ensure(sizeof(int) * 256);
       h->ews.spec_any.ensure(sizeof(int) * 4);
-      if (!h->spec) {
+      if (spec_ok && !h->spec) {
         HIPCHK(hipStreamCreateWithFlags(&h->spec, hipStreamNonBlocking));
         for (hipEvent_t& e : h->spec_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       }
@@ -1480,6 +1541,9 @@ struct Eig {
       bool spec_live = false;  // the restart expansion is in flight on the spec stream
       std::vector<float*> specE, specEW;
       float* spec_pending = nullptr;
+      bool lean_forked = false;  // lean: E_lean and its image EW_lean come from the spec stream
+      float* EW_lean = nullptr;
+      double th_fork = 0, th_forked = 0, th_sync0 = 0, tr0_c = 0;  // host clock (N2V2R_TRACE)
     rayleigh_ritz:
       {
       // Rayleigh-Ritz, all on the GPU, into the fp32 Ritz coefficients S (c x keep, ld keep)
@@ -1491,6 +1555,7 @@ struct Eig {
       double* trid = h->ews.tri.as<double>();
       materialize();  // W.back() (every other W block was stored by its expansion's Gram pass)
       const double tr0 = now_ms();
+      tr0_c = tr0;
       lds_poison();
       if (!dense_rr) {
         const std::vector<float*> loc = local_of(Q);
@@ -1500,12 +1565,52 @@ struct Eig {
         lds_poison();
         if (sturm_now) {
           const bool spec_fork = spec_ok && !spec_live;
+          const bool lean_fork = lean_ovl && !spec_live;
           HIPCHK(n2v2r_launch_rr_sturm(h->ews.hband.as<double>(), c, kry0 * b,
                                        h->theta.as<double>(), h->ews.sturm.as<double>(),
                                        h->ews.sturm.bytes / sizeof(double),
                                        h->ews.ytri.as<double>(), h->ews.csmall.as<float>(), keep,
                                        keep, h->ews.rrerr.as<int>(), st,
-                                       spec_fork ? h->spec_ev[0] : nullptr));
+                                       (spec_fork || lean_fork) ? h->spec_ev[0] : nullptr,
+                                       (lean_fork && h->inv_cus >= 0) ? h->inv_s : nullptr,
+                                       h->inv_ev));
+          th_fork = now_ms();
+          if (lean_fork) {
+            // fork: the restart block E = orth(W_last) against the old basis (its first, local
+            // pass leaves R with W_last - Q_loc C = E R: the residual estimates) and its image
+            // M E, on the expansion stream beside the inverse iteration.  Scratch of its own;
+            // the image stays pending in the split partials until the restart.
+            const hipStream_t sx = h->spec_m;
+            HIPCHK(hipStreamWaitEvent(sx, h->spec_ev[0], 0));
+            const hipStream_t st0 = st;
+            st = sx;
+            part_p = h->ews.spec_partial.as<double>();
+            gsm_p = h->ews.spec_gsmall.as<double>();
+            flg_p = h->ews.spec_flg.as<int>();
+            any_p = h->ews.spec_any.as<int>();
+            E_lean = take();
+            const std::vector<float*> loc = local_of(Q);
+            orthonormalize(E_lean, Q, W.back(), &loc, nullptr, false, h->ews.rres.as<double>());
+            // R goes to the host from this stream: the host synchronises both streams at the
+            // cycle end, and no GPU-side join is queued on the main stream (a wait on another
+            // queue's event cost ~150 us per cycle here, more than the overlap saves)
+            h->ensure_pin(pin_bytes);
+            HIPCHK(hipMemcpyAsync(static_cast<double*>(h->pin) + 2 * (size_t)keep + 4,
+                                  h->ews.rres.p, sizeof(double) * 64, hipMemcpyDeviceToHost, st));
+            EW_lean = take();
+            apply_M(E_lean, EW_lean);
+            spec_pending = pending;
+            pending = nullptr;
+            HIPCHK(hipEventRecord(h->spec_ev[1], st));
+            st = st0;
+            part_p = h->partial.as<double>();
+            gsm_p = h->ews.gsmall.as<double>();
+            flg_p = h->ews.flg.as<int>();
+            any_p = h->ews.anyflag.as<int>();
+            spec_live = true;
+            lean_forked = true;
+          }
+          th_forked = now_ms();
           if (spec_fork) {
             // fork: the spec stream starts when the inverse iteration does (an 80-wave kernel
             // of serial chains that leaves the CUs free; beside the all-CU multisection the
@@ -1602,7 +1707,9 @@ struct Eig {
         dbg(X[q], n * b, false, "Ritz vectors X = Q S");
         if (!lean) dbg(MX[q], n * b, false, "Ritz images MX = W S");
       }
-      if (lean) {
+      if (lean_forked) {
+        // R (read back) and the restart block come from the expansion stream
+      } else if (lean) {
         // the restart block now (it needs nothing from the Rayleigh-Ritz stage): its first,
         // local pass leaves R with W_last - Q_loc C = Z_{m+1} R, Z_{m+1} orthonormal
         E_lean = take();
@@ -1614,8 +1721,7 @@ struct Eig {
                                   h->resid.as<double>(), st));
         h->allreduce_f64(h->resid.as<double>(), keep);
       }
-      h->ensure_pin(sizeof(double) * 2 * (size_t)keep + 8 * sizeof(int) + sizeof(double) * 64 +
-                    sizeof(float) * 8 * (size_t)keep);
+      h->ensure_pin(pin_bytes);
       double* pres = static_cast<double*>(h->pin);
       double* pth = pres + keep;
       int* pflag = reinterpret_cast<int*>(pth + keep);
@@ -1623,7 +1729,8 @@ struct Eig {
       float* psl = reinterpret_cast<float*>(prr + 64);      // lean: last 8 rows of S
       for (int q = 0; q < 4; ++q) pflag[q] = 0;
       if (lean) {
-        HIPCHK(hipMemcpyAsync(prr, h->ews.rres.p, sizeof(double) * 64, hipMemcpyDeviceToHost, st));
+        if (!lean_forked)
+          HIPCHK(hipMemcpyAsync(prr, h->ews.rres.p, sizeof(double) * 64, hipMemcpyDeviceToHost, st));
         HIPCHK(hipMemcpyAsync(psl, h->ews.csmall.as<float>() + (size_t)(c - b) * keep,
                               sizeof(float) * 8 * (size_t)keep, hipMemcpyDeviceToHost, st));
       } else {
@@ -1638,7 +1745,13 @@ struct Eig {
       if (lazy)
         HIPCHK(hipMemcpyAsync(pflag + 1, h->ews.anyflag.as<int>() + 3, sizeof(int),
                               hipMemcpyDeviceToHost, st));
+      th_sync0 = now_ms();
       HIPCHK(hipStreamSynchronize(st));
+      if (lean_forked) HIPCHK(hipEventSynchronize(h->spec_ev[1]));
+      if (trace)
+        fprintf(stderr, "[n2v2r] cycle %d host: rr start %.3f, sturm launches %.3f, fork %.3f, "
+                "to sync %.3f, sync %.3f ms\n", cycle, tr0_c - t_start, th_fork - tr0_c,
+                th_forked - th_fork, th_sync0 - th_forked, now_ms() - th_sync0);
       if (lean) {  // ||M x_j - theta_j x_j||^2 = ||R s_j(last block)||^2 (Krylov-Schur), scaled
         for (int j = 0; j < keep; ++j) {
           double acc = 0.0;
@@ -1693,9 +1806,9 @@ struct Eig {
             refilled = 1;
             break;
           }
-      if (spec_live) {
+      if (spec_live && !lean_forked) {
         // join: the main stream waits for the expansion before any of its blocks (or the
-        // buffers it wrote) is used or given back
+        // buffers it wrote) is used or given back (lean fork: the host synchronised it above)
         HIPCHK(hipStreamWaitEvent(st, h->spec_ev[1], 0));
       }
       if (refilled) {  // a second pass refilled a column: expand this cycle again, 3 passes
@@ -1703,6 +1816,8 @@ struct Eig {
         for (float* p : specE) give(p);
         for (float* p : specEW) give(p);
         give(E_lean);
+        give(EW_lean);
+        spec_pending = nullptr;  // its partials are dropped with it
         for (int q = 0; q < pb; ++q) {
           give(X[q]);
           give(MX[q]);
@@ -1758,6 +1873,11 @@ struct Eig {
         // (their images by SpMM) decide
         ++lean_checks;
         const int qd = (d + b - 1) / b;
+        if (lean_forked && spec_pending) {  // these applications reuse the split partials
+          pending = spec_pending;
+          spec_pending = nullptr;
+          materialize();
+        }
         std::vector<float*> MV(qd);
         for (int q = 0; q < qd; ++q) {
           MV[q] = take();
@@ -1801,11 +1921,16 @@ struct Eig {
         for (float* p : specE) give(p);
         for (float* p : specEW) give(p);
         give(E_lean);
+        give(EW_lean);
         break;
       }
       // restart: [X | orth(W_last) against the old basis] (thick restart)
       std::vector<float*> E, EW;
-      if (lean) {
+      if (lean_forked) {
+        E.push_back(E_lean);
+        EW.push_back(EW_lean);
+        pending = spec_pending;  // (nullptr when a true-residual check stored it already)
+      } else if (lean) {
         E.push_back(E_lean);
         EW.push_back(take());
         apply_M(E_lean, EW[0]);
@@ -1995,6 +2120,9 @@ void n2v2r_destroy(n2v2r_handle* h) {
   for (hipEvent_t e : h->spec_ev)
     if (e) (void)hipEventDestroy(e);
   if (h->spec) (void)hipStreamDestroy(h->spec);
+  if (h->inv_s) (void)hipStreamDestroy(h->inv_s);
+  if (h->spec_m) (void)hipStreamDestroy(h->spec_m);
+  if (h->inv_ev) (void)hipEventDestroy(h->inv_ev);
   if (h->pin) (void)hipHostFree(h->pin);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -2673,7 +2801,7 @@ int n2v2r_rr_band_top(n2v2r_handle* h, int c, int kp, const double* hband, int64
       scr.ensure(sizeof(double) * n2v2r_rr_sturm_scratch(c, p));
       HIPCHK(n2v2r_launch_rr_sturm(hb.as<double>(), c, kp, th.as<double>(), scr.as<double>(),
                                    scr.bytes / sizeof(double), y.as<double>(), s.as<float>(), p,
-                                   p, er.as<int>(), h->stream, nullptr));
+                                   p, er.as<int>(), h->stream, nullptr, nullptr, nullptr));
       int e = 0;
       HIPCHK(hipMemcpyAsync(&e, er.p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
       HIPCHK(hipMemcpyAsync(w, th.p, sizeof(double) * p, hipMemcpyDeviceToHost, h->stream));

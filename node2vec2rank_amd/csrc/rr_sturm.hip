@@ -911,9 +911,10 @@ static size_t rs_inviter_lds(int c, int kp) {  // assembly + factor + f + y
 extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
                                            double* theta, double* scr, size_t scr_elems,
                                            double* Y, float* S, int ldS, int p, int* err,
-                                           hipStream_t stream, hipEvent_t before_vectors) {
+                                           hipStream_t stream, hipEvent_t before_vectors,
+                                           hipStream_t vec_stream, hipEvent_t after_vectors) {
   if (c < 9 || c > RS_MAXC || c % RS_W || kp % RS_W || kp + RS_W > c || p < 1 || p > c ||
-      ldS < p)
+      ldS < p || (vec_stream && !(before_vectors && after_vectors)))
     return hipErrorInvalidValue;
   const size_t wbis_off = (rs_asm_elems(c, kp) + 7) & ~(size_t)7;
   const int nt_ms = rs_msect_threads();
@@ -993,7 +994,18 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
   // N2V2R_INV_SOLVE=lane: lane 0 runs the band solves (A/B; read per launch)
   const char* inv_env = getenv("N2V2R_INV_SOLVE");
   const bool inv_par = !(inv_env && inv_env[0] == 'l');
-  hipLaunchKernelGGL(rr_sturm_inviter_kernel, dim3((unsigned)p), dim3(64), linv, stream, scr, c,
-                     kp, p, pm, wbis, 1e-9, theta, Y, S, ldS, err, inv_stop, inv_par);
-  return hipGetLastError();
+  // vec_stream (a stream on CUs of its own): the inverse iteration runs there, between the
+  // before_vectors record and an after_vectors record that `stream` waits for
+  if (vec_stream) {
+    e = hipStreamWaitEvent(vec_stream, before_vectors, 0);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(rr_sturm_inviter_kernel, dim3((unsigned)p), dim3(64), linv,
+                     vec_stream ? vec_stream : stream, scr, c, kp, p, pm, wbis, 1e-9, theta, Y, S,
+                     ldS, err, inv_stop, inv_par);
+  e = hipGetLastError();
+  if (e != hipSuccess || !vec_stream) return e;
+  e = hipEventRecord(after_vectors, vec_stream);
+  if (e != hipSuccess) return e;
+  return hipStreamWaitEvent(stream, after_vectors, 0);
 }
