@@ -748,7 +748,7 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
                                                               double* __restrict__ Y,
                                                               float* __restrict__ S, int ldS,
                                                               int* __restrict__ err, int inv_stop,
-                                                              bool inv_par) {
+                                                              bool inv_par, bool start_warm) {
   extern __shared__ __attribute__((aligned(16))) double il[];
   const int lane = threadIdx.x;
   const int j0 = blockIdx.x;
@@ -781,9 +781,15 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
       for (int a = 0; a < kp; ++a) acc += Xg[a * 8 + i] * Xg[a * 8 + jj] * dX[a];
       sch[lane] = acc;
     }
+    // start vector: for a wanted value j < kp, e_j (the kept Ritz vector j, which the new
+    // eigenvector j is close to once the order settles) plus a small random part so no
+    // component is zero; otherwise random.  From e_j one solve usually meets the
+    // single-solve test below (N2V2R_INV_START=rand: random starts, A/B)
+    const bool warm = start_warm && j < kp;
     for (int i = lane; i < c; i += 64) {
       const uint64_t hsh = splitmix64(0x9E3779B97F4A7C15ull ^ ((uint64_t)j << 32) ^ (uint64_t)i);
-      f[i] = (double)(hsh >> 11) * (1.0 / 9007199254740992.0) - 0.5;
+      const double u = (double)(hsh >> 11) * (1.0 / 9007199254740992.0) - 0.5;
+      f[i] = warm ? ((i == j ? 1.0 : 0.0) + 1e-4 * u) : u;
     }
     __syncthreads();
     if (stop == 2) { if (lane == 0) err[0] = 1; return; }
@@ -994,6 +1000,8 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
   // N2V2R_INV_SOLVE=lane: lane 0 runs the band solves (A/B; read per launch)
   const char* inv_env = getenv("N2V2R_INV_SOLVE");
   const bool inv_par = !(inv_env && inv_env[0] == 'l');
+  const char* start_env = getenv("N2V2R_INV_START");  // "rand": random start vectors (A/B)
+  const bool start_warm = !(start_env && start_env[0] == 'r');
   // vec_stream (a stream on CUs of its own): the inverse iteration runs there, between the
   // before_vectors record and an after_vectors record that `stream` waits for
   if (vec_stream) {
@@ -1002,7 +1010,7 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
   }
   hipLaunchKernelGGL(rr_sturm_inviter_kernel, dim3((unsigned)p), dim3(64), linv,
                      vec_stream ? vec_stream : stream, scr, c, kp, p, pm, wbis, 1e-9, theta, Y, S,
-                     ldS, err, inv_stop, inv_par);
+                     ldS, err, inv_stop, inv_par, start_warm);
   e = hipGetLastError();
   if (e != hipSuccess || !vec_stream) return e;
   e = hipEventRecord(after_vectors, vec_stream);

@@ -471,17 +471,52 @@ def test_uase_lean_images_selective_reorth(engine, monkeypatch, mode):
     assert np.array_equal(engine.embedding(), Y1)
 
 
-@pytest.mark.parametrize("lean", ["1", "0"])
+@pytest.mark.parametrize("mode", ["overlap_plain", "overlap_masked", "random_starts"])
+def test_uase_restart_overlap_and_inverse_iteration_starts(engine, monkeypatch, mode):
+    """A/B forms of the cycle end vs the default fit: the lean restart block and its image on a
+    second stream (N2V2R_LEAN_OVERLAP=1; the inverse iteration on the main stream, or on a
+    CU-masked stream of its own beside an expansion stream on the other CUs), and random
+    inverse-iteration starts instead of the kept Ritz vectors (N2V2R_INV_START=rand): same sigma
+    within fp32 tolerance, true residuals and orthonormal U on the host, bit-identical reruns."""
+    from node2vec2rank_amd import synthetic
+    layers = synthetic.er_layers(20_003, 16, 2)
+    d = 32
+    engine.set_layers(layers)
+    engine.uase(d, seed=13)
+    s_ref = engine.singular_values().copy()
+    if mode == "random_starts":
+        monkeypatch.setenv("N2V2R_INV_START", "rand")
+    else:
+        monkeypatch.setenv("N2V2R_LEAN_OVERLAP", "1")
+        monkeypatch.setenv("N2V2R_INV_CUS", "64" if mode == "overlap_masked" else "-1")
+    st = engine.uase(d, seed=13)
+    assert st["converged"] == d and st["rr_fallbacks"] == 0, st
+    s = engine.singular_values()
+    Y1 = engine.embedding().copy()
+    np.testing.assert_allclose(s, s_ref, rtol=1e-5)
+    X = engine.left_embedding().astype(np.float64) / np.sqrt(s)[None, :]
+    A = sp.hstack(layers).tocsr().astype(np.float64)
+    res = np.linalg.norm(A @ (A.T @ X) - X * (s ** 2)[None, :], axis=0) / s[0] ** 2
+    assert res.max() < 1e-5
+    np.testing.assert_allclose(X.T @ X, np.eye(d), atol=1e-5)
+    engine.uase(d, seed=13)
+    assert np.array_equal(engine.embedding(), Y1)
+
+
+@pytest.mark.parametrize("lean", ["1", "0", "overlap"])
 def test_uase_banded_rr_failure_fallbacks(engine, monkeypatch, lean):
     """Every banded Rayleigh-Ritz result forced to fail (test flag 8): the Sturm stage falls
     back to the reducing band path, that one to the dense Rayleigh-Ritz, and a lean-image fit
-    (which cannot form the dense H) reruns with every image kept.  The embedding still matches
-    the reference fixture."""
+    (which cannot form the dense H) reruns with every image kept (also with the restart block
+    in flight on the second stream when the failure is seen).  The embedding still matches the
+    reference fixture."""
     fx = load_fixture("er_cfg1")
     layers = fixture_layers(fx)
     d = int(fx["dims"].max())
     engine.set_layers(layers)
-    monkeypatch.setenv("N2V2R_LEAN_W", lean)
+    monkeypatch.setenv("N2V2R_LEAN_W", "0" if lean == "0" else "1")
+    if lean == "overlap":
+        monkeypatch.setenv("N2V2R_LEAN_OVERLAP", "1")
     st = engine.uase(d, seed=int(fx["seed"]), solver_flags=8)
     assert st["converged"] == d
     assert st["rr_fallbacks"] >= 1
