@@ -1384,6 +1384,13 @@ extern "C" hipError_t n2v2r_launch_chol_inv(const double* G, int b, float* Rinv,
 // refilled by counter deviates.  Every workgroup forms the same R from the same G (the
 // factorisation is deterministic); workgroup 0 alone writes flags / any_flag / sticky / save.
 // Same pivot rule as pip_chol_kernel (pivot <= 1e-10 max diag: unit row, zero R^{-1} column).
+// 1 / sqrt(p), p > 0: hardware estimate + two Newton steps (full fp64 precision)
+__device__ __forceinline__ double rsq_nr(double p) {
+  double r = __builtin_amdgcn_rsq(p);
+  r = r * fma(-0.5 * p * r, r, 1.5);
+  r = r * fma(-0.5 * p * r, r, 1.5);
+  return r;
+}
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
@@ -1397,7 +1404,8 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
                                                         int* any_flag, double* save, int save_row0,
                                                         int save_rows, int* sticky, uint64_t seed,
                                                         int64_t row0, double* rsave, float skip_tol,
-                                                        int* skipped) {
+                                                        int* skipped, int stop) {
+  // stop = k > 0: timing probe (N2V2R_PIP_STOP, tools/pip_probe.cpp), return after phase k
   const int tid = threadIdx.x;
   const bool lead = blockIdx.x == 0;
   if (cond && *cond == 0) {
@@ -1425,9 +1433,10 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
       reinterpret_cast<double2*>(gd)[min(e0 + 256 * u, ne2 - 1)] = t[u];
   }
   __syncthreads();
+  if (stop == 1) return;
   // the basis blocks this pass applies: all, or (skip_tol > 0: selective reorthogonalisation of
   // an in-place pass) those with max_ij |C_ij| / ||z_j|| > skip_tol; every workgroup decides
-  // alike from the same G.  Skipped blocks' C rows are zeroed so R factors the applied pass.
+  // alike from the same G.  C^T C sums the applied blocks only, so R factors the applied pass.
   // (skip_tol < 0: the whole pass, all blocks or none, by |skip_tol|)
   int* blist = badw + 4;  // compact list of applied blocks (<= 64)
   const int nblk = c >> 3;
@@ -1463,6 +1472,7 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
     }
   }
   __syncthreads();
+  if (stop == 2) return;
   const int napply = badw[1];
   if (skip_tol > 0.f) {
     if (napply == 0) {
@@ -1473,65 +1483,94 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
       }
       return;
     }
-    const unsigned long long m =
-        ((unsigned long long)(unsigned)badw[3] << 32) | (unsigned long long)(unsigned)badw[2];
-    for (int e = tid; e < c * 8; e += 256)
-      if (!((m >> (e >> 6)) & 1ull)) gd[e] = 0.0;
-    __syncthreads();
   }
   if (save && lead)
     for (int e = tid; e < save_rows * 8; e += 256) save[e] = gd[save_row0 * 8 + e];
-  for (int e = tid; e < c * 8; e += 256) cf[e] = (float)gd[e];
+  // fp32 coefficients and C^T C of the applied blocks only (a selective pass applies ~7 of 48
+  // at cfg2: the pass over all of C was 2.8 us of the launch, zeroing the skipped rows 1.0)
+  for (int e = tid; e < napply * 64; e += 256) {
+    const int g = blist[e >> 6] * 64 + (e & 63);
+    cf[g] = (float)gd[g];
+  }
+  if (stop == 4) return;
   {
     const int e = tid & 63, sl = tid >> 6, i = e >> 3, j = e & 7;
-    // 4 independent chains (k, k + 4, k + 8, k + 12): the LDS loads of the next steps issue
-    // while the fp64 adds of this one complete (one chain of c / 4 dependent adds was ~2 us)
+    // wave sl: list entries sl, sl + 4, ...; four independent chains (rows r mod 4)
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-    int k = sl;
-    for (; k + 12 < c; k += 16) {
-      a0 += gd[k * 8 + i] * gd[k * 8 + j];
-      a1 += gd[(k + 4) * 8 + i] * gd[(k + 4) * 8 + j];
-      a2 += gd[(k + 8) * 8 + i] * gd[(k + 8) * 8 + j];
-      a3 += gd[(k + 12) * 8 + i] * gd[(k + 12) * 8 + j];
+    for (int q = sl; q < napply; q += 4) {
+      const double* g = gd + blist[q] * 64;
+#pragma unroll
+      for (int r = 0; r < 8; r += 4) {
+        a0 += g[r * 8 + i] * g[r * 8 + j];
+        a1 += g[(r + 1) * 8 + i] * g[(r + 1) * 8 + j];
+        a2 += g[(r + 2) * 8 + i] * g[(r + 2) * 8 + j];
+        a3 += g[(r + 3) * 8 + i] * g[(r + 3) * 8 + j];
+      }
     }
-    for (; k < c; k += 4) a0 += gd[k * 8 + i] * gd[k * 8 + j];
     part[sl * 64 + e] = (a0 + a1) + (a2 + a3);
+  }
+  __syncthreads();
+  if (stop == 5) return;
+  if (tid < 64) {  // P = Z^T Z - C^T C (each lane reads only its own part[] entries)
+    const int i = tid >> 3, j = tid & 7;
+    const double v = 0.5 * (gd[(c + i) * 8 + j] + gd[(c + j) * 8 + i]);
+    part[tid] = v - part[tid] - part[64 + tid] - part[128 + tid] - part[192 + tid];
   }
   __syncthreads();
   if (tid < 64) {
     const int i = tid >> 3, j = tid & 7;
-    double v = 0.5 * (gd[(c + i) * 8 + j] + gd[(c + j) * 8 + i]);
-    v = v - part[tid] - part[64 + tid] - part[128 + tid] - part[192 + tid];
+    // every lane factors the whole 8 x 8 P = R^T R in registers: no cross-lane traffic, and
+    // pivots by rsq + Newton, so no division or square root on the chain (the lane-per-entry
+    // form, two fp64 shuffles and a division per step, was 2.5 us of every launch)
+    double R[8][8];
     double dmax = 0.0;
 #pragma unroll
-    for (int d = 0; d < 8; ++d) dmax = fmax(dmax, readlane_f64(v, d * 9));
+    for (int r = 0; r < 8; ++r) {
+#pragma unroll
+      for (int q = r; q < 8; ++q) R[r][q] = part[r * 8 + q];
+      dmax = fmax(dmax, R[r][r]);
+    }
     const double tiny = 1e-10 * dmax;
     int bad = 0;
+    double rinv[8];
     // right-looking Cholesky: row jj of R = row jj of the Schur complement / sqrt(pivot)
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
-      const double p = readlane_f64(v, jj * 9);
+      const double p = R[jj][jj];
       const bool bj = !(p > tiny);
-      const double piv = bj ? 0.0 : sqrt(p);
       bad |= (int)bj << jj;
-      if (i == jj) v = (j < jj) ? 0.0 : bj ? (j == jj ? 1.0 : 0.0) : (j == jj ? piv : v / piv);
-      const double rjr = __shfl(v, jj * 8 + i, 64);
-      const double rjc = __shfl(v, jj * 8 + j, 64);
-      if (i > jj && j >= i) v -= rjr * rjc;
+      const double r = rsq_nr(bj ? 1.0 : p);
+#pragma unroll
+      for (int q = jj + 1; q < 8; ++q) R[jj][q] = bj ? 0.0 : R[jj][q] * r;
+      R[jj][jj] = bj ? 1.0 : p * r;
+      rinv[jj] = bj ? 1.0 : r;
+#pragma unroll
+      for (int a = jj + 1; a < 8; ++a)
+#pragma unroll
+        for (int q = a; q < 8; ++q) R[a][q] -= R[jj][a] * R[jj][q];
     }
     // R (row-major, upper): Z - Q C = Z_out R; its columns' norms give the Krylov-Schur
     // residual estimates of the lean-image solver mode
-    if (rsave && lead) rsave[tid] = v;
-    // Gauss-Jordan on [R | I] from the last row up: x <- R^{-1}
-    double x = (i == j) ? 1.0 : 0.0;
+    if (rsave && lead) {
+      double rij = 0.0;
 #pragma unroll
-    for (int jj = 7; jj >= 0; --jj) {
-      const double inv = 1.0 / readlane_f64(v, jj * 9);
-      if (i == jj) x *= inv;
-      const double xj = __shfl(x, jj * 8 + j, 64);
-      const double rij = __shfl(v, i * 8 + jj, 64);
-      if (i < jj) x -= rij * xj;
+      for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int q = r; q < 8; ++q) rij = (i == r && j == q) ? R[r][q] : rij;
+      rsave[tid] = rij;
     }
+    // column j of R^{-1} by back substitution; this lane keeps entry i
+    double xv[8];
+#pragma unroll
+    for (int a = 7; a >= 0; --a) {
+      double t = (a == j) ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = a + 1; k < 8; ++k) t -= R[a][k] * xv[k];
+      xv[a] = t * rinv[a];
+    }
+    double x = xv[0];
+#pragma unroll
+    for (int a = 1; a < 8; ++a) x = (i == a) ? xv[a] : x;
     rv[tid] = ((bad >> j) & 1) ? 0.f : (float)x;
     if (tid == 0) badw[0] = bad;
     if (lead) {
@@ -1543,6 +1582,7 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
     }
   }
   __syncthreads();
+  if (stop == 6) return;
   // rows: wave w owns rows 32 NU w .. 32 NU (w + 1) - 1 of the workgroup's 128 NU, lane =
   // (row offset ro = lane >> 1, column half h = lane & 1) over NU 32-row parts u, so one load
   // instruction reads 32 consecutive 32-B rows of a block (1 KB contiguous)
@@ -1641,11 +1681,15 @@ extern "C" hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zi
     const char* s = getenv("N2V2R_PIP_ROWS");
     return (s && atoi(s) == 128) ? 128 : 256;
   }();
+  static const int pip_stop = [] {  // timing probe only: phases after k skipped
+    const char* s = getenv("N2V2R_PIP_STOP");
+    return s ? atoi(s) : 0;
+  }();
   const unsigned grid = (unsigned)((n + rows - 1) / rows);
 #define PIP_LAUNCH(QB_, NU_)                                                                   \
   hipLaunchKernelGGL((pip_fused_kernel<QB_, NU_>), dim3(grid ? grid : 1), dim3(256), lds, stream, Q, \
                      Zin, Zout, G, c, n, cond, flags, any_flag, save, save_row0, save_rows, sticky,  \
-                     seed, row0, rsave, skip_tol, skipped)
+                     seed, row0, rsave, skip_tol, skipped, pip_stop)
   if (rows == 256) {
     if (qb == 8) PIP_LAUNCH(8, 2); else PIP_LAUNCH(4, 2);
   } else {
