@@ -180,14 +180,17 @@ __global__ __launch_bounds__(1024) void reduce_cols_kernel(const double* __restr
   }
 }
 
-// out[e] = sum_c partial[c][e] for the Gram forms below (N2V2R_REDUCE=wave: the per-element
-// wave form, A/B)
+// out[e] = sum_c partial[c][e] for the Gram forms below: the per-element wave form for small
+// Grams (<= 512 entries: the local pass's 192 spread over 48 workgroups instead of 3; 12.1 ->
+// 10.8 us per local Gram + reduce at cfg2), the coalesced form otherwise (the full pass's 3136:
+// 32.6 vs 33.1 us).  N2V2R_REDUCE=wave / cols forces one form (A/B).
 static hipError_t launch_reduce(const double* partial, int64_t nchunks, int64_t elems, double* out,
                                 const int* cond, hipStream_t stream) {
-  static const bool wave_form = [] {
+  static const int force = [] {
     const char* s = getenv("N2V2R_REDUCE");
-    return s && strcmp(s, "wave") == 0;
+    return !s ? 0 : (strcmp(s, "wave") == 0 ? 1 : (strcmp(s, "cols") == 0 ? 2 : 0));
   }();
+  const bool wave_form = force == 1 || (force == 0 && elems <= 512);
   if (wave_form)
     hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((elems + 3) / 4)), dim3(256), 0,
                        stream, partial, (int)nchunks, elems, out, cond);
