@@ -78,17 +78,26 @@ __device__ __forceinline__ double rs_band_entry(const double* __restrict__ hband
   return (r <= cc) ? G[cc * W + r] : 0.0;
 }
 
-__global__ __launch_bounds__(256) void rr_sturm_prep_kernel(const double* __restrict__ hband,
+__global__ __launch_bounds__(256) void rr_sturm_prep_kernel(const double* hband,
                                                             int c, int kp,
                                                             const double* __restrict__ theta,
                                                             double* __restrict__ scr) {
   constexpr int W = RS_W;
   __shared__ double red[3][256];
+  extern __shared__ __attribute__((aligned(16))) double hb_lds[];
   const int tid = threadIdx.x;
   const int nb = c - kp;
   double* Xd = scr + RS_HDR;
   double* Xg = Xd + kp;
   double* Lb = Xg + (size_t)kp * W;
+  {
+    // the band store into LDS first: every entry below is read several times, and from global
+    // memory each read was a dependent round trip (26 us for the launch at c = 384)
+    const int hbe = (kp + W) * W + (nb / W - 1) * 2 * W * W;
+    stage_to_lds<256, 8>(hb_lds, hband, hbe, tid);
+    __syncthreads();
+    hband = hb_lds;
+  }
   for (int e = tid; e < (nb + RS_PADR) * RS_LD; e += 256) {
     const int rr = e / RS_LD, t = e % RS_LD;
     const int i = kp + rr, col = i - W + t;
@@ -941,6 +950,9 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     hipError_t a2 = hipFuncSetAttribute((const void*)rr_sturm_inviter_kernel,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    hipError_t a5 = hipFuncSetAttribute((const void*)rr_sturm_prep_kernel,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    if (a2 == hipSuccess) a2 = a5;
     hipError_t a3 = hipFuncSetAttribute((const void*)rr_msect_kernel<256>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     hipError_t a4 = hipFuncSetAttribute((const void*)rr_msect_kernel<512>,
@@ -956,7 +968,9 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
   const size_t lbis = sizeof(double) * (asm_d - RS_HDR);
   const size_t linv = rs_inviter_lds(c, kp);
   if (lbis > 150 * 1024 || linv > 150 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(rr_sturm_prep_kernel, dim3(1), dim3(256), 0, stream, hband, c, kp, theta, scr);
+  const size_t lprep = sizeof(double) * ((size_t)(kp + RS_W) * RS_W + (size_t)((c - kp) / RS_W - 1) * 2 * RS_W * RS_W);
+  if (lprep > 150 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rr_sturm_prep_kernel, dim3(1), dim3(256), lprep, stream, hband, c, kp, theta, scr);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   // theta holds the kept Ritz values (kp) until the prep kernel has copied them; the
