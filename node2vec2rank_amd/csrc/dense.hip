@@ -1822,17 +1822,26 @@ __global__ __launch_bounds__(256) void colmax_partial_kernel(const float* __rest
   }
 }
 
-// fold chunk keys -> best[col] (packed |u| bits and ~global row)
-__global__ void colmax_fold_kernel(const unsigned long long* __restrict__ keys, int nchunks,
-                                   int ncols_padded, unsigned long long* __restrict__ best_out) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= ncols_padded) return;
+// fold chunk keys -> best[col] (packed |u| bits and ~global row): one wave per column, lanes
+// stride the chunks, wave max (a maximum: any order gives the same key)
+__global__ __launch_bounds__(256) void colmax_fold_kernel(const unsigned long long* __restrict__ keys,
+                                                          int nchunks, int ncols_padded,
+                                                          unsigned long long* __restrict__ best_out) {
+  const int col = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (col >= ncols_padded) return;  // (wave-uniform)
   unsigned long long best = 0;
-  for (int c = 0; c < nchunks; ++c) {
+  for (int c = lane; c < nchunks; c += 64) {
     const unsigned long long k = keys[(int64_t)c * ncols_padded + col];
     best = k > best ? k : best;
   }
-  best_out[col] = best;
+  for (int o = 32; o >= 1; o >>= 1) {
+    const unsigned long long t =
+        ((unsigned long long)(unsigned)__shfl_xor((int)(best >> 32), o, 64) << 32) |
+        (unsigned long long)(unsigned)__shfl_xor((int)(best & 0xFFFFFFFFull), o, 64);
+    best = t > best ? t : best;
+  }
+  if (lane == 0) best_out[col] = best;
 }
 
 // sign[col] = sign of U at the winning row if this rank owns it, else 0 (summed over ranks)
@@ -1857,7 +1866,8 @@ extern "C" hipError_t n2v2r_launch_colmax_keys(const float* U, int64_t ldu, int6
                                                size_t key_elems, unsigned long long* best,
                                                hipStream_t stream) {
   const int tiles = (d + 31) / 32;
-  int64_t nchunks = (n + 4095) / 4096;
+  // ~256 rows per chunk (cfg2: 391 x 2 workgroups; 4096-row chunks kept 50 CUs busy, 139 us)
+  int64_t nchunks = (n + 255) / 256;
   if (nchunks > 1024) nchunks = 1024;
   if (nchunks < 1) nchunks = 1;
   if ((size_t)(nchunks * tiles * 32) > key_elems) nchunks = (int64_t)(key_elems / (tiles * 32));
@@ -1870,7 +1880,7 @@ extern "C" hipError_t n2v2r_launch_colmax_keys(const float* U, int64_t ldu, int6
                      U, ldu, n, d, rows, row0, keys);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(colmax_fold_kernel, dim3((tiles * 32 + 255) / 256), dim3(256), 0, stream,
+  hipLaunchKernelGGL(colmax_fold_kernel, dim3((tiles * 32 + 3) / 4), dim3(256), 0, stream,
                      keys, (int)nchunks, tiles * 32, best);
   return hipGetLastError();
 }
