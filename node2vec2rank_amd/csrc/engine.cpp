@@ -165,6 +165,8 @@ hipError_t n2v2r_launch_nonfinite(const void* p, int64_t count, int f64, int* fl
 hipError_t n2v2r_launch_ts_tn_zsum(const BlockList& A, int64_t n, const float* const* parts,
                                    int count, float* zout, double* partial, size_t partial_elems,
                                    double* out, hipStream_t stream);
+hipError_t n2v2r_launch_pack_words(const void* const* src, const int* dst_word, const int* words,
+                                   int count, void* dst, hipStream_t stream);
 hipError_t n2v2r_launch_zsum(const float* const* parts, int count, float* zout, int64_t n,
                              hipStream_t stream);
 hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp, double* theta, double* scr,
@@ -534,6 +536,7 @@ struct EigWorkspace {
   std::vector<std::unique_ptr<DevBuf>> zk;    // K stage-1 panels (local)
   DevBuf zg;                                  // K gathered stage-1 panels
   DevBuf rinv, flg, anyflag, gsmall, csmall;
+  DevBuf rback;  // the per-cycle read-back, packed on the device before one copy to the host
   DevBuf tri, refl, ytri, tscr;               // GPU Rayleigh-Ritz: [d|e|tau], reflectors, Y_T
   DevBuf hband, band, varr, taua, rrerr;      // banded RR: band columns, band matrix, arrow
   DevBuf fcoef;                               // fp32 [-C R^-1; R^-1] of the apply pass
@@ -1727,24 +1730,38 @@ struct Eig {
       int* pflag = reinterpret_cast<int*>(pth + keep);
       double* prr = reinterpret_cast<double*>(pflag + 8);   // lean: R (8 x 8)
       float* psl = reinterpret_cast<float*>(prr + 64);      // lean: last 8 rows of S
-      for (int q = 0; q < 4; ++q) pflag[q] = 0;
-      if (lean) {
-        if (!lean_forked)
-          HIPCHK(hipMemcpyAsync(prr, h->ews.rres.p, sizeof(double) * 64, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(psl, h->ews.csmall.as<float>() + (size_t)(c - b) * keep,
-                              sizeof(float) * 8 * (size_t)keep, hipMemcpyDeviceToHost, st));
-      } else {
-        HIPCHK(hipMemcpyAsync(pres, h->resid.as<double>(), sizeof(double) * keep,
-                              hipMemcpyDeviceToHost, st));
+      {
+        // one pack launch + one copy: [pres | pth | pflag[8] | prr | psl] (the layout above)
+        h->ews.rback.ensure(pin_bytes);
+        const int wres = 0, wth = 2 * keep, wflag = 4 * keep, wrr = wflag + 8, wsl = wrr + 128;
+        const void* src[8];
+        int dw[8], nw[8], ns = 0;
+        auto seg = [&](const void* sp, int d0, int n0) {
+          src[ns] = sp;
+          dw[ns] = d0;
+          nw[ns] = n0;
+          ++ns;
+        };
+        if (lean) {
+          if (!lean_forked) seg(h->ews.rres.p, wrr, 128);
+          seg(h->ews.csmall.as<float>() + (size_t)(c - b) * keep, wsl, 8 * keep);
+        } else {
+          seg(h->resid.p, wres, 2 * keep);
+        }
+        seg(h->theta.p, wth, 2 * keep);
+        seg(nullptr, wflag, 1);  // pflag[0]
+        if (lazy) seg(h->ews.anyflag.as<int>() + 3, wflag + 1, 1);
+        else seg(nullptr, wflag + 1, 1);
+        if (!dense_rr) seg(h->ews.rrerr.p, wflag + 2, 2);
+        else seg(nullptr, wflag + 2, 2);
+        HIPCHK(n2v2r_launch_pack_words(src, dw, nw, ns, h->ews.rback.p, st));
+        // (lean fork: R comes from the expansion stream's own copy into prr)
+        const size_t upto = (lean && !lean_forked) ? pin_bytes : sizeof(int) * (size_t)(wflag + 8);
+        HIPCHK(hipMemcpyAsync(h->pin, h->ews.rback.p, upto, hipMemcpyDeviceToHost, st));
+        if (lean && lean_forked)  // the last 8 rows of S sit after prr in the pinned block
+          HIPCHK(hipMemcpyAsync(psl, h->ews.rback.as<unsigned>() + wsl, sizeof(float) * 8 * keep,
+                                hipMemcpyDeviceToHost, st));
       }
-      HIPCHK(hipMemcpyAsync(pth, h->theta.as<double>(), sizeof(double) * keep,
-                            hipMemcpyDeviceToHost, st));
-      if (!dense_rr)
-        HIPCHK(hipMemcpyAsync(pflag + 2, h->ews.rrerr.as<int>(), 2 * sizeof(int),
-                              hipMemcpyDeviceToHost, st));
-      if (lazy)
-        HIPCHK(hipMemcpyAsync(pflag + 1, h->ews.anyflag.as<int>() + 3, sizeof(int),
-                              hipMemcpyDeviceToHost, st));
       th_sync0 = now_ms();
       HIPCHK(hipStreamSynchronize(st));
       if (lean_forked) HIPCHK(hipEventSynchronize(h->spec_ev[1]));
