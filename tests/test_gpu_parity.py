@@ -672,3 +672,17 @@ def test_uase_cycle_redo_path(engine):
     np.testing.assert_allclose(engine.singular_values(), s0, rtol=1e-5)
     np.testing.assert_allclose(engine.singular_values(), fx["sigma"], rtol=2e-5)
     assert st["converged"] == d
+
+
+@pytest.mark.parametrize("n,d", [(20_003, 24), (100_000, 64), (300_001, 40)])
+def test_uase_sign_convention(engine, n, d):
+    """Every column of U has its largest-magnitude entry positive (the svd_flip rule the engine
+    fixes signs with), at sizes whose column-max pass runs over hundreds to a thousand row
+    chunks, with d not a multiple of the 32-column tile."""
+    from node2vec2rank_amd import synthetic
+    engine.set_layers(synthetic.er_layers(n, 12, 2, seed_base=n % 97))
+    st = engine.uase(d, seed=3)
+    assert st["converged"] == d
+    U = engine.left_embedding()[:, :d]
+    r = np.abs(U).argmax(axis=0)
+    assert (U[r, np.arange(d)] > 0).all()
