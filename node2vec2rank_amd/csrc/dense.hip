@@ -720,28 +720,34 @@ __global__ void zsum_kernel(ZSum zs, int64_t n) {
 // The per-cycle read-back packed into one device staging block (then one copy to pinned host
 // memory): up to 8 segments, each a 4-byte-word copy (src) or zero fill (src == nullptr) into
 // disjoint ranges of dst.  Five separate small copies were ~4.7 us each on the GPU timeline.
+// A segment with `clear` set also zeroes its source words after copying them (the per-cycle
+// flags, so no separate memset launch re-arms them for the next cycle).
 struct PackSegs {
-  const unsigned* src[8];
+  unsigned* src[8];
   int dst_word[8];
   int words[8];
+  int clear[8];
   int count;
 };
 __global__ __launch_bounds__(256) void pack_words_kernel(PackSegs ps, unsigned* __restrict__ dst) {
   for (int s = 0; s < ps.count; ++s)
-    for (int w = threadIdx.x; w < ps.words[s]; w += 256)
+    for (int w = threadIdx.x; w < ps.words[s]; w += 256) {
       dst[ps.dst_word[s] + w] = ps.src[s] ? ps.src[s][w] : 0u;
+      if (ps.src[s] && ps.clear[s]) ps.src[s][w] = 0u;
+    }
 }
 
-extern "C" hipError_t n2v2r_launch_pack_words(const void* const* src, const int* dst_word,
-                                              const int* words, int count, void* dst,
-                                              hipStream_t stream) {
+extern "C" hipError_t n2v2r_launch_pack_words(void* const* src, const int* dst_word,
+                                              const int* words, const int* clear, int count,
+                                              void* dst, hipStream_t stream) {
   if (count < 1 || count > 8) return hipErrorInvalidValue;
   PackSegs ps{};
   ps.count = count;
   for (int s = 0; s < count; ++s) {
-    ps.src[s] = static_cast<const unsigned*>(src[s]);
+    ps.src[s] = static_cast<unsigned*>(src[s]);
     ps.dst_word[s] = dst_word[s];
     ps.words[s] = words[s];
+    ps.clear[s] = clear[s];
   }
   hipLaunchKernelGGL(pack_words_kernel, dim3(1), dim3(256), 0, stream, ps,
                      static_cast<unsigned*>(dst));

@@ -165,8 +165,8 @@ hipError_t n2v2r_launch_nonfinite(const void* p, int64_t count, int f64, int* fl
 hipError_t n2v2r_launch_ts_tn_zsum(const BlockList& A, int64_t n, const float* const* parts,
                                    int count, float* zout, double* partial, size_t partial_elems,
                                    double* out, hipStream_t stream);
-hipError_t n2v2r_launch_pack_words(const void* const* src, const int* dst_word, const int* words,
-                                   int count, void* dst, hipStream_t stream);
+hipError_t n2v2r_launch_pack_words(void* const* src, const int* dst_word, const int* words,
+                                   const int* clear, int count, void* dst, hipStream_t stream);
 hipError_t n2v2r_launch_zsum(const float* const* parts, int count, float* zout, int64_t n,
                              hipStream_t stream);
 hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp, double* theta, double* scr,
@@ -1473,6 +1473,7 @@ struct Eig {
     HIPCHK(hipMemsetAsync(h->ews.skipc.p, 0, sizeof(int) * 68, st));
     if (lean) h->ews.rres.ensure(sizeof(double) * 64);
     double est_scale = 1.0;  // lean: true / estimated residual seen at a failed final check
+    bool rr_armed = false;   // the Rayleigh-Ritz error words zeroed (then by every read-back)
     int lean_checks = 0;
     const bool spec_ok = band_rr && !h->comm && !lean && restart_overlap_enabled();
     const bool lean_ovl = lean && lean_overlap_enabled();
@@ -1522,7 +1523,8 @@ struct Eig {
     for (;; ++cycle) {
       dbg_cycle = cycle;
       const int q_start = (int)Q.size();
-      if (lazy) HIPCHK(hipMemsetAsync(h->ews.anyflag.as<int>() + 3, 0, sizeof(int), st));
+      // (cycle 0: armed here; later cycles: the previous cycle's read-back zeroed it)
+      if (lazy && cycle == 0) HIPCHK(hipMemsetAsync(h->ews.anyflag.as<int>() + 3, 0, sizeof(int), st));
       while ((int)Q.size() < nb_max) {
         expand_one(W.back(), Q, Q, W, /*save_band=*/true, lazy);
         ++apps;
@@ -1564,7 +1566,8 @@ struct Eig {
         const std::vector<float*> loc = local_of(Q);
         tn(blocks(loc, 0, (int)loc.size()), one(W.back()),
            h->ews.hband.as<double>() + band_off(nq - 1), nullptr);
-        HIPCHK(hipMemsetAsync(h->ews.rrerr.as<int>(), 0, 4 * sizeof(int), st));
+        if (!rr_armed) HIPCHK(hipMemsetAsync(h->ews.rrerr.as<int>(), 0, 4 * sizeof(int), st));
+        rr_armed = true;  // from here on each read-back zeroes the words it reads
         lds_poison();
         if (sturm_now) {
           const bool spec_fork = spec_ok && !spec_live;
@@ -1734,12 +1737,13 @@ struct Eig {
         // one pack launch + one copy: [pres | pth | pflag[8] | prr | psl] (the layout above)
         h->ews.rback.ensure(pin_bytes);
         const int wres = 0, wth = 2 * keep, wflag = 4 * keep, wrr = wflag + 8, wsl = wrr + 128;
-        const void* src[8];
-        int dw[8], nw[8], ns = 0;
-        auto seg = [&](const void* sp, int d0, int n0) {
+        void* src[8];
+        int dw[8], nw[8], clr[8], ns = 0;
+        auto seg = [&](void* sp, int d0, int n0, int cl = 0) {
           src[ns] = sp;
           dw[ns] = d0;
           nw[ns] = n0;
+          clr[ns] = cl;
           ++ns;
         };
         if (lean) {
@@ -1750,11 +1754,13 @@ struct Eig {
         }
         seg(h->theta.p, wth, 2 * keep);
         seg(nullptr, wflag, 1);  // pflag[0]
-        if (lazy) seg(h->ews.anyflag.as<int>() + 3, wflag + 1, 1);
+        // the sticky refill flag and the Rayleigh-Ritz error words are zeroed as they are read:
+        // they are armed for the next cycle (or a fallback Rayleigh-Ritz) without a memset
+        if (lazy) seg(h->ews.anyflag.as<int>() + 3, wflag + 1, 1, 1);
         else seg(nullptr, wflag + 1, 1);
-        if (!dense_rr) seg(h->ews.rrerr.p, wflag + 2, 2);
+        if (!dense_rr) seg(h->ews.rrerr.p, wflag + 2, 2, 1);
         else seg(nullptr, wflag + 2, 2);
-        HIPCHK(n2v2r_launch_pack_words(src, dw, nw, ns, h->ews.rback.p, st));
+        HIPCHK(n2v2r_launch_pack_words(src, dw, nw, clr, ns, h->ews.rback.p, st));
         // (lean fork: R comes from the expansion stream's own copy into prr)
         const size_t upto = (lean && !lean_forked) ? pin_bytes : sizeof(int) * (size_t)(wflag + 8);
         HIPCHK(hipMemcpyAsync(h->pin, h->ews.rback.p, upto, hipMemcpyDeviceToHost, st));
