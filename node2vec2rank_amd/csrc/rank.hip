@@ -99,13 +99,63 @@ __global__ __launch_bounds__(256) void distances_kernel(const float* __restrict_
   }
 }
 
+// The sequential strategy without correlation columns (the bench's and the reference's default):
+// the same sums in the same order as distances_kernel, with each thread's two embedding rows read
+// 16 dims at a time as float4 loads issued together (the scalar per-dim loads of the general form
+// touch a new line per lane per load: cfg2 132 us).  Needs ldy % 4 == 0 and ldy >= dmax rounded
+// up to 16 (rows padded to 64: checked by the launcher).
+__global__ __launch_bounds__(256) void distances_seq_kernel(const float* __restrict__ Y,
+                                                            int64_t n, int64_t ldy, int64_t lrows,
+                                                            int layer_i, DistPlan plan,
+                                                            double* __restrict__ out, int64_t ldo) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const int64_t lstride = lrows * ldy;
+  const float* y1 = Y + (int64_t)(layer_i - 1) * lstride + r * ldy;
+  const float* y2 = Y + (int64_t)layer_i * lstride + r * ldy;
+  double suv = 0, suu = 0, svv = 0, sdd = 0;
+  int next = 0;
+  for (int j0 = 0; j0 < plan.dmax; j0 += 16) {
+    f32x4 a[4], b[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      a[q] = *reinterpret_cast<const f32x4*>(y1 + j0 + 4 * q);
+      b[q] = *reinterpret_cast<const f32x4*>(y2 + j0 + 4 * q);
+    }
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int j = j0 + t;
+      if (j >= plan.dmax) break;
+      const double u = (double)a[t >> 2][t & 3], v = (double)b[t >> 2][t & 3];
+      suv += u * v;
+      suu += u * u;
+      svv += v * v;
+      const double df = u - v;
+      sdd += df * df;
+      while (next < plan.n_cols && plan.col_dim[next] == j + 1) {
+        const double res = plan.col_metric[next] == 1 ? sqrt(sdd)
+                                                      : clip02_keep_nan(1.0 - suv / sqrt(suu * svv));
+        out[(int64_t)plan.col_out[next] * ldo + r] = res;
+        ++next;
+      }
+    }
+  }
+}
+
 // Y: [K][lrows][ldy]; the first n rows are computed; column c of the output at out + c * ldo
 extern "C" hipError_t n2v2r_launch_distances(const float* Y, int K, int64_t n, int64_t ldy,
                                              int64_t lrows, int strategy, int layer_i,
                                              const DistPlan& plan, double* out, int64_t ldo,
                                              hipStream_t stream) {
-  hipLaunchKernelGGL(distances_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                     Y, K, n, ldy, lrows, strategy, layer_i, plan, out, ldo);
+  bool corr = false;
+  for (int c = 0; c < plan.n_cols; ++c) corr |= plan.col_metric[c] == 2;
+  if (strategy == 0 && !corr && layer_i >= 1 && ldy % 4 == 0 &&
+      ldy >= ((plan.dmax + 15) / 16) * 16 && (reinterpret_cast<uintptr_t>(Y) & 15) == 0)
+    hipLaunchKernelGGL(distances_seq_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       stream, Y, n, ldy, lrows, layer_i, plan, out, ldo);
+  else
+    hipLaunchKernelGGL(distances_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                       Y, K, n, ldy, lrows, strategy, layer_i, plan, out, ldo);
   return hipGetLastError();
 }
 
