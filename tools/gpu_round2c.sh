@@ -2,7 +2,7 @@
 # fit-level PMC of the cfg2 orthogonalisation kernels (separate passes, counters alone)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r02e
+O=gpurun_out/r02i
 mkdir -p $O
 export TMPDIR=/tmp
 for c in cfg1 cfg3 cfg4; do
