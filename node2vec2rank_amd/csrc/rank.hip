@@ -210,7 +210,7 @@ __device__ __forceinline__ uint64_t desc_key(double x) {
 }
 
 // keys/payload init + per-segment OR / AND of the keys (to skip constant digits).
-__global__ void borda_init_kernel(const double* __restrict__ vals, int64_t n, int nseg,
+__global__ __launch_bounds__(256) void borda_init_kernel(const double* __restrict__ vals, int64_t n, int nseg,
                                   uint64_t* __restrict__ keys, int32_t* __restrict__ idx,
                                   unsigned long long* __restrict__ seg_or,
                                   unsigned long long* __restrict__ seg_and) {
@@ -229,7 +229,21 @@ __global__ void borda_init_kernel(const double* __restrict__ vals, int64_t n, in
     kor |= (uint64_t)__shfl_xor((long long)kor, m, 64);
     kand &= (uint64_t)__shfl_xor((long long)kand, m, 64);
   }
+  // one atomic pair per workgroup, not per wave: 4x fewer on the segment's two words (every
+  // wave's atomics on one address serialise; per-wave they made the launch ~40 us at cfg2)
+  __shared__ unsigned long long wor[4], wand[4];
+  const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
+    wor[w] = kor;
+    wand[w] = kand;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nw = (int)(blockDim.x >> 6);
+    for (int q = 1; q < nw; ++q) {
+      kor |= wor[q];
+      kand &= wand[q];
+    }
     atomicOr(&seg_or[s], (unsigned long long)kor);
     atomicAnd(&seg_and[s], (unsigned long long)kand);
   }

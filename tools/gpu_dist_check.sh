@@ -8,4 +8,4 @@ tail -1 gpurun_out/dc/tests.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/dc/t -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/dc/b.json 2> gpurun_out/dc/b.err || { echo trace-fail; exit 1; }
 find gpurun_out/dc/t -name "*kernel_trace.csv" -delete
 f=$(find gpurun_out/dc/t -name "*kernel_stats.csv" | head -1)
-grep -i "distances" $f | cut -c1-160
+grep -iE "distances|borda_init" $f | cut -c1-160
