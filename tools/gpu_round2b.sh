@@ -2,7 +2,7 @@
 # rocprofv3 kernel stats of the cfg2 bench, SpMM PMC passes (FETCH_SIZE / WRITE_SIZE / trace)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r02h
+O=gpurun_out/r02j
 mkdir -p $O gpurun_out/meas
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu > $O/tests.log 2>&1 || { echo tests-fail; tail -30 $O/tests.log; exit 1; }
