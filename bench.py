@@ -1,27 +1,35 @@
-"""Benchmark: nodes ranked/s of the fit-and-rank path on MI355X.
+"""Benchmark: nodes ranked/s of the fit-and-rank path on MI355X, through the drop-in API.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg1|cfg4|cfg5]
-                    [--mode auto|replicas|partitioned]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg4|cfg1|cfg2|cfg3|cfg5]
+                    [--mode auto|replicas|partitioned] [--no-cpu-baseline] [--cpu-sample N]
 
-One step = ``fit_transform_rank()`` + ``aggregate_transform()`` of the engine on one synthetic
-2-layer graph whose CSR layers are already resident in HBM: UASE (block Krylov-Schur on the
-GPU), distances for every (dim, metric) column, Borda, and the copy of the distance table and
-Borda scores back to the host (what the reference API returns).  Default workload is
-BASELINE.json configs[1] (cfg2: 2-layer ER N=100k, avg-deg 20, d=64).
+One step = what a caller of the reference does: from host-resident
+scipy CSR layers (dense fp32 arrays for cfg3), ``N2V2R(graphs, nodes, config)`` +
+``fit_transform_rank()`` + ``aggregate_transform()`` -> host DataFrames of distances and int64
+Borda ranks (reference model.py:98-201).  Inside the step: the host->HBM copy of the layers,
+the GPU ingest (range check, transpose / symmetry detection), UASE, distances, the device->host
+copies, the DataFrames and the Borda of the frames.  ``value`` = nodes ranked/s = N x
+comparisons x steps / max-over-ranks wall time.  Default workload: BASELINE cfg4 (2-layer ER
+N=1M avg-deg 50, 10-column grid), the largest configuration that fits one GPU.
 
-Multi-GPU (torchrun, one process per GPU), two modes:
-  * replicas (default for cfg1/2/4): every rank ranks its own independent graph (different
-    generator seeds), no data-path collective, "scaling": "weak";
-  * partitioned (default for cfg5): ONE graph row-partitioned over the ranks (RCCL communicator
-    of the engine: panel all-gathers per SpMM stage, all-reduce of the Gram / Rayleigh-Ritz /
-    residual reductions), every rank builds only its own rows (counter-based ER generator),
-    "scaling": "strong".
-A gloo group provides the barrier, the max-over-ranks of the timed region and the broadcast
-of the RCCL unique id.
+Extra keys:
+  * ``device_resident``: the same work with the layers already in HBM (engine-level loop: UASE,
+    distances, Borda, copies of the tables to the host), for comparison;
+  * ``roofline``: the dominant kernel of the fit (the SpMM stage launch that takes the most
+    device time), timed by HIP events around every SpMM launch of one extra fit on the engine
+    stream (solver flag N2V2R_EIG_TIME_SPMM); achieved = SURVEY 8(d) algorithmic bytes per
+    launch (for the launch form that runs) / mean launch time; rocprofv3 summaries of the same
+    command are committed under profiles/;
+  * ``cpu_baseline`` (rank 0, N=1): BASELINE.md 3's faithful CPU restatement (ARPACK svds,
+    per-row scipy distances, O(C N^2) list.index Borda over a joblib pool) and its fast variant,
+    on all host cores available to the process (capped at 16, the box's CPU share), on a bounded
+    sample of the same graph family; full-size CPU time extrapolated (labelled) from it.
 
-Extra JSON fields: ``roofline`` (SpMM kernel, HIP-event timed on the engine stream at the
-Krylov panel width) and ``cpu_baseline`` (the reference algorithm restated in oracle/, on a
-bounded sample, rank 0 only).
+Multi-GPU (torchrun, one process per GPU): cfg1-4 run independent replicas (every rank its own
+graph through the API on its own GPU, "scaling": "weak"); cfg5 (or --mode partitioned) runs ONE
+row-partitioned graph over an RCCL communicator, every rank ingesting its own rows inside the
+timed step ("scaling": "strong").  A gloo group gives the barrier, the max-over-ranks and the
+broadcast of the RCCL unique id.
 """
 from __future__ import annotations
 
@@ -51,15 +59,11 @@ CONFIGS = {
                  desc="cfg5: 2-layer ER N=10M avg-deg 30, d=128, cosine+euclidean, sequential, "
                       "row-partitioned"),
 }
-CPU_SAMPLE = {"cfg1": 1000, "cfg2": 50_000, "cfg3": 2_000, "cfg4": 20_000, "cfg5": 20_000}
+# CPU-baseline sample sizes: ~10-30 s of host work
+CPU_SAMPLE = {"cfg1": 1000, "cfg2": 20_000, "cfg3": 2000, "cfg4": 10_000, "cfg5": 10_000}
 METRICS = ["cosine", "euclidean"]
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-# Scattered-line ceiling of the vector memory path: MI355X_MICROARCH.md's indexed-row gather
-# (1,152-B rows from an L2-resident table) runs 66-73 GB/s per CU = one 128-B line per ~4.4
-# cycles per CU, i.e. 256 CUs x 2.4 GHz / 4.4 = ~140 G lines/s.  A b = 8 SpMM touches one line
-# per stored entry (its 32-B panel row), whatever the locality (tools/spmm_locality.py: ER vs
-# a 256-wide band graph, 14.5 vs 12.6 us per 2M entries), so this, not HBM, bounds it.
-GATHER_LINE_PEAK_GLPS = 256 * 2.4 / 4.4
+MFMA_F32_PEAK_TFLOPS = 157.3
 
 
 def _dist_env():
@@ -85,21 +89,19 @@ class _Group:
         if self.dist:
             self.dist.barrier()
 
-    def max(self, x: float) -> float:
+    def _reduce(self, x, op):
         if not self.dist:
             return x
         import torch
         t = torch.tensor([x], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        self.dist.all_reduce(t, op=op)
         return float(t.item())
 
+    def max(self, x: float) -> float:
+        return self._reduce(x, self.dist.ReduceOp.MAX) if self.dist else x
+
     def sum(self, x: float) -> float:
-        if not self.dist:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
-        return float(t.item())
+        return self._reduce(x, self.dist.ReduceOp.SUM) if self.dist else x
 
     def bcast_bytes(self, b: bytes | None) -> bytes:
         if not self.dist:
@@ -122,67 +124,157 @@ def _torch_sync():
         pass
 
 
-def run_step(eng, cfg, seed, fetch=True, eig=None):
-    st = eng.uase(cfg["d"], seed=seed, **(eig or {}))
+def _config(cfg):
+    return dict(embed_dimensions=list(cfg["dims"]), distance_metrics=list(METRICS), seed=42,
+                comp_strategy="sequential", verbose=-1, save_dir=None)
+
+
+def api_step(layers, nodes, cfg, device):
+    """The reference's call sequence on the drop-in API (model.py:18, 98, 149)."""
+    from node2vec2rank_amd.model import N2V2R
+    model = N2V2R(layers, nodes, _config(cfg), device=device)
+    ranks = model.fit_transform_rank()
+    agg = model.aggregate_transform()
+    return model, ranks, agg
+
+
+def resident_step(eng, cfg, seed=42, flags=0):
+    st = eng.uase(cfg["d"], seed=seed, solver_flags=flags)
     ncmp, _ = eng.rank("sequential", cfg["dims"], METRICS)
-    out = []
-    if fetch:  # the reference API hands the distance table and the Borda scores to the caller
-        for c in range(ncmp):
-            out.append((eng.distances(c), eng.borda(c)))
+    out = [(eng.distances(c), eng.borda(c)) for c in range(ncmp)]
     return st, out
 
 
-def cpu_baseline(sample_n=20_000, avg_deg=20.0, d=64, dims=(64,), dense_layers=0):
-    """Reference algorithm (oracle/, faithful mode) on a bounded sample, 1 thread:
-    ARPACK svds + per-row scipy distances + the O(C N^2) list.index Borda."""
+def partitioned_step(eng, cfg, rows):
+    eng.set_layer_rows(cfg["n"], 2, rows)
+    return resident_step(eng, cfg)
+
+
+# ----------------------------------------------------------------------------- CPU baseline
+def _cpu_info():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    blas = []
+    try:
+        from threadpoolctl import threadpool_info
+        blas = [f"{d.get('internal_api')}:{d.get('num_threads')}" for d in threadpool_info()]
+    except Exception:
+        pass
+    return model, blas
+
+
+def _sample_layers(cfg, n, seed_base=7000):
+    from node2vec2rank_amd import synthetic
+    if cfg.get("dense"):
+        return synthetic.corr_layers(n, cfg["layers"], seed_base=seed_base)
+    return synthetic.er_layers(n, cfg["avg_deg"], 2, seed_base=seed_base)
+
+
+def cpu_baseline(cfg, n_faithful, workers, blas_threads=1):
+    """the repo's faithful CPU restatement of the reference (oracle/, checked
+    bit-exact against the reference's outputs) and its fast variant, timed on this host."""
     import scipy.sparse as sp
     from threadpoolctl import threadpool_limits
 
-    from node2vec2rank_amd import synthetic
     from oracle import n2v2r_oracle as orc
-    if dense_layers:
-        layers = [sp.csc_matrix(a) for a in synthetic.corr_layers(sample_n, dense_layers)]
-    else:
-        layers = synthetic.er_layers(sample_n, avg_deg, 2, seed_base=7000)
-    with threadpool_limits(1):
-        t0 = time.time()
-        Y, _, _ = orc.uase(layers, d, seed=42)
-        t1 = time.time()
-        ranks = orc.rank_distances(Y, list(dims), METRICS, "sequential", faithful=True)
-        t2 = time.time()
-        for _, (_, D) in ranks.items():
-            orc.borda_reference_loop(D)
-        t3 = time.time()
-    total = t3 - t0
-    fam = (f"{dense_layers}-layer dense |corrcoef| N={sample_n}" if dense_layers else
-           f"2-layer ER N={sample_n} avg-deg {avg_deg:g}")
+
+    layers = _sample_layers(cfg, n_faithful)
+    if cfg.get("dense"):
+        layers = [sp.csc_matrix(a) for a in layers]
+    with threadpool_limits(blas_threads):
+        t0 = time.perf_counter()
+        Y, _, _ = orc.uase(layers, cfg["d"], seed=42)
+        t_svds = time.perf_counter() - t0
+    stages = {}
+    for faithful in (True, False):
+        with threadpool_limits(blas_threads):
+            t1 = time.perf_counter()
+            ranks = orc.rank_distances(Y, list(cfg["dims"]), METRICS, "sequential",
+                                       faithful=faithful)
+            t2 = time.perf_counter()
+            for _, (_, D) in ranks.items():
+                if faithful:
+                    orc.borda_reference_parallel(D, n_jobs=workers)
+                else:
+                    orc.borda(D)
+            t3 = time.perf_counter()
+        stages[faithful] = {"svds": t_svds, "distances": t2 - t1, "borda": t3 - t2}
+    ncmp = len(ranks)
+    fa, fs = stages[True], stages[False]
+    n_fast = n_faithful
+    tot_fa = sum(fa.values())
+    tot_fs = sum(fs.values())
+    N = cfg["n"]
+    # extrapolation to the bench size (lower bound): svds + distances linear in N (ARPACK's
+    # application count only grows with N), Borda O(N^2) for the faithful loop
+    r = N / n_faithful
+    extra_fa = (fa["svds"] + fa["distances"]) * r + fa["borda"] * r * r
+    extra_fs = (fs["svds"] + fs["distances"] + fs["borda"]) * (N / n_fast)
+    model, blas = _cpu_info()
+    fam = ("{}-layer dense |corrcoef|".format(cfg["layers"]) if cfg.get("dense") else
+           f"2-layer ER avg-deg {cfg['avg_deg']:g}")
     return {
-        "value": sample_n * len(ranks) / total, "unit": "nodes/s", "cores": 1, "kind": "port",
-        "sample": (f"{fam}, d={d}, dims {list(dims)} x cosine+euclidean (the bench workload's "
-                   f"graph family at fewer nodes; the Borda stage is O(C N^2) so the "
-                   f"full-size rate is lower), oracle faithful mode, 1 thread"),
-        "stages_s": {"svds": round(t1 - t0, 3), "distances": round(t2 - t1, 3),
-                     "borda": round(t3 - t2, 3)},
+        "value": round(n_faithful * ncmp / tot_fa, 1), "unit": "nodes/s", "cores": workers,
+        "kind": "port",
+        "sample": (f"{fam} N={n_faithful}, d={cfg['d']}, dims {list(cfg['dims'])} x "
+                   f"cosine+euclidean, sequential: oracle faithful mode (ARPACK svds, per-row "
+                   f"scipy distances, O(C N^2) list.index Borda over a {workers}-process joblib "
+                   f"pool as model_utils.py:31-32), BLAS threads {blas_threads} (ARPACK's dense "
+                   f"updates at this size ran slower on more threads)"),
+        "stages_s": {k: round(v, 3) for k, v in fa.items()},
+        "fast": {"value": round(n_fast * ncmp / tot_fs, 1), "unit": "nodes/s",
+                 "sample": f"the same sample and svds: vectorised distances + argsort Borda",
+                 "stages_s": {k: round(v, 3) for k, v in fs.items()}},
+        "extrapolated_full_size_s": {"faithful_lower_bound": round(extra_fa, 1),
+                                     "fast_lower_bound": round(extra_fs, 1),
+                                     "note": "svds + distances scaled linearly in N (a lower "
+                                             "bound: ARPACK's application count grows with N), "
+                                             "faithful Borda as N^2; labelled extrapolated"},
+        "host": {"cpu_model": model, "os_cpu_count": os.cpu_count(), "blas": blas},
     }
 
 
-def _layers_partitioned(cfg, row0, n_local):
-    from node2vec2rank_amd import synthetic
-    return [synthetic.er_layer_rows(cfg["n"], cfg["avg_deg"], 2000 + k, row0, n_local)
-            for k in range(2)]
+# ----------------------------------------------------------------------------- roofline
+def roofline_from_stats(st, cfg, b):
+    """Dominant SpMM stage of the fit (HIP events around every launch, N2V2R_EIG_TIME_SPMM)."""
+    ms = st["gpu_ms_spmm"]
+    cnt = st["spmm_timed_launches"]
+    by = st["spmm_stage_bytes"]
+    j = int(np.argmax(ms))
+    if cnt[j] == 0:
+        return None
+    t = ms[j] / cnt[j]
+    bpl = by[j] / cnt[j]
+    out = {"bound": "hbm", "achieved": round(bpl / (t * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
+           "unit": "GB/s", "frac": round(bpl / (t * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+           "traffic": None, "stage": ["Z_k = A_k^T X", "W = sum_k A_k Z_k"][j],
+           "avg_launch_ms": round(t, 5), "launches_in_fit": int(cnt[j]),
+           "algo_bytes_per_launch": bpl,
+           "fit_spmm_gpu_ms": [round(x, 2) for x in ms], "fit_spmm_launches": [int(c) for c in cnt]}
+    if cfg.get("dense"):
+        flops = 2.0 * cfg["n"] * cfg["n"] * b  # one layer's GEMM per launch
+        out["kernel"] = "dense_gemm_kernel (A_k X, MFMA f32 32x32x2)"
+        out["mfma_tflops"] = round(flops / (t * 1e-3) / 1e12, 2)
+        out["mfma_frac"] = round(flops / (t * 1e-3) / 1e12 / MFMA_F32_PEAK_TFLOPS, 4)
+    return out
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="cfg4", choices=sorted(CONFIGS))
     ap.add_argument("--mode", default="auto", choices=["auto", "replicas", "partitioned"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=0)
-    ap.add_argument("--eig", default="", help='solver knobs as JSON, e.g. {"block": 16, '
-                    '"max_basis": 512, "keep": 320} (default: the engine defaults)')
+    ap.add_argument("--cpu-sample", type=int, default=0, help="faithful sample N override")
+    ap.add_argument("--resident-steps", type=int, default=3)
     args = ap.parse_args()
 
     world, rank, local = _dist_env()
@@ -191,10 +283,10 @@ def main():
     group = _Group(world)
     cfg = CONFIGS[args.config]
     mode = args.mode if args.mode != "auto" else cfg.get("mode", "replicas")
-    eig = json.loads(args.eig) if args.eig else {}
 
     from node2vec2rank_amd import _lib, synthetic
     t_build = time.perf_counter()
+    b = 32 if cfg.get("dense") else 8  # the solver's default panel width
     if mode == "partitioned":
         if world > 1:
             uid = group.bcast_bytes(_lib.comm_unique_id() if rank == 0 else None)
@@ -203,83 +295,92 @@ def main():
             eng = _lib.Engine(local)
         eng.set_layer_rows(cfg["n"], 2, [])  # partition first
         _, _, row0, n_local = eng.dist_info()
-        local_layers = _layers_partitioned(cfg, row0, n_local)
-        nnz = [int(group.sum(float(a.nnz))) for a in local_layers]
-        eng.set_layer_rows(cfg["n"], 2, local_layers)  # local CSR rows -> HBM, untimed
-        del local_layers
-        seed = 42
+        rows = [synthetic.er_layer_rows(cfg["n"], cfg["avg_deg"], 2000 + k, row0, n_local)
+                for k in range(2)]
+        nnz = [int(group.sum(float(a.nnz))) for a in rows]
         nodes_per_step = float(cfg["n"])  # one graph, ranked once, over all ranks
-    elif cfg.get("dense"):
-        eng = _lib.Engine(local)
-        layers = synthetic.corr_layers(cfg["n"], cfg["layers"], seed_base=17 * rank)
-        nnz = [int(cfg["n"]) ** 2] * cfg["layers"]
-        eng.set_layers(layers, storage="dense", symmetric=1)  # dense fp32 -> HBM, untimed
-        del layers
-        seed = 42 + rank
-        nodes_per_step = group.sum(float(cfg["n"]))
+        step = lambda: partitioned_step(eng, cfg, rows)  # noqa: E731
     else:
-        eng = _lib.Engine(local)
-        layers = synthetic.er_layers(cfg["n"], cfg["avg_deg"], 2, seed_base=1000 + 17 * rank)
-        nnz = [int(a.nnz) for a in layers]
-        eng.set_layers(layers)  # CSR -> HBM, untimed (inputs resident when timing starts)
-        del layers
-        seed = 42 + rank
+        if cfg.get("dense"):
+            layers = synthetic.corr_layers(cfg["n"], cfg["layers"], seed_base=17 * rank)
+            nnz = [int(cfg["n"]) ** 2] * cfg["layers"]
+        else:
+            layers = synthetic.er_layers(cfg["n"], cfg["avg_deg"], 2, seed_base=1000 + 17 * rank)
+            nnz = [int(a.nnz) for a in layers]
+        nodes = [f"n{i}" for i in range(cfg["n"])]
         nodes_per_step = group.sum(float(cfg["n"]))  # every rank ranks its own graph
+        step = lambda: api_step(layers, nodes, cfg, local)  # noqa: E731
     t_build = time.perf_counter() - t_build
-    fetch = mode == "replicas" or rank == 0
 
     for _ in range(args.warmup):
-        run_step(eng, cfg, seed, fetch, eig)
-    eng.synchronize()
+        step()
     _torch_sync()
     group.barrier()
     t0 = time.perf_counter()
-    stats = None
     for _ in range(args.steps):
-        stats, _ = run_step(eng, cfg, seed, fetch, eig)
-    eng.synchronize()
+        res = step()
     _torch_sync()
     group.barrier()
     elapsed = time.perf_counter() - t0
     elapsed_max = group.max(elapsed)
-    ncmp = eng.ncmp  # comparisons per step (K - 1 for "sequential")
+    ncmp = 1  # comparisons per step (K - 1 for "sequential" with K = 2; cfg3: 3)
+    if mode == "partitioned":
+        stats = res[0]
+    else:
+        model = res[0]
+        ncmp = len(res[1])
+        stats = model.eig_stats
     value = nodes_per_step * ncmp * args.steps / elapsed_max
 
-    # dominant kernel: the CSR x panel SpMM at the Krylov panel width, HIP events on the
-    # engine stream (same launch configuration as inside UASE; this rank's rows when
-    # partitioned)
-    b = int(eig.get("block", 0)) or (32 if cfg.get("dense") else 8)  # the solver's panel width
-    X = np.random.default_rng(0).standard_normal((cfg["n"], b)).astype(np.float32)
-    col_blocks = (not cfg.get("dense")) and eng.spmm_col_blocks(b)
-    nloc_rows = float(eng.dist_info()[3])
-    _, spmm_ms, spmm_bytes = eng.bench_spmm(0, X, reps=50, want_y=False)
-    del X
-    achieved = spmm_bytes / (spmm_ms * 1e-3) / 1e9
-    # panel rows gathered per launch (4 b bytes per nnz, served by L2 / Infinity Cache): not
-    # HBM bytes, reported beside the roofline
-    gathered = (None if cfg.get("dense") else
-                4.0 * b * float(nnz[0]) / max(1, world if mode == "partitioned" else 1))
-    lines_per_launch = (None if gathered is None else
-                        float(nnz[0]) / max(1, world if mode == "partitioned" else 1)
-                        * max(1, (4 * b) // 128))
-    ms_dist, ms_borda = eng.rank_timing()
-
-    traffic = None
+    # device-resident form of the same work, and one instrumented fit for the roofline
+    if mode == "partitioned":
+        reng = eng
+    else:
+        reng = _lib.Engine(local)  # a handle of its own (the API's shared one keeps its state)
+        if cfg.get("dense"):
+            reng.set_layers(layers, storage="dense", symmetric=1)
+        else:
+            reng.set_layers(layers)
+    reng.synchronize()
+    group.barrier()
+    t1 = time.perf_counter()
+    for _ in range(args.resident_steps):
+        resident_step(reng, cfg)
+    reng.synchronize()
+    group.barrier()
+    res_ms = group.max(time.perf_counter() - t1) / max(1, args.resident_steps) * 1e3
+    st_t, _ = resident_step(reng, cfg, flags=_lib.EIG_TIME_SPMM)
+    roof = roofline_from_stats(st_t, cfg, b)
+    if roof is not None and not cfg.get("dense"):
+        col_blocks = reng.spmm_col_blocks(b)
+        roof["kernel"] = ("spmm8_cb_kernel (XCD-local column blocks; + cb_reduce on a side "
+                          "stream)" if col_blocks else "spmm8_pipe_kernel (b = 8, XCD-split "
+                          "layers)" if b == 8 else f"spmm_csr_panel_kernel<{b}>")
+        # one 32-B panel row gathered per stored entry (served by L2 / Infinity Cache): the
+        # line-access rate, reported beside the HBM roofline
+        # entries per launch: every layer's in one row-kernel launch, one layer's per
+        # column-block launch
+        nnz_launch = float(sum(nnz)) / (world if mode == "partitioned" else 1)
+        ent = nnz_launch / len(nnz) if col_blocks else nnz_launch
+        roof["gathered_entries_per_launch"] = ent
+        roof["gather_G_entries_per_s"] = round(ent / (roof["avg_launch_ms"] * 1e-3) / 1e9, 1)
     tpath = os.path.join(REPO, "profiles", "spmm_traffic.json")
-    if os.path.exists(tpath) and world == 1:
+    if roof is not None and os.path.exists(tpath) and world == 1:
         try:
             t = json.load(open(tpath))
-            if t.get("config") == args.config and int(t.get("b", -1)) == b:
-                traffic = t.get("bytes_per_launch")
+            if t.get("config") == args.config and t.get("stage") == roof["stage"]:
+                roof["traffic"] = t.get("bytes_per_launch")
+                roof["traffic_source"] = t.get("source")
         except Exception:
-            traffic = None
+            pass
 
     if mode == "partitioned":
         par = f"row-partitioned x{world} (RCCL)" if world > 1 else "row-partitioned x1"
     else:
         par = f"replicas x{world}" if world > 1 else "single"
     result = {
-        "metric": "nodes ranked/sec (fit_transform_rank + aggregate_transform)",
+        "metric": "nodes ranked/sec (fit_transform_rank + aggregate_transform, host CSR in, "
+                  "host DataFrames out)",
         "value": round(value, 1),
         "unit": "nodes/s",
         "n_gpus": world,
@@ -294,46 +395,28 @@ def main():
         "config": {"workload": cfg["desc"], "nodes": cfg["n"], "layers": cfg.get("layers", 2),
                    "avg_degree": cfg["avg_deg"], "nnz_per_layer": nnz, "embed_dim": cfg["d"],
                    "columns": len(cfg["dims"]) * len(METRICS), "comparisons": ncmp,
-                   "parallelism": par},
-        "roofline": {"bound": "hbm",
-                     "kernel": ("dense_gemm_kernel<1> (A_k X, MFMA f32)" if cfg.get("dense")
-                                else ("spmm8_cb_kernel<*> + cb_reduce_kernel (b=8, XCD-local "
-                                      "column blocks)" if col_blocks
-                                      else ("spmm8_pipe_kernel<*> (b=8)" if b == 8
-                                            else f"spmm_csr_panel_kernel<{b},*>"))),
-                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "algo_bytes_per_launch": spmm_bytes, "avg_launch_ms": round(spmm_ms, 5),
-                     "gathered_bytes_per_launch": gathered,
-                     # column blocks: 8 partial outputs written and re-read by the reduce
-                     # (HBM bytes beyond the algorithmic ones)
-                     "partial_bytes_per_launch": (2.0 * 8 * 4 * 8 * nloc_rows
-                                                  if col_blocks else 0.0),
-                     "gather_GBps": (None if gathered is None else
-                                     round(gathered / (spmm_ms * 1e-3) / 1e9, 1)),
-                     # the bound that applies: 128-B lines touched by the panel-row gathers
-                     # (one per stored entry while a panel row fits one line)
-                     "gather_lines_per_launch": (None if gathered is None else
-                                                 lines_per_launch),
-                     "gather_line_rate_Glps": (None if gathered is None else
-                                               round(lines_per_launch / (spmm_ms * 1e-3) / 1e9, 1)),
-                     "gather_line_peak_Glps": round(GATHER_LINE_PEAK_GLPS, 1),
-                     "gather_line_frac": (None if gathered is None else
-                                          round(lines_per_launch / (spmm_ms * 1e-3) / 1e9
-                                                / GATHER_LINE_PEAK_GLPS, 4))},
-        "eig": {k: (float(f"{v:.4g}") if isinstance(v, float) else v) for k, v in stats.items()},
-        "eig_options": eig,
-        "rank_ms": {"distances": round(ms_dist, 3), "borda": round(ms_borda, 3)},
+                   "parallelism": par,
+                   "timed_path": ("per-rank CSR rows -> HBM + UASE + distances + Borda -> host"
+                                  if mode == "partitioned" else
+                                  "host CSR -> N2V2R -> fit_transform_rank -> "
+                                  "aggregate_transform -> host DataFrames (H2D included)")},
+        "device_resident": {"ms_per_step": round(res_ms, 3),
+                            "value": round(nodes_per_step * ncmp / (res_ms * 1e-3), 1)},
+        "roofline": roof,
+        "eig": {k: (float(f"{v:.4g}") if isinstance(v, float) else v)
+                for k, v in (stats or {}).items()},
         "setup_s": round(t_build, 2),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(
-            sample_n=args.cpu_sample or CPU_SAMPLE[args.config], avg_deg=cfg["avg_deg"],
-            d=cfg["d"], dims=tuple(cfg["dims"]),
-            dense_layers=cfg["layers"] if cfg.get("dense") else 0)
+        workers = max(1, min(16, os.cpu_count() or 1))
+        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample or CPU_SAMPLE[args.config],
+                                              workers)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    eng.close()
+    if mode == "partitioned":
+        eng.close()
+    else:
+        reng.close()
     group.close()
 
 

@@ -37,7 +37,8 @@ typedef enum {
   N2V2R_ERR_OUT_OF_MEMORY = 5,      /* -> MemoryError */
   N2V2R_ERR_NOT_READY = 6,          /* -> ValueError("No n2v2r embeddings found"), model.py:199 */
   N2V2R_ERR_UNSUPPORTED_AGG = 7,    /* -> NotImplementedError, model.py:182-183 */
-  N2V2R_ERR_INTERNAL = 8            /* -> RuntimeError (host-side failure, e.g. a thread) */
+  N2V2R_ERR_INTERNAL = 8,           /* -> RuntimeError (host-side failure, e.g. a thread) */
+  N2V2R_ERR_RCCL = 9                /* -> RuntimeError (an RCCL collective or communicator failed) */
 } n2v2r_status;
 
 /* comp_strategy (model.py:59-84) */
@@ -46,13 +47,19 @@ enum { N2V2R_SEQUENTIAL = 0, N2V2R_ONE_VS_BEFORE = 1, N2V2R_ONE_VS_REST = 2 };
 enum { N2V2R_COSINE = 0, N2V2R_EUCLIDEAN = 1, N2V2R_CORRELATION = 2 };
 /* symmetric hint for n2v2r_set_layer_csr */
 enum { N2V2R_SYM_DETECT = -1, N2V2R_SYM_NO = 0, N2V2R_SYM_YES = 1 };
+/* n2v2r_rank method: Borda (model.py:179-183), or distances only (the caller aggregates later
+ * through n2v2r_borda_columns, as aggregate_transform recomputes from the current frames) */
+enum { N2V2R_AGG_BORDA = 0, N2V2R_AGG_NONE = -1 };
 
 /* n2v2r_eig_opts.solver_flags */
 enum { N2V2R_EIG_FULL_FIRST_PASS = 1, N2V2R_EIG_DENSE_RR = 2,
        N2V2R_EIG_TEST_REDO_CYCLE = 4 /* tests: re-expand the first cycle as after a refill */,
        N2V2R_EIG_TEST_BAND_FAIL = 8 /* tests: every banded Rayleigh-Ritz result is treated as
                                        failed, so the reducing, then the dense fallback runs
-                                       (and a lean-image fit reruns with images kept) */ };
+                                       (and a lean-image fit reruns with images kept) */,
+       N2V2R_EIG_TIME_SPMM = 16 /* HIP events around every SpMM stage launch of the fit: fills
+                                   n2v2r_eig_stats.gpu_ms_spmm / spmm_timed_launches (the in-fit
+                                   roofline of bench.py; adds an event pair per launch) */ };
 
 typedef struct n2v2r_handle n2v2r_handle;
 typedef struct n2v2r_simgroup n2v2r_simgroup;
@@ -84,6 +91,14 @@ typedef struct {
   int stagnated;             /* 1: stopped at the fp32 residual floor (flat 8 cycles, <= 100x tol) */
   int rr_fallbacks;          /* Rayleigh-Ritz cycles whose Sturm/inverse-iteration vectors failed
                                 the residual check and were redone by the reducing path */
+  /* N2V2R_EIG_TIME_SPMM only (else 0): device time of the fit's SpMM stage launches (HIP events
+   * on the engine stream), their count and their algorithmic bytes (per launch
+   * form), split by stage: [0] = Z_k = A_k^T X (all layers), [1] = W = sum_k A_k Z_k */
+  double gpu_ms_spmm[2];
+  int64_t spmm_timed_launches[2];
+  double spmm_stage_bytes[2];
+  double est_scale;          /* lean images: the last true / estimated residual scale (1 = none) */
+  int lean_checks;           /* lean images: true-residual checks run */
 } n2v2r_eig_stats;
 
 /* lifecycle */
@@ -112,8 +127,10 @@ int n2v2r_create_sim(int device, n2v2r_simgroup* g, int rank, n2v2r_handle** out
 int n2v2r_dist_info(const n2v2r_handle* h, int* rank, int* world, int64_t* row0, int64_t* n_local);
 
 /* graph layers: K layers over the same N nodes.  CSR is copied to HBM (int64 row pointers are
- * accepted; int32 column indices; fp32 values).  symmetric: N2V2R_SYM_* (DETECT compares the
- * pattern and values with the transpose on the host).  Non-symmetric layers also keep A^T. */
+ * accepted; int32 column indices; fp32 values).  The column-index range check, the transpose
+ * (stable LSD radix sort of the entries by column on the GPU) and symmetric = N2V2R_SYM_DETECT
+ * (A compared with A^T entry by entry on the GPU) run on the device.  Non-symmetric layers also
+ * keep A^T. */
 int n2v2r_set_num_layers(n2v2r_handle* h, int num_layers, int64_t n);
 int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const int64_t* indptr,
                         const int32_t* indices, const float* data, int symmetric);
@@ -138,7 +155,8 @@ int n2v2r_set_embedding(n2v2r_handle* h, int num_layers, int64_t n, int d, const
 
 /* fit-and-rank tail: distances for every (comparison, dim, metric) column and their Borda
  * aggregate, all device-resident.  Columns: dims outer, metrics inner, cosine skipped at dim 1.
- * method: 0 = Borda (only one supported, model.py:179-183). */
+ * method: N2V2R_AGG_BORDA (the only aggregation, model.py:179-183) or N2V2R_AGG_NONE
+ * (distances only; n2v2r_get_borda then returns N2V2R_ERR_NOT_READY). */
 int n2v2r_rank(n2v2r_handle* h, int strategy, const int* dims, int n_dims, const int* metrics,
                int n_metrics, int method, int* n_comparisons, int* n_cols);
 int n2v2r_get_distances(n2v2r_handle* h, int comparison, double* D /* C*N, column-major */);

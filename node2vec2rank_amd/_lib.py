@@ -24,6 +24,9 @@ ERR_OUT_OF_MEMORY = 5
 ERR_NOT_READY = 6
 ERR_UNSUPPORTED_AGG = 7
 ERR_INTERNAL = 8
+ERR_RCCL = 9
+AGG_BORDA, AGG_NONE = 0, -1
+EIG_TIME_SPMM = 16
 
 STRATEGY = {"sequential": 0, "one_vs_before": 1, "one_vs_rest": 2}
 METRIC = {"cosine": 0, "euclidean": 1, "correlation": 2}
@@ -63,10 +66,17 @@ class EigStats(ctypes.Structure):
                 ("ms_spmm", ctypes.c_double), ("ms_ortho", ctypes.c_double),
                 ("ms_rr_host", ctypes.c_double), ("spmm_launches", ctypes.c_int64),
                 ("spmm_algo_bytes", ctypes.c_double), ("stagnated", ctypes.c_int),
-                ("rr_fallbacks", ctypes.c_int)]
+                ("rr_fallbacks", ctypes.c_int), ("gpu_ms_spmm", ctypes.c_double * 2),
+                ("spmm_timed_launches", ctypes.c_int64 * 2),
+                ("spmm_stage_bytes", ctypes.c_double * 2), ("est_scale", ctypes.c_double),
+                ("lean_checks", ctypes.c_int)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        out = {}
+        for k, _ in self._fields_:
+            v = getattr(self, k)
+            out[k] = list(v) if isinstance(v, ctypes.Array) else v
+        return out
 
 
 _lib = None
@@ -254,6 +264,8 @@ class Engine:
             raise MemoryError(msg)
         if st == ERR_BAD_ARG:
             raise ValueError(msg)
+        if st == ERR_RCCL:
+            raise RuntimeError(f"RCCL failure: {msg}")
         raise RuntimeError(msg)
 
     # -- layers ----------------------------------------------------------------------------
@@ -362,7 +374,9 @@ class Engine:
         self.num_layers, self.n, self.d = K, n, d
 
     # -- rank --------------------------------------------------------------------------------
-    def rank(self, strategy: str, dims, metrics, method: int = 0):
+    def rank(self, strategy: str, dims, metrics, method: int = AGG_BORDA):
+        """Distances for every (comparison, dim, metric) column on the GPU; their Borda aggregate
+        too unless ``method=AGG_NONE``."""
         if strategy not in STRATEGY:
             raise ValueError(f"unknown comp_strategy {strategy!r}")
         mids = []

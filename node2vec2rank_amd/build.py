@@ -16,7 +16,7 @@ LIB = os.path.join(OUT_DIR, "libn2v2r_hip.so")
 OBJ_DIR = os.path.join(OUT_DIR, "obj")
 
 HIP_SOURCES = ["spmm.hip", "dense.hip", "gemm.hip", "rank.hip", "rr.hip", "rr_band.hip",
-               "rr_sturm.hip", "engine.cpp"]
+               "rr_sturm.hip", "ingest.hip", "engine.cpp"]
 HOST_SOURCES: list = []
 HEADERS = ["common.h", "spmm_args.h", os.path.join("..", "..", "include", "n2v2r.h")]
 ARCH = os.environ.get("N2V2R_OFFLOAD_ARCH", "gfx950")

@@ -1495,6 +1495,13 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
     }
     __syncthreads();
   }
+  // a pass that would apply no block still runs when Z's own Gram is off the identity by more
+  // than skip_tol (its Cholesky step is what restores orthonormality inside the block)
+  int zz_off = 0;
+  if (skip_tol > 0.f && tid < 64) {
+    const int i = tid >> 3, j = tid & 7;
+    zz_off = __ballot(fabs(gd[(c + i) * 8 + j] - (i == j ? 1.0 : 0.0)) > (double)skip_tol) != 0ull;
+  }
   if (tid < 64) {
     bool on = tid < nblk;
     if (on && skip_tol > 0.f) on = bflag[tid] != 0;
@@ -1507,15 +1514,15 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
     if (skipped && lead && on && skip_tol > 0.f) atomicAdd(skipped + 1 + tid, 1);  // histogram
     if (tid == 0) {
       badw[1] = (int)__popcll(m);
-      badw[2] = (int)(unsigned)(m & 0xFFFFFFFFull);
-      badw[3] = (int)(unsigned)(m >> 32);
+      badw[2] = zz_off;
+      badw[3] = 0;
     }
   }
   __syncthreads();
   if (stop == 2) return;
   const int napply = badw[1];
   if (skip_tol > 0.f) {
-    if (napply == 0) {
+    if (napply == 0 && !badw[2]) {
       if (lead && tid < 8) flags[tid] = 0;
       if (lead && tid == 0) {
         *any_flag = 0;

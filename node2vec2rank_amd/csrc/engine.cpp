@@ -65,6 +65,16 @@ struct SpmmCbArgs {  // spmm.hip: column block j of one layer, partial j at P + 
   float* P;
   int64_t pstride;
 };
+struct SpmmTileArgs {  // spmm.hip: row tiles x column-block phases
+  const CsrBlk* blk;
+  const float* X[8];
+  float* Y[8];
+  int64_t ldx, ldy;
+  int64_t n;
+  int K;
+  int sum;
+  int tile_rows;
+};
 #define DIST_MAX_COLS 256
 struct DistPlan {
   int n_cols;
@@ -79,6 +89,9 @@ hipError_t n2v2r_launch_row_sums(const CsrDev& A, float* out, hipStream_t stream
 hipError_t n2v2r_launch_spmm_cb(const SpmmCbArgs& a, hipStream_t stream);
 hipError_t n2v2r_launch_cb_reduce(const float* P, int nparts, int64_t pstride, int64_t n,
                                   float* out, int64_t ldo, hipStream_t stream);
+hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, int rpw, hipStream_t stream);
+int n2v2r_spmm_tile_rows(int64_t n, int ncu);
+int n2v2r_cb_rpw(const CsrBlk* A, int64_t n);
 hipError_t n2v2r_launch_cb_count(const CsrDev& A, int64_t cw, int32_t* cnt, hipStream_t stream);
 hipError_t n2v2r_launch_cb_fill(const CsrDev& A, int64_t cw, const int64_t* rp, int32_t* idx,
                                 float* dat, hipStream_t stream);
@@ -174,6 +187,18 @@ hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp, double* the
                                  hipStream_t stream, hipEvent_t before_vectors,
                                  hipStream_t vec_stream, hipEvent_t after_vectors);
 size_t n2v2r_rr_sturm_scratch(int c, int p);
+hipError_t n2v2r_launch_csr_scan(const int64_t* ip, const int32_t* ix, const float* dv,
+                                 int64_t n_rows, int64_t n_cols, uint64_t* keys, int32_t* idx,
+                                 unsigned* flags, hipStream_t stream);
+hipError_t n2v2r_launch_csr_from_sorted(const uint64_t* keys, const int32_t* idx, const float* dv,
+                                        int64_t nnz, int64_t n_cols, int64_t* tp, int32_t* tx,
+                                        float* td, hipStream_t stream);
+hipError_t n2v2r_launch_csr_compare(const int64_t* ap, const int32_t* ax, const float* av,
+                                    const int64_t* bp, const int32_t* bx, const float* bv,
+                                    int64_t n_rows, int64_t nnz, unsigned* flag,
+                                    hipStream_t stream);
+hipError_t n2v2r_launch_csr_rebase(const int64_t* ip, int64_t r0, int64_t nr, int64_t* out,
+                                   hipStream_t stream);
 }
 
 // Rayleigh-Ritz at b = 8: the band Sturm / inverse-iteration form (rr_sturm.hip) unless
@@ -549,6 +574,7 @@ struct EigWorkspace {
   DevBuf spec_partial, spec_gsmall, spec_flg, spec_any;
   DevBuf rres;                                // lean images: R of the restart projection
   DevBuf skipc;                               // full passes skipped (selective reorthogonalisation)
+  DevBuf tblk;                                // tiled SpMM: CsrBlk [2][K][CB_NB] (stage 1, stage 2)
 };
 }  // namespace
 
@@ -605,6 +631,9 @@ struct n2v2r_handle {
   DevBuf Dloc;              // [ncmp][ncols][npad] fp64 (distributed)
   DevBuf Dgat;              // [world][npad] staging of one gathered column
   DevBuf borda;             // [ncmp][n] int64
+  bool have_borda = false;  // n2v2r_rank aggregated (N2V2R_AGG_BORDA)
+  // N2V2R_EIG_TIME_SPMM: event pairs around the fit's SpMM stage launches (reused across fits)
+  std::vector<hipEvent_t> tev;
   double ms_dist = 0, ms_borda = 0;
 
   // scratch
@@ -683,7 +712,7 @@ int guarded(n2v2r_handle* h, F&& f) {
     return N2V2R_ERR_HIP;
   } catch (const NcclFail& nf) {
     h->set_err("RCCL error %d (%s) at %s", (int)nf.r, ncclGetErrorString(nf.r), nf.where.c_str());
-    return N2V2R_ERR_HIP;
+    return N2V2R_ERR_RCCL;
   } catch (const StatusFail& sf) {
     h->err = sf.msg;
     return sf.code;
@@ -740,112 +769,6 @@ bool host_indices_in_range(int64_t nnz, const int32_t* ix, int64_t n) {
     res[t] = ok(p0, std::min<int64_t>(nnz, p0 + per)) ? 1 : 0;
   });
   for (char c : res)
-    if (!c) return false;
-  return true;
-}
-
-void host_transpose(int64_t n, int64_t nnz, const int64_t* ip, const int32_t* ix, const float* dv,
-                    std::vector<int64_t>& tp, std::vector<int32_t>& tx, std::vector<float>& td) {
-  tp.assign(n + 1, 0);
-  tx.resize(nnz);
-  td.resize(nnz);
-  // Counting sort.  Large layers: rows split into nt ordered chunks, per-chunk column counts,
-  // chunk t's entries of a column placed after chunks 0..t-1's, so every transpose row keeps
-  // ascending source-row order (the same output as the serial sort).
-  int nt = host_threads();
-  while (nt > 1 && (double)nt * (double)n * 8.0 > 1024.0 * 1024 * 1024) --nt;
-  if (nnz < (int64_t)1 << 22 || n < 4096) nt = 1;
-  if (nt == 1) {
-    for (int64_t p = 0; p < nnz; ++p) tp[ix[p] + 1]++;
-    for (int64_t i = 0; i < n; ++i) tp[i + 1] += tp[i];
-    std::vector<int64_t> cur(tp.begin(), tp.end() - 1);
-    for (int64_t r = 0; r < n; ++r)
-      for (int64_t p = ip[r]; p < ip[r + 1]; ++p) {
-        const int64_t q = cur[ix[p]]++;
-        tx[q] = (int32_t)r;
-        td[q] = dv[p];
-      }
-    return;
-  }
-  const int64_t per = (n + nt - 1) / nt;
-  std::vector<int64_t> cnt((size_t)nt * n, 0);  // [chunk][column] counts, then cursors
-  auto run = [&](auto&& fn) { parallel_chunks(nt, fn); };
-  run([&](int t) {
-    int64_t* c = cnt.data() + (size_t)t * n;
-    const int64_t r0 = std::min<int64_t>(n, t * per), r1 = std::min<int64_t>(n, r0 + per);
-    for (int64_t p = ip[r0]; p < ip[r1]; ++p) c[ix[p]]++;
-  });
-  run([&](int t) {  // column totals, for columns of slice t
-    const int64_t c0 = std::min<int64_t>(n, t * per), c1 = std::min<int64_t>(n, c0 + per);
-    for (int64_t col = c0; col < c1; ++col) {
-      int64_t s = 0;
-      for (int u = 0; u < nt; ++u) s += cnt[(size_t)u * n + col];
-      tp[col + 1] = s;
-    }
-  });
-  for (int64_t i = 0; i < n; ++i) tp[i + 1] += tp[i];
-  run([&](int t) {  // per-chunk start offsets, for columns of slice t
-    const int64_t c0 = std::min<int64_t>(n, t * per), c1 = std::min<int64_t>(n, c0 + per);
-    for (int64_t col = c0; col < c1; ++col) {
-      int64_t s = tp[col];
-      for (int u = 0; u < nt; ++u) {
-        const int64_t k = cnt[(size_t)u * n + col];
-        cnt[(size_t)u * n + col] = s;
-        s += k;
-      }
-    }
-  });
-  run([&](int t) {
-    int64_t* cur = cnt.data() + (size_t)t * n;
-    const int64_t r0 = std::min<int64_t>(n, t * per), r1 = std::min<int64_t>(n, r0 + per);
-    for (int64_t r = r0; r < r1; ++r)
-      for (int64_t p = ip[r]; p < ip[r + 1]; ++p) {
-        const int64_t q = cur[ix[p]]++;
-        tx[q] = (int32_t)r;
-        td[q] = dv[p];
-      }
-  });
-}
-
-bool host_is_symmetric(int64_t n, const int64_t* ip, const int32_t* ix, const float* dv,
-                       const std::vector<int64_t>& tp, const std::vector<int32_t>& tx,
-                       const std::vector<float>& td) {
-  // A == A^T iff row r of A equals row r of A^T as (sorted col, value) multisets.  Transpose
-  // rows come out column-sorted; a column-sorted row of A (the Python side sorts) compares in
-  // place, an unsorted one through a sorted copy.  Rows are split over up to 16 host threads.
-  auto rows_match = [&](int64_t r0, int64_t r1) -> bool {
-    std::vector<std::pair<int32_t, float>> ra, rb;
-    for (int64_t r = r0; r < r1; ++r) {
-      const int64_t a0 = ip[r], a1 = ip[r + 1], b0 = tp[r], b1 = tp[r + 1];
-      if (a1 - a0 != b1 - b0) return false;
-      bool sorted_a = true;
-      for (int64_t p = a0 + 1; p < a1; ++p)
-        if (ix[p] < ix[p - 1]) sorted_a = false;
-      if (sorted_a) {
-        for (int64_t i = 0; i < a1 - a0; ++i)
-          if (ix[a0 + i] != tx[b0 + i] || !(dv[a0 + i] == td[b0 + i])) return false;
-        continue;
-      }
-      ra.clear();
-      rb.clear();
-      for (int64_t p = a0; p < a1; ++p) ra.emplace_back(ix[p], dv[p]);
-      for (int64_t p = b0; p < b1; ++p) rb.emplace_back(tx[p], td[p]);
-      std::sort(ra.begin(), ra.end());
-      if (ra != rb) return false;
-    }
-    return true;
-  };
-  const int64_t nnz = ip[n];
-  int nt = host_threads();
-  if (nnz < (int64_t)1 << 20 || n < 4096) nt = 1;
-  if (nt == 1) return rows_match(0, n);
-  std::vector<char> ok(nt, 1);
-  const int64_t per = (n + nt - 1) / nt;
-  parallel_chunks(nt, [&](int t) {
-    const int64_t r0 = std::min<int64_t>(n, t * per), r1 = std::min<int64_t>(n, r0 + per);
-    ok[t] = rows_match(r0, r1) ? 1 : 0;
-  });
-  for (char c : ok)
     if (!c) return false;
   return true;
 }
@@ -923,6 +846,10 @@ struct Eig {
   bool full_first = false;  // N2V2R_EIG_FULL_FIRST_PASS
   bool band_rr = false;     // banded Rayleigh-Ritz (b = 8, c <= 512), else dense
   bool col_blocks = false;  // XCD-local column-block SpMM (b = 8, large panels)
+  // column blocks as row tiles x block phases with LDS accumulators (no partials, no reduce;
+  // N2V2R_SPMM_TILE=0: the partial + reduce form)
+  bool tiled = false;
+  int tile_rows = 0, tile_rpw[2] = {0, 0};
   // XCD-split second SpMM stage (b = 8, one GPU): A_k Z_k lands in per-layer partials on the
   // XCDs of layer k; the image W = sum_k of them is stored by the next Gram pass that reads it
   // (the local first pass of the next expansion), or by materialize() before any other use
@@ -946,6 +873,49 @@ struct Eig {
   double* gsm_p = nullptr;
   int* flg_p = nullptr;
   int* any_p = nullptr;
+
+  // N2V2R_EIG_TIME_SPMM: an event pair around every SpMM stage launch (h->tev, reused), its
+  // stage (0: A_k^T X, 1: A_k Z_k) and algorithmic bytes; summed after the fit's last sync
+  bool time_spmm = false;
+  std::vector<int> tkind;
+  std::vector<double> tbytes;
+  int tbeg() {
+    if (!time_spmm) return -1;
+    const size_t i = tkind.size();
+    while (h->tev.size() < 2 * (i + 1)) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreate(&e));
+      h->tev.push_back(e);
+    }
+    HIPCHK(hipEventRecord(h->tev[2 * i], st));
+    tkind.push_back(-1);
+    tbytes.push_back(0.0);
+    return (int)i;
+  }
+  void tend(int i, int kind, double bytes) {
+    if (i < 0) return;
+    HIPCHK(hipEventRecord(h->tev[2 * (size_t)i + 1], st));
+    tkind[i] = kind;
+    tbytes[i] = bytes;
+  }
+  void tsum(n2v2r_eig_stats* out) {
+    if (!time_spmm || !out) return;
+    HIPCHK(hipStreamSynchronize(st));
+    for (size_t i = 0; i < tkind.size(); ++i) {
+      if (tkind[i] < 0) continue;
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, h->tev[2 * i], h->tev[2 * i + 1]));
+      out->gpu_ms_spmm[tkind[i]] += ms;
+      out->spmm_timed_launches[tkind[i]] += 1;
+      out->spmm_stage_bytes[tkind[i]] += tbytes[i];
+    }
+  }
+  double layer_bytes(int k, bool transposed) const {
+    const LayerDev& L = *h->layers[k];
+    const bool t = transposed && !L.symmetric;
+    return spmm_algo_bytes(t ? L.t_nnz : L.nnz, t ? L.t_unit : L.unit, n,
+                           (int64_t)h->world * npad, b);
+  }
 
   // N2V2R_DEBUG_FINITE: stop at the first stage whose output holds a non-finite value
   int dbg_cycle = 0, dbg_apps = 0;
@@ -1049,9 +1019,13 @@ struct Eig {
     }
     if (h->dense_layers()) {
       // Z_k = A_k^T X, W = sum_k A_k Z_k (fixed layer order), dense GEMMs on the local rows
+      // per GEMM launch: the layer rows read once (4 n N) + the panel read and the output rows
+      const double gb = 4.0 * (double)n * (double)h->n + 4.0 * (double)(ng + n) * b;
       for (int k = 0; k < K; ++k) {
         const LayerDev& L = *h->layers[k];
+        const int te = tbeg();
         h->dense_apply(L.dense_at(), L.lda, xg, b, b, h->ews.zk[k]->as<float>(), b, 0.f, nullptr);
+        tend(te, 0, gb);
       }
       for (int k = 0; k < K; ++k) {
         const LayerDev& L = *h->layers[k];
@@ -1061,10 +1035,17 @@ struct Eig {
           h->gather_panel(h->ews.zk[k]->as<float>(), zgk, b);
           zin = zgk;
         }
+        const int te = tbeg();
         h->dense_apply(L.dense_a(), L.lda, zin, b, b, Wout, b, k == 0 ? 0.f : 1.f, nullptr);
-        algo_bytes += 2.0 * (4.0 * (double)n * (double)h->n + 8.0 * (double)n * b);
+        tend(te, 1, gb);
+        algo_bytes += 2.0 * gb;
       }
       launches += 2 * K;
+      t_spmm += now_ms() - t0;
+      return;
+    }
+    if (col_blocks && tiled) {
+      apply_M_tiled(xg, Wout, ng);
       t_spmm += now_ms() - t0;
       return;
     }
@@ -1085,7 +1066,14 @@ struct Eig {
       a.X[k] = xg;
       a.Y[k] = h->ews.zk[k]->as<float>();
     }
+    double sb0 = 0.0, sb1 = 0.0;
+    for (int k = 0; k < K; ++k) {
+      sb0 += layer_bytes(k, true);
+      sb1 += layer_bytes(k, false);
+    }
+    int te = tbeg();
     HIPCHK(n2v2r_launch_spmm(a, b, st));
+    tend(te, 0, sb0);
     SpmmArgs s{};
     s.K = K;
     s.sum = 1;
@@ -1110,7 +1098,9 @@ struct Eig {
       for (int k = 0; k < K; ++k) s.Y[k] = s2part(k);
       pending = Wout;
     }
+    te = tbeg();
     HIPCHK(n2v2r_launch_spmm(s, b, st));
+    tend(te, 1, sb1);
     for (int k = 0; k < K; ++k) {
       const LayerDev& L = *h->layers[k];
       algo_bytes += spmm_algo_bytes(L.nnz, L.unit, n, n, b) +
@@ -1119,6 +1109,46 @@ struct Eig {
     }
     launches += 2;
     t_spmm += now_ms() - t0;
+  }
+
+  // apply_M with the tiled column-block SpMM: one launch per stage over all layers
+  void apply_M_tiled(const float* xg, float* Wout, int64_t ng) {
+    const CsrBlk* tb = h->ews.tblk.as<CsrBlk>();
+    SpmmTileArgs a{};
+    a.blk = tb;
+    a.ldx = a.ldy = 8;
+    a.n = n;
+    a.K = K;
+    a.sum = 0;
+    a.tile_rows = tile_rows;
+    double b0 = 0.0, b1 = 0.0;
+    for (int k = 0; k < K; ++k) {
+      a.X[k] = xg;
+      a.Y[k] = h->ews.zk[k]->as<float>();
+      b0 += layer_bytes(k, true);
+      b1 += layer_bytes(k, false);
+    }
+    int te = tbeg();
+    HIPCHK(n2v2r_launch_spmm_tile(a, tile_rpw[0], st));
+    tend(te, 0, b0);
+    SpmmTileArgs s2 = a;
+    s2.blk = tb + (size_t)K * CB_NB;
+    s2.sum = 1;
+    for (int k = 0; k < K; ++k) {
+      s2.X[k] = h->ews.zk[k]->as<float>();
+      if (h->comm) {
+        float* zgk = h->ews.zg.as<float>() + (size_t)k * ng * b;
+        h->gather_panel(h->ews.zk[k]->as<float>(), zgk, b);
+        s2.X[k] = zgk;
+      }
+      s2.Y[k] = nullptr;
+    }
+    s2.Y[0] = Wout;
+    te = tbeg();
+    HIPCHK(n2v2r_launch_spmm_tile(s2, tile_rpw[1], st));
+    tend(te, 1, b1);
+    algo_bytes += b0 + b1;
+    launches += 2;
   }
 
   // apply_M with the column-block SpMM (spmm.hip): per layer one launch per stage writing
@@ -1145,7 +1175,9 @@ struct Eig {
         a.ldx = 8;
         a.P = part + (size_t)k * CB_NB * pst;
         a.pstride = pst;
+        const int te = tbeg();
         HIPCHK(n2v2r_launch_spmm_cb(a, st));
+        tend(te, 0, layer_bytes(k, true));
         HIPCHK(hipEventRecord(h->cb_ev[k], st));
         HIPCHK(hipStreamWaitEvent(h->side, h->cb_ev[k], 0));
         HIPCHK(n2v2r_launch_cb_reduce(a.P, CB_NB, pst, n, h->ews.zk[k]->as<float>(), 8, h->side));
@@ -1160,7 +1192,9 @@ struct Eig {
         a.ldx = 8;
         a.P = part + (size_t)k * CB_NB * pst;
         a.pstride = pst;
+        const int te = tbeg();
         HIPCHK(n2v2r_launch_spmm_cb(a, st));
+        tend(te, 1, layer_bytes(k, false));
       }
       HIPCHK(n2v2r_launch_cb_reduce(part, K * CB_NB, pst, n, Wout, 8, st));
       for (int k = 0; k < K; ++k) {
@@ -1180,7 +1214,9 @@ struct Eig {
       a.ldx = 8;
       a.P = part + (size_t)k * CB_NB * pst;
       a.pstride = pst;
+      const int te = tbeg();
       HIPCHK(n2v2r_launch_spmm_cb(a, st));
+      tend(te, 0, layer_bytes(k, true));
       HIPCHK(n2v2r_launch_cb_reduce(a.P, CB_NB, pst, n, h->ews.zk[k]->as<float>(), 8, st));
     }
     for (int k = 0; k < K; ++k) {
@@ -1197,7 +1233,9 @@ struct Eig {
       a.ldx = 8;
       a.P = part + (size_t)k * CB_NB * pst;
       a.pstride = pst;
+      const int te = tbeg();
       HIPCHK(n2v2r_launch_spmm_cb(a, st));
+      tend(te, 1, layer_bytes(k, false));
     }
     HIPCHK(n2v2r_launch_cb_reduce(part, K * CB_NB, pst, n, Wout, 8, st));
     for (int k = 0; k < K; ++k) {
@@ -1358,6 +1396,9 @@ struct Eig {
     if (h->inv_s) HIPCHK(hipStreamSynchronize(h->inv_s));
     seed = o.seed ? o.seed : 0x5EEDull;
     full_first = (o.solver_flags & N2V2R_EIG_FULL_FIRST_PASS) != 0;
+    time_spmm = (o.solver_flags & N2V2R_EIG_TIME_SPMM) != 0;
+    tkind.clear();
+    tbytes.clear();
     kry0 = 0;
     bool lazy = true;
     const bool test_redo = (o.solver_flags & N2V2R_EIG_TEST_REDO_CYCLE) != 0;
@@ -1413,7 +1454,29 @@ struct Eig {
     col_blocks = col_blocks_wanted(h, b);
     if (col_blocks) {
       for (auto& Lp : h->layers) col_blocks = ensure_col_blocks(*Lp, nglob, st) && col_blocks;
-      if (col_blocks) h->ews.cbpart.ensure(sizeof(float) * (size_t)K * CB_NB * npad * 8);
+      const char* te = std::getenv("N2V2R_SPMM_TILE");  // read per fit (A/B runs, tests)
+      tiled = col_blocks && !(te && te[0] == '0');
+      if (col_blocks && !tiled)
+        h->ews.cbpart.ensure(sizeof(float) * (size_t)K * CB_NB * npad * 8);
+      if (tiled) {
+        int ncu = 0;
+        HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
+        tile_rows = n2v2r_spmm_tile_rows(n, ncu);
+        std::vector<CsrBlk> hb((size_t)2 * K * CB_NB);
+        for (int k = 0; k < K; ++k) {
+          const LayerDev& L = *h->layers[k];
+          for (int j = 0; j < CB_NB; ++j) {
+            hb[(size_t)k * CB_NB + j] = (L.symmetric ? L.cb : L.cb_t).blk[j];
+            hb[(size_t)(K + k) * CB_NB + j] = L.cb.blk[j];
+          }
+        }
+        tile_rpw[0] = n2v2r_cb_rpw(hb.data(), n);
+        tile_rpw[1] = n2v2r_cb_rpw(hb.data() + (size_t)K * CB_NB, n);
+        h->ews.tblk.ensure(sizeof(CsrBlk) * hb.size());
+        HIPCHK(hipMemcpyAsync(h->ews.tblk.p, hb.data(), sizeof(CsrBlk) * hb.size(),
+                              hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));  // hb dies here
+      }
     }
     split2 = split2_wanted(h, b) && !col_blocks;
     pending = nullptr;
@@ -1465,7 +1528,9 @@ struct Eig {
       // few blocks, the kept Ritz vectors, that lost orthogonality).  N2V2R_REORTH_TOL=0: every
       // block of every full pass.
       const char* e = std::getenv("N2V2R_REORTH_TOL");
-      reorth_tol = e ? (float)std::atof(e) : (float)(0.1 * tol);
+      // capped at 1e-6: a loose residual tolerance must not loosen the basis orthogonality the
+      // Rayleigh-Ritz and the lean residual estimates assume
+      reorth_tol = e ? (float)std::atof(e) : (float)std::min(0.1 * tol, 1e-6);
       const char* m = std::getenv("N2V2R_REORTH_MODE");  // "whole": all blocks or none
       if (m && m[0] == 'w') reorth_tol = -reorth_tol;
     }
@@ -1717,10 +1782,13 @@ struct Eig {
         // R (read back) and the restart block come from the expansion stream
       } else if (lean) {
         // the restart block now (it needs nothing from the Rayleigh-Ritz stage): its first,
-        // local pass leaves R with W_last - Q_loc C = Z_{m+1} R, Z_{m+1} orthonormal
-        E_lean = take();
-        const std::vector<float*> loc = local_of(Q);
-        orthonormalize(E_lean, Q, W.back(), &loc, nullptr, false, h->ews.rres.as<double>());
+        // local pass leaves R with W_last - Q_loc C = Z_{m+1} R, Z_{m+1} orthonormal.  Built
+        // once per cycle: a Rayleigh-Ritz fallback (goto rayleigh_ritz) reuses it and R.
+        if (!E_lean) {
+          E_lean = take();
+          const std::vector<float*> loc = local_of(Q);
+          orthonormalize(E_lean, Q, W.back(), &loc, nullptr, false, h->ews.rres.as<double>());
+        }
       } else {
         HIPCHK(n2v2r_launch_resid(blocks(X, 0, pb), blocks(MX, 0, pb), h->theta.as<double>(), n,
                                   h->partial.as<double>(), h->partial_elems,
@@ -1914,7 +1982,7 @@ struct Eig {
                               hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         for (float* p : MV) give(p);
-        double worst = 0.0, ratio = 1.0;
+        double worst = 0.0, ratio = 0.0;
         int tconv = 0;
         for (int j = 0; j < d; ++j) {
           const double r = std::sqrt(std::max(pres[j], 0.0)) / th1;
@@ -1935,7 +2003,9 @@ struct Eig {
             stagnated = 1;
           } else {
             done = false;
-            est_scale *= 1.25 * ratio;  // the estimates trail the true residual: demand more
+            // the estimates (already scaled) trail the true residual by `ratio`: rescale from
+            // this check (it may also shrink back towards 1 after a pessimistic one)
+            if (ratio > 0.0) est_scale = std::max(1.0, est_scale * 1.25 * ratio);
             hist_res.clear();
           }
         }
@@ -2005,6 +2075,9 @@ struct Eig {
       stats->spmm_algo_bytes = algo_bytes;
       stats->stagnated = stagnated;
       stats->rr_fallbacks = stats_rr_fallbacks;
+      stats->est_scale = est_scale;
+      stats->lean_checks = lean_checks;
+      tsum(stats);
     }
     return (conv == d || stagnated) ? N2V2R_OK : N2V2R_ERR_NO_CONVERGENCE;
   }
@@ -2065,7 +2138,7 @@ int n2v2r_create(int device, n2v2r_handle** out) {
 int n2v2r_comm_unique_id(char* out, size_t len) {
   if (!out || len < sizeof(ncclUniqueId)) return N2V2R_ERR_BAD_ARG;
   ncclUniqueId id;
-  if (ncclGetUniqueId(&id) != ncclSuccess) return N2V2R_ERR_HIP;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return N2V2R_ERR_RCCL;
   std::memcpy(out, &id, sizeof(id));
   return N2V2R_OK;
 }
@@ -2083,7 +2156,7 @@ int n2v2r_create_rccl(int device, int rank, int world, const char* unique_id,
   c->world = world;
   if (ncclCommInitRank(&c->c, world, id, rank) != ncclSuccess) {
     n2v2r_destroy(h);
-    return N2V2R_ERR_HIP;
+    return N2V2R_ERR_RCCL;
   }
   h->rank = rank;
   h->world = world;
@@ -2147,6 +2220,7 @@ void n2v2r_destroy(n2v2r_handle* h) {
   if (h->spec_m) (void)hipStreamDestroy(h->spec_m);
   if (h->inv_ev) (void)hipEventDestroy(h->inv_ev);
   if (h->pin) (void)hipHostFree(h->pin);
+  for (hipEvent_t e : h->tev) (void)hipEventDestroy(e);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -2195,15 +2269,15 @@ int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const in
       h->set_err("layer %d: indptr must start at 0 and end at nnz", k);
       return N2V2R_ERR_BAD_ARG;
     }
+    if (nnz > (int64_t)INT32_MAX) {  // the transpose sort's payload is an int32 entry index
+      h->set_err("layer %d: more than 2^31 - 1 entries", k);
+      return N2V2R_ERR_BAD_ARG;
+    }
     for (int64_t r = 0; r < n; ++r)
       if (indptr[r + 1] < indptr[r]) {
         h->set_err("layer %d: indptr not monotone", k);
         return N2V2R_ERR_BAD_ARG;
       }
-    if (!host_indices_in_range(nnz, indices, n)) {
-      h->set_err("layer %d: column index out of range", k);
-      return N2V2R_ERR_BAD_ARG;
-    }
     for (int j = 0; j < h->K; ++j)
       if (j != k && h->layers[j]->loaded && h->layers[j]->dense) {
         h->err = "layers must be all CSR or all dense";
@@ -2211,22 +2285,151 @@ int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const in
       }
     LayerDev& L = *h->layers[k];
     L.dense = false;
+    L.loaded = false;
     L.drop_col_blocks();
     L.n_rows = h->nloc;
-    L.unit = upload_rows(h->stream, h->row0, h->nloc, indptr, indices, data, L.indptr, L.indices,
-                         L.data, L.nnz);
-    bool sym = symmetric == N2V2R_SYM_YES;
-    if (symmetric != N2V2R_SYM_YES) {
-      std::vector<int64_t> tp;
-      std::vector<int32_t> tx;
-      std::vector<float> td;
-      host_transpose(n, nnz, indptr, indices, data, tp, tx, td);
-      if (symmetric == N2V2R_SYM_DETECT)
-        sym = host_is_symmetric(n, indptr, indices, data, tp, tx, td);
-      if (!sym)
-        L.t_unit = upload_rows(h->stream, h->row0, h->nloc, tp.data(), tx.data(), td.data(),
-                               L.t_indptr, L.t_indices, L.t_data, L.t_nnz);
+    const hipStream_t st = h->stream;
+    // the whole layer to HBM (on one GPU straight into the layer's buffers; a partitioned
+    // handle keeps its row slice and the slice of the transpose)
+    const bool whole = !h->comm;
+    DevBuf gip, gix, gdv;
+    DevBuf& dip = whole ? L.indptr : gip;
+    DevBuf& dix = whole ? L.indices : gix;
+    DevBuf& ddv = whole ? L.data : gdv;
+    dip.ensure(sizeof(int64_t) * (n + 1));
+    dix.ensure(sizeof(int32_t) * std::max<int64_t>(nnz, 1));
+    ddv.ensure(sizeof(float) * std::max<int64_t>(nnz, 1));
+    HIPCHK(hipMemcpyAsync(dip.p, indptr, sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, st));
+    if (nnz) {
+      HIPCHK(hipMemcpyAsync(dix.p, indices, sizeof(int32_t) * nnz, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(ddv.p, data, sizeof(float) * nnz, hipMemcpyHostToDevice, st));
     }
+    const bool need_t = symmetric != N2V2R_SYM_YES;
+    DevBuf keys[2], pay[2], hist, flag;
+    flag.ensure(sizeof(unsigned) * 4, st);
+    HIPCHK(hipMemsetAsync(flag.p, 0, sizeof(unsigned) * 4, st));  // (N2V2R_POISON fills 0xFF)
+    if (need_t && nnz) {
+      keys[0].ensure(sizeof(uint64_t) * nnz);
+      pay[0].ensure(sizeof(int32_t) * nnz);
+    }
+    HIPCHK(n2v2r_launch_csr_scan(dip.as<int64_t>(), dix.as<int32_t>(), ddv.as<float>(), n, n,
+                                 need_t && nnz ? keys[0].as<uint64_t>() : nullptr,
+                                 need_t && nnz ? pay[0].as<int32_t>() : nullptr,
+                                 flag.as<unsigned>(), st));
+    unsigned fl = 0;
+    HIPCHK(hipMemcpyAsync(&fl, flag.p, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (fl & 1u) {
+      h->set_err("layer %d: column index out of range", k);
+      return N2V2R_ERR_BAD_ARG;
+    }
+    const bool unit = !(fl & 2u);
+    const bool sorted = !(fl & 4u);
+    // A^T = the entries stably sorted by column (LSD radix over the column digits only)
+    auto transpose = [&](const int64_t* ip_, const int32_t* ix_, const float* dv_, bool have_keys,
+                         DevBuf& tp, DevBuf& tx, DevBuf& td) {
+      tp.ensure(sizeof(int64_t) * (n + 1));
+      tx.ensure(sizeof(int32_t) * std::max<int64_t>(nnz, 1));
+      if (!unit) td.ensure(sizeof(float) * std::max<int64_t>(nnz, 1));
+      if (nnz == 0) {
+        HIPCHK(n2v2r_launch_csr_from_sorted(nullptr, nullptr, nullptr, 0, n, tp.as<int64_t>(),
+                                            nullptr, nullptr, st));
+        return;
+      }
+      keys[0].ensure(sizeof(uint64_t) * nnz);
+      pay[0].ensure(sizeof(int32_t) * nnz);
+      keys[1].ensure(sizeof(uint64_t) * nnz);
+      pay[1].ensure(sizeof(int32_t) * nnz);
+      if (!have_keys)
+        HIPCHK(n2v2r_launch_csr_scan(ip_, ix_, dv_, n, n, keys[0].as<uint64_t>(),
+                                     pay[0].as<int32_t>(), flag.as<unsigned>() + 1, st));
+      hist.ensure(sizeof(uint32_t) * 256 * (size_t)n2v2r_radix_tiles(nnz));
+      int bits = 1;
+      while (bits < 31 && ((int64_t)1 << bits) < n) ++bits;
+      int cur = 0;
+      for (int sh = 32; sh < 32 + bits; sh += 8) {
+        HIPCHK(n2v2r_launch_radix_pass(keys[cur].as<uint64_t>(), pay[cur].as<int32_t>(),
+                                       keys[cur ^ 1].as<uint64_t>(), pay[cur ^ 1].as<int32_t>(),
+                                       nnz, 1, sh, hist.as<uint32_t>(), st));
+        cur ^= 1;
+      }
+      HIPCHK(n2v2r_launch_csr_from_sorted(keys[cur].as<uint64_t>(), pay[cur].as<int32_t>(), dv_,
+                                          nnz, n, tp.as<int64_t>(), tx.as<int32_t>(),
+                                          unit ? nullptr : td.as<float>(), st));
+    };
+    bool sym = symmetric == N2V2R_SYM_YES;
+    DevBuf gtp, gtx, gtd;
+    DevBuf& tp = whole ? L.t_indptr : gtp;
+    DevBuf& tx = whole ? L.t_indices : gtx;
+    DevBuf& td = whole ? L.t_data : gtd;
+    if (need_t) {
+      transpose(dip.as<int64_t>(), dix.as<int32_t>(), ddv.as<float>(), true, tp, tx, td);
+      if (symmetric == N2V2R_SYM_DETECT) {
+        // unit layers compare their (absent) values as equal: both sides read A's values
+        const float* tv = unit ? ddv.as<float>() : td.as<float>();
+        HIPCHK(hipMemsetAsync(flag.as<unsigned>() + 2, 0, sizeof(unsigned), st));
+        if (sorted) {
+          HIPCHK(n2v2r_launch_csr_compare(dip.as<int64_t>(), dix.as<int32_t>(), ddv.as<float>(),
+                                          tp.as<int64_t>(), tx.as<int32_t>(), tv, n, nnz,
+                                          flag.as<unsigned>() + 2, st));
+        } else {  // A's rows sorted = (A^T)^T
+          DevBuf sp_, sx, sv;
+          transpose(tp.as<int64_t>(), tx.as<int32_t>(), tv, false, sp_, sx, sv);
+          HIPCHK(n2v2r_launch_csr_compare(sp_.as<int64_t>(), sx.as<int32_t>(),
+                                          unit ? ddv.as<float>() : sv.as<float>(),
+                                          tp.as<int64_t>(), tx.as<int32_t>(), tv, n, nnz,
+                                          flag.as<unsigned>() + 2, st));
+          HIPCHK(hipStreamSynchronize(st));
+        }
+        unsigned mism = 0;
+        HIPCHK(hipMemcpyAsync(&mism, flag.as<unsigned>() + 2, sizeof(unsigned),
+                              hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        sym = mism == 0;
+      }
+    }
+    HIPCHK(hipStreamSynchronize(st));  // the sort scratch dies here
+    keys[0].release();
+    keys[1].release();
+    pay[0].release();
+    pay[1].release();
+    // this rank's rows of A and (not symmetric) of A^T
+    auto slice = [&](DevBuf& sip, DevBuf& six, DevBuf& sdv, bool copy_values, DevBuf& oip,
+                     DevBuf& oix, DevBuf& odv, int64_t& onnz) {
+      int64_t p0 = 0, p1 = 0;
+      HIPCHK(hipMemcpyAsync(&p0, sip.as<int64_t>() + h->row0, sizeof(int64_t),
+                            hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(&p1, sip.as<int64_t>() + h->row0 + h->nloc, sizeof(int64_t),
+                            hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      onnz = p1 - p0;
+      oip.ensure(sizeof(int64_t) * (h->nloc + 1));
+      oix.ensure(sizeof(int32_t) * std::max<int64_t>(onnz, 1));
+      odv.ensure(sizeof(float) * std::max<int64_t>(onnz, 1));
+      HIPCHK(n2v2r_launch_csr_rebase(sip.as<int64_t>(), h->row0, h->nloc, oip.as<int64_t>(), st));
+      if (onnz) {
+        HIPCHK(hipMemcpyAsync(oix.p, six.as<int32_t>() + p0, sizeof(int32_t) * onnz,
+                              hipMemcpyDeviceToDevice, st));
+        if (copy_values)
+          HIPCHK(hipMemcpyAsync(odv.p, sdv.as<float>() + p0, sizeof(float) * onnz,
+                                hipMemcpyDeviceToDevice, st));
+      }
+      HIPCHK(hipStreamSynchronize(st));
+    };
+    if (whole) {
+      L.nnz = nnz;
+      L.t_nnz = nnz;
+      if (sym) {
+        L.t_indptr.release();
+        L.t_indices.release();
+        L.t_data.release();
+      }
+    } else {
+      slice(gip, gix, gdv, true, L.indptr, L.indices, L.data, L.nnz);
+      if (!sym) slice(gtp, gtx, gtd, !unit, L.t_indptr, L.t_indices, L.t_data, L.t_nnz);
+    }
+    L.unit = unit;
+    L.t_unit = unit;
     L.symmetric = sym;
     L.loaded = true;
     h->have_embedding = false;
@@ -2538,7 +2741,7 @@ static void run_borda(n2v2r_handle* h, const double* Ddev, int64_t n, int nseg, 
 int n2v2r_rank(n2v2r_handle* h, int strategy, const int* dims, int n_dims, const int* metrics,
                int n_metrics, int method, int* n_comparisons, int* n_cols) {
   return guarded(h, [&]() -> int {
-    if (method != 0) {
+    if (method != N2V2R_AGG_BORDA && method != N2V2R_AGG_NONE) {
       h->err = "Aggregation method not found. Available methods: Borda";
       return N2V2R_ERR_UNSUPPORTED_AGG;
     }
@@ -2623,7 +2826,8 @@ int n2v2r_rank(n2v2r_handle* h, int strategy, const int* dims, int n_dims, const
     }
     HIPCHK(hipStreamSynchronize(h->stream));
     const double t1 = now_ms();
-    run_borda(h, h->D.as<double>(), n, ncmp * C, C, h->borda.as<int64_t>());
+    h->have_borda = method == N2V2R_AGG_BORDA;
+    if (h->have_borda) run_borda(h, h->D.as<double>(), n, ncmp * C, C, h->borda.as<int64_t>());
     HIPCHK(hipStreamSynchronize(h->stream));
     h->ms_dist = t1 - t0;
     h->ms_borda = now_ms() - t1;
@@ -2648,6 +2852,10 @@ int n2v2r_get_distances(n2v2r_handle* h, int comparison, double* D) {
 int n2v2r_get_borda(n2v2r_handle* h, int comparison, int64_t* borda) {
   return guarded(h, [&]() -> int {
     if (comparison < 0 || comparison >= h->ncmp || !borda) return N2V2R_ERR_BAD_ARG;
+    if (!h->have_borda) {
+      h->err = "n2v2r_rank ran without aggregation (N2V2R_AGG_NONE)";
+      return N2V2R_ERR_NOT_READY;
+    }
     HIPCHK(hipMemcpyAsync(borda, h->borda.as<int64_t>() + (size_t)comparison * h->n,
                           sizeof(int64_t) * h->n, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
@@ -2830,8 +3038,13 @@ int n2v2r_rr_band_top(n2v2r_handle* h, int c, int kp, const double* hband, int64
       HIPCHK(hipMemcpyAsync(w, th.p, sizeof(double) * p, hipMemcpyDeviceToHost, h->stream));
       HIPCHK(hipMemcpyAsync(S, s.p, sizeof(float) * c * p, hipMemcpyDeviceToHost, h->stream));
       HIPCHK(hipStreamSynchronize(h->stream));
-      if (e) throw StatusFail{N2V2R_ERR_NO_CONVERGENCE, "Sturm Rayleigh-Ritz: residual check failed"};
-      return N2V2R_OK;
+      if (!e) return N2V2R_OK;
+      // a vector failed its residual check: the reducing path, as the solver falls back
+      HIPCHK(hipMemsetAsync(er.p, 0, 4 * sizeof(int), h->stream));
+      if (kp > 0)
+        HIPCHK(hipMemcpyAsync(th.p, theta_prev, sizeof(double) * kp, hipMemcpyHostToDevice,
+                              h->stream));
+      HIPCHK(hipStreamSynchronize(h->stream));
     }
     HIPCHK(n2v2r_launch_rr_band(hb.as<double>(), c, kp, th.as<double>(), ab.as<double>(),
                                 va.as<double>(), ta.as<double>(), tri.as<double>(),

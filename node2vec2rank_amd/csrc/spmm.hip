@@ -533,15 +533,22 @@ __global__ __launch_bounds__(256) void spmm8_cb_kernel(SpmmCbArgs a) {
   }
 }
 
-extern "C" hipError_t n2v2r_launch_spmm_cb(const SpmmCbArgs& a, hipStream_t stream) {
-  const int64_t n = a.A[0].n_rows;
-  double avg = 0.0;  // mean entries per block row, largest block
+// rows per wave of the column-block kernels from the mean entries per block row (largest
+// block): aim for ~3-4 gather steps of L/2 panel rows per row group
+extern "C" int n2v2r_cb_rpw(const CsrBlk* A, int64_t n) {
+  double avg = 0.0;
   for (int j = 0; j < CB_NB; ++j) {
-    const double m = (double)a.A[j].nnz / (double)(n > 0 ? n : 1);
+    const double m = (double)A[j].nnz / (double)(n > 0 ? n : 1);
     avg = m > avg ? m : avg;
   }
-  int rpw = 1;  // aim for ~3-4 gather steps of L/2 panel rows per row group
+  int rpw = 1;
   while (rpw < 16 && 64.0 / (rpw * 2) / 2.0 * 3.5 >= avg) rpw *= 2;
+  return rpw;
+}
+
+extern "C" hipError_t n2v2r_launch_spmm_cb(const SpmmCbArgs& a, hipStream_t stream) {
+  const int64_t n = a.A[0].n_rows;
+  int rpw = n2v2r_cb_rpw(a.A, n);
   static const int rpw_env = [] {  // N2V2R_CB_RPW / N2V2R_CB_WGS: tuning runs
     const char* s = getenv("N2V2R_CB_RPW");
     return s ? atoi(s) : 0;
@@ -569,6 +576,102 @@ extern "C" hipError_t n2v2r_launch_spmm_cb(const SpmmCbArgs& a, hipStream_t stre
     default: CB_LAUNCH(1); break;
   }
 #undef CB_LAUNCH
+  return hipGetLastError();
+}
+
+// ---- row tiles x column-block phases (b = 8, panels of 8-160 MB) ---------------------------
+// The column-block SpMM above writes 8 partial outputs per layer launch (2 x 8 x 32 B per row
+// of extra HBM traffic, then a reduce launch).  Here every workgroup owns a tile of rows whose
+// accumulators stay in LDS (tile x 32 B: 62.5 KB at N = 1M with 2 workgroups per CU) and walks
+// the column blocks in a fixed order 0..7 (the phases), gathering only from panel block p in
+// phase p.  All workgroups start together and their rows carry equal work (ER / uniform
+// graphs), so at any time the chip gathers from one 4 MB panel block, which every XCD's L2
+// holds: the gathers hit L2 as in the column-block form, and each output row is written once.
+// Sum mode (stage 2) accumulates the K layers into one output; otherwise (stage 1) each layer's
+// output is written after its 8 phases.  Each row belongs to one wave (fixed row groups), so
+// the LDS read-modify-writes need no barrier or atomic; per row the order is (layer, block,
+// entry) -- deterministic.
+struct SpmmTileArgs {
+  const CsrBlk* blk;      // device array [K][CB_NB]
+  const float* X[8];      // panel per layer (gathered, global rows)
+  float* Y[8];            // output per layer (sum: Y[0])
+  int64_t ldx, ldy;
+  int64_t n;              // rows
+  int K;
+  int sum;
+  int tile_rows;
+};
+
+template <int RPW>
+__global__ __launch_bounds__(1024, 8) void spmm8_tile_kernel(SpmmTileArgs a) {
+  constexpr int L = 64 / RPW;
+  extern __shared__ f32x4 tacc[];  // [tile_rows][2]
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nwave = blockDim.x >> 6;
+  const int li = lane % L;
+  const int64_t r0 = (int64_t)blockIdx.x * a.tile_rows;
+  const int64_t rem = a.n - r0;
+  const int nrows = (int)(rem < a.tile_rows ? rem : a.tile_rows);
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  for (int grp = wave; grp * RPW < nrows; grp += nwave) {
+    const int lr = grp * RPW + lane / L;
+    if (lr < nrows && li < 2) tacc[lr * 2 + li] = zero;
+  }
+  for (int k = 0; k < a.K; ++k) {
+    const float* X = a.X[k];
+    for (int p = 0; p < CB_NB; ++p) {
+      const CsrBlk A = a.blk[k * CB_NB + p];
+      for (int grp = wave; grp * RPW < nrows; grp += nwave) {
+        const int lr = grp * RPW + lane / L;
+        const bool ok = lr < nrows;
+        f32x4 acc = zero;
+        cb_row_accumulate<RPW>(A, X, a.ldx, r0 + lr, ok, lane, acc);
+#pragma unroll
+        for (int m = 2; m < L; m <<= 1) {
+          acc.x += __shfl_xor(acc.x, m, 64);
+          acc.y += __shfl_xor(acc.y, m, 64);
+          acc.z += __shfl_xor(acc.z, m, 64);
+          acc.w += __shfl_xor(acc.w, m, 64);
+        }
+        if (ok && li < 2) tacc[lr * 2 + li] += acc;
+      }
+    }
+    if (!a.sum || k == a.K - 1) {
+      float* Y = a.Y[a.sum ? 0 : k];
+      for (int grp = wave; grp * RPW < nrows; grp += nwave) {
+        const int lr = grp * RPW + lane / L;
+        if (lr < nrows && li < 2) {
+          *reinterpret_cast<f32x4*>(Y + (r0 + lr) * a.ldy + li * 4) = tacc[lr * 2 + li];
+          tacc[lr * 2 + li] = zero;
+        }
+      }
+    }
+  }
+}
+
+// rows per tile for the tiled form: 2 workgroups (1024 threads each) per CU, LDS <= 64 KB each
+extern "C" int n2v2r_spmm_tile_rows(int64_t n, int ncu) {
+  int64_t t = (n + 2 * (int64_t)ncu - 1) / (2 * (int64_t)ncu);
+  t = (t + 15) / 16 * 16;
+  if (t > 2048) t = 2048;
+  return (int)t;
+}
+
+extern "C" hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, int rpw, hipStream_t stream) {
+  if (a.K < 1 || a.K > 8 || a.tile_rows < 16 || a.n <= 0) return hipErrorInvalidValue;
+  const unsigned grid = (unsigned)((a.n + a.tile_rows - 1) / a.tile_rows);
+  const size_t lds = sizeof(float) * 8 * (size_t)a.tile_rows;
+#define TILE_LAUNCH(R) \
+  hipLaunchKernelGGL((spmm8_tile_kernel<R>), dim3(grid), dim3(1024), lds, stream, a)
+  switch (rpw) {
+    case 32: TILE_LAUNCH(32); break;
+    case 16: TILE_LAUNCH(16); break;
+    case 8: TILE_LAUNCH(8); break;
+    case 4: TILE_LAUNCH(4); break;
+    default: TILE_LAUNCH(2); break;
+  }
+#undef TILE_LAUNCH
   return hipGetLastError();
 }
 

@@ -17,6 +17,7 @@ import json
 import os
 import random
 import time
+import weakref
 from datetime import datetime
 
 import numpy as np
@@ -76,13 +77,22 @@ class N2V2R:
             with open(os.path.join(self.save_dir, "config.json"), 'w', encoding="utf-8") as f:
                 json.dump(self.config, f)
 
-        self._engine = _lib.Engine(device)  # one handle per model: it owns the layers in HBM
+        # one engine per device, shared by every model of the process (its allocations and
+        # solver workspace are reused across fits); the model that last loaded its layers owns it
+        self._device = device
         self._eig_options = dict(eig_options or {})
         self._layers_loaded = False
         self._keys = None
         self._cols = None
 
     # ------------------------------------------------------------------------------------
+    def _write_frames(self, frames, suffix):
+        """``{key}{suffix}.tsv`` per frame, tab-separated with the node-label index, as the
+        reference writes them (model.py:142-145, 193-196, 269-278, 306-309)."""
+        for key, frame in frames.items():
+            frame.to_csv(os.path.join(self.save_dir, str(key) + suffix + ".tsv"), sep='\t',
+                         index=True)
+
     def _node_index(self):
         """``pd.Index`` of the node labels, built once per label list (building it from a
         Python list is the slowest host step of a 1M-node call; every output frame shares it)."""
@@ -91,23 +101,49 @@ class N2V2R:
             self._index_src = self.node_names
         return self._index
 
+    @property
+    def _engine(self):
+        """The device's shared engine, taken over from the model that used it last (which first
+        copies to the host what it still needs from HBM: its embedding)."""
+        eng = _lib.default_engine(self._device)
+        ref = getattr(eng, "_owner", None)
+        prev = ref() if ref is not None else None
+        if prev is not self:
+            if prev is not None:
+                prev._hand_over()
+            eng._owner = weakref.ref(self)
+            self._layers_loaded = False
+        return eng
+
+    def _hand_over(self):
+        if self.eig_stats is not None and self._node_embeddings is None:
+            self._node_embeddings = _lib.default_engine(self._device).embedding().astype(np.float64)
+        self._layers_loaded = False
+
     def _load_layers(self):
+        eng = self._engine
         if not self._layers_loaded:
-            self._engine.set_layers([_as_layer(g) for g in self.graphs])
+            eng.set_layers([_as_layer(g) for g in self.graphs])
             self._layers_loaded = True
+        return eng
 
     def __fit(self):
         """UASE on the GPU (replaces ``se.UASE``, model.py:51-55)."""
-        self._load_layers()
+        eng = self._load_layers()
         seed = self._seed if self._seed is not None else int(np.random.randint(1, 2**31 - 1))
         opts = dict(seed=seed)
         opts.update(self._eig_options)
-        self.eig_stats = self._engine.uase(self.max_embed_dim, **opts)
+        self._node_embeddings = None
+        self.eig_stats = None
+        self.eig_stats = eng.uase(self.max_embed_dim, **opts)
 
     def __rank(self):
-        """Distances + Borda for every comparison on the GPU (model.py:57-96,149-201)."""
-        ncmp, ncols = self._engine.rank(self.comp_strategy, self.embed_dimensions,
-                                        self.distance_metrics)
+        """Distances for every comparison on the GPU (model.py:57-96).  The Borda aggregate is
+        computed by ``aggregate_transform`` from the frames as they are then, as the
+        reference does (model.py:167-180)."""
+        eng = self._engine
+        ncmp, ncols = eng.rank(self.comp_strategy, self.embed_dimensions,
+                               self.distance_metrics, method=_lib.AGG_NONE)
         if self.comp_strategy != 'one_vs_rest':
             keys = [str(i) for i in range(1, self.num_graphs)]
         else:
@@ -122,7 +158,7 @@ class N2V2R:
         self._keys, self._cols = keys, cols
         out = {}
         for c, key in enumerate(keys):
-            D = self._engine.distances(c)
+            D = eng.distances(c)
             out[key] = pd.DataFrame(D, index=self._node_index(), columns=cols)
         return out
 
@@ -138,8 +174,7 @@ class N2V2R:
         toc_uase = time.time()
         if self.config["verbose"] == 1:
             print(f"\tMulti-layer embedding in {round(toc_uase - tic_uase, 2)} seconds")
-        self._node_embeddings = None  # fetched lazily from HBM on first access
-        self.pairwise_ranks = self.__rank()
+        self.pairwise_ranks = self.__rank()  # (the embedding is fetched lazily from HBM)
         num_rankings = sum(len(df.columns) for df in self.pairwise_ranks.values())
         toc = time.time()
         self.stage_seconds.update(uase=toc_uase - tic_uase, rank=toc - toc_uase)
@@ -147,8 +182,7 @@ class N2V2R:
             print(f"n2v2r computed {num_rankings} rankings for {len(self.pairwise_ranks)} "
                   f"comparison(s) in {round(toc - tic, 2)} seconds")
         if self.save_dir:
-            for key, rank in self.pairwise_ranks.items():
-                rank.to_csv(os.path.join(self.save_dir, key + ".tsv"), sep='\t', index=True)
+            self._write_frames(self.pairwise_ranks, "")
         return self.pairwise_ranks
 
     @property
@@ -164,32 +198,38 @@ class N2V2R:
         self._node_embeddings = value
 
     def aggregate_transform(self, method='Borda'):
-        """Borda aggregation (reference ``model.py:149-201``); the scores were computed on the
-        GPU together with the distances.  Returns ``dict[str, DataFrame['borda_ranks']]``."""
+        """Borda aggregation (reference ``model.py:149-201``) of every column of the current
+        ``pairwise_ranks`` frames, on the GPU (radix sort per column, int64 sums).  As in the
+        reference each column is read against ``node_names`` (``pd.Series(col,
+        index=node_names)``, model.py:173): rows missing from a frame rank last (NaN).
+        Returns ``dict[str, DataFrame['borda_ranks']]``."""
         if self.pairwise_ranks:
             start = time.time()
             if self.config["verbose"] >= 0:
                 print("\nRank aggregation with Borda ...")
             if method.casefold() != 'borda':
                 raise NotImplementedError('Aggregation method not found. Available methods: Borda')
+            eng = self._engine
+            idx = self._node_index()
             out = {}
-            for c, key in enumerate(self._keys):
-                b = self._engine.borda(c)
-                out[key] = pd.DataFrame(b, index=self._node_index(), columns=['borda_ranks'])
+            for key, df in self.pairwise_ranks.items():
+                if df.index is not idx and not df.index.equals(idx):
+                    df = df.reindex(idx)
+                b = eng.borda_columns(df.to_numpy(dtype=np.float64))
+                out[key] = pd.DataFrame(b, index=idx, columns=['borda_ranks'])
             self.pairwise_aggregate_ranks = out
             if self.config["verbose"] == 1:
                 print(f"\tFinished aggregation in {round(time.time() - start, 2)} seconds")
             if self.save_dir:
-                for k, rank in self.pairwise_aggregate_ranks.items():
-                    rank.to_csv(os.path.join(self.save_dir, k + "_agg.tsv"), sep='\t', index=True)
+                self._write_frames(self.pairwise_aggregate_ranks, "_agg")
         else:
             raise ValueError("No n2v2r embeddings found")
         return self.pairwise_aggregate_ranks
 
     def degree_difference_ranking(self):
         """DeDi (reference ``model.py:282-311``): float32 column sums on the GPU."""
-        self._load_layers()
-        sums = [self._engine.column_sums(k) for k in range(self.num_graphs)]
+        eng = self._load_layers()
+        sums = [eng.column_sums(k) for k in range(self.num_graphs)]
         out = {}
         for i in range(1, self.num_graphs):
             dedi = sums[i - 1] - sums[i]
@@ -198,8 +238,7 @@ class N2V2R:
             out[str(i)] = ranking
         self.prior_singed_ranks = [v.iloc[:, 0] for v in out.values()]
         if self.save_dir:
-            for k, rank in out.items():
-                rank.to_csv(os.path.join(self.save_dir, k + "_degDif.tsv"), sep='\t', index=True)
+            self._write_frames(out, "_degDif")
         return out
 
     def signed_ranks_transform(self, prior_signed_ranks=None):
@@ -222,23 +261,25 @@ class N2V2R:
             df = self.pairwise_ranks[key]
             keep = df.index.isin(prior.index)
             sub = df.loc[keep]
-            sign = np.where(prior.reindex(sub.index).to_numpy() > 0, 1.0, -1.0)
-            signed[key] = pd.DataFrame(sub.to_numpy() * sign[:, None], index=sub.index,
+            pos = prior.reindex(sub.index).to_numpy() > 0  # NaN prior: negated, as `> 0` fails
+            vals = sub.to_numpy()
+            # negation (not a multiplication by -1, which keeps a NaN's sign bit)
+            signed[key] = pd.DataFrame(np.where(pos[:, None], vals, -vals), index=sub.index,
                                        columns=df.columns)
             if self.pairwise_aggregate_ranks:
-                agg = self.pairwise_aggregate_ranks[key].iloc[:, 0].loc[keep]
-                signed_agg[key] = pd.DataFrame(agg.to_numpy() * sign.astype(np.int64),
-                                               index=agg.index, columns=["signed_agg_ranks"])
+                agg = self.pairwise_aggregate_ranks[key].iloc[:, 0]
+                agg = agg.loc[agg.index.isin(prior.index)]
+                pos = prior.reindex(agg.index).to_numpy() > 0
+                a = agg.to_numpy()
+                signed_agg[key] = pd.DataFrame(np.where(pos, a, -a), index=agg.index,
+                                               columns=["signed_agg_ranks"])
         self.pairwise_signed_ranks = signed
         if self.pairwise_aggregate_ranks:
             self.pairwise_signed_aggregate_ranks = signed_agg
         if self.config["verbose"] == 1:
             print(f"\tFinished signed transformation in {round(time.time() - start, 2)} seconds")
         if self.save_dir:
-            for k, v in self.pairwise_signed_ranks.items():
-                v.to_csv(os.path.join(self.save_dir, k + "_signed.tsv"), sep='\t', index=True)
+            self._write_frames(self.pairwise_signed_ranks, "_signed")
             if self.pairwise_aggregate_ranks:
-                for k, v in self.pairwise_signed_aggregate_ranks.items():
-                    v.to_csv(os.path.join(self.save_dir, str(k) + "_agg_signed.tsv"), sep='\t',
-                             index=True)
+                self._write_frames(self.pairwise_signed_aggregate_ranks, "_agg_signed")
         return self.pairwise_signed_ranks

@@ -86,6 +86,17 @@ def er_layer_rows(n: int, avg_deg: float, seed: int, row0: int = 0, n_rows: int 
                          shape=(n_rows, n))
 
 
+def fingerprint(layers) -> np.ndarray:
+    """Cheap fingerprint of regenerated layers (nnz, sum of column indices, a row-pointer hash
+    per layer): fixtures that store a generator instead of the CSR check it."""
+    out = []
+    for a in layers:
+        a = sp.csr_matrix(a)
+        out.append([int(a.nnz), int(a.indices.astype(np.int64).sum()),
+                    int((a.indptr.astype(np.int64) * 7919 % 1000003).sum())])
+    return np.asarray(out, dtype=np.int64)
+
+
 def er_layer_p(n: int, p: float, seed: int) -> sp.csr_matrix:
     """ER with edge probability p (BASELINE cfg1: N=1000, p=0.01)."""
     return er_layer(n, p * (n - 1), seed)

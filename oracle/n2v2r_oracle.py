@@ -203,6 +203,28 @@ def borda_reference_loop(D):
     return out
 
 
+def _get_ranking(ranking, index):
+    """``model_utils.py:22-25``: N - position of every node of ``index`` in ``ranking``."""
+    n = len(index)
+    return [n - ranking.index(node) for node in index]
+
+
+def borda_reference_parallel(D, n_jobs=-2):
+    """``borda_aggregate_parallel`` (``model_utils.py:28-36``) as the reference runs it: the
+    per-column rankings as Python lists of node ids (``model.py:171-175``), the O(N^2)
+    ``list.index`` scoring fanned out over a joblib process pool, int64 sums; returned in node
+    order (``model.py:185``).  Baseline timing only (small N)."""
+    from joblib import Parallel, delayed
+    D = np.asarray(D, dtype=np.float64)
+    n, c = D.shape
+    rankings = [list(_descending_order_pandas(D[:, j], "quicksort")) for j in range(c)]
+    index = rankings[0]
+    res = np.asarray(Parallel(n_jobs=n_jobs)(delayed(_get_ranking)(r, index) for r in rankings))
+    out = np.empty(n, dtype=np.int64)
+    out[np.asarray(index)] = res.sum(axis=0)
+    return out
+
+
 # --------------------------------------------------------------------------------------
 # Whole path + DeDi (model.py:282-311)
 # --------------------------------------------------------------------------------------
@@ -223,6 +245,20 @@ def degree_difference(layers):
         dedi = a - b
         out[str(i)] = (dedi, np.abs(dedi))
     return out
+
+
+def signed_transform_single(ranks, prior):
+    """``signed_transform_single`` (``model_utils.py:7-19``), literally: for every node of
+    ``ranks`` (a Series) that the prior's index holds, the rank if the prior's value is > 0,
+    else its negation; returns a Series in ``ranks``' order.  Small inputs only (a Python loop
+    with ``prior.loc`` per node, as the reference)."""
+    import pandas as pd
+    names, vals = [], []
+    for index, rank in ranks.items():
+        if index in prior.index:
+            names.append(index)
+            vals.append(rank if prior.loc[index] > 0 else -rank)
+    return pd.Series(vals, index=names)
 
 
 # --------------------------------------------------------------------------------------

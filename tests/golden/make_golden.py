@@ -120,9 +120,119 @@ def _pack_case(name, layers, nodes, dims, metrics, strategies, seed, N2V2R):
     print(f"wrote {path} ({os.path.getsize(path) / 1024:.0f} KB)")
 
 
+def make_cfg2(N2V2R):
+    """BASELINE cfg2 at its own size (2-layer ER N=100k, avg-deg 20, d=64, cosine + euclidean,
+    sequential; the bench's rank-0 graph, synthetic.er_layers(..., seed_base=1000)).  Sparse
+    layers go to the reference N2V2R directly (``csc_matrix(sparse)`` at model.py:53).  Y and
+    the layers are not stored (100 MB / 16 MB): the test regenerates the layers and checks the
+    fingerprint."""
+    from node2vec2rank_amd import synthetic
+    from oracle import n2v2r_oracle as orc
+    n, deg, seed = 100_000, 20.0, 42
+    layers = synthetic.er_layers(n, deg, 2, seed_base=1000)
+    nodes = list(range(n))
+    config = dict(embed_dimensions=[64], distance_metrics=["cosine", "euclidean"], seed=seed,
+                  comp_strategy="sequential", verbose=1, save_dir=None)
+    model = N2V2R(graphs=[sp.csr_matrix(a) for a in layers], nodes=nodes, config=config)
+    ranks = model.fit_transform_rank()
+    agg = model.aggregate_transform()
+    D = ranks["1"].to_numpy(dtype=np.float64)
+    b = agg["1"]["borda_ranks"].to_numpy(dtype=np.int64)
+    Yo, so, _ = orc.uase([sp.csc_matrix(g) for g in layers], 64, seed=seed)
+    assert np.array_equal(Yo, np.asarray(model.node_embeddings)), "cfg2: oracle UASE differs"
+    oD = orc.rank_distances(Yo, [64], ["cosine", "euclidean"], "sequential", faithful=True)["1"][1]
+    assert np.array_equal(oD, D)
+    assert np.array_equal(orc.borda(D, faithful=True), b), "cfg2: oracle Borda differs"
+    out = {"n": np.int64(n), "avg_deg": np.float64(deg), "seed_base": np.int64(1000),
+           "num_layers": np.int64(2), "checksum": synthetic.fingerprint(layers),
+           "dims": np.asarray([64], dtype=np.int64),
+           "metrics": np.asarray(["cosine", "euclidean"]),
+           "strategies": np.asarray(["sequential"]), "seed": np.int64(seed), "sigma": so,
+           "sequential/keys": np.asarray(["1"]), "sequential/1/D": D,
+           "sequential/1/cols": np.asarray(list(ranks["1"].columns)),
+           "sequential/1/borda": b, "sequential/1/borda_stable": orc.borda(D, faithful=False)}
+    path = os.path.join(HERE, "er_cfg2.npz")
+    np.savez_compressed(path, **out)
+    print(f"wrote {path} ({os.path.getsize(path) / 1024:.0f} KB)")
+
+
+def make_cfg2_env(_N2V2R=None):
+    """The reference's own seed-to-seed envelope at cfg2, added to er_cfg2.npz: the oracle
+    (bit-exact with the reference's model.py on this graph, checked by make_cfg2) re-run from
+    the ARPACK start vectors of seeds 43 and 44 against the reference's seed-42 outputs: the
+    largest distance difference and the lowest Kendall tau / top-100 overlap of the Borda
+    ranks."""
+    from scipy.stats import kendalltau
+
+    from node2vec2rank_amd import synthetic
+    from oracle import n2v2r_oracle as orc
+    path = os.path.join(HERE, "er_cfg2.npz")
+    z = np.load(path, allow_pickle=False)
+    out = {k: z[k] for k in z.files}
+    layers = synthetic.er_layers(int(out["n"]), float(out["avg_deg"]), 2,
+                                 seed_base=int(out["seed_base"]))
+    Dr, br = out["sequential/1/D"], out["sequential/1/borda"]
+    top = lambda b: set(np.argsort(-b, kind="stable")[:100].tolist())  # noqa: E731
+    derr, taus, tops = [], [], []
+    for seed in (43, 44):
+        Y, _, _ = orc.uase(layers, 64, seed=seed)
+        D = orc.rank_distances(Y, [64], ["cosine", "euclidean"], "sequential",
+                               faithful=True)["1"][1]
+        b = orc.borda(D, faithful=True)
+        derr.append(np.abs(D - Dr).max(axis=0))
+        taus.append(kendalltau(b, br).statistic)
+        tops.append(len(top(b) & top(br)))
+        print(f"seed {seed}: distance diff {derr[-1]}, tau {taus[-1]:.6f}, top-100 {tops[-1]}")
+    out["env_distance_per_col"] = np.max(np.asarray(derr), axis=0)
+    out["env_tau"] = np.float64(min(taus))
+    out["env_top100"] = np.int64(min(tops))
+    np.savez_compressed(path, **out)
+    print(f"wrote {path}")
+
+
+def make_writer(N2V2R):
+    """The reference's output files (model.py:40-48 config.json, :142-145 {key}.tsv,
+    :193-196 {key}_agg.tsv, :306-309 {key}_degDif.tsv, :269-278 {key}_signed.tsv and
+    {key}_agg_signed.tsv) for the er_cfg1 graphs, written with save_dir="out" from inside a
+    scratch directory (so config.json holds the relative path) and the timestamp directory
+    renamed away.  Copied byte for byte into tests/golden/writer_er_cfg1/."""
+    import glob
+    import shutil
+    import tempfile
+    from node2vec2rank_amd import synthetic
+    layers = [synthetic.er_layer_p(1000, 0.01, 1000 + k) for k in range(2)]
+    dense = [np.asarray(a.todense(), dtype=np.float32) for a in layers]
+    nodes = [f"g{i}" for i in range(1000)]
+    dst = os.path.join(HERE, "writer_er_cfg1")
+    os.makedirs(dst, exist_ok=True)
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as tmp:
+        os.chdir(tmp)
+        try:
+            config = dict(embed_dimensions=[2, 8], distance_metrics=["cosine", "euclidean"],
+                          seed=42, comp_strategy="sequential", verbose=-1, save_dir="out")
+            model = N2V2R(graphs=dense, nodes=nodes, config=config)
+            model.fit_transform_rank()
+            model.aggregate_transform()
+            model.degree_difference_ranking()
+            model.signed_ranks_transform()
+            (run,) = glob.glob(os.path.join(tmp, "out", "*"))
+            for f in sorted(os.listdir(run)):
+                shutil.copyfile(os.path.join(run, f), os.path.join(dst, f))
+                print(f"wrote {os.path.join(dst, f)}")
+        finally:
+            os.chdir(cwd)
+
+
 def main():
     N2V2R, network_transform = _import_reference()
     from node2vec2rank_amd import synthetic
+    only = sys.argv[1:]
+    if only:
+        for name in only:
+            {"er_cfg2": make_cfg2, "er_cfg2_env": make_cfg2_env,
+             "writer": make_writer}[name](N2V2R)
+        return
 
     # 1. the reference's demo graphs (data/networks/demo, configs/config_demo_adj.json)
     demo_dir = os.path.join(REF, "data", "networks", "demo")

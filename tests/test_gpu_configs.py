@@ -1,0 +1,199 @@
+"""BASELINE.json's configurations at their own sizes on one MI355X (needs the GPU).
+
+* cfg2 (2-layer ER N=100k, avg-deg 20, d=64): end to end through N2V2R against the reference's
+  own outputs (tests/golden/er_cfg2.npz, made by running the reference model.py on the same
+  regenerated graph): singular values, distances, and the integer ranks by SURVEY 8(c)(4)'s
+  bar (Kendall tau >= 0.998, identical top-100 set).
+* cfg4 (2-layer ER N=1M, avg-deg 50, dims {8..128} x {cos, euc}): the full fit; host fp64
+  true residuals and orthonormality of the returned vectors, distances vs the oracle from the
+  returned embedding, Borda bit-exact vs the stable oracle.
+* cfg3 (4 dense |corrcoef| layers, N=20k, d=256, MFMA path): the full fit; host residuals and
+  orthonormality, ranking consistency.
+* cfg5's code path (row partition over W ranks): W = 8 ranks of the thread communicator at
+  N = 1M (cfg5's degree 30), each ingesting only its own rows, vs the single-GPU engine.
+The reference itself cannot run at cfg3/cfg4 sizes (svds alone exceeded 55 min at cfg4,
+BASELINE.md 2), so those are checked through size-independent properties.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+from scipy.stats import kendalltau
+
+from conftest import load_fixture
+from oracle import n2v2r_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _top(b, k):
+    return set(np.argsort(-np.asarray(b), kind="stable")[:k].tolist())
+
+
+def _host_residuals(layers, U, theta, cols):
+    """||M u_j - theta_j u_j|| / theta_1 for the given columns, fp64 on the host."""
+    X = U[:, cols].astype(np.float64)
+    MX = np.zeros_like(X)
+    for A in layers:
+        if sp.issparse(A):
+            A64 = A.astype(np.float64)
+            MX += A64 @ (A64.T @ X)
+        else:
+            MX += A.astype(np.float64) @ (A.T.astype(np.float64) @ X)
+    R = MX - X * theta[cols][None, :]
+    return np.linalg.norm(R, axis=0) / theta[0]
+
+
+def test_cfg2_end_to_end_vs_reference():
+    from node2vec2rank_amd import synthetic
+    from node2vec2rank_amd.model import N2V2R
+    fx = load_fixture("er_cfg2")
+    n = int(fx["n"])
+    layers = synthetic.er_layers(n, float(fx["avg_deg"]), int(fx["num_layers"]),
+                                 seed_base=int(fx["seed_base"]))
+    np.testing.assert_array_equal(synthetic.fingerprint(layers), fx["checksum"])  # same graph
+    dims = [int(x) for x in fx["dims"]]
+    metrics = [str(x) for x in fx["metrics"]]
+    cfg = dict(embed_dimensions=dims, distance_metrics=metrics, seed=int(fx["seed"]),
+               comp_strategy="sequential", verbose=-1, save_dir=None)
+    m = N2V2R(layers, list(range(n)), cfg)
+    ranks = m.fit_transform_rank()
+    agg = m.aggregate_transform()
+    assert m.eig_stats["converged"] == 64, m.eig_stats
+    np.testing.assert_allclose(m._engine.singular_values(), fx["sigma"], rtol=2e-5)
+    D = ranks["1"].to_numpy()
+    assert list(ranks["1"].columns) == [str(c) for c in fx["sequential/1/cols"]]
+    derr = np.abs(D - fx["sequential/1/D"]).max(axis=0)
+    # SURVEY 8(c)(2) asks for 1e-4; at cfg2 the reference's own distances move by up to
+    # env (1.1e-3 for the cosine column, 1.0e-4 for the euclidean one) between two ARPACK start
+    # vectors (make_golden.py er_cfg2_env), so the bar is max(1e-4, env) per column
+    env = fx["env_distance_per_col"]
+    b = agg["1"]["borda_ranks"].to_numpy()
+    ref = fx["sequential/1/borda"]
+    tau = kendalltau(b, ref).statistic
+    top = len(_top(b, 100) & _top(ref, 100))
+    print(f"cfg2: distance err {derr} (reference envelope {env}), Kendall tau {tau:.6f} "
+          f"(reference envelope {float(fx['env_tau']):.6f}), top-100 overlap {top}")
+    assert np.all(derr <= np.maximum(1e-4, env)), (derr, env)
+    assert tau >= 0.998, tau        # SURVEY 8(c)(4); the reference's own tau is 0.99926
+    assert top == 100, top
+
+
+@pytest.fixture(scope="module")
+def cfg4_layers():
+    from node2vec2rank_amd import synthetic
+    return synthetic.er_layers(1_000_000, 50.0, 2, seed_base=1000)
+
+
+def test_cfg4_full_size(engine, cfg4_layers):
+    layers = cfg4_layers
+    dims = [8, 16, 32, 64, 128]
+    metrics = ["cosine", "euclidean"]
+    engine.set_layers(layers)
+    st = engine.uase(128, seed=42)
+    assert st["converged"] == 128 and st["max_residual"] <= 1e-6, st
+    s = engine.singular_values()
+    assert np.all(np.diff(s) <= 0)
+    theta = s ** 2
+    U = engine.left_embedding() / np.sqrt(s)[None, :].astype(np.float32)
+    # orthonormality of all 128 vectors, true residuals of 8 of them (first, last, a middle
+    # run), both in fp64 on the host
+    G = U.T.astype(np.float64) @ U.astype(np.float64)
+    assert np.abs(G - np.eye(128)).max() < 1e-5
+    cols = [0, 1, 2, 63, 64, 125, 126, 127]
+    res = _host_residuals(layers, U, theta, cols)
+    print(f"cfg4: {st['block_applications']} block applications, host residuals "
+          f"max {res.max():.2e}")
+    assert res.max() < 5e-6, res
+    # distances from the returned embedding (fp64 on both sides) and Borda bit-exact
+    ncmp, ncols = engine.rank("sequential", dims, metrics)
+    assert (ncmp, ncols) == (1, 10)
+    Y = engine.embedding().astype(np.float64)
+    Dref = orc.rank_distances(Y, dims, metrics, "sequential")["1"][1]
+    D = engine.distances(0)
+    np.testing.assert_allclose(D, Dref, rtol=0, atol=1e-9)
+    np.testing.assert_array_equal(engine.borda(0), orc.borda(D))
+
+
+def test_cfg4_api_matches_engine(engine, cfg4_layers):
+    """The drop-in API path at cfg4 (host CSR -> GPU ingest -> fit -> frames -> Borda of the
+    frames): the same numbers as the engine-level fit of the same graph and seed."""
+    from node2vec2rank_amd.model import N2V2R
+    n = cfg4_layers[0].shape[0]
+    cfg = dict(embed_dimensions=[8, 16, 32, 64, 128], distance_metrics=["cosine", "euclidean"],
+               seed=42, comp_strategy="sequential", verbose=-1, save_dir=None)
+    m = N2V2R(cfg4_layers, [f"n{i}" for i in range(n)], cfg)
+    ranks = m.fit_transform_rank()
+    agg = m.aggregate_transform()
+    engine.set_layers(cfg4_layers)
+    engine.uase(128, seed=42)
+    engine.rank("sequential", cfg["embed_dimensions"], cfg["distance_metrics"])
+    np.testing.assert_array_equal(ranks["1"].to_numpy(), engine.distances(0))
+    np.testing.assert_array_equal(agg["1"]["borda_ranks"].to_numpy(), engine.borda(0))
+
+
+def test_cfg3_dense_full_size(engine):
+    from node2vec2rank_amd import synthetic
+    layers = synthetic.corr_layers(20_000, 4)
+    engine.set_layers(layers, storage="dense", symmetric=1)
+    st = engine.uase(256, seed=42)
+    assert st["converged"] == 256 or st["stagnated"], st
+    s = engine.singular_values()
+    theta = s ** 2
+    U = engine.left_embedding() / np.sqrt(s)[None, :].astype(np.float32)
+    G = U.T.astype(np.float64) @ U.astype(np.float64)
+    assert np.abs(G - np.eye(256)).max() < 1e-5
+    cols = [0, 1, 2, 3, 127, 128, 253, 254, 255]
+    res = _host_residuals(layers, U, theta, cols)
+    print(f"cfg3: {st['block_applications']} block applications, residual max {res.max():.2e}")
+    assert res.max() < 1e-5, res
+    ncmp, ncols = engine.rank("sequential", [256], ["cosine", "euclidean"])
+    assert (ncmp, ncols) == (3, 2)
+    Y = engine.embedding().astype(np.float64)
+    ref = orc.rank_distances(Y, [256], ["cosine", "euclidean"], "sequential")
+    for c, key in enumerate(["1", "2", "3"]):
+        D = engine.distances(c)
+        np.testing.assert_allclose(D, ref[key][1], rtol=0, atol=1e-9)
+        np.testing.assert_array_equal(engine.borda(c), orc.borda(D))
+
+
+def test_cfg5_path_w8_one_million(engine):
+    """cfg5's row-partitioned path at >= 1M nodes: 8 ranks (thread communicator, one GPU), each
+    ingesting only its own rows of the counter-based ER layers bench.py's cfg5 uses, vs the
+    single-GPU engine on the whole graph."""
+    from node2vec2rank_amd import synthetic
+    from test_gpu_dist import _run_ranks
+    n, deg, d, world = 1_000_000, 30.0, 64, 8
+    full = [synthetic.er_layer_rows(n, deg, 2000 + k, 0, n) for k in range(2)]
+    dims, metrics = [16, 64], ["cosine", "euclidean"]
+
+    def fn(eng, r):
+        eng.set_layer_rows(n, 2, [])
+        _, _, row0, nl = eng.dist_info()
+        eng.set_layer_rows(n, 2, [A[row0:row0 + nl] for A in full])
+        st = eng.uase(d, seed=9)
+        eng.rank("sequential", dims, metrics)
+        return dict(st=st, s=eng.singular_values(), Y=eng.embedding(), X=eng.left_embedding(),
+                    D=eng.distances(0), B=eng.borda(0))
+
+    res = _run_ranks(world, fn, timeout=600)
+    for r in res:
+        assert r["st"]["converged"] == d or r["st"]["stagnated"] == 1, r["st"]
+    for r in res[1:]:
+        np.testing.assert_array_equal(r["s"], res[0]["s"])
+        np.testing.assert_array_equal(r["D"], res[0]["D"])
+        np.testing.assert_array_equal(r["B"], res[0]["B"])
+    engine.set_layers(full, symmetric=1)
+    engine.uase(d, seed=9)
+    engine.rank("sequential", dims, metrics)
+    s1 = engine.singular_values()
+    np.testing.assert_allclose(res[0]["s"], s1, rtol=1e-5)
+    X = np.concatenate([r["X"] for r in res], axis=0)
+    U = X / np.sqrt(res[0]["s"])[None, :].astype(np.float32)
+    res_h = _host_residuals(full, U, res[0]["s"] ** 2, [0, 1, 31, 62, 63])
+    print(f"cfg5 path W=8 N=1M: host residuals max {res_h.max():.2e}")
+    assert res_h.max() < 5e-6, res_h
+    Y = np.concatenate([r["Y"] for r in res], axis=1).astype(np.float64)
+    Yal = orc.align_signs(Y, engine.embedding().astype(np.float64))
+    assert np.abs(Yal - engine.embedding()).max() <= 2e-3 * np.abs(Yal).max()
+    tau = kendalltau(res[0]["B"], engine.borda(0)).statistic
+    assert tau > 0.995, tau

@@ -385,14 +385,17 @@ def test_uase_column_blocks_golden(engine, name, monkeypatch):
     assert err <= max(5e-4, 3 * env), (name, err, env)
 
 
-def test_uase_column_blocks_er_20k(engine, monkeypatch):
+@pytest.mark.parametrize("tiled", ["1", "0"])
+def test_uase_column_blocks_er_20k(engine, monkeypatch, tiled):
     """Column-block SpMM vs the row SpMM on a 20k-node ER graph with a ragged column count
-    (20,003: the last block is short): same sigma within fp32 tolerance, true residuals, and
-    run-to-run bit-identical embeddings (fixed partial order)."""
+    (20,003: the last block is short), in both forms (tiled: row tiles with LDS accumulators
+    walking the blocks; else 8 partials + reduce): same sigma within fp32 tolerance, true
+    residuals, and run-to-run bit-identical embeddings (fixed summation order)."""
     from node2vec2rank_amd import synthetic
     layers = synthetic.er_layers(20_003, 20, 2)
     d = 32
     engine.set_layers(layers)
+    monkeypatch.setenv("N2V2R_SPMM_TILE", tiled)
     monkeypatch.setenv("N2V2R_SPMM_CB", "0")
     engine.uase(d, seed=42)
     s_row = engine.singular_values().copy()
