@@ -265,6 +265,37 @@ def roofline_from_stats(st, cfg, b):
     return out
 
 
+def strong_scaling(group, cfg, args, local, rank, world):
+    """One graph of the bench's family row-partitioned over every rank (RCCL), timed like the
+    main loop: per step each rank's CSR rows -> HBM, UASE, distances, Borda, tables to host."""
+    from node2vec2rank_amd import _lib, synthetic
+    uid = group.bcast_bytes(_lib.comm_unique_id() if rank == 0 else None)
+    peng = _lib.Engine.rccl(local, rank, world, uid)
+    try:
+        peng.set_layer_rows(cfg["n"], 2, [])
+        _, _, row0, nl = peng.dist_info()
+        rows = [synthetic.er_layer_rows(cfg["n"], cfg["avg_deg"], 2000 + k, row0, nl)
+                for k in range(2)]
+        partitioned_step(peng, cfg, rows)  # warm-up
+        peng.synchronize()
+        group.barrier()
+        t0 = time.perf_counter()
+        steps = max(1, args.steps)
+        for _ in range(steps):
+            st, _ = partitioned_step(peng, cfg, rows)
+        peng.synchronize()
+        group.barrier()
+        t = group.max(time.perf_counter() - t0) / steps
+    finally:
+        peng.close()
+    return {"value": round(cfg["n"] / t, 1), "unit": "nodes/s", "ms_per_step": round(t * 1e3, 3),
+            "scaling": "strong", "n_gpus": world, "steps": steps,
+            "graph": f"one {cfg['n']}-node graph of the same family (counter-based ER, "
+                     f"synthetic.er_layer_rows), rows partitioned over {world} ranks, each "
+                     f"rank's CSR rows -> HBM inside the step",
+            "block_applications": st.get("block_applications")}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -374,6 +405,18 @@ def main():
         except Exception:
             pass
 
+    # N > 1 replicas: the same graph family ALSO as one graph row-partitioned over every rank
+    # (RCCL all-gathers of the panels, all-reduces of the Gram / Rayleigh-Ritz / residual
+    # reductions), strong scaling -- the multi-GPU path SURVEY 8(e) describes, measured beside
+    # the weak-scaling value (N2V2R_BENCH_PARTITIONED=0 skips it)
+    strong = None
+    if (world > 1 and mode == "replicas" and not cfg.get("dense")
+            and os.environ.get("N2V2R_BENCH_PARTITIONED", "1") != "0"):
+        try:
+            strong = strong_scaling(group, cfg, args, local, rank, world)
+        except Exception as e:  # reported in the line; the weak-scaling value stands
+            strong = {"error": repr(e)[:300]}
+
     if mode == "partitioned":
         par = f"row-partitioned x{world} (RCCL)" if world > 1 else "row-partitioned x1"
     else:
@@ -407,6 +450,8 @@ def main():
                 for k, v in (stats or {}).items()},
         "setup_s": round(t_build, 2),
     }
+    if strong is not None:
+        result["partitioned_same_family"] = strong
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         workers = max(1, min(16, os.cpu_count() or 1))
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample or CPU_SAMPLE[args.config],

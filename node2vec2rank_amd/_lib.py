@@ -303,8 +303,9 @@ class Engine:
                 raise ValueError("all layers must be square and share the node set")
         self._check(self.lib.n2v2r_set_num_layers(self.h, len(mats), n), "set_num_layers")
         for k, m in enumerate(mats):
-            m.sum_duplicates()
-            m.sort_indices()
+            # no sum_duplicates / sort_indices here (an O(nnz) host pass each): the engine
+            # checks row order on the GPU and compares unsorted layers through (A^T)^T, and a
+            # duplicate entry adds into every product exactly as its summed value would
             indptr = np.ascontiguousarray(m.indptr, dtype=np.int64)
             indices = np.ascontiguousarray(m.indices, dtype=np.int32)
             data = np.ascontiguousarray(m.data, dtype=np.float32)

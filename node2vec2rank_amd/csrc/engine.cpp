@@ -48,7 +48,8 @@
 
 // ---- kernel launchers (spmm.hip, dense.hip, rank.hip) ------------------------------------
 #include "spmm_args.h"
-#define CB_NB 8
+#define CB_NB 8   // column blocks of the partials form (one per XCD)
+#define CB_MAX 32  // column blocks of the tiled form (N2V2R_SPMM_TILE_NB)
 struct CsrBlk {  // spmm.hip: one column block, int32 row pointers relative to base
   const int32_t* rp;
   const int32_t* indices;
@@ -72,6 +73,7 @@ struct SpmmTileArgs {  // spmm.hip: row tiles x column-block phases
   int64_t ldx, ldy;
   int64_t n;
   int K;
+  int nb;
   int sum;
   int tile_rows;
 };
@@ -91,10 +93,15 @@ hipError_t n2v2r_launch_cb_reduce(const float* P, int nparts, int64_t pstride, i
                                   float* out, int64_t ldo, hipStream_t stream);
 hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, int rpw, hipStream_t stream);
 int n2v2r_spmm_tile_rows(int64_t n, int ncu);
-int n2v2r_cb_rpw(const CsrBlk* A, int64_t n);
-hipError_t n2v2r_launch_cb_count(const CsrDev& A, int64_t cw, int32_t* cnt, hipStream_t stream);
-hipError_t n2v2r_launch_cb_fill(const CsrDev& A, int64_t cw, const int64_t* rp, int32_t* idx,
-                                float* dat, hipStream_t stream);
+int n2v2r_cb_rpw(const CsrBlk* A, int nb, int64_t n);
+hipError_t n2v2r_launch_cb_count(const CsrDev& A, int64_t cw, int nb, int32_t* cnt,
+                                 hipStream_t stream);
+hipError_t n2v2r_launch_cb_rowptrs(const int32_t* cnt, int64_t n, int nb, int64_t nnz,
+                                   int64_t* tsum, size_t tsum_elems, int64_t* rp, int32_t* rp32,
+                                   hipStream_t stream);
+int64_t n2v2r_cb_scan_tiles(int64_t n, int nb);
+hipError_t n2v2r_launch_cb_fill(const CsrDev& A, int64_t cw, int nb, const int64_t* rp,
+                                int32_t* idx, float* dat, hipStream_t stream);
 hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n, double* partial,
                               size_t partial_elems, double* out, const int* cond,
                               hipStream_t stream);
@@ -359,8 +366,9 @@ struct LayerDev {
   }
   // column-block form of A and (directed) A^T for the XCD-local SpMM (built on first use)
   struct ColBlocks {
-    DevBuf rp, idx, dat;   // [CB_NB][n_rows + 1] int32 row pointers (relative); entries; values
-    CsrBlk blk[CB_NB];
+    DevBuf rp, idx, dat;   // [nb][n_rows + 1] int32 row pointers (relative); entries; values
+    CsrBlk blk[CB_MAX];
+    int nb = 0;            // blocks (CB_NB = 8 for the partials form; 8 or 16 tiled)
     int64_t ncols = 0;     // column count the blocks were cut for
     bool built = false;
     bool usable = false;   // every block under 2^31 entries (int32 row pointers)
@@ -379,63 +387,56 @@ struct LayerDev {
 // Split a CSR into CB_NB column blocks of ceil(ncols / CB_NB) columns (spmm.hip, XCD-local
 // SpMM): per-row counts on the GPU, row-pointer scan on the host, scatter on the GPU (each
 // row's entries keep their order).  One-off per layer; not part of a fit's timed work.
-void build_col_blocks(const CsrDev& A, int64_t ncols, LayerDev::ColBlocks& out, hipStream_t st) {
+void build_col_blocks(const CsrDev& A, int64_t ncols, LayerDev::ColBlocks& out, hipStream_t st,
+                      int nb) {
   const int64_t n = A.n_rows;
-  const int64_t cw = (ncols + CB_NB - 1) / CB_NB;
+  const int64_t cw = (ncols + nb - 1) / nb;
   out.ncols = ncols;
+  out.nb = nb;
   out.built = true;
   out.usable = false;
-  DevBuf cnt;
-  cnt.ensure(sizeof(int32_t) * CB_NB * std::max<int64_t>(n, 1), st);
-  HIPCHK(n2v2r_launch_cb_count(A, cw, cnt.as<int32_t>(), st));
-  std::vector<int32_t> hc((size_t)CB_NB * n);
-  if (n > 0)
-    HIPCHK(hipMemcpyAsync(hc.data(), cnt.p, sizeof(int32_t) * hc.size(), hipMemcpyDeviceToHost,
-                          st));
-  HIPCHK(hipStreamSynchronize(st));
-  std::vector<int64_t> rp((size_t)CB_NB * (n + 1));  // absolute, for the scatter
-  std::vector<int32_t> rp32((size_t)CB_NB * (n + 1));  // relative to the block's base
-  int64_t pos = 0;
-  int64_t base[CB_NB];
-  for (int j = 0; j < CB_NB; ++j) {
-    int64_t* r = rp.data() + (size_t)j * (n + 1);
-    int32_t* r32 = rp32.data() + (size_t)j * (n + 1);
-    base[j] = pos;
-    for (int64_t i = 0; i < n; ++i) {
-      r[i] = pos;
-      r32[i] = (int32_t)(pos - base[j]);
-      pos += hc[(size_t)j * n + i];
-    }
-    r[n] = pos;
-    if (pos - base[j] > (int64_t)INT32_MAX) return;  // too large for int32: row kernel
-    r32[n] = (int32_t)(pos - base[j]);
+  if (n <= 0) return;
+  // per-row block counts, then every row pointer by a device scan (no host round trip)
+  DevBuf cnt, rp64, tsum;
+  cnt.ensure(sizeof(int32_t) * nb * n, st);
+  HIPCHK(n2v2r_launch_cb_count(A, cw, nb, cnt.as<int32_t>(), st));
+  const int64_t ntiles = n2v2r_cb_scan_tiles(n, nb);
+  tsum.ensure(sizeof(int64_t) * ntiles, st);
+  rp64.ensure(sizeof(int64_t) * nb * (n + 1), st);
+  out.rp.ensure(sizeof(int32_t) * nb * (n + 1), st);
+  HIPCHK(n2v2r_launch_cb_rowptrs(cnt.as<int32_t>(), n, nb, A.nnz, tsum.as<int64_t>(),
+                                 (size_t)ntiles, rp64.as<int64_t>(), out.rp.as<int32_t>(), st));
+  // block bases and ends: rp[j][0], rp[j][n]
+  std::vector<int64_t> ends(2 * (size_t)nb);
+  for (int j = 0; j < nb; ++j) {
+    HIPCHK(hipMemcpyAsync(&ends[2 * j], rp64.as<int64_t>() + (size_t)j * (n + 1),
+                          sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&ends[2 * j + 1], rp64.as<int64_t>() + (size_t)j * (n + 1) + n,
+                          sizeof(int64_t), hipMemcpyDeviceToHost, st));
   }
-  if (pos != A.nnz) throw StatusFail{N2V2R_ERR_HIP, "column-block split lost entries"};
-  DevBuf rp64;
-  rp64.ensure(sizeof(int64_t) * rp.size(), st);
-  out.rp.ensure(sizeof(int32_t) * rp32.size(), st);
+  HIPCHK(hipStreamSynchronize(st));
+  if (ends[2 * (nb - 1) + 1] != A.nnz || ends[0] != 0)
+    throw StatusFail{N2V2R_ERR_INTERNAL, "column-block split lost entries"};
+  for (int j = 0; j < nb; ++j)
+    if (ends[2 * j + 1] - ends[2 * j] > (int64_t)INT32_MAX) return;  // int32 pointers: row kernel
   out.idx.ensure(sizeof(int32_t) * std::max<int64_t>(A.nnz, 1), st);
   if (!A.unit) out.dat.ensure(sizeof(float) * std::max<int64_t>(A.nnz, 1), st);
-  HIPCHK(hipMemcpyAsync(rp64.p, rp.data(), sizeof(int64_t) * rp.size(), hipMemcpyHostToDevice,
-                        st));
-  HIPCHK(hipMemcpyAsync(out.rp.p, rp32.data(), sizeof(int32_t) * rp32.size(),
-                        hipMemcpyHostToDevice, st));
-  HIPCHK(n2v2r_launch_cb_fill(A, cw, rp64.as<int64_t>(), out.idx.as<int32_t>(),
+  HIPCHK(n2v2r_launch_cb_fill(A, cw, nb, rp64.as<int64_t>(), out.idx.as<int32_t>(),
                               A.unit ? nullptr : out.dat.as<float>(), st));
   HIPCHK(hipStreamSynchronize(st));
-  for (int j = 0; j < CB_NB; ++j) {
-    const int64_t* r = rp.data() + (size_t)j * (n + 1);
+  for (int j = 0; j < nb; ++j)
     out.blk[j] = CsrBlk{out.rp.as<int32_t>() + (size_t)j * (n + 1), out.idx.as<int32_t>(),
-                        A.unit ? nullptr : out.dat.as<float>(), base[j], n, r[n] - r[0], A.unit};
-  }
+                        A.unit ? nullptr : out.dat.as<float>(), ends[2 * j], n,
+                        ends[2 * j + 1] - ends[2 * j], A.unit};
   out.usable = true;
 }
 
 // false when a block would exceed int32 row pointers (then the row kernel runs)
-bool ensure_col_blocks(LayerDev& L, int64_t ncols, hipStream_t st) {
-  if (!L.cb.built || L.cb.ncols != ncols) build_col_blocks(L.csr(), ncols, L.cb, st);
-  if (!L.symmetric && (!L.cb_t.built || L.cb_t.ncols != ncols))
-    build_col_blocks(L.csr_t(), ncols, L.cb_t, st);
+bool ensure_col_blocks(LayerDev& L, int64_t ncols, hipStream_t st, int nb = CB_NB) {
+  if (!L.cb.built || L.cb.ncols != ncols || L.cb.nb != nb)
+    build_col_blocks(L.csr(), ncols, L.cb, st, nb);
+  if (!L.symmetric && (!L.cb_t.built || L.cb_t.ncols != ncols || L.cb_t.nb != nb))
+    build_col_blocks(L.csr_t(), ncols, L.cb_t, st, nb);
   return L.cb.usable && (L.symmetric || L.cb_t.usable);
 }
 
@@ -574,7 +575,7 @@ struct EigWorkspace {
   DevBuf spec_partial, spec_gsmall, spec_flg, spec_any;
   DevBuf rres;                                // lean images: R of the restart projection
   DevBuf skipc;                               // full passes skipped (selective reorthogonalisation)
-  DevBuf tblk;                                // tiled SpMM: CsrBlk [2][K][CB_NB] (stage 1, stage 2)
+  DevBuf tblk;                                // tiled SpMM: CsrBlk [2][K][nb] (stage 1, stage 2)
 };
 }  // namespace
 
@@ -693,6 +694,21 @@ struct n2v2r_handle {
     }
     comm->allgather(local, global, sizeof(float) * npad * w, stream);
   }
+  // the same on the collective stream, started once `ready` (recorded on the engine stream)
+  // has fired; `done` is recorded behind it (SpMM stage 1 of layer k + 1 runs meanwhile)
+  hipStream_t cstream = nullptr;
+  hipEvent_t cev[2 * SPMM_MAX_LAYERS] = {};
+  void gather_panel_async(const float* local, float* global, int w, int slot) {
+    if (!cstream) {
+      HIPCHK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+      for (hipEvent_t& e : cev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    HIPCHK(hipEventRecord(cev[2 * slot], stream));
+    HIPCHK(hipStreamWaitEvent(cstream, cev[2 * slot], 0));
+    comm->allgather(local, global, sizeof(float) * npad * w, cstream);
+    HIPCHK(hipEventRecord(cev[2 * slot + 1], cstream));
+  }
+  void gather_wait(int slot) { HIPCHK(hipStreamWaitEvent(stream, cev[2 * slot + 1], 0)); }
   void allreduce_f64(double* buf, size_t count) {
     if (comm) comm->allreduce_sum_f64(buf, count, stream);
   }
@@ -811,6 +827,13 @@ double spmm_algo_bytes(int64_t nnz, bool unit, int64_t rows, int64_t panel_rows,
 // Read on every call, so a test can switch it between fits.
 bool col_blocks_wanted(const n2v2r_handle* h, int b);
 
+// Partitioned handles: the stage-1 panel Z_k of each layer all-gathered on a stream of its own
+// while the next layer's stage 1 runs, unless N2V2R_GATHER_OVERLAP=0.  Read per call.
+bool gather_overlap() {
+  const char* e = std::getenv("N2V2R_GATHER_OVERLAP");
+  return !(e && e[0] == '0');
+}
+
 // XCD-split second SpMM stage: b = 8 CSR layers on one GPU whose K stage-2 panels together
 // exceed an XCD's 4 MB L2 (cfg2: 33.5 -> 24 us per stage; at N = 30k, where both panels fit,
 // 4 % slower).  N2V2R_SPMM_SPLIT=1 / 0 forces it on / off.
@@ -849,7 +872,7 @@ struct Eig {
   // column blocks as row tiles x block phases with LDS accumulators (no partials, no reduce;
   // N2V2R_SPMM_TILE=0: the partial + reduce form)
   bool tiled = false;
-  int tile_rows = 0, tile_rpw[2] = {0, 0};
+  int tile_rows = 0, tile_rpw[2] = {0, 0}, tile_nb = CB_NB;
   // XCD-split second SpMM stage (b = 8, one GPU): A_k Z_k lands in per-layer partials on the
   // XCDs of layer k; the image W = sum_k of them is stored by the next Gram pass that reads it
   // (the local first pass of the next expansion), or by materialize() before any other use
@@ -1071,9 +1094,30 @@ struct Eig {
       sb0 += layer_bytes(k, true);
       sb1 += layer_bytes(k, false);
     }
-    int te = tbeg();
-    HIPCHK(n2v2r_launch_spmm(a, b, st));
-    tend(te, 0, sb0);
+    // partitioned: stage 1 one layer per launch, each layer's Z_k all-gathered on the
+    // collective stream while the next layer's stage 1 runs (N2V2R_GATHER_OVERLAP=0: in line)
+    const bool ovl = h->comm && K > 1 && gather_overlap() && st == h->stream;
+    int te = -1;
+    if (ovl) {
+      for (int k = 0; k < K; ++k) {
+        SpmmArgs a1 = a;
+        a1.K = 1;
+        a1.split = 0;
+        a1.A[0] = a.A[k];
+        a1.X[0] = xg;
+        a1.Y[0] = a.Y[k];
+        te = tbeg();
+        HIPCHK(n2v2r_launch_spmm(a1, b, st));
+        tend(te, 0, layer_bytes(k, true));
+        h->gather_panel_async(h->ews.zk[k]->as<float>(),
+                              h->ews.zg.as<float>() + (size_t)k * ng * b, b, k);
+      }
+      for (int k = 0; k < K; ++k) h->gather_wait(k);
+    } else {
+      te = tbeg();
+      HIPCHK(n2v2r_launch_spmm(a, b, st));
+      tend(te, 0, sb0);
+    }
     SpmmArgs s{};
     s.K = K;
     s.sum = 1;
@@ -1084,7 +1128,7 @@ struct Eig {
       s.A[k] = h->layers[k]->csr();
       if (h->comm) {
         float* zgk = h->ews.zg.as<float>() + (size_t)k * ng * b;
-        h->gather_panel(h->ews.zk[k]->as<float>(), zgk, b);
+        if (!ovl) h->gather_panel(h->ews.zk[k]->as<float>(), zgk, b);
         s.X[k] = zgk;
       } else {
         s.X[k] = h->ews.zk[k]->as<float>();
@@ -1119,6 +1163,7 @@ struct Eig {
     a.ldx = a.ldy = 8;
     a.n = n;
     a.K = K;
+    a.nb = tile_nb;
     a.sum = 0;
     a.tile_rows = tile_rows;
     double b0 = 0.0, b1 = 0.0;
@@ -1128,17 +1173,36 @@ struct Eig {
       b0 += layer_bytes(k, true);
       b1 += layer_bytes(k, false);
     }
-    int te = tbeg();
-    HIPCHK(n2v2r_launch_spmm_tile(a, tile_rpw[0], st));
-    tend(te, 0, b0);
+    // partitioned: one launch per layer, Z_k gathered while layer k + 1 runs (as apply_M)
+    const bool ovl = h->comm && K > 1 && gather_overlap() && st == h->stream;
+    int te = -1;
+    if (ovl) {
+      for (int k = 0; k < K; ++k) {
+        SpmmTileArgs a1 = a;
+        a1.K = 1;
+        a1.blk = tb + (size_t)k * tile_nb;
+        a1.X[0] = xg;
+        a1.Y[0] = a.Y[k];
+        te = tbeg();
+        HIPCHK(n2v2r_launch_spmm_tile(a1, tile_rpw[0], st));
+        tend(te, 0, layer_bytes(k, true));
+        h->gather_panel_async(h->ews.zk[k]->as<float>(),
+                              h->ews.zg.as<float>() + (size_t)k * ng * b, b, k);
+      }
+      for (int k = 0; k < K; ++k) h->gather_wait(k);
+    } else {
+      te = tbeg();
+      HIPCHK(n2v2r_launch_spmm_tile(a, tile_rpw[0], st));
+      tend(te, 0, b0);
+    }
     SpmmTileArgs s2 = a;
-    s2.blk = tb + (size_t)K * CB_NB;
+    s2.blk = tb + (size_t)K * tile_nb;
     s2.sum = 1;
     for (int k = 0; k < K; ++k) {
       s2.X[k] = h->ews.zk[k]->as<float>();
       if (h->comm) {
         float* zgk = h->ews.zg.as<float>() + (size_t)k * ng * b;
-        h->gather_panel(h->ews.zk[k]->as<float>(), zgk, b);
+        if (!ovl) h->gather_panel(h->ews.zk[k]->as<float>(), zgk, b);
         s2.X[k] = zgk;
       }
       s2.Y[k] = nullptr;
@@ -1453,25 +1517,33 @@ struct Eig {
     }
     col_blocks = col_blocks_wanted(h, b);
     if (col_blocks) {
-      for (auto& Lp : h->layers) col_blocks = ensure_col_blocks(*Lp, nglob, st) && col_blocks;
       const char* te = std::getenv("N2V2R_SPMM_TILE");  // read per fit (A/B runs, tests)
-      tiled = col_blocks && !(te && te[0] == '0');
+      tiled = !(te && te[0] == '0');
+      // tiled: blocks of N2V2R_SPMM_TILE_NB (default 16: a 2 MB panel block per phase at N = 1M
+      // leaves half of an XCD's L2 to the index stream and to waves a phase apart)
+      const char* tn_ = std::getenv("N2V2R_SPMM_TILE_NB");
+      tile_nb = tiled ? (tn_ ? std::atoi(tn_) : 16) : CB_NB;
+      if (tile_nb != 8 && tile_nb != 16 && tile_nb != 32) tile_nb = 16;
+      for (auto& Lp : h->layers)
+        col_blocks = ensure_col_blocks(*Lp, nglob, st, tile_nb) && col_blocks;
+      tiled = tiled && col_blocks;
       if (col_blocks && !tiled)
         h->ews.cbpart.ensure(sizeof(float) * (size_t)K * CB_NB * npad * 8);
       if (tiled) {
         int ncu = 0;
         HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
         tile_rows = n2v2r_spmm_tile_rows(n, ncu);
-        std::vector<CsrBlk> hb((size_t)2 * K * CB_NB);
+        const int nb = tile_nb;
+        std::vector<CsrBlk> hb((size_t)2 * K * nb);
         for (int k = 0; k < K; ++k) {
           const LayerDev& L = *h->layers[k];
-          for (int j = 0; j < CB_NB; ++j) {
-            hb[(size_t)k * CB_NB + j] = (L.symmetric ? L.cb : L.cb_t).blk[j];
-            hb[(size_t)(K + k) * CB_NB + j] = L.cb.blk[j];
+          for (int j = 0; j < nb; ++j) {
+            hb[(size_t)k * nb + j] = (L.symmetric ? L.cb : L.cb_t).blk[j];
+            hb[(size_t)(K + k) * nb + j] = L.cb.blk[j];
           }
         }
-        tile_rpw[0] = n2v2r_cb_rpw(hb.data(), n);
-        tile_rpw[1] = n2v2r_cb_rpw(hb.data() + (size_t)K * CB_NB, n);
+        tile_rpw[0] = n2v2r_cb_rpw(hb.data(), nb, n);
+        tile_rpw[1] = n2v2r_cb_rpw(hb.data() + (size_t)K * nb, nb, n);
         h->ews.tblk.ensure(sizeof(CsrBlk) * hb.size());
         HIPCHK(hipMemcpyAsync(h->ews.tblk.p, hb.data(), sizeof(CsrBlk) * hb.size(),
                               hipMemcpyHostToDevice, st));
@@ -1519,8 +1591,11 @@ struct Eig {
     // the restart expansion (orth(W_last) against the old basis, then its SpMM) needs nothing
     // from the Rayleigh-Ritz stage: issue it on the spec stream beside the stage (one GPU,
     // banded Rayleigh-Ritz; N2V2R_RESTART_OVERLAP=0 keeps it in line)
+    // Lean images on a partitioned handle too: every quantity they read back (R of the restart
+    // projection, the Ritz values and coefficients, the true residuals) is all-reduced first,
+    // so every rank takes the same decisions.
     const bool lean =
-        b == 8 && pip_fused() && band_rr && sturm && !h->comm && !lean_off && lean_enabled();
+        b == 8 && pip_fused() && band_rr && sturm && !lean_off && lean_enabled();
     {
       // default: a tenth of the residual tolerance.  The residuals stall near the level of
       // orthogonality left in the basis (~1.5x it in cfg2 sweeps: 2e-6 stalls at 3e-6); at
@@ -1541,7 +1616,7 @@ struct Eig {
     bool rr_armed = false;   // the Rayleigh-Ritz error words zeroed (then by every read-back)
     int lean_checks = 0;
     const bool spec_ok = band_rr && !h->comm && !lean && restart_overlap_enabled();
-    const bool lean_ovl = lean && lean_overlap_enabled();
+    const bool lean_ovl = lean && !h->comm && lean_overlap_enabled();
     // pinned read-back per cycle: residuals, Ritz values (keep each), flags, R (8 x 8), S's last rows
     const size_t pin_bytes = sizeof(double) * 2 * (size_t)keep + 8 * sizeof(int) +
                              sizeof(double) * 64 + sizeof(float) * 8 * (size_t)keep;
@@ -1978,6 +2053,7 @@ struct Eig {
         HIPCHK(n2v2r_launch_resid(blocks(X, 0, qd), blocks(MV, 0, qd), h->theta.as<double>(), n,
                                   h->partial.as<double>(), h->partial_elems,
                                   h->resid.as<double>(), st));
+        h->allreduce_f64(h->resid.as<double>(), (size_t)qd * b);
         HIPCHK(hipMemcpyAsync(pres, h->resid.as<double>(), sizeof(double) * qd * b,
                               hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -2221,6 +2297,10 @@ void n2v2r_destroy(n2v2r_handle* h) {
   if (h->inv_ev) (void)hipEventDestroy(h->inv_ev);
   if (h->pin) (void)hipHostFree(h->pin);
   for (hipEvent_t e : h->tev) (void)hipEventDestroy(e);
+  if (h->cstream) (void)hipStreamSynchronize(h->cstream);
+  for (hipEvent_t& e : h->cev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->cstream) (void)hipStreamDestroy(h->cstream);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }

@@ -18,7 +18,33 @@
 
 #include "common.h"
 
-#define DG_KC 64  // k rows of X staged per LDS round
+#define DG_KC 64  // k columns of A (rows of X) staged per LDS round
+#define DG_AP (DG_KC + 4)  // padded LDS row pitch of the A tile (16-B reads conflict-free)
+
+// A tile rows x DG_KC: thread t loads rows u * 16 + t / 16 (u = 0..7), 16 B at k = 4 (t % 16):
+// every wave-instruction reads 4 rows x 256 B contiguous (the lane-per-row form read 32 rows
+// x 32 B per instruction: 0.32 of HBM at cfg3).  Out-of-range rows / k read as zero.
+__device__ __forceinline__ void dg_load_a(const float* __restrict__ A, int64_t lda, int64_t rows,
+                                          int64_t tile_r0, int64_t k0, int64_t k_end,
+                                          f32x4 (&v)[8]) {
+  const int t = threadIdx.x;
+  const int kq = (t & 15) * 4;
+  const int64_t kg = k0 + kq;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int64_t r = tile_r0 + u * 16 + (t >> 4);
+    const bool rok = r < rows;
+    const float* p = A + (rok ? r : 0) * lda + kg;
+    if (rok && kg + 4 <= k_end) {
+      v[u] = *reinterpret_cast<const f32x4*>(p);
+    } else {
+      f32x4 w = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int m = 0; m < 4; ++m) w[m] = (rok && kg + m < k_end) ? p[m] : 0.f;
+      v[u] = w;
+    }
+  }
+}
 
 template <int NT>
 __global__ __launch_bounds__(256) void dense_gemm_kernel(const float* __restrict__ A, int64_t lda,
@@ -28,42 +54,36 @@ __global__ __launch_bounds__(256) void dense_gemm_kernel(const float* __restrict
                                                          int64_t ldo, int64_t slab) {
   constexpr int XP = NT * 32 + 4;  // padded LDS row pitch
   __shared__ float xs[DG_KC][XP];
+  __shared__ __attribute__((aligned(16))) float as[128][DG_AP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i = lane & 31, h = lane >> 5;
-  const int64_t r0 = (int64_t)blockIdx.x * 128 + wave * 32;
-  const int64_t row = r0 + i;
-  const bool row_ok = row < rows;
+  const int64_t tile_r0 = (int64_t)blockIdx.x * 128;
+  const int64_t r0 = tile_r0 + wave * 32;
   const int64_t k_begin = (int64_t)blockIdx.y * kper;
   int64_t k_end = k_begin + kper;
   if (k_end > kdim) k_end = kdim;
-  const float* arow = A + (row_ok ? row : 0) * lda;
   f32x16 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f32x16{0.f};
+  f32x4 nxt[8];
+  if (k_begin < k_end) dg_load_a(A, lda, rows, tile_r0, k_begin, k_end, nxt);
   for (int64_t k0 = k_begin; k0 < k_end; k0 += DG_KC) {
     const int kn = (k_end - k0) < DG_KC ? (int)(k_end - k0) : DG_KC;
-    __syncthreads();
+    __syncthreads();  // the previous round's LDS reads are done
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      *reinterpret_cast<f32x4*>(&as[u * 16 + (threadIdx.x >> 4)][(threadIdx.x & 15) * 4]) = nxt[u];
     for (int e = threadIdx.x; e < DG_KC * NT * 32; e += 256) {
       const int kk = e / (NT * 32), j = e % (NT * 32);
       xs[kk][j] = (kk < kn && j < b) ? X[(k0 + kk) * ldx + j] : 0.f;
     }
     __syncthreads();
+    // the next round's A tile in flight while this round's MFMAs run
+    if (k0 + DG_KC < k_end) dg_load_a(A, lda, rows, tile_r0, k0 + DG_KC, k_end, nxt);
     if (r0 < rows) {
       for (int kk = 0; kk < kn; kk += 16) {
-        f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-        const int64_t kg = k0 + kk + 8 * h;
-        if (row_ok) {
-          if (kg + 8 <= k_end) {
-            a0 = *reinterpret_cast<const f32x4*>(arow + kg);
-            a1 = *reinterpret_cast<const f32x4*>(arow + kg + 4);
-          } else {
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-              a0[m] = (kg + m < k_end) ? arow[kg + m] : 0.f;
-              a1[m] = (kg + 4 + m < k_end) ? arow[kg + 4 + m] : 0.f;
-            }
-          }
-        }
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(&as[wave * 32 + i][kk + 8 * h]);
+        const f32x4 a1 = *reinterpret_cast<const f32x4*>(&as[wave * 32 + i][kk + 8 * h + 4]);
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
           const float av = m < 4 ? a0[m] : a1[m - 4];

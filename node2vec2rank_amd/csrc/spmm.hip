@@ -535,9 +535,9 @@ __global__ __launch_bounds__(256) void spmm8_cb_kernel(SpmmCbArgs a) {
 
 // rows per wave of the column-block kernels from the mean entries per block row (largest
 // block): aim for ~3-4 gather steps of L/2 panel rows per row group
-extern "C" int n2v2r_cb_rpw(const CsrBlk* A, int64_t n) {
+extern "C" int n2v2r_cb_rpw(const CsrBlk* A, int nb, int64_t n) {
   double avg = 0.0;
-  for (int j = 0; j < CB_NB; ++j) {
+  for (int j = 0; j < nb; ++j) {
     const double m = (double)A[j].nnz / (double)(n > 0 ? n : 1);
     avg = m > avg ? m : avg;
   }
@@ -548,7 +548,7 @@ extern "C" int n2v2r_cb_rpw(const CsrBlk* A, int64_t n) {
 
 extern "C" hipError_t n2v2r_launch_spmm_cb(const SpmmCbArgs& a, hipStream_t stream) {
   const int64_t n = a.A[0].n_rows;
-  int rpw = n2v2r_cb_rpw(a.A, n);
+  int rpw = n2v2r_cb_rpw(a.A, CB_NB, n);
   static const int rpw_env = [] {  // N2V2R_CB_RPW / N2V2R_CB_WGS: tuning runs
     const char* s = getenv("N2V2R_CB_RPW");
     return s ? atoi(s) : 0;
@@ -592,12 +592,13 @@ extern "C" hipError_t n2v2r_launch_spmm_cb(const SpmmCbArgs& a, hipStream_t stre
 // the LDS read-modify-writes need no barrier or atomic; per row the order is (layer, block,
 // entry) -- deterministic.
 struct SpmmTileArgs {
-  const CsrBlk* blk;      // device array [K][CB_NB]
+  const CsrBlk* blk;      // device array [K][nb]
   const float* X[8];      // panel per layer (gathered, global rows)
   float* Y[8];            // output per layer (sum: Y[0])
   int64_t ldx, ldy;
   int64_t n;              // rows
   int K;
+  int nb;                 // column blocks (phases) per layer
   int sum;
   int tile_rows;
 };
@@ -620,8 +621,8 @@ __global__ __launch_bounds__(1024, 8) void spmm8_tile_kernel(SpmmTileArgs a) {
   }
   for (int k = 0; k < a.K; ++k) {
     const float* X = a.X[k];
-    for (int p = 0; p < CB_NB; ++p) {
-      const CsrBlk A = a.blk[k * CB_NB + p];
+    for (int p = 0; p < a.nb; ++p) {
+      const CsrBlk A = a.blk[k * a.nb + p];
       for (int grp = wave; grp * RPW < nrows; grp += nwave) {
         const int lr = grp * RPW + lane / L;
         const bool ok = lr < nrows;
@@ -636,6 +637,9 @@ __global__ __launch_bounds__(1024, 8) void spmm8_tile_kernel(SpmmTileArgs a) {
         }
         if (ok && li < 2) tacc[lr * 2 + li] += acc;
       }
+      // the workgroup's waves move to the next panel block together (drifting waves would
+      // want several blocks in L2 at once); each wave only touches its own rows' LDS entries
+      __syncthreads();
     }
     if (!a.sum || k == a.K - 1) {
       float* Y = a.Y[a.sum ? 0 : k];
@@ -733,54 +737,186 @@ extern "C" hipError_t n2v2r_launch_cb_reduce(const float* P, int nparts, int64_t
 }
 
 // Column-block split, step 1: cnt[j * n + r] = entries of row r in column block j
-// (block j = columns [j * cw, (j + 1) * cw)).
+// (block j = columns [j * cw, (j + 1) * cw)); NB blocks (8, 16 or 32).
+template <int NB>
 __global__ void cb_count_kernel(CsrDev A, int64_t cw, int32_t* __restrict__ cnt) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= A.n_rows) return;
-  int c[CB_NB] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int c[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) c[j] = 0;
   for (int64_t p = A.indptr[r]; p < A.indptr[r + 1]; ++p) {
     const int jb = (int)(A.indices[p] / cw);
 #pragma unroll
-    for (int j = 0; j < CB_NB; ++j) c[j] += jb == j;
+    for (int j = 0; j < NB; ++j) c[j] += jb == j;
   }
 #pragma unroll
-  for (int j = 0; j < CB_NB; ++j) cnt[(int64_t)j * A.n_rows + r] = c[j];
+  for (int j = 0; j < NB; ++j) cnt[(int64_t)j * A.n_rows + r] = c[j];
 }
 
 // step 2 (after the host scan): scatter each row's entries to rp[j][r] + running count,
 // keeping their order inside the row.
+template <int NB>
 __global__ void cb_fill_kernel(CsrDev A, int64_t cw, const int64_t* __restrict__ rp,
                                int32_t* __restrict__ idx, float* __restrict__ dat) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= A.n_rows) return;
-  int64_t pos[CB_NB];
+  int64_t pos[NB];
 #pragma unroll
-  for (int j = 0; j < CB_NB; ++j) pos[j] = rp[(int64_t)j * (A.n_rows + 1) + r];
+  for (int j = 0; j < NB; ++j) pos[j] = rp[(int64_t)j * (A.n_rows + 1) + r];
   for (int64_t p = A.indptr[r]; p < A.indptr[r + 1]; ++p) {
     const int32_t col = A.indices[p];
     const int jb = (int)(col / cw);
     int64_t q = 0;
 #pragma unroll
-    for (int j = 0; j < CB_NB; ++j)
+    for (int j = 0; j < NB; ++j)
       if (jb == j) q = pos[j]++;
     idx[q] = col;
     if (!A.unit) dat[q] = A.data[p];
   }
 }
 
-extern "C" hipError_t n2v2r_launch_cb_count(const CsrDev& A, int64_t cw, int32_t* cnt,
-                                            hipStream_t stream) {
-  if (A.n_rows <= 0) return hipSuccess;
-  hipLaunchKernelGGL(cb_count_kernel, dim3((unsigned)((A.n_rows + 255) / 256)), dim3(256), 0,
-                     stream, A, cw, cnt);
+// Row pointers of the column blocks from the counts, on the GPU: an exclusive scan of the
+// counts flattened block-major (cnt[j][r]) gives every entry's absolute position in the
+// block-major entry array, rp[j][r] (int64, [nb][n + 1]); rp[j][n] = rp[j + 1][0] (nnz for the
+// last block); rp32[j][r] = rp[j][r] - rp[j][0] (int32, relative to the block's base).
+#define SCAN_T 256
+#define SCAN_IT 8
+#define SCAN_TILE (SCAN_T * SCAN_IT)
+
+__global__ __launch_bounds__(SCAN_T) void scan_tile_sums_kernel(const int32_t* __restrict__ in,
+                                                                int64_t len,
+                                                                int64_t* __restrict__ tsum) {
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
+  int64_t s = 0;
+#pragma unroll
+  for (int u = 0; u < SCAN_IT; ++u) {
+    const int64_t i = base + u * SCAN_T + threadIdx.x;
+    if (i < len) s += in[i];
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+  __shared__ int64_t ws[SCAN_T / 64];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t t = 0;
+    for (int w = 0; w < SCAN_T / 64; ++w) t += ws[w];
+    tsum[blockIdx.x] = t;
+  }
+}
+
+// exclusive scan of the tile sums in place, one workgroup, chunks of 1024 with a carry
+__global__ __launch_bounds__(1024) void scan_tile_offsets_kernel(int64_t* __restrict__ tsum,
+                                                                 int64_t ntiles) {
+  __shared__ int64_t sh[1024];
+  int64_t carry = 0;
+  for (int64_t c0 = 0; c0 < ntiles; c0 += 1024) {
+    const int64_t i = c0 + threadIdx.x;
+    const int64_t v = i < ntiles ? tsum[i] : 0;
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+      const int64_t t = threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
+      __syncthreads();
+      sh[threadIdx.x] += t;
+      __syncthreads();
+    }
+    if (i < ntiles) tsum[i] = carry + sh[threadIdx.x] - v;
+    const int64_t tot = sh[1023];
+    __syncthreads();
+    carry += tot;
+  }
+}
+
+// exclusive positions of one tile: thread-local running sums over SCAN_IT consecutive counts,
+// a workgroup scan of the thread sums, the tile's offset; element e = j * n + r -> rp[j][r]
+__global__ __launch_bounds__(SCAN_T) void scan_tile_write_kernel(const int32_t* __restrict__ in,
+                                                                 int64_t n, int nb,
+                                                                 const int64_t* __restrict__ toff,
+                                                                 int64_t* __restrict__ rp) {
+  const int64_t len = (int64_t)nb * n;
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_IT;
+  int32_t v[SCAN_IT];
+  int64_t s = 0;
+#pragma unroll
+  for (int u = 0; u < SCAN_IT; ++u) {
+    v[u] = base + u < len ? in[base + u] : 0;
+    s += v[u];
+  }
+  __shared__ int64_t sh[SCAN_T];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 1; off < SCAN_T; off <<= 1) {
+    const int64_t t = threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
+    __syncthreads();
+    sh[threadIdx.x] += t;
+    __syncthreads();
+  }
+  int64_t run = toff[blockIdx.x] + sh[threadIdx.x] - s;
+#pragma unroll
+  for (int u = 0; u < SCAN_IT; ++u) {
+    const int64_t e = base + u;
+    if (e < len) {
+      const int64_t j = e / n, r = e - j * n;
+      rp[j * (n + 1) + r] = run;
+    }
+    run += v[u];
+  }
+}
+
+__global__ void cb_rp_finish_kernel(int64_t* __restrict__ rp, int32_t* __restrict__ rp32,
+                                    int64_t n, int nb, int64_t nnz) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)nb * (n + 1)) return;
+  const int64_t j = e / (n + 1), r = e - j * (n + 1);
+  int64_t v;
+  if (r == n) v = j + 1 < nb ? rp[(j + 1) * (n + 1)] : nnz;
+  else v = rp[e];
+  if (r == n) rp[e] = v;
+  rp32[e] = (int32_t)(v - rp[j * (n + 1)]);
+}
+
+extern "C" hipError_t n2v2r_launch_cb_rowptrs(const int32_t* cnt, int64_t n, int nb, int64_t nnz,
+                                              int64_t* tsum, size_t tsum_elems, int64_t* rp,
+                                              int32_t* rp32, hipStream_t stream) {
+  const int64_t len = (int64_t)nb * n;
+  const int64_t ntiles = (len + SCAN_TILE - 1) / SCAN_TILE;
+  if (ntiles < 1 || (size_t)ntiles > tsum_elems) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(scan_tile_sums_kernel, dim3((unsigned)ntiles), dim3(SCAN_T), 0, stream, cnt,
+                     len, tsum);
+  hipLaunchKernelGGL(scan_tile_offsets_kernel, dim3(1), dim3(1024), 0, stream, tsum, ntiles);
+  hipLaunchKernelGGL(scan_tile_write_kernel, dim3((unsigned)ntiles), dim3(SCAN_T), 0, stream, cnt,
+                     n, nb, tsum, rp);
+  const int64_t tot = (int64_t)nb * (n + 1);
+  hipLaunchKernelGGL(cb_rp_finish_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                     stream, rp, rp32, n, nb, nnz);
   return hipGetLastError();
 }
 
-extern "C" hipError_t n2v2r_launch_cb_fill(const CsrDev& A, int64_t cw, const int64_t* rp,
+extern "C" int64_t n2v2r_cb_scan_tiles(int64_t n, int nb) {
+  return ((int64_t)nb * n + SCAN_TILE - 1) / SCAN_TILE;
+}
+
+extern "C" hipError_t n2v2r_launch_cb_count(const CsrDev& A, int64_t cw, int nb, int32_t* cnt,
+                                            hipStream_t stream) {
+  if (A.n_rows <= 0) return hipSuccess;
+  const dim3 g((unsigned)((A.n_rows + 255) / 256));
+  if (nb == 8) hipLaunchKernelGGL(cb_count_kernel<8>, g, dim3(256), 0, stream, A, cw, cnt);
+  else if (nb == 16) hipLaunchKernelGGL(cb_count_kernel<16>, g, dim3(256), 0, stream, A, cw, cnt);
+  else if (nb == 32) hipLaunchKernelGGL(cb_count_kernel<32>, g, dim3(256), 0, stream, A, cw, cnt);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+extern "C" hipError_t n2v2r_launch_cb_fill(const CsrDev& A, int64_t cw, int nb, const int64_t* rp,
                                            int32_t* idx, float* dat, hipStream_t stream) {
   if (A.n_rows <= 0) return hipSuccess;
-  hipLaunchKernelGGL(cb_fill_kernel, dim3((unsigned)((A.n_rows + 255) / 256)), dim3(256), 0,
-                     stream, A, cw, rp, idx, dat);
+  const dim3 g((unsigned)((A.n_rows + 255) / 256));
+  if (nb == 8) hipLaunchKernelGGL(cb_fill_kernel<8>, g, dim3(256), 0, stream, A, cw, rp, idx, dat);
+  else if (nb == 16) hipLaunchKernelGGL(cb_fill_kernel<16>, g, dim3(256), 0, stream, A, cw, rp, idx, dat);
+  else if (nb == 32) hipLaunchKernelGGL(cb_fill_kernel<32>, g, dim3(256), 0, stream, A, cw, rp, idx, dat);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -129,7 +129,9 @@ class N2V2R:
 
     def __fit(self):
         """UASE on the GPU (replaces ``se.UASE``, model.py:51-55)."""
+        t0 = time.time()
         eng = self._load_layers()
+        self.stage_seconds["load"] = time.time() - t0
         seed = self._seed if self._seed is not None else int(np.random.randint(1, 2**31 - 1))
         opts = dict(seed=seed)
         opts.update(self._eig_options)

@@ -8,6 +8,9 @@ from oracle import n2v2r_oracle as orc
 
 pytestmark = pytest.mark.gpu
 
+# fixtures held to SURVEY 8(c)(4)'s end-to-end rank bar (tau >= 0.998, identical top set)
+END_TO_END_STRICT = ("demo", "er_cfg1", "ties_nan", "directed_weighted")
+
 
 # ----------------------------------------------------------------------------- SpMM
 @pytest.mark.parametrize("b", [8, 16, 32, 64])
@@ -296,10 +299,21 @@ def test_model_end_to_end(name):
             if not corr.any():
                 np.testing.assert_array_equal(ref_b, fx[f"{strategy}/{key}/borda_stable"])
             tau = kendalltau(b, ref_b).statistic
-            # tau >= 0.995, or the reference's own seed-to-seed tau minus 0.02
-            # where near-tied distances (communities in low dimension) make ranks noise-level
+            k = min(100, len(nodes) // 10)
+            top = len(set(np.argsort(-b, kind="stable")[:k]) &
+                      set(np.argsort(-ref_b, kind="stable")[:k]))
             tau_env = _tau_envelope(Y_other, fx, strategy, key)
-            assert tau >= min(0.995, tau_env - 0.02), (name, strategy, key, tau, tau_env)
+            print(f"{name}/{strategy}/{key}: Kendall tau {tau:.6f} (reference envelope "
+                  f"{tau_env:.6f}), top-{k} overlap {top}")
+            if name in END_TO_END_STRICT:
+                # tau >= 0.998 and the identical top-100 set (top N/10 below
+                # 1000 nodes); measured 0.99995-1.0 on these fixtures
+                assert tau >= 0.998 and top == k, (name, strategy, key, tau, top)
+            else:
+                # k4_strategies (400-node SBM, dims 1..6, correlation columns): near-tied
+                # distances make its ranks noise-level even for the reference, whose own
+                # seed-to-seed tau is 0.966-0.998 here: the bar is that envelope minus 0.02
+                assert tau >= min(0.998, tau_env - 0.02), (name, strategy, key, tau, tau_env)
         Y = model.node_embeddings
         assert Y.shape == fx["Y"].shape
 
