@@ -383,16 +383,17 @@ def main():
     st_t, _ = resident_step(reng, cfg, flags=_lib.EIG_TIME_SPMM)
     roof = roofline_from_stats(st_t, cfg, b)
     if roof is not None and not cfg.get("dense"):
-        col_blocks = reng.spmm_col_blocks(b)
-        roof["kernel"] = ("spmm8_cb_kernel (XCD-local column blocks; + cb_reduce on a side "
-                          "stream)" if col_blocks else "spmm8_pipe_kernel (b = 8, XCD-split "
-                          "layers)" if b == 8 else f"spmm_csr_panel_kernel<{b}>")
+        form = int(st_t.get("spmm_form", 0))
+        roof["kernel"] = {0: "spmm8_pipe_kernel (b = 8)",
+                          1: "spmm8_pipe_kernel (b = 8, layers split over the XCDs)",
+                          2: "spmm8_cb_kernel (XCD-local column blocks; + cb_reduce)",
+                          3: "spmm8_tile_kernel (row tiles x column-block phases, LDS "
+                             "accumulators)"}.get(form, str(form))
         # one 32-B panel row gathered per stored entry (served by L2 / Infinity Cache): the
-        # line-access rate, reported beside the HBM roofline
-        # entries per launch: every layer's in one row-kernel launch, one layer's per
-        # column-block launch
+        # line-access rate, reported beside the HBM roofline.  Entries per launch: every
+        # layer's (row kernel, tiled), one layer's (column blocks + partials)
         nnz_launch = float(sum(nnz)) / (world if mode == "partitioned" else 1)
-        ent = nnz_launch / len(nnz) if col_blocks else nnz_launch
+        ent = nnz_launch / len(nnz) if form == 2 else nnz_launch
         roof["gathered_entries_per_launch"] = ent
         roof["gather_G_entries_per_s"] = round(ent / (roof["avg_launch_ms"] * 1e-3) / 1e9, 1)
     tpath = os.path.join(REPO, "profiles", "spmm_traffic.json")

@@ -57,6 +57,9 @@ enum { N2V2R_EIG_FULL_FIRST_PASS = 1, N2V2R_EIG_DENSE_RR = 2,
        N2V2R_EIG_TEST_BAND_FAIL = 8 /* tests: every banded Rayleigh-Ritz result is treated as
                                        failed, so the reducing, then the dense fallback runs
                                        (and a lean-image fit reruns with images kept) */,
+       N2V2R_EIG_TEST_STURM_FAIL = 32 /* tests: only the Sturm Rayleigh-Ritz result is treated
+                                         as failed (the reducing band path then runs and is
+                                         accepted) */,
        N2V2R_EIG_TIME_SPMM = 16 /* HIP events around every SpMM stage launch of the fit: fills
                                    n2v2r_eig_stats.gpu_ms_spmm / spmm_timed_launches (the in-fit
                                    roofline of bench.py; adds an event pair per launch) */ };
@@ -99,6 +102,10 @@ typedef struct {
   double spmm_stage_bytes[2];
   double est_scale;          /* lean images: the last true / estimated residual scale (1 = none) */
   int lean_checks;           /* lean images: true-residual checks run */
+  int pool_blocks;           /* Krylov blocks the handle's solver pool holds after the fit */
+  int spmm_form;             /* SpMM form of the fit: 0 row kernel, 1 row kernel with the layers
+                                split over the XCDs, 2 column blocks + partial reduce, 3 tiled
+                                column blocks (one launch per stage over all layers), 4 dense */
 } n2v2r_eig_stats;
 
 /* lifecycle */
@@ -171,9 +178,10 @@ int n2v2r_borda_columns(n2v2r_handle* h, const double* D /* C*N column-major */,
 int n2v2r_column_sums(n2v2r_handle* h, int k, float* out /* N */);
 
 /* bipartite projection of a non-square layer (preprocessing_utils.py:16-32): out = W^T W
- * (n x n) when on_columns, else W W^T (m x m), for a host row-major m x n fp32 W. */
-int n2v2r_project(n2v2r_handle* h, int64_t m, int64_t n, const float* W, int on_columns,
-                  float* out);
+ * (n x n) when on_columns, else W W^T (m x m), for a host row-major m x n fp64 W; fp64
+ * arithmetic (fp64 MFMA) as the reference's float64 np.matmul, exactly symmetric output. */
+int n2v2r_project(n2v2r_handle* h, int64_t m, int64_t n, const double* W, int on_columns,
+                  double* out);
 
 /* device sync */
 int n2v2r_synchronize(n2v2r_handle* h);

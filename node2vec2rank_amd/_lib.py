@@ -69,7 +69,8 @@ class EigStats(ctypes.Structure):
                 ("rr_fallbacks", ctypes.c_int), ("gpu_ms_spmm", ctypes.c_double * 2),
                 ("spmm_timed_launches", ctypes.c_int64 * 2),
                 ("spmm_stage_bytes", ctypes.c_double * 2), ("est_scale", ctypes.c_double),
-                ("lean_checks", ctypes.c_int)]
+                ("lean_checks", ctypes.c_int), ("pool_blocks", ctypes.c_int),
+                ("spmm_form", ctypes.c_int)]
 
     def as_dict(self):
         out = {}
@@ -80,7 +81,7 @@ class EigStats(ctypes.Structure):
 
 
 _lib = None
-_lock = threading.Lock()
+_lock = threading.RLock()  # re-entered: acquire_engine -> Engine() -> load()
 
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
@@ -136,7 +137,7 @@ def load(path: str | None = None):
             "n2v2r_rr_band_top": (_i, [_vp, _i, _i, _p(np.float64), ctypes.c_int64, _vp, _i,
                                        _p(np.float64), _p(np.float32)]),
             "n2v2r_set_layer_dense": (_i, [_vp, _i, _i64, _p(np.float32), _i]),
-            "n2v2r_project": (_i, [_vp, _i64, _i64, _p(np.float32), _i, _p(np.float32)]),
+            "n2v2r_project": (_i, [_vp, _i64, _i64, _p(np.float64), _i, _p(np.float64)]),
             "n2v2r_comm_unique_id": (_i, [ctypes.c_char_p, ctypes.c_size_t]),
             "n2v2r_create_rccl": (_i, [_i, _i, _i, ctypes.c_char_p, ctypes.POINTER(_vp)]),
             "n2v2r_simgroup_create": (_i, [_i, ctypes.POINTER(_vp)]),
@@ -466,14 +467,15 @@ class Engine:
         return r == 1
 
     def project(self, W, on: str = "columns"):
-        """W^T W (on="columns") or W W^T (on="rows") of a dense m x n matrix, fp32 on the GPU."""
-        W = np.ascontiguousarray(np.asarray(W), dtype=np.float32)
+        """W^T W (on="columns") or W W^T (on="rows") of a dense m x n matrix, fp64 on the GPU
+        (the reference's float64 ``np.matmul``, ``preprocessing_utils.py:22-24``)."""
+        W = np.ascontiguousarray(np.asarray(W), dtype=np.float64)
         m, n = W.shape
         oc = on.casefold() == "columns"
         if not oc and on.casefold() != "rows":
             raise ValueError("Unknown projection type, options are columns or rows")
         k = n if oc else m
-        out = np.empty((k, k), dtype=np.float32)
+        out = np.empty((k, k), dtype=np.float64)
         self._check(self.lib.n2v2r_project(self.h, m, n, W, int(oc), out), "project")
         return out
 
@@ -515,3 +517,39 @@ def default_engine(device: int = 0) -> Engine:
         e = Engine(device)
         _default[device] = e
     return e
+
+
+# Handles per device for the drop-in N2V2R models: a handle whose owner model is gone (or has
+# none) is reused with its device allocations; a new one is made while every handle is owned,
+# up to POOL_MAX, beyond which the least recently acquired handle is taken over (its owner's
+# ``_hand_over()`` first copies what it still needs to the host).
+POOL_MAX = 4
+_pool = {}
+_pool_tick = [0]
+
+
+def engine_owner(eng: Engine):
+    ref = getattr(eng, "_owner", None)
+    return ref() if ref is not None else None
+
+
+def acquire_engine(device: int, owner) -> Engine:
+    import weakref
+    with _lock:
+        handles = _pool.setdefault(device, [])
+        handles[:] = [e for e in handles if e.h is not None]
+        free = [e for e in handles if engine_owner(e) is None]
+        if free:
+            eng = free[0]
+        elif len(handles) < POOL_MAX:
+            eng = Engine(device)
+            handles.append(eng)
+        else:
+            eng = min(handles, key=lambda e: getattr(e, "_tick", 0))
+            prev = engine_owner(eng)
+            if prev is not None and hasattr(prev, "_hand_over"):
+                prev._hand_over()
+        _pool_tick[0] += 1
+        eng._tick = _pool_tick[0]
+        eng._owner = weakref.ref(owner)
+        return eng

@@ -22,7 +22,6 @@
 // + an all-reduce, so every rank holds identical small matrices and runs the identical host
 // Rayleigh-Ritz.  Communicators: RCCL (one process per GPU) or an in-process thread group
 // (W ranks on one GPU, for testing the partitioned algorithm without W devices).
-#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -76,6 +75,7 @@ struct SpmmTileArgs {  // spmm.hip: row tiles x column-block phases
   int nb;
   int sum;
   int tile_rows;
+  int pair;
 };
 #define DIST_MAX_COLS 256
 struct DistPlan {
@@ -92,7 +92,7 @@ hipError_t n2v2r_launch_spmm_cb(const SpmmCbArgs& a, hipStream_t stream);
 hipError_t n2v2r_launch_cb_reduce(const float* P, int nparts, int64_t pstride, int64_t n,
                                   float* out, int64_t ldo, hipStream_t stream);
 hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, int rpw, hipStream_t stream);
-int n2v2r_spmm_tile_rows(int64_t n, int ncu);
+int n2v2r_spmm_tile_rows(int64_t n, int ncu, int wpc);
 int n2v2r_cb_rpw(const CsrBlk* A, int nb, int64_t n);
 hipError_t n2v2r_launch_cb_count(const CsrDev& A, int64_t cw, int nb, int32_t* cnt,
                                  hipStream_t stream);
@@ -168,6 +168,8 @@ hipError_t n2v2r_launch_dense_gemm(const float* A, int64_t lda, int64_t rows, in
                                    const float* X, int ldx, int b, float* Y, int64_t ldy,
                                    float beta, const float* colscale, float* work,
                                    size_t work_elems, hipStream_t stream);
+hipError_t n2v2r_launch_syrk_f64(const double* W, int64_t sk, int64_t si, int64_t kd, int64_t r,
+                                 double* out, int64_t ldo, hipStream_t stream);
 hipError_t n2v2r_launch_transpose(const float* in, int64_t ldi, int64_t rows, int64_t cols,
                                   float* out, int64_t ldo, hipStream_t stream);
 hipError_t n2v2r_launch_mismatch(const float* a, const float* b, int64_t ld, int64_t rows,
@@ -191,8 +193,7 @@ hipError_t n2v2r_launch_zsum(const float* const* parts, int count, float* zout, 
                              hipStream_t stream);
 hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp, double* theta, double* scr,
                                  size_t scr_elems, double* Y, float* S, int ldS, int p, int* err,
-                                 hipStream_t stream, hipEvent_t before_vectors,
-                                 hipStream_t vec_stream, hipEvent_t after_vectors);
+                                 hipStream_t stream);
 size_t n2v2r_rr_sturm_scratch(int c, int p);
 hipError_t n2v2r_launch_csr_scan(const int64_t* ip, const int32_t* ix, const float* dv,
                                  int64_t n_rows, int64_t n_cols, uint64_t* keys, int32_t* idx,
@@ -229,35 +230,6 @@ static bool lean_enabled() {
   return !(e && e[0] == '0');
 }
 
-// N2V2R_RESTART_OVERLAP=1: the thick-restart expansion issued on a second stream beside the
-// inverse iteration (A/B switch, off by default: cfg2 39.85 vs 39.46 ms per step although the
-// trace shows the expansion inside the inverse iteration's span).  Read per fit.
-static bool restart_overlap_enabled() {
-  const char* e = std::getenv("N2V2R_RESTART_OVERLAP");
-  return e && e[0] == '1';
-}
-
-// N2V2R_LEAN_OVERLAP=1 (A/B, off by default): under lean images the restart block (orth(W_last)
-// against the old basis) and its SpMM image are issued on a second stream beside the inverse
-// iteration of the Sturm Rayleigh-Ritz (they need nothing from it), the host joining the two
-// streams at the cycle end.  Measured cfg2 36.4-36.9 vs 35.8-36.0 ms per step: the trace under
-// rocprofv3 shows the expansion inside the inverse iteration's span (cycle ~140 us shorter), but
-// unprofiled every form with a second queue lost (GPU-side join +0.9 ms, host join +0.6-0.9 ms,
-// inverse iteration on a CU-masked stream of its own +2-3 ms).  Read per fit.
-static bool lean_overlap_enabled() {
-  const char* e = std::getenv("N2V2R_LEAN_OVERLAP");
-  return e && e[0] == '1';
-}
-
-// N2V2R_INV_CUS=k > 0: the inverse iteration runs on a stream of its own with k CUs and the
-// restart expansion on the other CUs (disjoint hipExtStreamCreateWithCUMask masks); 0: the same
-// on two plain streams; -1 (default): the inverse iteration stays on the main stream.  A/B only:
-// the main stream then waits for the inverse-iteration stream's event, and such a wait on
-// another queue cost ~150 us per cycle on MI355X (cfg2 +2 ms per fit).
-static int inv_cus_wanted() {
-  const char* e = std::getenv("N2V2R_INV_CUS");
-  return e ? std::atoi(e) : -1;
-}
 
 namespace {
 
@@ -570,9 +542,6 @@ struct EigWorkspace {
   DevBuf dbgflag;                             // N2V2R_DEBUG_FINITE result flag
   DevBuf s2part;                              // [K][npad][8] XCD-split second-stage outputs
   DevBuf sturm;                               // Sturm Rayleigh-Ritz: assembled arrow + band
-  // the restart expansion run beside the Rayleigh-Ritz stage (spec stream): its own Gram
-  // partials, Gram and flags, so it shares no scratch with the stage
-  DevBuf spec_partial, spec_gsmall, spec_flg, spec_any;
   DevBuf rres;                                // lean images: R of the restart projection
   DevBuf skipc;                               // full passes skipped (selective reorthogonalisation)
   DevBuf tblk;                                // tiled SpMM: CsrBlk [2][K][nb] (stage 1, stage 2)
@@ -585,14 +554,6 @@ struct n2v2r_handle {
   // side stream + events for the column-block SpMM's stage-1 reduce overlap
   hipStream_t side = nullptr;
   hipEvent_t cb_ev[2 * SPMM_MAX_LAYERS] = {};
-  // stream + events of the restart expansion overlapped with the Rayleigh-Ritz stage
-  hipStream_t spec = nullptr;
-  hipEvent_t spec_ev[2] = {};
-  // lean-image restart overlap: the inverse iteration's stream and the expansion's stream, on
-  // disjoint CU masks (inv_cus CUs for the former; 0: plain streams)
-  hipStream_t inv_s = nullptr, spec_m = nullptr;
-  hipEvent_t inv_ev = nullptr;
-  int inv_cus = -1;
   // pinned host staging of the per-cycle read-back (residuals, Ritz values, flags): the copies
   // are asynchronous and one stream synchronisation ends the cycle (pageable targets made each
   // copy a host round trip of its own)
@@ -872,7 +833,7 @@ struct Eig {
   // column blocks as row tiles x block phases with LDS accumulators (no partials, no reduce;
   // N2V2R_SPMM_TILE=0: the partial + reduce form)
   bool tiled = false;
-  int tile_rows = 0, tile_rpw[2] = {0, 0}, tile_nb = CB_NB;
+  int tile_rows = 0, tile_rpw[2] = {0, 0}, tile_nb = CB_NB, tile_pair = 1;
   // XCD-split second SpMM stage (b = 8, one GPU): A_k Z_k lands in per-layer partials on the
   // XCDs of layer k; the image W = sum_k of them is stored by the next Gram pass that reads it
   // (the local first pass of the next expansion), or by materialize() before any other use
@@ -964,8 +925,7 @@ struct Eig {
     EigWorkspace& w = h->ews;
     for (DevBuf* d : {&w.rinv, &w.flg, &w.anyflag, &w.gsmall, &w.csmall, &w.tri, &w.refl,
                       &w.ytri, &w.tscr, &w.hband, &w.band, &w.varr, &w.taua, &w.rrerr, &w.fcoef,
-                      &w.cbpart, &h->partial, &h->theta, &h->resid, &w.spec_partial,
-                      &w.spec_gsmall, &w.spec_flg, &w.spec_any})
+                      &w.cbpart, &h->partial, &h->theta, &h->resid})
       if (d->p) HIPCHK(hipMemsetAsync(d->p, 0xFF, d->bytes, st));
     for (auto& d : w.pool) HIPCHK(hipMemsetAsync(d->p, 0xFF, d->bytes, st));
     for (auto& d : w.zk) HIPCHK(hipMemsetAsync(d->p, 0xFF, d->bytes, st));
@@ -1166,6 +1126,7 @@ struct Eig {
     a.nb = tile_nb;
     a.sum = 0;
     a.tile_rows = tile_rows;
+    a.pair = tile_pair;
     double b0 = 0.0, b1 = 0.0;
     for (int k = 0; k < K; ++k) {
       a.X[k] = xg;
@@ -1426,38 +1387,10 @@ struct Eig {
     ws.push_back(w);
   }
 
-  // the lean-image restart overlap's streams: the inverse iteration on inv_cus CUs, the
-  // expansion on the others (hipExtStreamCreateWithCUMask); without masks two plain streams
-  void make_overlap_streams() {
-    const int want = inv_cus_wanted();
-    if (h->inv_s && h->inv_cus == want) return;
-    if (h->inv_s) HIPCHK(hipStreamDestroy(h->inv_s));
-    if (h->spec_m) HIPCHK(hipStreamDestroy(h->spec_m));
-    h->inv_s = h->spec_m = nullptr;
-    if (!h->inv_ev) HIPCHK(hipEventCreateWithFlags(&h->inv_ev, hipEventDisableTiming));
-    if (!h->spec_ev[0])
-      for (hipEvent_t& e : h->spec_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    int ncu = 0;
-    HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
-    if (want > 0 && want < ncu) {
-      std::vector<uint32_t> ma((ncu + 31) / 32, 0u), mb((ncu + 31) / 32, 0u);
-      for (int i = 0; i < ncu; ++i) (i < want ? ma : mb)[i / 32] |= 1u << (i % 32);
-      HIPCHK(hipExtStreamCreateWithCUMask(&h->inv_s, (uint32_t)ma.size(), ma.data()));
-      HIPCHK(hipExtStreamCreateWithCUMask(&h->spec_m, (uint32_t)mb.size(), mb.data()));
-    } else {
-      HIPCHK(hipStreamCreateWithFlags(&h->inv_s, hipStreamNonBlocking));
-      HIPCHK(hipStreamCreateWithFlags(&h->spec_m, hipStreamNonBlocking));
-    }
-    h->inv_cus = want;
-  }
 
   int run(int d_, const n2v2r_eig_opts& o, std::vector<double>& theta_out, float* Uout,
           int ldu) {
     d = d_;
-    // a previous fit that ended in an exception may have left a restart expansion in flight
-    if (h->spec) HIPCHK(hipStreamSynchronize(h->spec));
-    if (h->spec_m) HIPCHK(hipStreamSynchronize(h->spec_m));
-    if (h->inv_s) HIPCHK(hipStreamSynchronize(h->inv_s));
     seed = o.seed ? o.seed : 0x5EEDull;
     full_first = (o.solver_flags & N2V2R_EIG_FULL_FIRST_PASS) != 0;
     time_spmm = (o.solver_flags & N2V2R_EIG_TIME_SPMM) != 0;
@@ -1467,6 +1400,7 @@ struct Eig {
     bool lazy = true;
     const bool test_redo = (o.solver_flags & N2V2R_EIG_TEST_REDO_CYCLE) != 0;
     const bool test_band_fail = (o.solver_flags & N2V2R_EIG_TEST_BAND_FAIL) != 0;
+    const bool test_sturm_fail = (o.solver_flags & N2V2R_EIG_TEST_STURM_FAIL) != 0;
     const double tol = o.tol > 0 ? o.tol : 1e-6;
     const int max_restarts = o.max_restarts > 0 ? o.max_restarts : 2000;
     // default panel width: 8 for CSR layers (vector-applications grow with b); 32 for dense
@@ -1483,7 +1417,8 @@ struct Eig {
       // default basis: 3.2 keep for the dense Rayleigh-Ritz (its cost grows as c^3); 4.8 keep
       // (<= 512) for the banded one (b = 8), where fewer, longer cycles win (cfg2: 14 cycles
       // at c = 256, 7 at c = 384, 13 % fewer block applications)
-      const bool band_ok = b == 8 && !(o.solver_flags & N2V2R_EIG_DENSE_RR);
+      // (a keep that does not fit the banded form's 512-column basis takes the dense one's)
+      const bool band_ok = b == 8 && !(o.solver_flags & N2V2R_EIG_DENSE_RR) && keep + b <= 512;
       maxc = o.max_basis ? o.max_basis
                          : (band_ok ? std::min(512, std::max(keep + 3 * b, (24 * keep) / 5))
                                     : std::max(keep + 3 * b, (16 * keep) / 5));
@@ -1519,11 +1454,12 @@ struct Eig {
     if (col_blocks) {
       const char* te = std::getenv("N2V2R_SPMM_TILE");  // read per fit (A/B runs, tests)
       tiled = !(te && te[0] == '0');
-      // tiled: blocks of N2V2R_SPMM_TILE_NB (default 16: a 2 MB panel block per phase at N = 1M
-      // leaves half of an XCD's L2 to the index stream and to waves a phase apart)
+      // tiled: N2V2R_SPMM_TILE_NB column blocks (4, 8, 16 or 32; default 8 -- cfg4 device-
+      // resident step 1848 ms at 8, 2051 at 16, 2726 at 32: every further block adds a row-
+      // pointer pass and a phase of short rows)
       const char* tn_ = std::getenv("N2V2R_SPMM_TILE_NB");
-      tile_nb = tiled ? (tn_ ? std::atoi(tn_) : 16) : CB_NB;
-      if (tile_nb != 8 && tile_nb != 16 && tile_nb != 32) tile_nb = 16;
+      tile_nb = tiled ? (tn_ ? std::atoi(tn_) : 8) : CB_NB;
+      if (tile_nb != 4 && tile_nb != 8 && tile_nb != 16 && tile_nb != 32) tile_nb = 8;
       for (auto& Lp : h->layers)
         col_blocks = ensure_col_blocks(*Lp, nglob, st, tile_nb) && col_blocks;
       tiled = tiled && col_blocks;
@@ -1532,7 +1468,12 @@ struct Eig {
       if (tiled) {
         int ncu = 0;
         HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
-        tile_rows = n2v2r_spmm_tile_rows(n, ncu);
+        // N2V2R_TILE_PAIR=0/1/2: guarded loads / clamped batched loads / two row groups per
+        // wave step at one workgroup per CU (A/B)
+        const char* tp = std::getenv("N2V2R_TILE_PAIR");
+        tile_pair = tp ? std::atoi(tp) : 1;
+        if (tile_pair < 0 || tile_pair > 2) tile_pair = 1;
+        tile_rows = n2v2r_spmm_tile_rows(n, ncu, tile_pair == 2 ? 1 : 2);
         const int nb = tile_nb;
         std::vector<CsrBlk> hb((size_t)2 * K * nb);
         for (int k = 0; k < K; ++k) {
@@ -1615,22 +1556,9 @@ struct Eig {
     double est_scale = 1.0;  // lean: true / estimated residual seen at a failed final check
     bool rr_armed = false;   // the Rayleigh-Ritz error words zeroed (then by every read-back)
     int lean_checks = 0;
-    const bool spec_ok = band_rr && !h->comm && !lean && restart_overlap_enabled();
-    const bool lean_ovl = lean && !h->comm && lean_overlap_enabled();
     // pinned read-back per cycle: residuals, Ritz values (keep each), flags, R (8 x 8), S's last rows
     const size_t pin_bytes = sizeof(double) * 2 * (size_t)keep + 8 * sizeof(int) +
                              sizeof(double) * 64 + sizeof(float) * 8 * (size_t)keep;
-    if (lean_ovl) make_overlap_streams();
-    if (spec_ok || lean_ovl) {
-      h->ews.spec_partial.ensure(sizeof(double) * h->partial_elems);
-      h->ews.spec_gsmall.ensure(sizeof(double) * (size_t)c_max * c_max);
-      h->ews.spec_flg.ensure(sizeof(int) * 256);
-      h->ews.spec_any.ensure(sizeof(int) * 4);
-      if (spec_ok && !h->spec) {
-        HIPCHK(hipStreamCreateWithFlags(&h->spec, hipStreamNonBlocking));
-        for (hipEvent_t& e : h->spec_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      }
-    }
 
     h->ews.dbgflag.ensure(sizeof(int) * 4);
     poison_scratch();
@@ -1683,12 +1611,7 @@ struct Eig {
       bool dense_rr = !band_rr;
       bool sturm_now = sturm;  // this cycle's banded form (the reducing one after a failure)
       int rr_err = 0;
-      bool spec_live = false;  // the restart expansion is in flight on the spec stream
-      std::vector<float*> specE, specEW;
-      float* spec_pending = nullptr;
-      bool lean_forked = false;  // lean: E_lean and its image EW_lean come from the spec stream
-      float* EW_lean = nullptr;
-      double th_fork = 0, th_forked = 0, th_sync0 = 0, tr0_c = 0;  // host clock (N2V2R_TRACE)
+      double th_sync0 = 0, tr0_c = 0;  // host clock (N2V2R_TRACE)
     rayleigh_ritz:
       {
       // Rayleigh-Ritz, all on the GPU, into the fp32 Ritz coefficients S (c x keep, ld keep)
@@ -1710,77 +1633,11 @@ struct Eig {
         rr_armed = true;  // from here on each read-back zeroes the words it reads
         lds_poison();
         if (sturm_now) {
-          const bool spec_fork = spec_ok && !spec_live;
-          const bool lean_fork = lean_ovl && !spec_live;
           HIPCHK(n2v2r_launch_rr_sturm(h->ews.hband.as<double>(), c, kry0 * b,
                                        h->theta.as<double>(), h->ews.sturm.as<double>(),
                                        h->ews.sturm.bytes / sizeof(double),
                                        h->ews.ytri.as<double>(), h->ews.csmall.as<float>(), keep,
-                                       keep, h->ews.rrerr.as<int>(), st,
-                                       (spec_fork || lean_fork) ? h->spec_ev[0] : nullptr,
-                                       (lean_fork && h->inv_cus >= 0) ? h->inv_s : nullptr,
-                                       h->inv_ev));
-          th_fork = now_ms();
-          if (lean_fork) {
-            // fork: the restart block E = orth(W_last) against the old basis (its first, local
-            // pass leaves R with W_last - Q_loc C = E R: the residual estimates) and its image
-            // M E, on the expansion stream beside the inverse iteration.  Scratch of its own;
-            // the image stays pending in the split partials until the restart.
-            const hipStream_t sx = h->spec_m;
-            HIPCHK(hipStreamWaitEvent(sx, h->spec_ev[0], 0));
-            const hipStream_t st0 = st;
-            st = sx;
-            part_p = h->ews.spec_partial.as<double>();
-            gsm_p = h->ews.spec_gsmall.as<double>();
-            flg_p = h->ews.spec_flg.as<int>();
-            any_p = h->ews.spec_any.as<int>();
-            E_lean = take();
-            const std::vector<float*> loc = local_of(Q);
-            orthonormalize(E_lean, Q, W.back(), &loc, nullptr, false, h->ews.rres.as<double>());
-            // R goes to the host from this stream: the host synchronises both streams at the
-            // cycle end, and no GPU-side join is queued on the main stream (a wait on another
-            // queue's event cost ~150 us per cycle here, more than the overlap saves)
-            h->ensure_pin(pin_bytes);
-            HIPCHK(hipMemcpyAsync(static_cast<double*>(h->pin) + 2 * (size_t)keep + 4,
-                                  h->ews.rres.p, sizeof(double) * 64, hipMemcpyDeviceToHost, st));
-            EW_lean = take();
-            apply_M(E_lean, EW_lean);
-            spec_pending = pending;
-            pending = nullptr;
-            HIPCHK(hipEventRecord(h->spec_ev[1], st));
-            st = st0;
-            part_p = h->partial.as<double>();
-            gsm_p = h->ews.gsmall.as<double>();
-            flg_p = h->ews.flg.as<int>();
-            any_p = h->ews.anyflag.as<int>();
-            spec_live = true;
-            lean_forked = true;
-          }
-          th_forked = now_ms();
-          if (spec_fork) {
-            // fork: the spec stream starts when the inverse iteration does (an 80-wave kernel
-            // of serial chains that leaves the CUs free; beside the all-CU multisection the
-            // expansion only delayed it).  The expansion's own scratch (Gram partials, Gram,
-            // flags; its SpMM panels are not used by the stage) and its pending split image
-            // are kept apart until the join at the restart.
-            HIPCHK(hipStreamWaitEvent(h->spec, h->spec_ev[0], 0));
-            const hipStream_t st0 = st;
-            st = h->spec;
-            part_p = h->ews.spec_partial.as<double>();
-            gsm_p = h->ews.spec_gsmall.as<double>();
-            flg_p = h->ews.spec_flg.as<int>();
-            any_p = h->ews.spec_any.as<int>();
-            expand_one(W.back(), Q, specE, specEW);
-            spec_pending = pending;
-            pending = nullptr;
-            HIPCHK(hipEventRecord(h->spec_ev[1], st));
-            st = st0;
-            part_p = h->partial.as<double>();
-            gsm_p = h->ews.gsmall.as<double>();
-            flg_p = h->ews.flg.as<int>();
-            any_p = h->ews.anyflag.as<int>();
-            spec_live = true;
-          }
+                                       keep, h->ews.rrerr.as<int>(), st));
         } else {
           HIPCHK(n2v2r_launch_rr_band(h->ews.hband.as<double>(), c, kry0 * b, h->theta.as<double>(),
                                       h->ews.band.as<double>(), h->ews.varr.as<double>(),
@@ -1853,9 +1710,7 @@ struct Eig {
         dbg(X[q], n * b, false, "Ritz vectors X = Q S");
         if (!lean) dbg(MX[q], n * b, false, "Ritz images MX = W S");
       }
-      if (lean_forked) {
-        // R (read back) and the restart block come from the expansion stream
-      } else if (lean) {
+      if (lean) {
         // the restart block now (it needs nothing from the Rayleigh-Ritz stage): its first,
         // local pass leaves R with W_last - Q_loc C = Z_{m+1} R, Z_{m+1} orthonormal.  Built
         // once per cycle: a Rayleigh-Ritz fallback (goto rayleigh_ritz) reuses it and R.
@@ -1890,7 +1745,7 @@ struct Eig {
           ++ns;
         };
         if (lean) {
-          if (!lean_forked) seg(h->ews.rres.p, wrr, 128);
+          seg(h->ews.rres.p, wrr, 128);
           seg(h->ews.csmall.as<float>() + (size_t)(c - b) * keep, wsl, 8 * keep);
         } else {
           seg(h->resid.p, wres, 2 * keep);
@@ -1904,20 +1759,14 @@ struct Eig {
         if (!dense_rr) seg(h->ews.rrerr.p, wflag + 2, 2, 1);
         else seg(nullptr, wflag + 2, 2);
         HIPCHK(n2v2r_launch_pack_words(src, dw, nw, clr, ns, h->ews.rback.p, st));
-        // (lean fork: R comes from the expansion stream's own copy into prr)
-        const size_t upto = (lean && !lean_forked) ? pin_bytes : sizeof(int) * (size_t)(wflag + 8);
+        const size_t upto = lean ? pin_bytes : sizeof(int) * (size_t)(wflag + 8);
         HIPCHK(hipMemcpyAsync(h->pin, h->ews.rback.p, upto, hipMemcpyDeviceToHost, st));
-        if (lean && lean_forked)  // the last 8 rows of S sit after prr in the pinned block
-          HIPCHK(hipMemcpyAsync(psl, h->ews.rback.as<unsigned>() + wsl, sizeof(float) * 8 * keep,
-                                hipMemcpyDeviceToHost, st));
       }
       th_sync0 = now_ms();
       HIPCHK(hipStreamSynchronize(st));
-      if (lean_forked) HIPCHK(hipEventSynchronize(h->spec_ev[1]));
       if (trace)
-        fprintf(stderr, "[n2v2r] cycle %d host: rr start %.3f, sturm launches %.3f, fork %.3f, "
-                "to sync %.3f, sync %.3f ms\n", cycle, tr0_c - t_start, th_fork - tr0_c,
-                th_forked - th_fork, th_sync0 - th_forked, now_ms() - th_sync0);
+        fprintf(stderr, "[n2v2r] cycle %d host: rr start %.3f, to sync %.3f, sync %.3f ms\n",
+                cycle, tr0_c - t_start, th_sync0 - tr0_c, now_ms() - th_sync0);
       if (lean) {  // ||M x_j - theta_j x_j||^2 = ||R s_j(last block)||^2 (Krylov-Schur), scaled
         for (int j = 0; j < keep; ++j) {
           double acc = 0.0;
@@ -1932,7 +1781,7 @@ struct Eig {
         std::copy(pres, pres + keep, res2.begin());
       }
       std::copy(pth, pth + keep, wh.begin());
-      if (!dense_rr) rr_err = test_band_fail ? 1 : pflag[2];
+      if (!dense_rr) rr_err = (test_band_fail || (test_sturm_fail && sturm_now)) ? 1 : pflag[2];
       if (trace && !dense_rr && sturm_now)
         fprintf(stderr, "[n2v2r] cycle %d: %d of %d Ritz vectors took a second solve\n", cycle,
                 pflag[3], keep);
@@ -1972,18 +1821,9 @@ struct Eig {
             refilled = 1;
             break;
           }
-      if (spec_live && !lean_forked) {
-        // join: the main stream waits for the expansion before any of its blocks (or the
-        // buffers it wrote) is used or given back (lean fork: the host synchronised it above)
-        HIPCHK(hipStreamWaitEvent(st, h->spec_ev[1], 0));
-      }
       if (refilled) {  // a second pass refilled a column: expand this cycle again, 3 passes
         if (trace) fprintf(stderr, "[n2v2r] rank-deficient block, cycle %d expanded again\n", cycle);
-        for (float* p : specE) give(p);
-        for (float* p : specEW) give(p);
         give(E_lean);
-        give(EW_lean);
-        spec_pending = nullptr;  // its partials are dropped with it
         for (int q = 0; q < pb; ++q) {
           give(X[q]);
           give(MX[q]);
@@ -2039,11 +1879,6 @@ struct Eig {
         // (their images by SpMM) decide
         ++lean_checks;
         const int qd = (d + b - 1) / b;
-        if (lean_forked && spec_pending) {  // these applications reuse the split partials
-          pending = spec_pending;
-          spec_pending = nullptr;
-          materialize();
-        }
         std::vector<float*> MV(qd);
         for (int q = 0; q < qd; ++q) {
           MV[q] = take();
@@ -2087,26 +1922,15 @@ struct Eig {
         }
       }
       if (done) {
-        for (float* p : specE) give(p);
-        for (float* p : specEW) give(p);
         give(E_lean);
-        give(EW_lean);
         break;
       }
       // restart: [X | orth(W_last) against the old basis] (thick restart)
       std::vector<float*> E, EW;
-      if (lean_forked) {
-        E.push_back(E_lean);
-        EW.push_back(EW_lean);
-        pending = spec_pending;  // (nullptr when a true-residual check stored it already)
-      } else if (lean) {
+      if (lean) {
         E.push_back(E_lean);
         EW.push_back(take());
         apply_M(E_lean, EW[0]);
-      } else if (spec_live) {
-        E = specE;
-        EW = specEW;
-        pending = spec_pending;
       } else {
         expand_one(W.back(), Q, E, EW);
       }
@@ -2153,6 +1977,11 @@ struct Eig {
       stats->rr_fallbacks = stats_rr_fallbacks;
       stats->est_scale = est_scale;
       stats->lean_checks = lean_checks;
+      stats->pool_blocks = (int)h->ews.pool.size();
+      stats->spmm_form = h->dense_layers() ? 4
+                         : (col_blocks && tiled) ? 3
+                         : col_blocks ? 2
+                         : split2 ? 1 : 0;
       tsum(stats);
     }
     return (conv == d || stagnated) ? N2V2R_OK : N2V2R_ERR_NO_CONVERGENCE;
@@ -2289,12 +2118,6 @@ void n2v2r_destroy(n2v2r_handle* h) {
   for (hipEvent_t& e : h->cb_ev)
     if (e) (void)hipEventDestroy(e);
   if (h->side) (void)hipStreamDestroy(h->side);
-  for (hipEvent_t e : h->spec_ev)
-    if (e) (void)hipEventDestroy(e);
-  if (h->spec) (void)hipStreamDestroy(h->spec);
-  if (h->inv_s) (void)hipStreamDestroy(h->inv_s);
-  if (h->spec_m) (void)hipStreamDestroy(h->spec_m);
-  if (h->inv_ev) (void)hipEventDestroy(h->inv_ev);
   if (h->pin) (void)hipHostFree(h->pin);
   for (hipEvent_t e : h->tev) (void)hipEventDestroy(e);
   if (h->cstream) (void)hipStreamSynchronize(h->cstream);
@@ -2538,14 +2361,19 @@ int n2v2r_set_layer_dense(n2v2r_handle* h, int k, int64_t n, const float* A, int
                        sizeof(float) * n, h->nloc, hipMemcpyHostToDevice));
     bool sym = symmetric == N2V2R_SYM_YES;
     if (!sym) {
-      // A^T rows [row0, row0 + nloc) = columns of A: stage all of A once, transpose the block
+      // A^T rows [row0, row0 + nloc) = columns of A: a partitioned handle stages all of A once
+      // (one GPU: the rows already uploaded are all of A)
       DevBuf full;
-      full.ensure(sizeof(float) * n * L.lda);
-      HIPCHK(hipMemcpy2D(full.p, sizeof(float) * L.lda, A, sizeof(float) * n, sizeof(float) * n,
-                         n, hipMemcpyHostToDevice));
+      const float* src = L.dA.as<float>();
+      if (h->comm) {
+        full.ensure(sizeof(float) * n * L.lda);
+        HIPCHK(hipMemcpy2D(full.p, sizeof(float) * L.lda, A, sizeof(float) * n,
+                           sizeof(float) * n, n, hipMemcpyHostToDevice));
+        src = full.as<float>();
+      }
       L.dAT.ensure(sizeof(float) * nl * L.lda);
-      HIPCHK(n2v2r_launch_transpose(full.as<float>() + h->row0, L.lda, n, h->nloc,
-                                    L.dAT.as<float>(), L.lda, h->stream));
+      HIPCHK(n2v2r_launch_transpose(src + h->row0, L.lda, n, h->nloc, L.dAT.as<float>(), L.lda,
+                                    h->stream));
       if (symmetric == N2V2R_SYM_DETECT) {
         DevBuf cnt;
         cnt.ensure(sizeof(unsigned long long));
@@ -2614,8 +2442,10 @@ int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_sta
         h->err = "a layer was not loaded";
         return N2V2R_ERR_BAD_ARG;
       }
-    if (d < 1 || d > 256 || d >= h->n) {
-      h->set_err("embedding dimension %d out of range [1, min(256, n-1)]", d);
+    // d <= 600: the kept Ritz vectors (max(d + 16, 5 d / 4)) plus one block must fit the
+    // Rayleigh-Ritz kernels' 768-column basis
+    if (d < 1 || d > 600 || d >= h->n) {
+      h->set_err("embedding dimension %d out of range [1, min(600, n-1)]", d);
       return N2V2R_ERR_BAD_ARG;
     }
     n2v2r_eig_opts o{};
@@ -3015,36 +2845,22 @@ int n2v2r_column_sums(n2v2r_handle* h, int k, float* out) {
 }
 
 // Bipartite projection (replaces bipartite_to_unipartite_projection, preprocessing_utils.py:16-32,
-// which network_transform applies to non-square layers, :128-130): out = W^T W (n x n,
-// on_columns) or W W^T (m x m) for a host row-major m x n fp32 W, as 64-column MFMA GEMM slices
-// on the GPU (fp32 accumulation; the reference multiplies in the CSV's dtype, float64).
-int n2v2r_project(n2v2r_handle* h, int64_t m, int64_t n, const float* W, int on_columns,
-                  float* out) {
+// which network_transform applies to non-square layers, :130-132): out = W^T W (n x n,
+// on_columns) or W W^T (m x m) for a host row-major m x n fp64 W, in fp64 as the reference's
+// float64 np.matmul (syrk_f64_kernel: v_mfma_f64_16x16x4_f64, exactly symmetric output).
+int n2v2r_project(n2v2r_handle* h, int64_t m, int64_t n, const double* W, int on_columns,
+                  double* out) {
   return guarded(h, [&]() -> int {
     if (m < 1 || n < 1 || !W || !out) return N2V2R_ERR_BAD_ARG;
-    const int64_t ldw = (n + 63) / 64 * 64, ldt = (m + 63) / 64 * 64;
-    DevBuf w, wt, o, work;
-    w.ensure(sizeof(float) * m * ldw);
-    wt.ensure(sizeof(float) * n * ldt);
-    HIPCHK(hipMemcpy2D(w.p, sizeof(float) * ldw, W, sizeof(float) * n, sizeof(float) * n, m,
-                       hipMemcpyHostToDevice));
-    HIPCHK(n2v2r_launch_transpose(w.as<float>(), ldw, m, n, wt.as<float>(), ldt, h->stream));
-    // columns: A = W^T (n x m), X = W (m x n);  rows: A = W (m x n), X = W^T (n x m)
-    const float* A = on_columns ? wt.as<float>() : w.as<float>();
-    const int64_t lda = on_columns ? ldt : ldw;
-    const int64_t rows = on_columns ? n : m, kdim = on_columns ? m : n;
-    const float* X = on_columns ? w.as<float>() : wt.as<float>();
-    const int64_t ldx = on_columns ? ldw : ldt;
-    o.ensure(sizeof(float) * rows * rows);
-    const size_t welems = (size_t)rows * 64 * 8;
-    work.ensure(sizeof(float) * welems);
-    for (int64_t j = 0; j < rows; j += 64) {
-      const int bw = (int)std::min<int64_t>(64, rows - j);
-      HIPCHK(n2v2r_launch_dense_gemm(A, lda, rows, kdim, X + j, (int)ldx, bw, o.as<float>() + j,
-                                     rows, 0.f, nullptr, work.as<float>(), welems, h->stream));
-    }
-    HIPCHK(hipMemcpyAsync(out, o.p, sizeof(float) * rows * rows, hipMemcpyDeviceToHost,
-                          h->stream));
+    DevBuf w, o;
+    w.ensure(sizeof(double) * m * n);
+    HIPCHK(hipMemcpyAsync(w.p, W, sizeof(double) * m * n, hipMemcpyHostToDevice, h->stream));
+    // columns: X = W (k = row of W, i = column); rows: X = W^T (k = column, i = row)
+    const int64_t r = on_columns ? n : m, kd = on_columns ? m : n;
+    const int64_t sk = on_columns ? n : 1, si = on_columns ? 1 : n;
+    o.ensure(sizeof(double) * r * r);
+    HIPCHK(n2v2r_launch_syrk_f64(w.as<double>(), sk, si, kd, r, o.as<double>(), r, h->stream));
+    HIPCHK(hipMemcpyAsync(out, o.p, sizeof(double) * r * r, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     return N2V2R_OK;
   });
@@ -3112,7 +2928,7 @@ int n2v2r_rr_band_top(n2v2r_handle* h, int c, int kp, const double* hband, int64
       scr.ensure(sizeof(double) * n2v2r_rr_sturm_scratch(c, p));
       HIPCHK(n2v2r_launch_rr_sturm(hb.as<double>(), c, kp, th.as<double>(), scr.as<double>(),
                                    scr.bytes / sizeof(double), y.as<double>(), s.as<float>(), p,
-                                   p, er.as<int>(), h->stream, nullptr, nullptr, nullptr));
+                                   p, er.as<int>(), h->stream));
       int e = 0;
       HIPCHK(hipMemcpyAsync(&e, er.p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
       HIPCHK(hipMemcpyAsync(w, th.p, sizeof(double) * p, hipMemcpyDeviceToHost, h->stream));

@@ -5,16 +5,20 @@
 //
 //   dense_gemm_kernel<NT>  Y[r0:r0+rows, 0:b] (+)= A[rows x kdim] X[kdim x b]:
 //     v_mfma_f32_32x32x2_f32, one wave per 32 output rows x NT*32 columns, 4 waves per WG
-//     (128 rows); A rows read as two 16-B loads per lane covering 16 consecutive k (the k order
-//     inside each 16-group is permuted identically for A and X: lane half h carries k
-//     8h..8h+7, MFMA m sums k = {m, 8+m}); X staged through LDS 64 k-rows at a time (row pitch
-//     padded by 4 floats so the two half-waves hit different banks); split-K over grid.y when
-//     the row tiles alone cannot fill the chip, fp32 partial slabs folded by dense_fold_kernel.
+//     (128 rows).  The 128 x 64 A tile of a round is loaded with 16-B loads, every
+//     wave-instruction 4 rows x 256 B contiguous, into registers one round ahead (in flight
+//     across the current round's MFMAs), then stored to LDS (row pitch 68 floats: the 16-B
+//     operand reads are conflict-free); each lane reads its row's 16 consecutive k from LDS
+//     (lane half h carries k 8h..8h+7, MFMA m sums k = {m, 8+m}; X's k order is permuted
+//     identically).  X staged through LDS 64 k-rows at a time (row pitch padded by 4 floats).
+//     Split-K over grid.y when the row tiles alone cannot fill the chip, fp32 partial slabs
+//     folded by dense_fold_kernel.
 //   transpose_kernel       32x32 LDS tiles (A^T of a directed layer, once at ingest).
 //   mismatch_kernel        counts A != A^T entries (symmetry detection at ingest).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -27,33 +31,61 @@
 __device__ __forceinline__ void dg_load_a(const float* __restrict__ A, int64_t lda, int64_t rows,
                                           int64_t tile_r0, int64_t k0, int64_t k_end,
                                           f32x4 (&v)[8]) {
+  // clamped addresses and unconditional 16-B loads, masked afterwards: all eight loads issue
+  // as one batch (a guarded load per element compiles to a branch and a wait each)
   const int t = threadIdx.x;
   const int kq = (t & 15) * 4;
   const int64_t kg = k0 + kq;
+  const int64_t kc = kg + 4 <= lda ? kg : lda - 4;  // lda % 4 == 0: always in the row
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int64_t r = tile_r0 + u * 16 + (t >> 4);
-    const bool rok = r < rows;
-    const float* p = A + (rok ? r : 0) * lda + kg;
-    if (rok && kg + 4 <= k_end) {
-      v[u] = *reinterpret_cast<const f32x4*>(p);
-    } else {
-      f32x4 w = {0.f, 0.f, 0.f, 0.f};
+    const int64_t rc = r < rows ? r : rows - 1;
+    v[u] = *reinterpret_cast<const f32x4*>(A + rc * lda + kc);
+  }
+}
+
+// the tile loaded by dg_load_a into LDS, rows >= rows and k >= k_end zeroed (applied at store
+// time, so the loads stay in flight across the MFMAs of the previous round)
+__device__ __forceinline__ void dg_store_a(float (*as)[DG_AP], const f32x4 (&v)[8], int64_t rows,
+                                           int64_t tile_r0, int64_t k0, int64_t k_end) {
+  const int t = threadIdx.x;
+  const int64_t kg = k0 + (t & 15) * 4;
 #pragma unroll
-      for (int m = 0; m < 4; ++m) w[m] = (rok && kg + m < k_end) ? p[m] : 0.f;
-      v[u] = w;
+  for (int u = 0; u < 8; ++u) {
+    const bool rok = tile_r0 + u * 16 + (t >> 4) < rows;
+    f32x4 w = v[u];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) w[m] = (rok && kg + m < k_end) ? w[m] : 0.f;
+    *reinterpret_cast<f32x4*>(&as[u * 16 + (t >> 4)][(t & 15) * 4]) = w;
+  }
+}
+
+// X operand values of one k round for lane (i, h): X[k0 + kk + 8h + m][t * 32 + i] at
+// xr[t][kk / 16 * 8 + m] (kk = 0, 16, 32, 48; m = 0..7), clamped loads (masked when used)
+template <int NT>
+__device__ __forceinline__ void dg_load_x(const float* __restrict__ X, int ldx, int b, int64_t k0,
+                                          int64_t k_end, float (&xr)[NT][32]) {
+  const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int j = t * 32 + i < b ? t * 32 + i : b - 1;
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+      const int64_t k = k0 + (q >> 3) * 16 + 8 * h + (q & 7);
+      xr[t][q] = X[(k < k_end ? k : k_end - 1) * ldx + j];
     }
   }
 }
 
-template <int NT>
+template <int NT, bool XREG>
 __global__ __launch_bounds__(256) void dense_gemm_kernel(const float* __restrict__ A, int64_t lda,
                                                          int64_t rows, int64_t kdim,
                                                          int64_t kper, const float* __restrict__ X,
                                                          int ldx, int b, float* __restrict__ out,
                                                          int64_t ldo, int64_t slab) {
   constexpr int XP = NT * 32 + 4;  // padded LDS row pitch
-  __shared__ float xs[DG_KC][XP];
+  __shared__ float xs[XREG ? 1 : DG_KC][XREG ? 1 : XP];
   __shared__ __attribute__((aligned(16))) float as[128][DG_AP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i = lane & 31, h = lane >> 5;
@@ -66,31 +98,77 @@ __global__ __launch_bounds__(256) void dense_gemm_kernel(const float* __restrict
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f32x16{0.f};
   f32x4 nxt[8];
-  if (k_begin < k_end) dg_load_a(A, lda, rows, tile_r0, k_begin, k_end, nxt);
+  float xn[XREG ? NT : 1][32], xc[XREG ? NT : 1][32];
+  if (k_begin < k_end) {
+    dg_load_a(A, lda, rows, tile_r0, k_begin, k_end, nxt);
+    if constexpr (XREG) dg_load_x<NT>(X, ldx, b, k_begin, k_end, xn);
+  }
   for (int64_t k0 = k_begin; k0 < k_end; k0 += DG_KC) {
     const int kn = (k_end - k0) < DG_KC ? (int)(k_end - k0) : DG_KC;
     __syncthreads();  // the previous round's LDS reads are done
+    dg_store_a(as, nxt, rows, tile_r0, k0, k_end);
+    if constexpr (XREG) {
+      // this round's X operands (X rows past k_end and columns past b as zero)
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      *reinterpret_cast<f32x4*>(&as[u * 16 + (threadIdx.x >> 4)][(threadIdx.x & 15) * 4]) = nxt[u];
-    for (int e = threadIdx.x; e < DG_KC * NT * 32; e += 256) {
-      const int kk = e / (NT * 32), j = e % (NT * 32);
-      xs[kk][j] = (kk < kn && j < b) ? X[(k0 + kk) * ldx + j] : 0.f;
+      for (int t = 0; t < (XREG ? NT : 1); ++t)
+#pragma unroll
+        for (int q = 0; q < 32; ++q) {
+          const int kk = (q >> 3) * 16 + 8 * (lane >> 5) + (q & 7);
+          xc[t][q] = (kk < kn && t * 32 + i < b) ? xn[t][q] : 0.f;
+        }
+    } else {
+      // X rows k0 .. k0 + 63: clamped unconditional loads (one batch), masked LDS stores
+      constexpr int XN = DG_KC * NT * 32 / 256;
+      float xv[XN];
+#pragma unroll
+      for (int u = 0; u < XN; ++u) {
+        const int e = threadIdx.x + 256 * u;
+        const int kk = e / (NT * 32), j = e % (NT * 32);
+        const int64_t kr = k0 + (kk < kn ? kk : kn - 1);
+        xv[u] = X[kr * ldx + (j < b ? j : b - 1)];
+      }
+#pragma unroll
+      for (int u = 0; u < XN; ++u) {
+        const int e = threadIdx.x + 256 * u;
+        const int kk = e / (NT * 32), j = e % (NT * 32);
+        xs[kk][j] = (kk < kn && j < b) ? xv[u] : 0.f;
+      }
     }
     __syncthreads();
-    // the next round's A tile in flight while this round's MFMAs run
-    if (k0 + DG_KC < k_end) dg_load_a(A, lda, rows, tile_r0, k0 + DG_KC, k_end, nxt);
+    // the next round's A tile (and X operands) in flight while this round's MFMAs run
+    if (k0 + DG_KC < k_end) {
+      dg_load_a(A, lda, rows, tile_r0, k0 + DG_KC, k_end, nxt);
+      if constexpr (XREG) dg_load_x<NT>(X, ldx, b, k0 + DG_KC, k_end, xn);
+    }
     if (r0 < rows) {
-      for (int kk = 0; kk < kn; kk += 16) {
-        const f32x4 a0 = *reinterpret_cast<const f32x4*>(&as[wave * 32 + i][kk + 8 * h]);
-        const f32x4 a1 = *reinterpret_cast<const f32x4*>(&as[wave * 32 + i][kk + 8 * h + 4]);
+      if constexpr (XREG) {
+        // full rounds unrolled (the X operands index registers); a short last round's missing
+        // k are zero in xc and in the A tile
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
-          const float av = m < 4 ? a0[m] : a1[m - 4];
+        for (int g = 0; g < 4; ++g) {
+          const int kk = g * 16;
+          const f32x4 a0 = *reinterpret_cast<const f32x4*>(&as[wave * 32 + i][kk + 8 * h]);
+          const f32x4 a1 = *reinterpret_cast<const f32x4*>(&as[wave * 32 + i][kk + 8 * h + 4]);
 #pragma unroll
-          for (int t = 0; t < NT; ++t)
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xs[kk + 8 * h + m][t * 32 + i],
-                                                          acc[t], 0, 0, 0);
+          for (int m = 0; m < 8; ++m) {
+            const float av = m < 4 ? a0[m] : a1[m - 4];
+#pragma unroll
+            for (int t = 0; t < (XREG ? NT : 1); ++t)
+              acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xc[t][g * 8 + m], acc[t], 0, 0, 0);
+          }
+        }
+      } else {
+        for (int kk = 0; kk < kn; kk += 16) {
+          const f32x4 a0 = *reinterpret_cast<const f32x4*>(&as[wave * 32 + i][kk + 8 * h]);
+          const f32x4 a1 = *reinterpret_cast<const f32x4*>(&as[wave * 32 + i][kk + 8 * h + 4]);
+#pragma unroll
+          for (int m = 0; m < 8; ++m) {
+            const float av = m < 4 ? a0[m] : a1[m - 4];
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+              acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xs[kk + 8 * h + m][t * 32 + i],
+                                                            acc[t], 0, 0, 0);
+          }
         }
       }
     }
@@ -137,8 +215,17 @@ extern "C" hipError_t n2v2r_launch_dense_gemm(const float* A, int64_t lda, int64
   const int64_t tiles = (rows + 127) / 128;
   // split K until ~2 workgroups per CU, 256-aligned k ranges, slabs within `work`
   int64_t nsplit = 1;
+  static const int split_env = [] {  // N2V2R_DG_SPLIT: workgroups aimed at (A/B)
+    const char* s = getenv("N2V2R_DG_SPLIT");
+    return s ? atoi(s) : 0;
+  }();
+  static const bool xreg = [] {  // N2V2R_DG_XREG=0: X operands staged through LDS (A/B)
+    const char* s = getenv("N2V2R_DG_XREG");
+    return !(s && s[0] == '0');
+  }();
   if (work) {
-    nsplit = (512 + tiles - 1) / tiles;
+    // default: ~2 workgroups per CU (rounded up); N2V2R_DG_SPLIT=w: at most w workgroups
+    nsplit = split_env > 0 ? split_env / tiles : (512 + tiles - 1) / tiles;
     const int64_t kmax = (kdim + 255) / 256;
     if (nsplit > kmax) nsplit = kmax;
     if (nsplit < 1) nsplit = 1;
@@ -155,12 +242,17 @@ extern "C" hipError_t n2v2r_launch_dense_gemm(const float* A, int64_t lda, int64
   const int64_t ldo = work ? b : ldy;
   const int64_t slab = work ? rows * b : 0;
   const dim3 grid((unsigned)tiles, (unsigned)nsplit);
-  if (b <= 32)
-    hipLaunchKernelGGL(dense_gemm_kernel<1>, grid, dim3(256), 0, stream, A, lda, rows, kdim, kper,
-                       X, ldx, b, dst, ldo, slab);
-  else
-    hipLaunchKernelGGL(dense_gemm_kernel<2>, grid, dim3(256), 0, stream, A, lda, rows, kdim, kper,
-                       X, ldx, b, dst, ldo, slab);
+#define DG_LAUNCH(NT, XR)                                                                      \
+  hipLaunchKernelGGL((dense_gemm_kernel<NT, XR>), grid, dim3(256), 0, stream, A, lda, rows, kdim, \
+                     kper, X, ldx, b, dst, ldo, slab)
+  if (b <= 32) {
+    if (xreg) DG_LAUNCH(1, true);
+    else DG_LAUNCH(1, false);
+  } else {
+    if (xreg) DG_LAUNCH(2, true);
+    else DG_LAUNCH(2, false);
+  }
+#undef DG_LAUNCH
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !work) return e;
   const int64_t elems = rows * b;
@@ -213,5 +305,96 @@ extern "C" hipError_t n2v2r_launch_mismatch(const float* a, const float* b, int6
                                             hipStream_t stream) {
   hipLaunchKernelGGL(mismatch_kernel, dim3(2048), dim3(256), 0, stream, a, b, ld, rows, cols,
                      count);
+  return hipGetLastError();
+}
+
+// ---- bipartite projection in fp64 (preprocessing_utils.py:16-32 multiplies in float64) -------
+// out (r x r, row-major) = X^T X, X(k, i) = W[k * sk + i * si] (k < kd, i < r): W^T W with
+// (sk, si) = (n, 1), W W^T with (1, n).  One workgroup per 64 x 64 output tile of the upper
+// triangle (bj >= bi), written to both (bi, bj) and its mirror, so the result is exactly
+// symmetric like numpy's syrk path for `W.T @ W`.  Four waves, each a 32 x 32 quarter as 2 x 2
+// v_mfma_f64_16x16x4_f64 tiles; X staged through LDS in chunks of 16 k (loads ordered along
+// whichever of k / i is contiguous in W); the tile goes back through LDS so both the tile and its
+// mirror are stored as contiguous rows.
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void syrk_f64_kernel(const double* __restrict__ W, int64_t sk,
+                                                       int64_t si, int64_t kd, int64_t r,
+                                                       double* __restrict__ out, int64_t ldo,
+                                                       int nt) {
+  __shared__ double xa[16][68], xb[16][68];
+  __shared__ double tt[64][65];
+  int64_t idx = blockIdx.x;
+  int bi = 0;
+  while (idx >= nt - bi) {
+    idx -= nt - bi;
+    ++bi;
+  }
+  const int bj = bi + (int)idx;
+  const int64_t i0 = (int64_t)bi * 64, j0 = (int64_t)bj * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wi = (wave & 1) * 32, wj = (wave >> 1) * 32;
+  f64x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = (f64x4){0.0, 0.0, 0.0, 0.0};
+  const bool irow = si == 1;  // i contiguous in W (W^T W), else k contiguous (W W^T)
+  for (int64_t k0 = 0; k0 < kd; k0 += 16) {
+#pragma unroll
+    for (int rep = 0; rep < 4; ++rep) {
+      const int e = tid + rep * 256;
+      const int kk = irow ? (e >> 6) : (e & 15);
+      const int ii = irow ? (e & 63) : (e >> 4);
+      const int64_t k = k0 + kk, ia = i0 + ii, ja = j0 + ii;
+      xa[kk][ii] = (k < kd && ia < r) ? W[k * sk + ia * si] : 0.0;
+      xb[kk][ii] = (k < kd && ja < r) ? W[k * sk + ja * si] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 16; ks += 4) {
+      double av[2], bv[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        av[t] = xa[ks + (lane >> 4)][wi + t * 16 + (lane & 15)];
+        bv[t] = xb[ks + (lane >> 4)][wj + t * 16 + (lane & 15)];
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // f64 16x16x4 C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        tt[wi + a * 16 + (lane >> 4) + 4 * q][wj + b * 16 + (lane & 15)] = acc[a][b][q];
+  __syncthreads();
+  for (int e = tid; e < 64 * 64; e += 256) {
+    const int ii = e >> 6, jj = e & 63;
+    if (i0 + ii < r && j0 + jj < r) out[(i0 + ii) * ldo + j0 + jj] = tt[ii][jj];
+  }
+  if (bi != bj) {
+    for (int e = tid; e < 64 * 64; e += 256) {
+      const int jj = e >> 6, ii = e & 63;
+      if (i0 + ii < r && j0 + jj < r) out[(j0 + jj) * ldo + i0 + ii] = tt[ii][jj];
+    }
+  }
+}
+
+extern "C" hipError_t n2v2r_launch_syrk_f64(const double* W, int64_t sk, int64_t si, int64_t kd,
+                                            int64_t r, double* out, int64_t ldo,
+                                            hipStream_t stream) {
+  const int64_t nt = (r + 63) / 64;
+  const int64_t tiles = nt * (nt + 1) / 2;
+  if (r < 1 || kd < 1 || tiles > 0x7fffffffLL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(syrk_f64_kernel, dim3((unsigned)tiles), dim3(256), 0, stream, W, sk, si, kd,
+                     r, out, ldo, (int)nt);
   return hipGetLastError();
 }

@@ -926,10 +926,9 @@ static size_t rs_inviter_lds(int c, int kp) {  // assembly + factor + f + y
 extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
                                            double* theta, double* scr, size_t scr_elems,
                                            double* Y, float* S, int ldS, int p, int* err,
-                                           hipStream_t stream, hipEvent_t before_vectors,
-                                           hipStream_t vec_stream, hipEvent_t after_vectors) {
+                                           hipStream_t stream) {
   if (c < 9 || c > RS_MAXC || c % RS_W || kp % RS_W || kp + RS_W > c || p < 1 || p > c ||
-      ldS < p || (vec_stream && !(before_vectors && after_vectors)))
+      ldS < p)
     return hipErrorInvalidValue;
   const size_t wbis_off = (rs_asm_elems(c, kp) + 7) & ~(size_t)7;
   const int nt_ms = rs_msect_threads();
@@ -1003,10 +1002,6 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
   }
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (before_vectors) {  // the caller may start other work beside the inverse iteration
-    e = hipEventRecord(before_vectors, stream);
-    if (e != hipSuccess) return e;
-  }
   static const int inv_stop = [] {  // N2V2R_INVITER_STOP=k: timing probe, phases after k skipped
     const char* v = getenv("N2V2R_INVITER_STOP");
     return v ? atoi(v) : 0;
@@ -1016,18 +1011,7 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
   const bool inv_par = !(inv_env && inv_env[0] == 'l');
   const char* start_env = getenv("N2V2R_INV_START");  // "rand": random start vectors (A/B)
   const bool start_warm = !(start_env && start_env[0] == 'r');
-  // vec_stream (a stream on CUs of its own): the inverse iteration runs there, between the
-  // before_vectors record and an after_vectors record that `stream` waits for
-  if (vec_stream) {
-    e = hipStreamWaitEvent(vec_stream, before_vectors, 0);
-    if (e != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL(rr_sturm_inviter_kernel, dim3((unsigned)p), dim3(64), linv,
-                     vec_stream ? vec_stream : stream, scr, c, kp, p, pm, wbis, 1e-9, theta, Y, S,
-                     ldS, err, inv_stop, inv_par, start_warm);
-  e = hipGetLastError();
-  if (e != hipSuccess || !vec_stream) return e;
-  e = hipEventRecord(after_vectors, vec_stream);
-  if (e != hipSuccess) return e;
-  return hipStreamWaitEvent(stream, after_vectors, 0);
+  hipLaunchKernelGGL(rr_sturm_inviter_kernel, dim3((unsigned)p), dim3(64), linv, stream, scr, c,
+                     kp, p, pm, wbis, 1e-9, theta, Y, S, ldS, err, inv_stop, inv_par, start_warm);
+  return hipGetLastError();
 }

@@ -505,6 +505,102 @@ __device__ __forceinline__ void cb_row_accumulate(const CsrBlk& A, const float* 
   }
 }
 
+// Two row groups of one column block at once (the tiled kernel): both groups' row pointers,
+// then both groups' first two group-widths of column indices, then all their gathers, issued
+// as batches -- clamped addresses and zero weights instead of guarded loads, so no load waits
+// behind a branch (entries past a row's end gather panel row `beg` or 0 with weight 0: the
+// sums are bit-identical).  Rows longer than 2L entries finish in a plain loop.
+template <int RPW, bool TWO>
+__device__ __forceinline__ void cb_rows2_accumulate(const CsrBlk& A, const float* __restrict__ X,
+                                                    int64_t ldx, int64_t rowA, bool okA,
+                                                    int64_t rowB, bool okB, int lane,
+                                                    f32x4& accA, f32x4& accB) {
+  constexpr int L = 64 / RPW;
+  constexpr int NPS = L / 2;
+  const int g = lane / L;
+  const int li = lane % L;
+  const int sub = li & 1;
+  const int srcbase = g * L + (li >> 1);
+  const int64_t rA = okA ? rowA : 0, rB = (TWO && okB) ? rowB : 0;
+  const int32_t a0 = A.rp[rA], a1 = A.rp[rA + 1];
+  int32_t b0 = 0, b1 = 0;
+  if constexpr (TWO) {
+    b0 = A.rp[rB];
+    b1 = A.rp[rB + 1];
+  }
+  const int64_t begA = A.base + a0, begB = A.base + b0;
+  const int64_t lenA = okA ? (int64_t)(a1 - a0) : 0;
+  const int64_t lenB = (TWO && okB) ? (int64_t)(b1 - b0) : 0;
+  int64_t mx = lenA > lenB ? lenA : lenB;
+#pragma unroll
+  for (int m = L; m < 64; m <<= 1) {
+    const int64_t o = __shfl_xor(mx, m, 64);
+    mx = o > mx ? o : mx;
+  }
+  // first 2L entries of both rows, unconditionally (index 0 of the block's entries when past
+  // the end; A.nnz >= 1 whenever any row of the block has an entry, else mx == 0 below)
+  int cA[2], cB[2];
+  float vA[2], vB[2];
+  if (mx > 0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t p = u * L + li;
+      const int64_t qa = p < lenA ? begA + p : A.base;
+      const int64_t qb = p < lenB ? begB + p : A.base;
+      cA[u] = A.indices[qa];
+      vA[u] = p < lenA ? (A.unit ? 1.f : A.data[qa]) : 0.f;
+      if constexpr (TWO) {
+        cB[u] = A.indices[qb];
+        vB[u] = p < lenB ? (A.unit ? 1.f : A.data[qb]) : 0.f;
+      }
+    }
+    f32x4 xa[4], xb[4];
+    float wa[4], wb[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int u = s >> 1;
+      const int src = srcbase + (s & 1) * NPS;
+      const int ca = __shfl(cA[u], src, 64);
+      wa[s] = __shfl(vA[u], src, 64);
+      xa[s] = *reinterpret_cast<const f32x4*>(X + (int64_t)ca * ldx + sub * 4);
+      if constexpr (TWO) {
+        const int cb = __shfl(cB[u], src, 64);
+        wb[s] = __shfl(vB[u], src, 64);
+        xb[s] = *reinterpret_cast<const f32x4*>(X + (int64_t)cb * ldx + sub * 4);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      accA += wa[s] * xa[s];
+      if constexpr (TWO) accB += wb[s] * xb[s];
+    }
+  }
+  // long rows: the rest one group-width at a time
+  for (int64_t off = 2 * L; off < mx; off += L) {
+    const int64_t p = off + li;
+    const int ca = p < lenA ? A.indices[begA + p] : 0;
+    const float va = p < lenA ? (A.unit ? 1.f : A.data[begA + p]) : 0.f;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int src = srcbase + s * NPS;
+      const int c0 = __shfl(ca, src, 64);
+      const float w0 = __shfl(va, src, 64);
+      accA += w0 * *reinterpret_cast<const f32x4*>(X + (int64_t)c0 * ldx + sub * 4);
+    }
+    if constexpr (TWO) {
+      const int cb = p < lenB ? A.indices[begB + p] : 0;
+      const float vb = p < lenB ? (A.unit ? 1.f : A.data[begB + p]) : 0.f;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int src = srcbase + s * NPS;
+        const int c1 = __shfl(cb, src, 64);
+        const float w1 = __shfl(vb, src, 64);
+        accB += w1 * *reinterpret_cast<const f32x4*>(X + (int64_t)c1 * ldx + sub * 4);
+      }
+    }
+  }
+}
+
 template <int RPW>
 __global__ __launch_bounds__(256) void spmm8_cb_kernel(SpmmCbArgs a) {
   constexpr int L = 64 / RPW;
@@ -601,10 +697,14 @@ struct SpmmTileArgs {
   int nb;                 // column blocks (phases) per layer
   int sum;
   int tile_rows;
+  int pair;               // row-group form (PAIR of spmm8_tile_kernel)
 };
 
-template <int RPW>
-__global__ __launch_bounds__(1024, 8) void spmm8_tile_kernel(SpmmTileArgs a) {
+// PAIR = 1: one row group per step with clamped batched loads, 2 workgroups (32 waves) per CU;
+// PAIR = 2: two row groups per step (two load chains per wave), 1 workgroup (16 waves) per CU
+// with twice the rows; PAIR = 0: one row group per step with guarded loads (cb_row_accumulate)
+template <int RPW, int PAIR>
+__global__ __launch_bounds__(1024, PAIR == 2 ? 4 : 8) void spmm8_tile_kernel(SpmmTileArgs a) {
   constexpr int L = 64 / RPW;
   extern __shared__ f32x4 tacc[];  // [tile_rows][2]
   const int lane = threadIdx.x & 63;
@@ -623,19 +723,31 @@ __global__ __launch_bounds__(1024, 8) void spmm8_tile_kernel(SpmmTileArgs a) {
     const float* X = a.X[k];
     for (int p = 0; p < a.nb; ++p) {
       const CsrBlk A = a.blk[k * a.nb + p];
-      for (int grp = wave; grp * RPW < nrows; grp += nwave) {
-        const int lr = grp * RPW + lane / L;
-        const bool ok = lr < nrows;
-        f32x4 acc = zero;
-        cb_row_accumulate<RPW>(A, X, a.ldx, r0 + lr, ok, lane, acc);
+      // PAIR row groups per step (grp, grp + nwave): PAIR independent load chains per wave
+      for (int grp = wave; grp * RPW < nrows; grp += (PAIR == 2 ? 2 : 1) * nwave) {
+        const int lrA = grp * RPW + lane / L, lrB = lrA + nwave * RPW;
+        const bool okA = lrA < nrows, okB = PAIR == 2 && lrB < nrows;
+        f32x4 accA = zero, accB = zero;
+        if constexpr (PAIR == 0)
+          cb_row_accumulate<RPW>(A, X, a.ldx, r0 + lrA, okA, lane, accA);
+        else
+          cb_rows2_accumulate<RPW, PAIR == 2>(A, X, a.ldx, r0 + lrA, okA, r0 + lrB, okB, lane,
+                                              accA, accB);
 #pragma unroll
         for (int m = 2; m < L; m <<= 1) {
-          acc.x += __shfl_xor(acc.x, m, 64);
-          acc.y += __shfl_xor(acc.y, m, 64);
-          acc.z += __shfl_xor(acc.z, m, 64);
-          acc.w += __shfl_xor(acc.w, m, 64);
+          accA.x += __shfl_xor(accA.x, m, 64);
+          accA.y += __shfl_xor(accA.y, m, 64);
+          accA.z += __shfl_xor(accA.z, m, 64);
+          accA.w += __shfl_xor(accA.w, m, 64);
+          if constexpr (PAIR == 2) {
+            accB.x += __shfl_xor(accB.x, m, 64);
+            accB.y += __shfl_xor(accB.y, m, 64);
+            accB.z += __shfl_xor(accB.z, m, 64);
+            accB.w += __shfl_xor(accB.w, m, 64);
+          }
         }
-        if (ok && li < 2) tacc[lr * 2 + li] += acc;
+        if (okA && li < 2) tacc[lrA * 2 + li] += accA;
+        if (PAIR == 2 && okB && li < 2) tacc[lrB * 2 + li] += accB;
       }
       // the workgroup's waves move to the next panel block together (drifting waves would
       // want several blocks in L2 at once); each wave only touches its own rows' LDS entries
@@ -654,11 +766,13 @@ __global__ __launch_bounds__(1024, 8) void spmm8_tile_kernel(SpmmTileArgs a) {
   }
 }
 
-// rows per tile for the tiled form: 2 workgroups (1024 threads each) per CU, LDS <= 64 KB each
-extern "C" int n2v2r_spmm_tile_rows(int64_t n, int ncu) {
-  int64_t t = (n + 2 * (int64_t)ncu - 1) / (2 * (int64_t)ncu);
+// rows per tile for the tiled form: `wpc` workgroups (1024 threads each) per CU sharing its
+// 160 KB of LDS (32 B of accumulators per row)
+extern "C" int n2v2r_spmm_tile_rows(int64_t n, int ncu, int wpc) {
+  int64_t t = (n + wpc * (int64_t)ncu - 1) / (wpc * (int64_t)ncu);
   t = (t + 15) / 16 * 16;
-  if (t > 2048) t = 2048;
+  const int64_t cap = (wpc == 1 ? 4096 : 2048);
+  if (t > cap) t = cap;
   return (int)t;
 }
 
@@ -666,8 +780,25 @@ extern "C" hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, int rpw, hip
   if (a.K < 1 || a.K > 8 || a.tile_rows < 16 || a.n <= 0) return hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.n + a.tile_rows - 1) / a.tile_rows);
   const size_t lds = sizeof(float) * 8 * (size_t)a.tile_rows;
-#define TILE_LAUNCH(R) \
-  hipLaunchKernelGGL((spmm8_tile_kernel<R>), dim3(grid), dim3(1024), lds, stream, a)
+  if (a.pair < 0 || a.pair > 2) return hipErrorInvalidValue;
+  if (lds > 64 * 1024) {
+    static bool attr = false;
+    if (!attr) {
+      for (const void* f : {(const void*)spmm8_tile_kernel<32, 2>, (const void*)spmm8_tile_kernel<16, 2>,
+                            (const void*)spmm8_tile_kernel<8, 2>, (const void*)spmm8_tile_kernel<4, 2>,
+                            (const void*)spmm8_tile_kernel<2, 2>})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipGetLastError();
+      attr = true;
+    }
+  }
+#define TILE_LAUNCH(R)                                                                     \
+  if (a.pair == 2)                                                                         \
+    hipLaunchKernelGGL((spmm8_tile_kernel<R, 2>), dim3(grid), dim3(1024), lds, stream, a); \
+  else if (a.pair == 1)                                                                    \
+    hipLaunchKernelGGL((spmm8_tile_kernel<R, 1>), dim3(grid), dim3(1024), lds, stream, a); \
+  else                                                                                     \
+    hipLaunchKernelGGL((spmm8_tile_kernel<R, 0>), dim3(grid), dim3(1024), lds, stream, a)
   switch (rpw) {
     case 32: TILE_LAUNCH(32); break;
     case 16: TILE_LAUNCH(16); break;
@@ -902,7 +1033,8 @@ extern "C" hipError_t n2v2r_launch_cb_count(const CsrDev& A, int64_t cw, int nb,
                                             hipStream_t stream) {
   if (A.n_rows <= 0) return hipSuccess;
   const dim3 g((unsigned)((A.n_rows + 255) / 256));
-  if (nb == 8) hipLaunchKernelGGL(cb_count_kernel<8>, g, dim3(256), 0, stream, A, cw, cnt);
+  if (nb == 4) hipLaunchKernelGGL(cb_count_kernel<4>, g, dim3(256), 0, stream, A, cw, cnt);
+  else if (nb == 8) hipLaunchKernelGGL(cb_count_kernel<8>, g, dim3(256), 0, stream, A, cw, cnt);
   else if (nb == 16) hipLaunchKernelGGL(cb_count_kernel<16>, g, dim3(256), 0, stream, A, cw, cnt);
   else if (nb == 32) hipLaunchKernelGGL(cb_count_kernel<32>, g, dim3(256), 0, stream, A, cw, cnt);
   else return hipErrorInvalidValue;
@@ -913,7 +1045,8 @@ extern "C" hipError_t n2v2r_launch_cb_fill(const CsrDev& A, int64_t cw, int nb, 
                                            int32_t* idx, float* dat, hipStream_t stream) {
   if (A.n_rows <= 0) return hipSuccess;
   const dim3 g((unsigned)((A.n_rows + 255) / 256));
-  if (nb == 8) hipLaunchKernelGGL(cb_fill_kernel<8>, g, dim3(256), 0, stream, A, cw, rp, idx, dat);
+  if (nb == 4) hipLaunchKernelGGL(cb_fill_kernel<4>, g, dim3(256), 0, stream, A, cw, rp, idx, dat);
+  else if (nb == 8) hipLaunchKernelGGL(cb_fill_kernel<8>, g, dim3(256), 0, stream, A, cw, rp, idx, dat);
   else if (nb == 16) hipLaunchKernelGGL(cb_fill_kernel<16>, g, dim3(256), 0, stream, A, cw, rp, idx, dat);
   else if (nb == 32) hipLaunchKernelGGL(cb_fill_kernel<32>, g, dim3(256), 0, stream, A, cw, rp, idx, dat);
   else return hipErrorInvalidValue;

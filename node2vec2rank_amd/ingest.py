@@ -128,8 +128,7 @@ def transform(layer: Layer, threshold=None, top_percent_keep=100, binarize=False
             from node2vec2rank_amd import _lib
             engine = _lib.default_engine()
         on = project_unipartite_on.casefold()
-        proj = engine.project(m.toarray().astype(np.float32), on)
-        m = sp.csr_matrix(proj.astype(np.float64))
+        m = sp.csr_matrix(engine.project(m.toarray(), on))
         rows = cols = (cols if on == "columns" else rows)
     m.eliminate_zeros()
     if m.nnz == 0:

@@ -103,22 +103,23 @@ class N2V2R:
 
     @property
     def _engine(self):
-        """The device's shared engine, taken over from the model that used it last (which first
-        copies to the host what it still needs from HBM: its embedding)."""
-        eng = _lib.default_engine(self._device)
-        ref = getattr(eng, "_owner", None)
-        prev = ref() if ref is not None else None
-        if prev is not self:
-            if prev is not None:
-                prev._hand_over()
-            eng._owner = weakref.ref(self)
-            self._layers_loaded = False
-        return eng
+        """This model's engine handle, from the device's pool (``_lib.acquire_engine``): a handle
+        no live model owns is reused with its allocations and solver workspace; when every
+        handle is owned, the least recently used one is taken over and its previous owner first
+        copies to the host what it still needs from HBM (its embedding)."""
+        eng = getattr(self, "_eng", None)
+        if eng is not None and eng.h is not None and _lib.engine_owner(eng) is self:
+            return eng
+        self._eng = _lib.acquire_engine(self._device, self)
+        self._layers_loaded = False
+        return self._eng
 
     def _hand_over(self):
+        """Called by the pool before another model takes this model's handle."""
         if self.eig_stats is not None and self._node_embeddings is None:
-            self._node_embeddings = _lib.default_engine(self._device).embedding().astype(np.float64)
+            self._node_embeddings = self._eng.embedding().astype(np.float64)
         self._layers_loaded = False
+        self._eng = None
 
     def _load_layers(self):
         eng = self._engine

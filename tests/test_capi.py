@@ -50,3 +50,46 @@ def test_null_handle_is_rejected():
     assert lib.n2v2r_synchronize(None) == _lib.ERR_BAD_ARG
 
 
+
+
+def test_engine_pool_reuse_and_takeover(monkeypatch):
+    """The per-device handle pool behind N2V2R (_lib.acquire_engine), with a stub handle whose
+    constructor loads the library as Engine's does (the pool lock is re-entered): a handle whose
+    owner is gone is reused, a new one is made while all are owned (up to POOL_MAX), and beyond
+    that the least recently acquired one is taken over after its owner's _hand_over()."""
+    import gc
+    import threading
+    from node2vec2rank_amd import _lib
+
+    class Stub:
+        def __init__(self, device):
+            _lib.load()
+            self.h = object()
+
+    class Owner:
+        handed = 0
+
+        def _hand_over(self):
+            Owner.handed += 1
+
+    monkeypatch.setattr(_lib, "Engine", Stub)
+    monkeypatch.setattr(_lib, "_pool", {})
+    out = {}
+
+    def work():
+        owners = [Owner() for _ in range(_lib.POOL_MAX)]
+        engs = [_lib.acquire_engine(7, o) for o in owners]
+        out["distinct"] = len({id(e) for e in engs})
+        extra = Owner()
+        e5 = _lib.acquire_engine(7, extra)
+        out["takeover"] = e5 is engs[0] and Owner.handed == 1
+        out["owner"] = _lib.engine_owner(e5) is extra
+        del owners[1]
+        gc.collect()
+        out["reuse"] = _lib.acquire_engine(7, Owner()) is engs[1]
+
+    t = threading.Thread(target=work, daemon=True)
+    t.start()
+    t.join(30)
+    assert not t.is_alive(), "acquire_engine deadlocked"
+    assert out == dict(distinct=_lib.POOL_MAX, takeover=True, owner=True, reuse=True), out

@@ -58,11 +58,13 @@ def test_ingest_matches_reference(name):
 @pytest.mark.parametrize("name", PROJ)
 def test_ingest_projection_matches_reference(engine, name):
     ours, ref, _ = _run(name, engine=engine)
-    # fp32 MFMA projection vs the reference's float64 matmul; the percentile cut may move
-    # entries within fp32 rounding of the cut-off
-    scale = np.abs(ref).max()
-    close = np.abs(ours - ref) <= 1e-5 * scale
-    assert close.mean() > 0.995, (name, close.mean())
+    # fp64 projection (fp64 MFMA) vs the reference's float64 matmul, both cast to float32 at
+    # the end (preprocessing_utils.py:141): the same entries survive the percentile cut, and
+    # the values agree exactly but for a float64 summation-order difference that lands on a
+    # float32 rounding boundary (at most 1 ulp)
+    assert ((ours != 0) == (ref != 0)).all(), name
+    np.testing.assert_array_max_ulp(ours, ref, maxulp=1)
+    print(f"{name}: {int((ours != ref).sum())} of {ref.size} entries differ (<= 1 ulp)")
 
 
 def test_ingest_into_model_matches_dense_path():
