@@ -388,7 +388,9 @@ def main():
                           1: "spmm8_pipe_kernel (b = 8, layers split over the XCDs)",
                           2: "spmm8_cb_kernel (XCD-local column blocks; + cb_reduce)",
                           3: "spmm8_tile_kernel (row tiles x column-block phases, LDS "
-                             "accumulators)"}.get(form, str(form))
+                             "accumulators)",
+                          5: "spmm8_flat_kernel (row tiles x column-block phases, packed flat "
+                             "windows, LDS accumulators)"}.get(form, str(form))
         # one 32-B panel row gathered per stored entry (served by L2 / Infinity Cache): the
         # line-access rate, reported beside the HBM roofline.  Entries per launch: every
         # layer's (row kernel, tiled), one layer's (column blocks + partials)

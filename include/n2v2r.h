@@ -105,7 +105,9 @@ typedef struct {
   int pool_blocks;           /* Krylov blocks the handle's solver pool holds after the fit */
   int spmm_form;             /* SpMM form of the fit: 0 row kernel, 1 row kernel with the layers
                                 split over the XCDs, 2 column blocks + partial reduce, 3 tiled
-                                column blocks (one launch per stage over all layers), 4 dense */
+                                column blocks (one launch per stage over all layers, row
+                                groups), 4 dense, 5 tiled column blocks with packed flat
+                                windows (the default tiled form) */
 } n2v2r_eig_stats;
 
 /* lifecycle */

@@ -47,36 +47,6 @@
 
 // ---- kernel launchers (spmm.hip, dense.hip, rank.hip) ------------------------------------
 #include "spmm_args.h"
-#define CB_NB 8   // column blocks of the partials form (one per XCD)
-#define CB_MAX 32  // column blocks of the tiled form (N2V2R_SPMM_TILE_NB)
-struct CsrBlk {  // spmm.hip: one column block, int32 row pointers relative to base
-  const int32_t* rp;
-  const int32_t* indices;
-  const float* data;
-  int64_t base;
-  int64_t n_rows;
-  int64_t nnz;
-  int unit;
-};
-struct SpmmCbArgs {  // spmm.hip: column block j of one layer, partial j at P + j * pstride
-  CsrBlk A[CB_NB];
-  const float* X;
-  int64_t ldx;
-  float* P;
-  int64_t pstride;
-};
-struct SpmmTileArgs {  // spmm.hip: row tiles x column-block phases
-  const CsrBlk* blk;
-  const float* X[8];
-  float* Y[8];
-  int64_t ldx, ldy;
-  int64_t n;
-  int K;
-  int nb;
-  int sum;
-  int tile_rows;
-  int pair;
-};
 #define DIST_MAX_COLS 256
 struct DistPlan {
   int n_cols;
@@ -101,7 +71,7 @@ hipError_t n2v2r_launch_cb_rowptrs(const int32_t* cnt, int64_t n, int nb, int64_
                                    hipStream_t stream);
 int64_t n2v2r_cb_scan_tiles(int64_t n, int nb);
 hipError_t n2v2r_launch_cb_fill(const CsrDev& A, int64_t cw, int nb, const int64_t* rp,
-                                int32_t* idx, float* dat, hipStream_t stream);
+                                int32_t* idx, float* dat, int cbits, hipStream_t stream);
 hipError_t n2v2r_launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n, double* partial,
                               size_t partial_elems, double* out, const int* cond,
                               hipStream_t stream);
@@ -340,7 +310,9 @@ struct LayerDev {
   struct ColBlocks {
     DevBuf rp, idx, dat;   // [nb][n_rows + 1] int32 row pointers (relative); entries; values
     CsrBlk blk[CB_MAX];
-    int nb = 0;            // blocks (CB_NB = 8 for the partials form; 8 or 16 tiled)
+    int nb = 0;            // blocks (CB_NB = 8 for the partials form; 4-32 tiled)
+    int cbits = 0;         // packed entries for the flat tiled form (0: global columns)
+    bool packed = false;   // built packed (requested and the column bits fit)
     int64_t ncols = 0;     // column count the blocks were cut for
     bool built = false;
     bool usable = false;   // every block under 2^31 entries (int32 row pointers)
@@ -360,11 +332,15 @@ struct LayerDev {
 // SpMM): per-row counts on the GPU, row-pointer scan on the host, scatter on the GPU (each
 // row's entries keep their order).  One-off per layer; not part of a fit's timed work.
 void build_col_blocks(const CsrDev& A, int64_t ncols, LayerDev::ColBlocks& out, hipStream_t st,
-                      int nb) {
+                      int nb, bool packed) {
   const int64_t n = A.n_rows;
   const int64_t cw = (ncols + nb - 1) / nb;
+  int cbits = 1;
+  while (((int64_t)1 << cbits) < cw) ++cbits;
   out.ncols = ncols;
   out.nb = nb;
+  out.packed = packed;
+  out.cbits = packed && cbits + CB_WIN_BITS <= 31 ? cbits : 0;
   out.built = true;
   out.usable = false;
   if (n <= 0) return;
@@ -394,21 +370,25 @@ void build_col_blocks(const CsrDev& A, int64_t ncols, LayerDev::ColBlocks& out, 
   out.idx.ensure(sizeof(int32_t) * std::max<int64_t>(A.nnz, 1), st);
   if (!A.unit) out.dat.ensure(sizeof(float) * std::max<int64_t>(A.nnz, 1), st);
   HIPCHK(n2v2r_launch_cb_fill(A, cw, nb, rp64.as<int64_t>(), out.idx.as<int32_t>(),
-                              A.unit ? nullptr : out.dat.as<float>(), st));
+                              A.unit ? nullptr : out.dat.as<float>(), out.cbits, st));
   HIPCHK(hipStreamSynchronize(st));
   for (int j = 0; j < nb; ++j)
     out.blk[j] = CsrBlk{out.rp.as<int32_t>() + (size_t)j * (n + 1), out.idx.as<int32_t>(),
                         A.unit ? nullptr : out.dat.as<float>(), ends[2 * j], n,
-                        ends[2 * j + 1] - ends[2 * j], A.unit};
+                        ends[2 * j + 1] - ends[2 * j], A.unit, out.cbits, (int64_t)j * cw};
   out.usable = true;
 }
 
 // false when a block would exceed int32 row pointers (then the row kernel runs)
-bool ensure_col_blocks(LayerDev& L, int64_t ncols, hipStream_t st, int nb = CB_NB) {
-  if (!L.cb.built || L.cb.ncols != ncols || L.cb.nb != nb)
-    build_col_blocks(L.csr(), ncols, L.cb, st, nb);
-  if (!L.symmetric && (!L.cb_t.built || L.cb_t.ncols != ncols || L.cb_t.nb != nb))
-    build_col_blocks(L.csr_t(), ncols, L.cb_t, st, nb);
+// packed: entries for the flat tiled form (LayerDev::ColBlocks::cbits; falls back to plain
+// global columns when the column bits do not fit, check cb.cbits)
+bool ensure_col_blocks(LayerDev& L, int64_t ncols, hipStream_t st, int nb = CB_NB,
+                       bool packed = false) {
+  auto stale = [&](const LayerDev::ColBlocks& c) {
+    return !c.built || c.ncols != ncols || c.nb != nb || c.packed != packed;
+  };
+  if (stale(L.cb)) build_col_blocks(L.csr(), ncols, L.cb, st, nb, packed);
+  if (!L.symmetric && stale(L.cb_t)) build_col_blocks(L.csr_t(), ncols, L.cb_t, st, nb, packed);
   return L.cb.usable && (L.symmetric || L.cb_t.usable);
 }
 
@@ -833,7 +813,7 @@ struct Eig {
   // column blocks as row tiles x block phases with LDS accumulators (no partials, no reduce;
   // N2V2R_SPMM_TILE=0: the partial + reduce form)
   bool tiled = false;
-  int tile_rows = 0, tile_rpw[2] = {0, 0}, tile_nb = CB_NB, tile_pair = 1;
+  int tile_rows = 0, tile_rpw[2] = {0, 0}, tile_nb = CB_NB, tile_form = 0;
   // XCD-split second SpMM stage (b = 8, one GPU): A_k Z_k lands in per-layer partials on the
   // XCDs of layer k; the image W = sum_k of them is stored by the next Gram pass that reads it
   // (the local first pass of the next expansion), or by materialize() before any other use
@@ -1126,7 +1106,7 @@ struct Eig {
     a.nb = tile_nb;
     a.sum = 0;
     a.tile_rows = tile_rows;
-    a.pair = tile_pair;
+    a.form = tile_form;
     double b0 = 0.0, b1 = 0.0;
     for (int k = 0; k < K; ++k) {
       a.X[k] = xg;
@@ -1460,20 +1440,23 @@ struct Eig {
       const char* tn_ = std::getenv("N2V2R_SPMM_TILE_NB");
       tile_nb = tiled ? (tn_ ? std::atoi(tn_) : 8) : CB_NB;
       if (tile_nb != 4 && tile_nb != 8 && tile_nb != 16 && tile_nb != 32) tile_nb = 8;
+      // tiled forms: packed flat windows (default) or row groups (N2V2R_TILE_FLAT=0; with
+      // N2V2R_TILE_PAIR=2, two row groups per wave step at one workgroup per CU)
+      const char* tf = std::getenv("N2V2R_TILE_FLAT");
+      const char* tp = std::getenv("N2V2R_TILE_PAIR");
+      tile_form = !tiled ? 0 : (tp && tp[0] == '2') ? 2 : (tf && tf[0] == '0') ? 0 : 1;
       for (auto& Lp : h->layers)
-        col_blocks = ensure_col_blocks(*Lp, nglob, st, tile_nb) && col_blocks;
+        col_blocks = ensure_col_blocks(*Lp, nglob, st, tile_nb, tile_form == 1) && col_blocks;
       tiled = tiled && col_blocks;
+      if (tile_form == 1)  // packed only where the column bits fit (else plain columns)
+        for (auto& Lp : h->layers)
+          if (Lp->cb.cbits == 0 || (!Lp->symmetric && Lp->cb_t.cbits == 0)) tile_form = 0;
       if (col_blocks && !tiled)
         h->ews.cbpart.ensure(sizeof(float) * (size_t)K * CB_NB * npad * 8);
       if (tiled) {
         int ncu = 0;
         HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
-        // N2V2R_TILE_PAIR=0/1/2: guarded loads / clamped batched loads / two row groups per
-        // wave step at one workgroup per CU (A/B)
-        const char* tp = std::getenv("N2V2R_TILE_PAIR");
-        tile_pair = tp ? std::atoi(tp) : 1;
-        if (tile_pair < 0 || tile_pair > 2) tile_pair = 1;
-        tile_rows = n2v2r_spmm_tile_rows(n, ncu, tile_pair == 2 ? 1 : 2);
+        tile_rows = n2v2r_spmm_tile_rows(n, ncu, tile_form == 2 ? 1 : 2);
         const int nb = tile_nb;
         std::vector<CsrBlk> hb((size_t)2 * K * nb);
         for (int k = 0; k < K; ++k) {
@@ -1979,7 +1962,7 @@ struct Eig {
       stats->lean_checks = lean_checks;
       stats->pool_blocks = (int)h->ews.pool.size();
       stats->spmm_form = h->dense_layers() ? 4
-                         : (col_blocks && tiled) ? 3
+                         : (col_blocks && tiled) ? (tile_form == 1 ? 5 : 3)
                          : col_blocks ? 2
                          : split2 ? 1 : 0;
       tsum(stats);
@@ -2456,6 +2439,9 @@ int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_sta
     HIPCHK(hipMemsetAsync(h->U.p, 0, sizeof(float) * h->npad * ldu, h->stream));
     std::vector<double> theta;
     int st = 0, b = 0;
+    // the fit's tiled column-block configuration, reused for the embedding images below
+    bool ytile = false;
+    int ytile_rows = 0, ytile_nb = 0, ytile_form = 0, ytile_rpw = 0;
     for (int attempt = 0;; ++attempt) {
       Eig eig{};
       eig.h = h;
@@ -2475,6 +2461,11 @@ int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_sta
         continue;
       }
       b = eig.b;
+      ytile = eig.col_blocks && eig.tiled && eig.b == 8;
+      ytile_rows = eig.tile_rows;
+      ytile_nb = eig.tile_nb;
+      ytile_form = eig.tile_form;
+      ytile_rpw = eig.tile_rpw[0];
       break;
     }
     // deterministic signs: largest-magnitude entry of every column of U positive
@@ -2521,7 +2512,38 @@ int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_sta
                          h->colscale.as<float>() + q * 64);
       }
     }
-    for (int q = 0; !h->dense_layers() && q * b < ldu; ++q) {
+    if (!h->dense_layers() && ytile) {
+      // the fit's tiled SpMM (stage-1 blocks, A_k^T) on b-column slices of U copied to a
+      // contiguous panel, then one column scaling of every Y_k (the row kernel below gathers
+      // 32 B out of each 512-B row of U -- a 512 MB panel at cfg4 -- and scales in-kernel)
+      const int64_t ng = h->comm ? (int64_t)h->world * h->npad : h->npad;
+      DevBuf panel;
+      panel.ensure(sizeof(float) * ng * 8);
+      SpmmTileArgs a{};
+      a.blk = h->ews.tblk.as<CsrBlk>();
+      a.ldx = 8;
+      a.ldy = ldu;
+      a.n = h->nloc;
+      a.K = h->K;
+      a.nb = ytile_nb;
+      a.sum = 0;
+      a.tile_rows = ytile_rows;
+      a.form = ytile_form;
+      for (int q = 0; q * 8 < ldu; ++q) {
+        HIPCHK(hipMemcpy2DAsync(panel.p, sizeof(float) * 8, ug + q * 8, sizeof(float) * ldu,
+                                sizeof(float) * 8, ng, hipMemcpyDeviceToDevice, h->stream));
+        for (int k = 0; k < h->K; ++k) {
+          a.X[k] = panel.as<float>();
+          a.Y[k] = h->Y.as<float>() + (size_t)k * h->npad * ldu + q * 8;
+        }
+        HIPCHK(n2v2r_launch_spmm_tile(a, ytile_rpw, h->stream));
+      }
+      for (int k = 0; k < h->K; ++k)
+        HIPCHK(n2v2r_launch_scale_cols(h->Y.as<float>() + (size_t)k * h->npad * ldu, ldu,
+                                       h->npad, h->colscale.as<float>(), h->stream));
+      HIPCHK(hipStreamSynchronize(h->stream));  // the panel dies here
+    }
+    for (int q = 0; !h->dense_layers() && !ytile && q * b < ldu; ++q) {
       SpmmArgs a{};
       a.K = h->K;
       a.sum = 0;

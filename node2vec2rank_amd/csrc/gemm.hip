@@ -5,20 +5,16 @@
 //
 //   dense_gemm_kernel<NT>  Y[r0:r0+rows, 0:b] (+)= A[rows x kdim] X[kdim x b]:
 //     v_mfma_f32_32x32x2_f32, one wave per 32 output rows x NT*32 columns, 4 waves per WG
-//     (128 rows).  The 128 x 64 A tile of a round is loaded with 16-B loads, every
-//     wave-instruction 4 rows x 256 B contiguous, into registers one round ahead (in flight
-//     across the current round's MFMAs), then stored to LDS (row pitch 68 floats: the 16-B
-//     operand reads are conflict-free); each lane reads its row's 16 consecutive k from LDS
-//     (lane half h carries k 8h..8h+7, MFMA m sums k = {m, 8+m}; X's k order is permuted
-//     identically).  X staged through LDS 64 k-rows at a time (row pitch padded by 4 floats).
-//     Split-K over grid.y when the row tiles alone cannot fill the chip, fp32 partial slabs
-//     folded by dense_fold_kernel.
+//     (128 rows); A rows read as two 16-B loads per lane covering 16 consecutive k (the k order
+//     inside each 16-group is permuted identically for A and X: lane half h carries k
+//     8h..8h+7, MFMA m sums k = {m, 8+m}); X staged through LDS 64 k-rows at a time (row pitch
+//     padded by 4 floats so the two half-waves hit different banks); split-K over grid.y when
+//     the row tiles alone cannot fill the chip, fp32 partial slabs folded by dense_fold_kernel.
 //   transpose_kernel       32x32 LDS tiles (A^T of a directed layer, once at ingest).
 //   mismatch_kernel        counts A != A^T entries (symmetry detection at ingest).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
-#include <cstdlib>
 
 #include "common.h"
 
@@ -31,61 +27,33 @@
 __device__ __forceinline__ void dg_load_a(const float* __restrict__ A, int64_t lda, int64_t rows,
                                           int64_t tile_r0, int64_t k0, int64_t k_end,
                                           f32x4 (&v)[8]) {
-  // clamped addresses and unconditional 16-B loads, masked afterwards: all eight loads issue
-  // as one batch (a guarded load per element compiles to a branch and a wait each)
   const int t = threadIdx.x;
   const int kq = (t & 15) * 4;
   const int64_t kg = k0 + kq;
-  const int64_t kc = kg + 4 <= lda ? kg : lda - 4;  // lda % 4 == 0: always in the row
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int64_t r = tile_r0 + u * 16 + (t >> 4);
-    const int64_t rc = r < rows ? r : rows - 1;
-    v[u] = *reinterpret_cast<const f32x4*>(A + rc * lda + kc);
-  }
-}
-
-// the tile loaded by dg_load_a into LDS, rows >= rows and k >= k_end zeroed (applied at store
-// time, so the loads stay in flight across the MFMAs of the previous round)
-__device__ __forceinline__ void dg_store_a(float (*as)[DG_AP], const f32x4 (&v)[8], int64_t rows,
-                                           int64_t tile_r0, int64_t k0, int64_t k_end) {
-  const int t = threadIdx.x;
-  const int64_t kg = k0 + (t & 15) * 4;
+    const bool rok = r < rows;
+    const float* p = A + (rok ? r : 0) * lda + kg;
+    if (rok && kg + 4 <= k_end) {
+      v[u] = *reinterpret_cast<const f32x4*>(p);
+    } else {
+      f32x4 w = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const bool rok = tile_r0 + u * 16 + (t >> 4) < rows;
-    f32x4 w = v[u];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) w[m] = (rok && kg + m < k_end) ? w[m] : 0.f;
-    *reinterpret_cast<f32x4*>(&as[u * 16 + (t >> 4)][(t & 15) * 4]) = w;
-  }
-}
-
-// X operand values of one k round for lane (i, h): X[k0 + kk + 8h + m][t * 32 + i] at
-// xr[t][kk / 16 * 8 + m] (kk = 0, 16, 32, 48; m = 0..7), clamped loads (masked when used)
-template <int NT>
-__device__ __forceinline__ void dg_load_x(const float* __restrict__ X, int ldx, int b, int64_t k0,
-                                          int64_t k_end, float (&xr)[NT][32]) {
-  const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int j = t * 32 + i < b ? t * 32 + i : b - 1;
-#pragma unroll
-    for (int q = 0; q < 32; ++q) {
-      const int64_t k = k0 + (q >> 3) * 16 + 8 * h + (q & 7);
-      xr[t][q] = X[(k < k_end ? k : k_end - 1) * ldx + j];
+      for (int m = 0; m < 4; ++m) w[m] = (rok && kg + m < k_end) ? p[m] : 0.f;
+      v[u] = w;
     }
   }
 }
 
-template <int NT, bool XREG>
+template <int NT>
 __global__ __launch_bounds__(256) void dense_gemm_kernel(const float* __restrict__ A, int64_t lda,
                                                          int64_t rows, int64_t kdim,
                                                          int64_t kper, const float* __restrict__ X,
                                                          int ldx, int b, float* __restrict__ out,
                                                          int64_t ldo, int64_t slab) {
   constexpr int XP = NT * 32 + 4;  // padded LDS row pitch
-  __shared__ float xs[XREG ? 1 : DG_KC][XREG ? 1 : XP];
+  __shared__ float xs[DG_KC][XP];
   __shared__ __attribute__((aligned(16))) float as[128][DG_AP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i = lane & 31, h = lane >> 5;
@@ -98,77 +66,31 @@ __global__ __launch_bounds__(256) void dense_gemm_kernel(const float* __restrict
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f32x16{0.f};
   f32x4 nxt[8];
-  float xn[XREG ? NT : 1][32], xc[XREG ? NT : 1][32];
-  if (k_begin < k_end) {
-    dg_load_a(A, lda, rows, tile_r0, k_begin, k_end, nxt);
-    if constexpr (XREG) dg_load_x<NT>(X, ldx, b, k_begin, k_end, xn);
-  }
+  if (k_begin < k_end) dg_load_a(A, lda, rows, tile_r0, k_begin, k_end, nxt);
   for (int64_t k0 = k_begin; k0 < k_end; k0 += DG_KC) {
     const int kn = (k_end - k0) < DG_KC ? (int)(k_end - k0) : DG_KC;
     __syncthreads();  // the previous round's LDS reads are done
-    dg_store_a(as, nxt, rows, tile_r0, k0, k_end);
-    if constexpr (XREG) {
-      // this round's X operands (X rows past k_end and columns past b as zero)
 #pragma unroll
-      for (int t = 0; t < (XREG ? NT : 1); ++t)
-#pragma unroll
-        for (int q = 0; q < 32; ++q) {
-          const int kk = (q >> 3) * 16 + 8 * (lane >> 5) + (q & 7);
-          xc[t][q] = (kk < kn && t * 32 + i < b) ? xn[t][q] : 0.f;
-        }
-    } else {
-      // X rows k0 .. k0 + 63: clamped unconditional loads (one batch), masked LDS stores
-      constexpr int XN = DG_KC * NT * 32 / 256;
-      float xv[XN];
-#pragma unroll
-      for (int u = 0; u < XN; ++u) {
-        const int e = threadIdx.x + 256 * u;
-        const int kk = e / (NT * 32), j = e % (NT * 32);
-        const int64_t kr = k0 + (kk < kn ? kk : kn - 1);
-        xv[u] = X[kr * ldx + (j < b ? j : b - 1)];
-      }
-#pragma unroll
-      for (int u = 0; u < XN; ++u) {
-        const int e = threadIdx.x + 256 * u;
-        const int kk = e / (NT * 32), j = e % (NT * 32);
-        xs[kk][j] = (kk < kn && j < b) ? xv[u] : 0.f;
-      }
+    for (int u = 0; u < 8; ++u)
+      *reinterpret_cast<f32x4*>(&as[u * 16 + (threadIdx.x >> 4)][(threadIdx.x & 15) * 4]) = nxt[u];
+    for (int e = threadIdx.x; e < DG_KC * NT * 32; e += 256) {
+      const int kk = e / (NT * 32), j = e % (NT * 32);
+      xs[kk][j] = (kk < kn && j < b) ? X[(k0 + kk) * ldx + j] : 0.f;
     }
     __syncthreads();
-    // the next round's A tile (and X operands) in flight while this round's MFMAs run
-    if (k0 + DG_KC < k_end) {
-      dg_load_a(A, lda, rows, tile_r0, k0 + DG_KC, k_end, nxt);
-      if constexpr (XREG) dg_load_x<NT>(X, ldx, b, k0 + DG_KC, k_end, xn);
-    }
+    // the next round's A tile in flight while this round's MFMAs run
+    if (k0 + DG_KC < k_end) dg_load_a(A, lda, rows, tile_r0, k0 + DG_KC, k_end, nxt);
     if (r0 < rows) {
-      if constexpr (XREG) {
-        // full rounds unrolled (the X operands index registers); a short last round's missing
-        // k are zero in xc and in the A tile
+      for (int kk = 0; kk < kn; kk += 16) {
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(&as[wave * 32 + i][kk + 8 * h]);
+        const f32x4 a1 = *reinterpret_cast<const f32x4*>(&as[wave * 32 + i][kk + 8 * h + 4]);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int kk = g * 16;
-          const f32x4 a0 = *reinterpret_cast<const f32x4*>(&as[wave * 32 + i][kk + 8 * h]);
-          const f32x4 a1 = *reinterpret_cast<const f32x4*>(&as[wave * 32 + i][kk + 8 * h + 4]);
+        for (int m = 0; m < 8; ++m) {
+          const float av = m < 4 ? a0[m] : a1[m - 4];
 #pragma unroll
-          for (int m = 0; m < 8; ++m) {
-            const float av = m < 4 ? a0[m] : a1[m - 4];
-#pragma unroll
-            for (int t = 0; t < (XREG ? NT : 1); ++t)
-              acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xc[t][g * 8 + m], acc[t], 0, 0, 0);
-          }
-        }
-      } else {
-        for (int kk = 0; kk < kn; kk += 16) {
-          const f32x4 a0 = *reinterpret_cast<const f32x4*>(&as[wave * 32 + i][kk + 8 * h]);
-          const f32x4 a1 = *reinterpret_cast<const f32x4*>(&as[wave * 32 + i][kk + 8 * h + 4]);
-#pragma unroll
-          for (int m = 0; m < 8; ++m) {
-            const float av = m < 4 ? a0[m] : a1[m - 4];
-#pragma unroll
-            for (int t = 0; t < NT; ++t)
-              acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xs[kk + 8 * h + m][t * 32 + i],
-                                                            acc[t], 0, 0, 0);
-          }
+          for (int t = 0; t < NT; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xs[kk + 8 * h + m][t * 32 + i],
+                                                          acc[t], 0, 0, 0);
         }
       }
     }
@@ -215,17 +137,8 @@ extern "C" hipError_t n2v2r_launch_dense_gemm(const float* A, int64_t lda, int64
   const int64_t tiles = (rows + 127) / 128;
   // split K until ~2 workgroups per CU, 256-aligned k ranges, slabs within `work`
   int64_t nsplit = 1;
-  static const int split_env = [] {  // N2V2R_DG_SPLIT: workgroups aimed at (A/B)
-    const char* s = getenv("N2V2R_DG_SPLIT");
-    return s ? atoi(s) : 0;
-  }();
-  static const bool xreg = [] {  // N2V2R_DG_XREG=0: X operands staged through LDS (A/B)
-    const char* s = getenv("N2V2R_DG_XREG");
-    return !(s && s[0] == '0');
-  }();
   if (work) {
-    // default: ~2 workgroups per CU (rounded up); N2V2R_DG_SPLIT=w: at most w workgroups
-    nsplit = split_env > 0 ? split_env / tiles : (512 + tiles - 1) / tiles;
+    nsplit = (512 + tiles - 1) / tiles;
     const int64_t kmax = (kdim + 255) / 256;
     if (nsplit > kmax) nsplit = kmax;
     if (nsplit < 1) nsplit = 1;
@@ -242,17 +155,12 @@ extern "C" hipError_t n2v2r_launch_dense_gemm(const float* A, int64_t lda, int64
   const int64_t ldo = work ? b : ldy;
   const int64_t slab = work ? rows * b : 0;
   const dim3 grid((unsigned)tiles, (unsigned)nsplit);
-#define DG_LAUNCH(NT, XR)                                                                      \
-  hipLaunchKernelGGL((dense_gemm_kernel<NT, XR>), grid, dim3(256), 0, stream, A, lda, rows, kdim, \
-                     kper, X, ldx, b, dst, ldo, slab)
-  if (b <= 32) {
-    if (xreg) DG_LAUNCH(1, true);
-    else DG_LAUNCH(1, false);
-  } else {
-    if (xreg) DG_LAUNCH(2, true);
-    else DG_LAUNCH(2, false);
-  }
-#undef DG_LAUNCH
+  if (b <= 32)
+    hipLaunchKernelGGL(dense_gemm_kernel<1>, grid, dim3(256), 0, stream, A, lda, rows, kdim, kper,
+                       X, ldx, b, dst, ldo, slab);
+  else
+    hipLaunchKernelGGL(dense_gemm_kernel<2>, grid, dim3(256), 0, stream, A, lda, rows, kdim, kper,
+                       X, ldx, b, dst, ldo, slab);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !work) return e;
   const int64_t elems = rows * b;

@@ -432,28 +432,6 @@ extern "C" hipError_t n2v2r_launch_spmm(const SpmmArgs& args_in, int B, hipStrea
 // partial output (N x 8 fp32); cb_reduce sums the partials in fixed block order (then layer
 // order), so the result is deterministic.  Extra traffic: 2 x 8 x N x 32 B of partials per
 // layer launch.
-#define CB_NB 8
-
-// One column block: int32 row pointers relative to `base` (the block's first entry in the
-// shared index / value arrays; half the row-pointer bytes of int64).
-struct CsrBlk {
-  const int32_t* rp;      // n_rows + 1
-  const int32_t* indices; // shared by the 8 blocks of a layer
-  const float* data;      // shared (nullptr when unit)
-  int64_t base;
-  int64_t n_rows;
-  int64_t nnz;
-  int unit;
-};
-
-struct SpmmCbArgs {
-  CsrBlk A[CB_NB];   // column block j of one layer
-  const float* X;    // gathered panel, global column index = panel row
-  int64_t ldx;
-  float* P;          // partial j at P + j * pstride, rows of 8 fp32
-  int64_t pstride;
-};
-
 // b = 8 row accumulation for the column blocks: block rows are short (N avg-deg / 8 entries),
 // so the index loads of two group-widths are issued together before the gathers (one
 // index -> gather latency per 2L entries instead of per L).  Same per-lane entry order as
@@ -510,7 +488,7 @@ __device__ __forceinline__ void cb_row_accumulate(const CsrBlk& A, const float* 
 // as batches -- clamped addresses and zero weights instead of guarded loads, so no load waits
 // behind a branch (entries past a row's end gather panel row `beg` or 0 with weight 0: the
 // sums are bit-identical).  Rows longer than 2L entries finish in a plain loop.
-template <int RPW, bool TWO>
+template <int RPW>
 __device__ __forceinline__ void cb_rows2_accumulate(const CsrBlk& A, const float* __restrict__ X,
                                                     int64_t ldx, int64_t rowA, bool okA,
                                                     int64_t rowB, bool okB, int lane,
@@ -521,16 +499,10 @@ __device__ __forceinline__ void cb_rows2_accumulate(const CsrBlk& A, const float
   const int li = lane % L;
   const int sub = li & 1;
   const int srcbase = g * L + (li >> 1);
-  const int64_t rA = okA ? rowA : 0, rB = (TWO && okB) ? rowB : 0;
-  const int32_t a0 = A.rp[rA], a1 = A.rp[rA + 1];
-  int32_t b0 = 0, b1 = 0;
-  if constexpr (TWO) {
-    b0 = A.rp[rB];
-    b1 = A.rp[rB + 1];
-  }
+  const int64_t rA = okA ? rowA : 0, rB = okB ? rowB : 0;
+  const int32_t a0 = A.rp[rA], a1 = A.rp[rA + 1], b0 = A.rp[rB], b1 = A.rp[rB + 1];
   const int64_t begA = A.base + a0, begB = A.base + b0;
-  const int64_t lenA = okA ? (int64_t)(a1 - a0) : 0;
-  const int64_t lenB = (TWO && okB) ? (int64_t)(b1 - b0) : 0;
+  const int64_t lenA = okA ? (int64_t)(a1 - a0) : 0, lenB = okB ? (int64_t)(b1 - b0) : 0;
   int64_t mx = lenA > lenB ? lenA : lenB;
 #pragma unroll
   for (int m = L; m < 64; m <<= 1) {
@@ -548,11 +520,9 @@ __device__ __forceinline__ void cb_rows2_accumulate(const CsrBlk& A, const float
       const int64_t qa = p < lenA ? begA + p : A.base;
       const int64_t qb = p < lenB ? begB + p : A.base;
       cA[u] = A.indices[qa];
+      cB[u] = A.indices[qb];
       vA[u] = p < lenA ? (A.unit ? 1.f : A.data[qa]) : 0.f;
-      if constexpr (TWO) {
-        cB[u] = A.indices[qb];
-        vB[u] = p < lenB ? (A.unit ? 1.f : A.data[qb]) : 0.f;
-      }
+      vB[u] = p < lenB ? (A.unit ? 1.f : A.data[qb]) : 0.f;
     }
     f32x4 xa[4], xb[4];
     float wa[4], wb[4];
@@ -560,19 +530,16 @@ __device__ __forceinline__ void cb_rows2_accumulate(const CsrBlk& A, const float
     for (int s = 0; s < 4; ++s) {
       const int u = s >> 1;
       const int src = srcbase + (s & 1) * NPS;
-      const int ca = __shfl(cA[u], src, 64);
+      const int ca = __shfl(cA[u], src, 64), cb = __shfl(cB[u], src, 64);
       wa[s] = __shfl(vA[u], src, 64);
+      wb[s] = __shfl(vB[u], src, 64);
       xa[s] = *reinterpret_cast<const f32x4*>(X + (int64_t)ca * ldx + sub * 4);
-      if constexpr (TWO) {
-        const int cb = __shfl(cB[u], src, 64);
-        wb[s] = __shfl(vB[u], src, 64);
-        xb[s] = *reinterpret_cast<const f32x4*>(X + (int64_t)cb * ldx + sub * 4);
-      }
+      xb[s] = *reinterpret_cast<const f32x4*>(X + (int64_t)cb * ldx + sub * 4);
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       accA += wa[s] * xa[s];
-      if constexpr (TWO) accB += wb[s] * xb[s];
+      accB += wb[s] * xb[s];
     }
   }
   // long rows: the rest one group-width at a time
@@ -587,16 +554,14 @@ __device__ __forceinline__ void cb_rows2_accumulate(const CsrBlk& A, const float
       const float w0 = __shfl(va, src, 64);
       accA += w0 * *reinterpret_cast<const f32x4*>(X + (int64_t)c0 * ldx + sub * 4);
     }
-    if constexpr (TWO) {
-      const int cb = p < lenB ? A.indices[begB + p] : 0;
-      const float vb = p < lenB ? (A.unit ? 1.f : A.data[begB + p]) : 0.f;
+    const int cb = p < lenB ? A.indices[begB + p] : 0;
+    const float vb = p < lenB ? (A.unit ? 1.f : A.data[begB + p]) : 0.f;
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int src = srcbase + s * NPS;
-        const int c1 = __shfl(cb, src, 64);
-        const float w1 = __shfl(vb, src, 64);
-        accB += w1 * *reinterpret_cast<const f32x4*>(X + (int64_t)c1 * ldx + sub * 4);
-      }
+    for (int s = 0; s < 2; ++s) {
+      const int src = srcbase + s * NPS;
+      const int c1 = __shfl(cb, src, 64);
+      const float w1 = __shfl(vb, src, 64);
+      accB += w1 * *reinterpret_cast<const f32x4*>(X + (int64_t)c1 * ldx + sub * 4);
     }
   }
 }
@@ -687,22 +652,12 @@ extern "C" hipError_t n2v2r_launch_spmm_cb(const SpmmCbArgs& a, hipStream_t stre
 // output is written after its 8 phases.  Each row belongs to one wave (fixed row groups), so
 // the LDS read-modify-writes need no barrier or atomic; per row the order is (layer, block,
 // entry) -- deterministic.
-struct SpmmTileArgs {
-  const CsrBlk* blk;      // device array [K][nb]
-  const float* X[8];      // panel per layer (gathered, global rows)
-  float* Y[8];            // output per layer (sum: Y[0])
-  int64_t ldx, ldy;
-  int64_t n;              // rows
-  int K;
-  int nb;                 // column blocks (phases) per layer
-  int sum;
-  int tile_rows;
-  int pair;               // row-group form (PAIR of spmm8_tile_kernel)
-};
 
-// PAIR = 1: one row group per step with clamped batched loads, 2 workgroups (32 waves) per CU;
-// PAIR = 2: two row groups per step (two load chains per wave), 1 workgroup (16 waves) per CU
-// with twice the rows; PAIR = 0: one row group per step with guarded loads (cb_row_accumulate)
+// PAIR = 0 (default): one row group per wave step (cb_row_accumulate), 2 workgroups (32 waves)
+// per CU.  PAIR = 2 (N2V2R_TILE_PAIR=2, A/B): two row groups per step with clamped batched loads
+// (two load chains per wave, cb_rows2_accumulate), 1 workgroup (16 waves) per CU with twice the
+// rows: cfg4 0.815 vs 0.795 ms per stage launch.  A one-group clamped form at 32 waves per CU
+// spilled 14-18 VGPRs (64-register cap) and ran 0.995 ms.
 template <int RPW, int PAIR>
 __global__ __launch_bounds__(1024, PAIR == 2 ? 4 : 8) void spmm8_tile_kernel(SpmmTileArgs a) {
   constexpr int L = 64 / RPW;
@@ -731,8 +686,7 @@ __global__ __launch_bounds__(1024, PAIR == 2 ? 4 : 8) void spmm8_tile_kernel(Spm
         if constexpr (PAIR == 0)
           cb_row_accumulate<RPW>(A, X, a.ldx, r0 + lrA, okA, lane, accA);
         else
-          cb_rows2_accumulate<RPW, PAIR == 2>(A, X, a.ldx, r0 + lrA, okA, r0 + lrB, okB, lane,
-                                              accA, accB);
+          cb_rows2_accumulate<RPW>(A, X, a.ldx, r0 + lrA, okA, r0 + lrB, okB, lane, accA, accB);
 #pragma unroll
         for (int m = 2; m < L; m <<= 1) {
           accA.x += __shfl_xor(accA.x, m, 64);
@@ -766,11 +720,147 @@ __global__ __launch_bounds__(1024, PAIR == 2 ? 4 : 8) void spmm8_tile_kernel(Spm
   }
 }
 
+// Packed flat windows (form 1): a wave owns windows of CB_WIN rows of the tile; a window's
+// entries in column block p are one contiguous run of the block's index array (rows are in
+// order), so the wave walks that run 32 entries per step -- lane pair i takes entry i, reads its
+// packed word (row in window, column in block), gathers the 32-B panel row as two 16-B halves
+// and adds weight x row into the row's LDS accumulator (ds_add_f32).  Every lane carries an
+// entry whatever the row lengths are (the row-group form idles the lanes of short rows: a
+// block row averages 6 entries at cfg4, the longest of a 16-row group ~12), and only the two
+// row pointers bounding a window are read per phase.  Up to 4 steps' index words and gathers
+// are issued as one batch.  One wave owns each window, so the LDS adds of a row come from one
+// wave in program order: the sums are deterministic (per row: layer, block, entry order).
+// a wave-uniform pointer loaded from memory, moved to SGPRs and tagged as global: loads through
+// it become global_load with a scalar base (a flat pointer's loads count on lgkmcnt too, so
+// every wait for them would also wait for the LDS adds)
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* uniform_global(const T* p) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (const __attribute__((address_space(1))) T*)(((uint64_t)hi << 32) | lo);
+}
+
+// NS steps of 32 entries of one window run as straight-line code: index words, gathers and
+// LDS adds each issued as one batch (no branch between a load and its batch-mates; idle lanes
+// gather a valid row and add into `trash`)
+template <int NS, bool UNIT>
+__device__ __forceinline__ void flat_steps(const __attribute__((address_space(1))) int32_t* ind,
+                                           const __attribute__((address_space(1))) float* dat,
+                                           int64_t beg, int left,
+                                           const __attribute__((address_space(1))) float* Xb,
+                                           uint32_t ldx, int32_t cmask, int cbits, int pr,
+                                           int sub, float* accw, float* trash) {
+  int wd[NS];
+  float v[NS];
+  f32x4 x[NS];
+#pragma unroll
+  for (int u = 0; u < NS; ++u) {
+    const int q = u * 32 + pr;
+    const int64_t e = beg + (q < left ? q : 0);
+    wd[u] = ind[e];
+    v[u] = UNIT ? 1.f : dat[e];
+  }
+#pragma unroll
+  for (int u = 0; u < NS; ++u)
+    x[u] = *reinterpret_cast<const __attribute__((address_space(1))) f32x4*>(
+        Xb + ((uint32_t)(wd[u] & cmask) * ldx + sub * 4));
+#pragma unroll
+  for (int u = 0; u < NS; ++u) {
+    float* dst = (u * 32 + pr < left) ? accw + (wd[u] >> cbits) * 8 : trash;
+    const f32x4 c = v[u] * x[u];
+    atomicAdd(dst + 0, c.x);
+    atomicAdd(dst + 1, c.y);
+    atomicAdd(dst + 2, c.z);
+    atomicAdd(dst + 3, c.w);
+  }
+}
+
+__global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
+  extern __shared__ float tacf[];  // [tile_rows + 1][8]: the last row takes the idle lanes' adds
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nwave = blockDim.x >> 6;
+  const int pr = lane >> 1, sub = lane & 1;
+  const int64_t r0 = (int64_t)blockIdx.x * a.tile_rows;
+  const int64_t rem = a.n - r0;
+  const int nrows = (int)(rem < a.tile_rows ? rem : a.tile_rows);
+  const int nwin = (nrows + CB_WIN - 1) / CB_WIN;
+  const uint32_t ldx = (uint32_t)a.ldx;
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  f32x4* tacc = reinterpret_cast<f32x4*>(tacf);
+  float* trash = tacf + (size_t)a.tile_rows * 8 + sub * 4;
+  // zero / write back by the same window -> wave map as the adds (no barrier needed)
+  for (int w = wave; w < nwin; w += nwave) {
+    const int lr = w * CB_WIN + pr;
+    if (lr < nrows) tacc[lr * 2 + sub] = zero;
+  }
+  for (int k = 0; k < a.K; ++k) {
+    const float* X = a.X[k];
+    for (int p = 0; p < a.nb; ++p) {
+      const CsrBlk& A = a.blk[k * a.nb + p];
+      const int cbits = __builtin_amdgcn_readfirstlane(A.cbits);
+      const int unit = __builtin_amdgcn_readfirstlane(A.unit);
+      const auto rp = uniform_global(A.rp);
+      const auto ind = uniform_global(A.indices);
+      const auto dat = uniform_global(A.data);
+      const int64_t base =
+          ((int64_t)__builtin_amdgcn_readfirstlane((uint32_t)(A.base >> 32)) << 32) |
+          (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)A.base);
+      const int64_t col0 =
+          ((int64_t)__builtin_amdgcn_readfirstlane((uint32_t)(A.col0 >> 32)) << 32) |
+          (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)A.col0);
+      const int32_t cmask = (1 << cbits) - 1;
+      // the block's panel rows (uniform base; each lane adds its half, sub * 4, per gather)
+      const auto Xb = uniform_global(X + col0 * a.ldx);
+      for (int w = wave; w < nwin; w += nwave) {
+        const int wr = w * CB_WIN;
+        const int we = wr + CB_WIN < nrows ? wr + CB_WIN : nrows;
+        const int32_t e0 = __builtin_amdgcn_readfirstlane(rp[r0 + wr]);
+        const int32_t e1 = __builtin_amdgcn_readfirstlane(rp[r0 + we]);
+        const int64_t beg = base + e0;
+        const int len = e1 - e0;
+        float* accw = tacf + (size_t)wr * 8 + sub * 4;
+        // steps of 32 entries in batches of up to 4 (the batch size a uniform choice)
+#define FLAT_STEPS(U)                                                                           \
+  for (int off = 0; off < len; off += 128) {                                                    \
+    const int left = len - off;                                                                 \
+    if (left > 96)                                                                              \
+      flat_steps<4, U>(ind, dat, beg + off, left, Xb, ldx, cmask, cbits, pr, sub, accw, trash);      \
+    else if (left > 64)                                                                         \
+      flat_steps<3, U>(ind, dat, beg + off, left, Xb, ldx, cmask, cbits, pr, sub, accw, trash);      \
+    else if (left > 32)                                                                         \
+      flat_steps<2, U>(ind, dat, beg + off, left, Xb, ldx, cmask, cbits, pr, sub, accw, trash);      \
+    else                                                                                        \
+      flat_steps<1, U>(ind, dat, beg + off, left, Xb, ldx, cmask, cbits, pr, sub, accw, trash);      \
+  }
+        if (unit) {
+          FLAT_STEPS(true)
+        } else {
+          FLAT_STEPS(false)
+        }
+#undef FLAT_STEPS
+      }
+      __syncthreads();  // all waves on the same panel block (see spmm8_tile_kernel)
+    }
+    if (!a.sum || k == a.K - 1) {
+      float* Y = a.Y[a.sum ? 0 : k];
+      for (int w = wave; w < nwin; w += nwave) {
+        const int lr = w * CB_WIN + pr;
+        if (lr < nrows) {
+          *reinterpret_cast<f32x4*>(Y + (r0 + lr) * a.ldy + sub * 4) = tacc[lr * 2 + sub];
+          tacc[lr * 2 + sub] = zero;
+        }
+      }
+    }
+  }
+}
+
 // rows per tile for the tiled form: `wpc` workgroups (1024 threads each) per CU sharing its
-// 160 KB of LDS (32 B of accumulators per row)
+// 160 KB of LDS (32 B of accumulators per row); a multiple of CB_WIN (the packed windows)
 extern "C" int n2v2r_spmm_tile_rows(int64_t n, int ncu, int wpc) {
   int64_t t = (n + wpc * (int64_t)ncu - 1) / (wpc * (int64_t)ncu);
-  t = (t + 15) / 16 * 16;
+  t = (t + CB_WIN - 1) / CB_WIN * CB_WIN;
   const int64_t cap = (wpc == 1 ? 4096 : 2048);
   if (t > cap) t = cap;
   return (int)t;
@@ -780,7 +870,20 @@ extern "C" hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, int rpw, hip
   if (a.K < 1 || a.K > 8 || a.tile_rows < 16 || a.n <= 0) return hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.n + a.tile_rows - 1) / a.tile_rows);
   const size_t lds = sizeof(float) * 8 * (size_t)a.tile_rows;
-  if (a.pair < 0 || a.pair > 2) return hipErrorInvalidValue;
+  if (a.form < 0 || a.form > 2 || a.tile_rows % CB_WIN != 0) return hipErrorInvalidValue;
+  if (a.form == 1) {  // + the trash row of the idle lanes
+    const size_t flds = lds + 8 * sizeof(float);
+    static const bool fattr = [] {
+      (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      (void)hipGetLastError();
+      return true;
+    }();
+    (void)fattr;
+    if (flds > 80 * 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(spmm8_flat_kernel, dim3(grid), dim3(1024), flds, stream, a);
+    return hipGetLastError();
+  }
   if (lds > 64 * 1024) {
     static bool attr = false;
     if (!attr) {
@@ -793,10 +896,8 @@ extern "C" hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, int rpw, hip
     }
   }
 #define TILE_LAUNCH(R)                                                                     \
-  if (a.pair == 2)                                                                         \
+  if (a.form == 2)                                                                         \
     hipLaunchKernelGGL((spmm8_tile_kernel<R, 2>), dim3(grid), dim3(1024), lds, stream, a); \
-  else if (a.pair == 1)                                                                    \
-    hipLaunchKernelGGL((spmm8_tile_kernel<R, 1>), dim3(grid), dim3(1024), lds, stream, a); \
   else                                                                                     \
     hipLaunchKernelGGL((spmm8_tile_kernel<R, 0>), dim3(grid), dim3(1024), lds, stream, a)
   switch (rpw) {
@@ -887,9 +988,10 @@ __global__ void cb_count_kernel(CsrDev A, int64_t cw, int32_t* __restrict__ cnt)
 
 // step 2 (after the host scan): scatter each row's entries to rp[j][r] + running count,
 // keeping their order inside the row.
+// cbits > 0: packed entries ((r % CB_WIN) << cbits | (col - block start)) for the flat form.
 template <int NB>
 __global__ void cb_fill_kernel(CsrDev A, int64_t cw, const int64_t* __restrict__ rp,
-                               int32_t* __restrict__ idx, float* __restrict__ dat) {
+                               int32_t* __restrict__ idx, float* __restrict__ dat, int cbits) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= A.n_rows) return;
   int64_t pos[NB];
@@ -902,7 +1004,7 @@ __global__ void cb_fill_kernel(CsrDev A, int64_t cw, const int64_t* __restrict__
 #pragma unroll
     for (int j = 0; j < NB; ++j)
       if (jb == j) q = pos[j]++;
-    idx[q] = col;
+    idx[q] = cbits ? (int32_t)(((r % CB_WIN) << cbits) | (col - (int64_t)jb * cw)) : col;
     if (!A.unit) dat[q] = A.data[p];
   }
 }
@@ -1042,14 +1144,17 @@ extern "C" hipError_t n2v2r_launch_cb_count(const CsrDev& A, int64_t cw, int nb,
 }
 
 extern "C" hipError_t n2v2r_launch_cb_fill(const CsrDev& A, int64_t cw, int nb, const int64_t* rp,
-                                           int32_t* idx, float* dat, hipStream_t stream) {
+                                           int32_t* idx, float* dat, int cbits,
+                                           hipStream_t stream) {
   if (A.n_rows <= 0) return hipSuccess;
   const dim3 g((unsigned)((A.n_rows + 255) / 256));
-  if (nb == 4) hipLaunchKernelGGL(cb_fill_kernel<4>, g, dim3(256), 0, stream, A, cw, rp, idx, dat);
-  else if (nb == 8) hipLaunchKernelGGL(cb_fill_kernel<8>, g, dim3(256), 0, stream, A, cw, rp, idx, dat);
-  else if (nb == 16) hipLaunchKernelGGL(cb_fill_kernel<16>, g, dim3(256), 0, stream, A, cw, rp, idx, dat);
-  else if (nb == 32) hipLaunchKernelGGL(cb_fill_kernel<32>, g, dim3(256), 0, stream, A, cw, rp, idx, dat);
+#define FILL(NB) hipLaunchKernelGGL(cb_fill_kernel<NB>, g, dim3(256), 0, stream, A, cw, rp, idx, dat, cbits)
+  if (nb == 4) FILL(4);
+  else if (nb == 8) FILL(8);
+  else if (nb == 16) FILL(16);
+  else if (nb == 32) FILL(32);
   else return hipErrorInvalidValue;
+#undef FILL
   return hipGetLastError();
 }
 

@@ -195,6 +195,30 @@ def test_distances_kernel_vs_oracle(engine, name):
             np.testing.assert_array_equal(engine.borda(c), orc.borda(D, faithful=False))
 
 
+@pytest.mark.parametrize("name", ["demo", "er_cfg1", "directed_weighted"])
+def test_spectral_uase_seam(name):
+    """``spectral.UASE`` -- the replacement of ``se.UASE(sparce_graphs, d)`` (model.py:53-55):
+    ``(XA, YA)`` with YA of shape (K, N, d) indexed as model.py:75-84 indexes it, matching the
+    reference's embedding to its seed envelope; XA = U diag(sqrt(sigma)), so that
+    YA_k = A_k^T XA diag(sigma)^-1."""
+    from node2vec2rank_amd import spectral
+    fx = load_fixture(name)
+    layers = fixture_layers(fx)
+    d = int(fx["dims"].max())
+    XA, YA = spectral.UASE([sp.csc_matrix(A) for A in layers], d, seed=int(fx["seed"]))
+    n = layers[0].shape[0]
+    assert XA.shape == (n, d) and YA.shape == (len(layers), n, d)
+    assert XA.dtype == np.float64 and YA.dtype == np.float64
+    env, _ = _envelope(layers, d, int(fx["seed"]))
+    Ya = orc.align_signs(YA, fx["Y"])
+    assert np.abs(Ya - fx["Y"]).max() / np.abs(fx["Y"]).max() <= max(5e-4, 3 * env)
+    sigma = np.linalg.norm(XA, axis=0) ** 2
+    np.testing.assert_allclose(sigma, fx["sigma"], rtol=2e-5)
+    for k, A in enumerate(layers):
+        Yk = (A.T.astype(np.float64) @ XA) / sigma[None, :]
+        assert np.abs(Yk - YA[k]).max() <= 1e-4 * np.abs(YA[k]).max()
+
+
 def test_pairwise_seam(engine):
     rng = np.random.default_rng(0)
     a = rng.standard_normal((500, 7))
@@ -399,17 +423,20 @@ def test_uase_column_blocks_golden(engine, name, monkeypatch):
     assert err <= max(5e-4, 3 * env), (name, err, env)
 
 
-@pytest.mark.parametrize("tiled", ["1", "0"])
-def test_uase_column_blocks_er_20k(engine, monkeypatch, tiled):
+@pytest.mark.parametrize("form", ["flat", "rows", "pair", "partials"])
+def test_uase_column_blocks_er_20k(engine, monkeypatch, form):
     """Column-block SpMM vs the row SpMM on a 20k-node ER graph with a ragged column count
-    (20,003: the last block is short), in both forms (tiled: row tiles with LDS accumulators
-    walking the blocks; else 8 partials + reduce): same sigma within fp32 tolerance, true
-    residuals, and run-to-run bit-identical embeddings (fixed summation order)."""
+    (20,003: the last block is short), in every form (tiled with packed flat windows -- the
+    default --, tiled with row groups, tiled with row-group pairs, 8 partials + reduce): same
+    sigma within fp32 tolerance, true residuals, and run-to-run bit-identical embeddings (fixed
+    summation order; the flat form's LDS adds of a row all come from one wave)."""
     from node2vec2rank_amd import synthetic
     layers = synthetic.er_layers(20_003, 20, 2)
     d = 32
     engine.set_layers(layers)
-    monkeypatch.setenv("N2V2R_SPMM_TILE", tiled)
+    monkeypatch.setenv("N2V2R_SPMM_TILE", "0" if form == "partials" else "1")
+    monkeypatch.setenv("N2V2R_TILE_FLAT", "1" if form == "flat" else "0")
+    monkeypatch.setenv("N2V2R_TILE_PAIR", "2" if form == "pair" else "0")
     monkeypatch.setenv("N2V2R_SPMM_CB", "0")
     engine.uase(d, seed=42)
     s_row = engine.singular_values().copy()
@@ -423,8 +450,14 @@ def test_uase_column_blocks_er_20k(engine, monkeypatch, tiled):
     A = sp.hstack(layers).tocsr().astype(np.float64)
     res = np.linalg.norm(A @ (A.T @ X) - X * (s ** 2)[None, :], axis=0) / s[0] ** 2
     assert res.max() < 1e-5
+    # the embedding images (the fit's SpMM form): Y_k = A_k^T U diag(sigma)^-1/2
+    for k, Ak in enumerate(layers):
+        Yk = (Ak.T.astype(np.float64) @ X) / np.sqrt(s)[None, :]  # X = U here
+        assert np.abs(Y1[k] - Yk).max() <= 1e-5 * np.abs(Yk).max(), k
     engine.uase(d, seed=42)
     assert np.array_equal(engine.embedding(), Y1)
+    if form in ("flat", "rows"):
+        assert st["spmm_form"] == (5 if form == "flat" else 3), st["spmm_form"]
 
 
 @pytest.mark.parametrize("layers_k", [2, 3])

@@ -4,9 +4,9 @@
 
 Each rep builds a fresh ``N2V2R`` from host scipy CSR layers and times
 ``fit_transform_rank()`` + ``aggregate_transform()`` end to end: host->HBM copy of the CSR
-layers, UASE, distances, Borda, the device->host copies and the DataFrame construction.
-``bench.py``'s ``value`` excludes the host->HBM copy (layers resident before the timed
-region); this is the rate a caller of the Python API sees.
+layers, UASE, distances, Borda, the device->host copies and the DataFrame construction --
+the same path ``bench.py``'s ``value`` times (its ``device_resident`` key is the fit on layers
+already in HBM).  Here each rep is a fresh model and graph object, so per-call set-up shows.
 """
 from __future__ import annotations
 

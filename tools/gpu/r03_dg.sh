@@ -3,7 +3,10 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/dg
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_ingest.py tests/test_gpu_dense.py -q -rf -s --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/dg/tests.log 2>&1
+( while true; do date +%T >> gpurun_out/dg/heartbeat.txt; sleep 30; done ) &
+HB=$!
+trap "kill $HB" EXIT
+timeout -k 10 300 python -u -m pytest tests/test_ingest.py tests/test_gpu_dense.py -v -rf -s --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/dg/tests.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/dg/tests.log
 case $rc in 0|1) ;; *) echo "pytest crashed rc=$rc"; exit 1;; esac
 for v in "1 0" "0 0" "1 512" "1 768" "1 1024" "0 768"; do
