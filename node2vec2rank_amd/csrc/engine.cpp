@@ -1440,11 +1440,12 @@ struct Eig {
       const char* tn_ = std::getenv("N2V2R_SPMM_TILE_NB");
       tile_nb = tiled ? (tn_ ? std::atoi(tn_) : 8) : CB_NB;
       if (tile_nb != 4 && tile_nb != 8 && tile_nb != 16 && tile_nb != 32) tile_nb = 8;
-      // tiled forms: packed flat windows (default) or row groups (N2V2R_TILE_FLAT=0; with
-      // N2V2R_TILE_PAIR=2, two row groups per wave step at one workgroup per CU)
+      // tiled forms: row groups (default; cfg4 0.807 ms per stage launch), packed flat
+      // windows (N2V2R_TILE_FLAT=1: 0.897 ms) or two row groups per wave step at one workgroup
+      // per CU (N2V2R_TILE_PAIR=2: 0.815 ms)
       const char* tf = std::getenv("N2V2R_TILE_FLAT");
       const char* tp = std::getenv("N2V2R_TILE_PAIR");
-      tile_form = !tiled ? 0 : (tp && tp[0] == '2') ? 2 : (tf && tf[0] == '0') ? 0 : 1;
+      tile_form = !tiled ? 0 : (tp && tp[0] == '2') ? 2 : (tf && tf[0] == '1') ? 1 : 0;
       for (auto& Lp : h->layers)
         col_blocks = ensure_col_blocks(*Lp, nglob, st, tile_nb, tile_form == 1) && col_blocks;
       tiled = tiled && col_blocks;

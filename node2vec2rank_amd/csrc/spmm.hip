@@ -720,19 +720,25 @@ __global__ __launch_bounds__(1024, PAIR == 2 ? 4 : 8) void spmm8_tile_kernel(Spm
   }
 }
 
-// Packed flat windows (form 1): a wave owns windows of CB_WIN rows of the tile; a window's
+// Packed flat windows (form 1): a wave owns windows of CB_WIN = 32 rows of the tile; a window's
 // entries in column block p are one contiguous run of the block's index array (rows are in
 // order), so the wave walks that run 32 entries per step -- lane pair i takes entry i, reads its
 // packed word (row in window, column in block), gathers the 32-B panel row as two 16-B halves
-// and adds weight x row into the row's LDS accumulator (ds_add_f32).  Every lane carries an
-// entry whatever the row lengths are (the row-group form idles the lanes of short rows: a
-// block row averages 6 entries at cfg4, the longest of a 16-row group ~12), and only the two
-// row pointers bounding a window are read per phase.  Up to 4 steps' index words and gathers
-// are issued as one batch.  One wave owns each window, so the LDS adds of a row come from one
-// wave in program order: the sums are deterministic (per row: layer, block, entry order).
+// and stages weight x row in a 1-KB per-wave LDS slot; then lane pair r (owner of window row r)
+// adds the staged entries of its row in entry order to a register accumulator, and after the
+// window's last step adds that to the row's LDS accumulator.  Every lane gathers an entry
+// whatever the row lengths are (the row-group form idles the lanes of short rows: a block row
+// averages 6 entries at cfg4, the longest of a 16-row group ~12), and a window reads its row
+// pointers with one load.  No atomics: one wave owns each window, so every sum has a fixed
+// order (per row: layer, block, entry).  Index words and gathers of up to 4 steps are issued as
+// one batch.  (A first form added every entry with ds_add_f32 into the row accumulators: 4.4 vs
+// 0.8 ms per cfg4 stage launch -- LDS float atomics on shared addresses serialise.)  Measured:
+// 0.897 ms per cfg4 stage launch against 0.807 for the row-group form (N2V2R_TILE_FLAT=1 to
+// select it): full lanes did not raise the gather rate (~124 G entries/s either way), so the
+// 32-B L2 gathers themselves, not idle lanes, bound the SpMM.
 // a wave-uniform pointer loaded from memory, moved to SGPRs and tagged as global: loads through
 // it become global_load with a scalar base (a flat pointer's loads count on lgkmcnt too, so
-// every wait for them would also wait for the LDS adds)
+// every wait for them would also wait for the LDS traffic)
 template <class T>
 __device__ __forceinline__ const __attribute__((address_space(1))) T* uniform_global(const T* p) {
   const uint64_t v = (uint64_t)p;
@@ -741,23 +747,27 @@ __device__ __forceinline__ const __attribute__((address_space(1))) T* uniform_gl
   return (const __attribute__((address_space(1))) T*)(((uint64_t)hi << 32) | lo);
 }
 
-// NS steps of 32 entries of one window run as straight-line code: index words, gathers and
-// LDS adds each issued as one batch (no branch between a load and its batch-mates; idle lanes
-// gather a valid row and add into `trash`)
+__device__ __forceinline__ int64_t uniform_i64(int64_t v) {
+  return ((int64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+
+// NS steps of 32 entries of one window: index words and gathers of all NS steps issued as
+// straight-line batches, then per step: stage, and the row owners fold their entries
 template <int NS, bool UNIT>
 __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1))) int32_t* ind,
                                            const __attribute__((address_space(1))) float* dat,
-                                           int64_t beg, int left,
+                                           int64_t beg, int off, int left,
                                            const __attribute__((address_space(1))) float* Xb,
-                                           uint32_t ldx, int32_t cmask, int cbits, int pr,
-                                           int sub, float* accw, float* trash) {
+                                           uint32_t ldx, int32_t cmask, int pr, int sub,
+                                           int rs, int re, f32x4* stage, f32x4& acc) {
   int wd[NS];
   float v[NS];
   f32x4 x[NS];
 #pragma unroll
   for (int u = 0; u < NS; ++u) {
     const int q = u * 32 + pr;
-    const int64_t e = beg + (q < left ? q : 0);
+    const int64_t e = beg + off + (q < left ? q : 0);
     wd[u] = ind[e];
     v[u] = UNIT ? 1.f : dat[e];
   }
@@ -767,17 +777,17 @@ __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1)
         Xb + ((uint32_t)(wd[u] & cmask) * ldx + sub * 4));
 #pragma unroll
   for (int u = 0; u < NS; ++u) {
-    float* dst = (u * 32 + pr < left) ? accw + (wd[u] >> cbits) * 8 : trash;
-    const f32x4 c = v[u] * x[u];
-    atomicAdd(dst + 0, c.x);
-    atomicAdd(dst + 1, c.y);
-    atomicAdd(dst + 2, c.z);
-    atomicAdd(dst + 3, c.w);
+    stage[pr * 2 + sub] = v[u] * x[u];  // entries past the end are never read
+    const int s0 = off + u * 32;
+    const int lo = (rs > s0 ? rs : s0) - s0;
+    const int hi = (re < s0 + 32 ? re : s0 + 32) - s0;
+    for (int j = lo; j < hi; ++j) acc += stage[j * 2 + sub];
   }
 }
 
 __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
-  extern __shared__ float tacf[];  // [tile_rows + 1][8]: the last row takes the idle lanes' adds
+  // [tile_rows][8] row accumulators, then a 1-KB staging slot per wave
+  extern __shared__ float tacf[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nwave = blockDim.x >> 6;
@@ -789,7 +799,7 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
   const uint32_t ldx = (uint32_t)a.ldx;
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
   f32x4* tacc = reinterpret_cast<f32x4*>(tacf);
-  float* trash = tacf + (size_t)a.tile_rows * 8 + sub * 4;
+  f32x4* stage = reinterpret_cast<f32x4*>(tacf + (size_t)a.tile_rows * 8) + wave * 64;
   // zero / write back by the same window -> wave map as the adds (no barrier needed)
   for (int w = wave; w < nwin; w += nwave) {
     const int lr = w * CB_WIN + pr;
@@ -804,35 +814,33 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
       const auto rp = uniform_global(A.rp);
       const auto ind = uniform_global(A.indices);
       const auto dat = uniform_global(A.data);
-      const int64_t base =
-          ((int64_t)__builtin_amdgcn_readfirstlane((uint32_t)(A.base >> 32)) << 32) |
-          (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)A.base);
-      const int64_t col0 =
-          ((int64_t)__builtin_amdgcn_readfirstlane((uint32_t)(A.col0 >> 32)) << 32) |
-          (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)A.col0);
+      const int64_t base = uniform_i64(A.base);
+      const int64_t col0 = uniform_i64(A.col0);
       const int32_t cmask = (1 << cbits) - 1;
-      // the block's panel rows (uniform base; each lane adds its half, sub * 4, per gather)
       const auto Xb = uniform_global(X + col0 * a.ldx);
       for (int w = wave; w < nwin; w += nwave) {
         const int wr = w * CB_WIN;
         const int we = wr + CB_WIN < nrows ? wr + CB_WIN : nrows;
-        const int32_t e0 = __builtin_amdgcn_readfirstlane(rp[r0 + wr]);
-        const int32_t e1 = __builtin_amdgcn_readfirstlane(rp[r0 + we]);
+        // the window's row boundaries: lane pair r holds rows wr + r's [rs, re)
+        const int rr = wr + pr < we ? wr + pr : we;
+        const int32_t ps = rp[r0 + rr];
+        const int32_t pe = rp[r0 + (wr + pr < we ? wr + pr + 1 : we)];
+        const int32_t e0 = __builtin_amdgcn_readfirstlane(ps);
+        const int len = __builtin_amdgcn_readlane(pe, 2 * (we - wr - 1)) - e0;
+        const int rs = ps - e0, re = pe - e0;
         const int64_t beg = base + e0;
-        const int len = e1 - e0;
-        float* accw = tacf + (size_t)wr * 8 + sub * 4;
-        // steps of 32 entries in batches of up to 4 (the batch size a uniform choice)
-#define FLAT_STEPS(U)                                                                           \
-  for (int off = 0; off < len; off += 128) {                                                    \
-    const int left = len - off;                                                                 \
-    if (left > 96)                                                                              \
-      flat_steps<4, U>(ind, dat, beg + off, left, Xb, ldx, cmask, cbits, pr, sub, accw, trash);      \
-    else if (left > 64)                                                                         \
-      flat_steps<3, U>(ind, dat, beg + off, left, Xb, ldx, cmask, cbits, pr, sub, accw, trash);      \
-    else if (left > 32)                                                                         \
-      flat_steps<2, U>(ind, dat, beg + off, left, Xb, ldx, cmask, cbits, pr, sub, accw, trash);      \
-    else                                                                                        \
-      flat_steps<1, U>(ind, dat, beg + off, left, Xb, ldx, cmask, cbits, pr, sub, accw, trash);      \
+        f32x4 acc = zero;
+#define FLAT_STEPS(U)                                                                          \
+  for (int off = 0; off < len; off += 128) {                                                   \
+    const int left = len - off;                                                                \
+    if (left > 96)                                                                             \
+      flat_steps<4, U>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+    else if (left > 64)                                                                        \
+      flat_steps<3, U>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+    else if (left > 32)                                                                        \
+      flat_steps<2, U>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+    else                                                                                       \
+      flat_steps<1, U>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
   }
         if (unit) {
           FLAT_STEPS(true)
@@ -840,6 +848,7 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
           FLAT_STEPS(false)
         }
 #undef FLAT_STEPS
+        if (wr + pr < we) tacc[(wr + pr) * 2 + sub] += acc;
       }
       __syncthreads();  // all waves on the same panel block (see spmm8_tile_kernel)
     }
@@ -871,8 +880,8 @@ extern "C" hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, int rpw, hip
   const unsigned grid = (unsigned)((a.n + a.tile_rows - 1) / a.tile_rows);
   const size_t lds = sizeof(float) * 8 * (size_t)a.tile_rows;
   if (a.form < 0 || a.form > 2 || a.tile_rows % CB_WIN != 0) return hipErrorInvalidValue;
-  if (a.form == 1) {  // + the trash row of the idle lanes
-    const size_t flds = lds + 8 * sizeof(float);
+  if (a.form == 1) {  // + a 1-KB staging slot per wave
+    const size_t flds = lds + 16 * 1024;
     static const bool fattr = [] {
       (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);

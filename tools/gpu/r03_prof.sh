@@ -18,10 +18,10 @@ run() {  # name, limit, rocprofv3 args..., -- , command
 run kt4 400 --kernel-trace --stats -d $O/cfg4/kt -o run -- python -u $B4
 run kt2 300 --kernel-trace --stats -d $O/cfg2/kt -o run -- python -u $B2
 run kt3 300 --kernel-trace --stats -d $O/cfg3/kt -o run -- python -u $B3
-K4="spmm8_tile_kernel"
-run p4f 400 --pmc FETCH_SIZE --kernel-include-regex $K4 -d $O/cfg4/fetch -o run -- python -u $B4
-run p4w 400 --pmc WRITE_SIZE --kernel-include-regex $K4 -d $O/cfg4/write -o run -- python -u $B4
-run p4h 400 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex $K4 -d $O/cfg4/hit -o run -- python -u $B4
+K4="spmm8_tile_kernel|spmm8_flat_kernel"
+run p4f 400 --pmc FETCH_SIZE --kernel-include-regex "$K4" -d $O/cfg4/fetch -o run -- python -u $B4
+run p4w 400 --pmc WRITE_SIZE --kernel-include-regex "$K4" -d $O/cfg4/write -o run -- python -u $B4
+run p4h 400 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "$K4" -d $O/cfg4/hit -o run -- python -u $B4
 K3="dense_gemm_kernel|ritz_nn_kernel"
 run p3f 300 --pmc FETCH_SIZE --kernel-include-regex "$K3" -d $O/cfg3/fetch -o run -- python -u $B3
 run p3w 300 --pmc WRITE_SIZE --kernel-include-regex "$K3" -d $O/cfg3/write -o run -- python -u $B3
