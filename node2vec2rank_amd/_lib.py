@@ -280,7 +280,7 @@ class Engine:
             storage = "csr"
             if all(not sp.issparse(a) for a in layers):
                 arrs = [np.asarray(a) for a in layers]
-                if all(np.count_nonzero(a) > a.size // 4 for a in arrs):
+                if all(_denser_than_quarter(a) for a in arrs):
                     storage = "dense"
         if storage == "dense":
             arrs = [np.ascontiguousarray(np.asarray(a.todense() if sp.issparse(a) else a),
@@ -517,6 +517,23 @@ def default_engine(device: int = 0) -> Engine:
         e = Engine(device)
         _default[device] = e
     return e
+
+
+def _denser_than_quarter(a) -> bool:
+    """count_nonzero(a) > a.size // 4, counted in row blocks that stop as soon as the answer is
+    known (a dense co-expression layer is decided after a quarter of its entries)."""
+    a2 = a.reshape(a.shape[0], -1) if a.ndim > 1 else a.reshape(1, -1)
+    need = a.size // 4
+    rows = a2.shape[0]
+    step = max(1, (1 << 24) // max(1, a2.shape[1]))
+    nz = 0
+    for r in range(0, rows, step):
+        nz += int(np.count_nonzero(a2[r:r + step]))
+        if nz > need:
+            return True
+        if nz + (rows - r - step) * a2.shape[1] <= need:
+            return False
+    return nz > need
 
 
 # Handles per device for the drop-in N2V2R models: a handle whose owner model is gone (or has

@@ -3,18 +3,22 @@
 // N x b panel.  At b = 8..64 the GEMM streams A once (N^2 fp32) and does 2 N^2 b flops, i.e.
 // 4..32 flop/B: HBM-bound at small b, MFMA-bound near b = 64.
 //
-//   dense_gemm_kernel<NT>  Y[r0:r0+rows, 0:b] (+)= A[rows x kdim] X[kdim x b]:
+//   dense_gemm_kernel<NT, XT>  Y[r0:r0+rows, 0:b] (+)= A[rows x kdim] X[kdim x b]:
 //     v_mfma_f32_32x32x2_f32, one wave per 32 output rows x NT*32 columns, 4 waves per WG
-//     (128 rows); A rows read as two 16-B loads per lane covering 16 consecutive k (the k order
-//     inside each 16-group is permuted identically for A and X: lane half h carries k
-//     8h..8h+7, MFMA m sums k = {m, 8+m}); X staged through LDS 64 k-rows at a time (row pitch
-//     padded by 4 floats so the two half-waves hit different banks); split-K over grid.y when
-//     the row tiles alone cannot fill the chip, fp32 partial slabs folded by dense_fold_kernel.
+//     (128 rows).  The 128 x 64 A tile of a round is loaded with 16-B loads, every
+//     wave-instruction 4 rows x 256 B contiguous, into registers one round ahead (in flight
+//     across the current round's MFMAs), then stored to LDS (row pitch 68 floats); each lane
+//     reads its row's 16 consecutive k of a group from LDS (lane half h carries k 8h..8h+7, MFMA
+//     m sums k = {m, 8+m}; X's k order is permuted identically).  X staged through LDS 64
+//     k-rows at a time, transposed (XT) so its operands are 16-B reads too.  Split-K over
+//     grid.y when the row tiles alone cannot fill the chip, fp32 partial slabs folded by
+//     dense_fold_kernel.
 //   transpose_kernel       32x32 LDS tiles (A^T of a directed layer, once at ingest).
 //   mismatch_kernel        counts A != A^T entries (symmetry detection at ingest).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -23,37 +27,49 @@
 
 // A tile rows x DG_KC: thread t loads rows u * 16 + t / 16 (u = 0..7), 16 B at k = 4 (t % 16):
 // every wave-instruction reads 4 rows x 256 B contiguous (the lane-per-row form read 32 rows
-// x 32 B per instruction: 0.32 of HBM at cfg3).  Out-of-range rows / k read as zero.
+// x 32 B per instruction: 0.32 of HBM at cfg3).  Clamped addresses and unconditional 16-B
+// loads: all eight issue as one batch (a guarded load per element compiles to a branch and a
+// wait each); out-of-range rows / k are zeroed at the LDS store (dg_store_a), so the loads stay
+// in flight across the MFMAs of the previous round.
 __device__ __forceinline__ void dg_load_a(const float* __restrict__ A, int64_t lda, int64_t rows,
-                                          int64_t tile_r0, int64_t k0, int64_t k_end,
-                                          f32x4 (&v)[8]) {
+                                          int64_t tile_r0, int64_t k0, f32x4 (&v)[8]) {
   const int t = threadIdx.x;
-  const int kq = (t & 15) * 4;
-  const int64_t kg = k0 + kq;
+  const int64_t kg = k0 + (t & 15) * 4;
+  const int64_t kc = kg + 4 <= lda ? kg : lda - 4;  // lda % 4 == 0: always in the row
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int64_t r = tile_r0 + u * 16 + (t >> 4);
-    const bool rok = r < rows;
-    const float* p = A + (rok ? r : 0) * lda + kg;
-    if (rok && kg + 4 <= k_end) {
-      v[u] = *reinterpret_cast<const f32x4*>(p);
-    } else {
-      f32x4 w = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int m = 0; m < 4; ++m) w[m] = (rok && kg + m < k_end) ? p[m] : 0.f;
-      v[u] = w;
-    }
+    const int64_t rc = r < rows ? r : rows - 1;
+    v[u] = *reinterpret_cast<const f32x4*>(A + rc * lda + kc);
   }
 }
 
-template <int NT>
+__device__ __forceinline__ void dg_store_a(float (*as)[DG_AP], const f32x4 (&v)[8], int64_t rows,
+                                           int64_t tile_r0, int64_t k0, int64_t k_end) {
+  const int t = threadIdx.x;
+  const int64_t kg = k0 + (t & 15) * 4;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const bool rok = tile_r0 + u * 16 + (t >> 4) < rows;
+    f32x4 w = v[u];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) w[m] = (rok && kg + m < k_end) ? w[m] : 0.f;
+    *reinterpret_cast<f32x4*>(&as[u * 16 + (t >> 4)][(t & 15) * 4]) = w;
+  }
+}
+
+// XT = true (default): X staged transposed, xt[column][k] (pitch DG_AP), so a lane reads its 8
+// consecutive k of a 16-k group as two 16-B LDS reads, like its A operands (4 reads per group
+// instead of 8 one-float reads).  XT = false: xs[k][column], one LDS read per MFMA (A/B,
+// N2V2R_DG_XT=0).
+template <int NT, bool XT>
 __global__ __launch_bounds__(256) void dense_gemm_kernel(const float* __restrict__ A, int64_t lda,
                                                          int64_t rows, int64_t kdim,
                                                          int64_t kper, const float* __restrict__ X,
                                                          int ldx, int b, float* __restrict__ out,
                                                          int64_t ldo, int64_t slab) {
-  constexpr int XP = NT * 32 + 4;  // padded LDS row pitch
-  __shared__ float xs[DG_KC][XP];
+  constexpr int XP = NT * 32 + 4;  // padded LDS row pitch of xs
+  __shared__ __attribute__((aligned(16))) float xs[XT ? NT * 32 : DG_KC][XT ? DG_AP : XP];
   __shared__ __attribute__((aligned(16))) float as[128][DG_AP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i = lane & 31, h = lane >> 5;
@@ -66,31 +82,64 @@ __global__ __launch_bounds__(256) void dense_gemm_kernel(const float* __restrict
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f32x16{0.f};
   f32x4 nxt[8];
-  if (k_begin < k_end) dg_load_a(A, lda, rows, tile_r0, k_begin, k_end, nxt);
+  if (k_begin < k_end) dg_load_a(A, lda, rows, tile_r0, k_begin, nxt);
   for (int64_t k0 = k_begin; k0 < k_end; k0 += DG_KC) {
     const int kn = (k_end - k0) < DG_KC ? (int)(k_end - k0) : DG_KC;
     __syncthreads();  // the previous round's LDS reads are done
+    dg_store_a(as, nxt, rows, tile_r0, k0, k_end);
+    {
+      // X rows k0 .. k0 + 63: clamped unconditional loads (one batch), masked LDS stores
+      constexpr int XN = DG_KC * NT * 32 / 256;
+      float xv[XN];
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      *reinterpret_cast<f32x4*>(&as[u * 16 + (threadIdx.x >> 4)][(threadIdx.x & 15) * 4]) = nxt[u];
-    for (int e = threadIdx.x; e < DG_KC * NT * 32; e += 256) {
-      const int kk = e / (NT * 32), j = e % (NT * 32);
-      xs[kk][j] = (kk < kn && j < b) ? X[(k0 + kk) * ldx + j] : 0.f;
+      for (int u = 0; u < XN; ++u) {
+        const int e = threadIdx.x + 256 * u;
+        const int kk = e / (NT * 32), j = e % (NT * 32);
+        const int64_t kr = k0 + (kk < kn ? kk : kn - 1);
+        xv[u] = X[kr * ldx + (j < b ? j : b - 1)];
+      }
+#pragma unroll
+      for (int u = 0; u < XN; ++u) {
+        const int e = threadIdx.x + 256 * u;
+        const int kk = e / (NT * 32), j = e % (NT * 32);
+        const float x = (kk < kn && j < b) ? xv[u] : 0.f;
+        if constexpr (XT)
+          xs[j][kk] = x;
+        else
+          xs[kk][j] = x;
+      }
     }
     __syncthreads();
     // the next round's A tile in flight while this round's MFMAs run
-    if (k0 + DG_KC < k_end) dg_load_a(A, lda, rows, tile_r0, k0 + DG_KC, k_end, nxt);
+    if (k0 + DG_KC < k_end) dg_load_a(A, lda, rows, tile_r0, k0 + DG_KC, nxt);
     if (r0 < rows) {
       for (int kk = 0; kk < kn; kk += 16) {
         const f32x4 a0 = *reinterpret_cast<const f32x4*>(&as[wave * 32 + i][kk + 8 * h]);
         const f32x4 a1 = *reinterpret_cast<const f32x4*>(&as[wave * 32 + i][kk + 8 * h + 4]);
+        if constexpr (XT) {
+          f32x4 x0[NT], x1[NT];
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
-          const float av = m < 4 ? a0[m] : a1[m - 4];
+          for (int t = 0; t < NT; ++t) {
+            x0[t] = *reinterpret_cast<const f32x4*>(&xs[t * 32 + i][kk + 8 * h]);
+            x1[t] = *reinterpret_cast<const f32x4*>(&xs[t * 32 + i][kk + 8 * h + 4]);
+          }
 #pragma unroll
-          for (int t = 0; t < NT; ++t)
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xs[kk + 8 * h + m][t * 32 + i],
-                                                          acc[t], 0, 0, 0);
+          for (int m = 0; m < 8; ++m) {
+            const float av = m < 4 ? a0[m] : a1[m - 4];
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+              acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, m < 4 ? x0[t][m] : x1[t][m - 4],
+                                                            acc[t], 0, 0, 0);
+          }
+        } else {
+#pragma unroll
+          for (int m = 0; m < 8; ++m) {
+            const float av = m < 4 ? a0[m] : a1[m - 4];
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+              acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xs[kk + 8 * h + m][t * 32 + i],
+                                                            acc[t], 0, 0, 0);
+          }
         }
       }
     }
@@ -155,12 +204,21 @@ extern "C" hipError_t n2v2r_launch_dense_gemm(const float* A, int64_t lda, int64
   const int64_t ldo = work ? b : ldy;
   const int64_t slab = work ? rows * b : 0;
   const dim3 grid((unsigned)tiles, (unsigned)nsplit);
-  if (b <= 32)
-    hipLaunchKernelGGL(dense_gemm_kernel<1>, grid, dim3(256), 0, stream, A, lda, rows, kdim, kper,
-                       X, ldx, b, dst, ldo, slab);
-  else
-    hipLaunchKernelGGL(dense_gemm_kernel<2>, grid, dim3(256), 0, stream, A, lda, rows, kdim, kper,
-                       X, ldx, b, dst, ldo, slab);
+  static const bool xt = [] {  // N2V2R_DG_XT=0: X staged k-major, one LDS read per MFMA (A/B)
+    const char* s = getenv("N2V2R_DG_XT");
+    return !(s && s[0] == '0');
+  }();
+#define DG_LAUNCH(NT, XT)                                                                      \
+  hipLaunchKernelGGL((dense_gemm_kernel<NT, XT>), grid, dim3(256), 0, stream, A, lda, rows, kdim, \
+                     kper, X, ldx, b, dst, ldo, slab)
+  if (b <= 32) {
+    if (xt) DG_LAUNCH(1, true);
+    else DG_LAUNCH(1, false);
+  } else {
+    if (xt) DG_LAUNCH(2, true);
+    else DG_LAUNCH(2, false);
+  }
+#undef DG_LAUNCH
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !work) return e;
   const int64_t elems = rows * b;
