@@ -129,6 +129,7 @@ hipError_t n2v2r_launch_borda_init(const double* vals, int64_t n, int nseg, uint
                                    int32_t* idx, unsigned long long* seg_or,
                                    unsigned long long* seg_and, hipStream_t stream);
 int n2v2r_radix_tiles(int64_t n);
+size_t n2v2r_radix_hist_elems(int64_t n, int nseg);
 hipError_t n2v2r_launch_radix_pass(const uint64_t* kin, const int32_t* pin, uint64_t* kout,
                                    int32_t* pout, int64_t n, int nseg, int shift, uint32_t* hist,
                                    hipStream_t stream);
@@ -2230,7 +2231,7 @@ int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const in
       if (!have_keys)
         HIPCHK(n2v2r_launch_csr_scan(ip_, ix_, dv_, n, n, keys[0].as<uint64_t>(),
                                      pay[0].as<int32_t>(), flag.as<unsigned>() + 1, st));
-      hist.ensure(sizeof(uint32_t) * 256 * (size_t)n2v2r_radix_tiles(nnz));
+      hist.ensure(sizeof(uint32_t) * n2v2r_radix_hist_elems(nnz, 1));
       int bits = 1;
       while (bits < 31 && ((int64_t)1 << bits) < n) ++bits;
       int cur = 0;
@@ -2642,8 +2643,7 @@ static void run_borda(n2v2r_handle* h, const double* Ddev, int64_t n, int nseg, 
     h->rs_idx[i].ensure(sizeof(int32_t) * tot);
   }
   h->rs_pos.ensure(sizeof(int32_t) * tot);
-  const int ntiles = n2v2r_radix_tiles(n);
-  h->rs_hist.ensure(sizeof(uint32_t) * (size_t)nseg * 256 * ntiles);
+  h->rs_hist.ensure(sizeof(uint32_t) * n2v2r_radix_hist_elems(n, nseg));
   h->rs_or.ensure(sizeof(unsigned long long) * nseg);
   h->rs_and.ensure(sizeof(unsigned long long) * nseg);
   HIPCHK(n2v2r_launch_borda_init(Ddev, n, nseg, h->rs_keys[0].as<uint64_t>(),

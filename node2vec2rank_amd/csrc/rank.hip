@@ -269,32 +269,92 @@ __global__ __launch_bounds__(RS_THREADS) void radix_hist_kernel(const uint64_t* 
   hist[((int64_t)s * 256 + threadIdx.x) * ntiles + t] = h[threadIdx.x];
 }
 
-// exclusive scan of hist[s][*][*] (256 * ntiles entries) in place; one workgroup per segment.
-__global__ __launch_bounds__(1024) void radix_scan_kernel(uint32_t* __restrict__ hist, int ntiles) {
-  __shared__ uint32_t part[1024];
-  const int s = blockIdx.x;
-  uint32_t* hp = hist + (int64_t)s * 256 * ntiles;
-  const int64_t len = (int64_t)256 * ntiles;
-  const int64_t per = (len + blockDim.x - 1) / blockDim.x;
-  const int64_t lo = threadIdx.x * per;
-  int64_t hi = lo + per;
-  if (hi > len) hi = len;
-  uint32_t sum = 0;
-  for (int64_t i = lo; i < hi; ++i) sum += hp[i];
-  part[threadIdx.x] = sum;
+// exclusive scan of hist[s][*][*] (256 * ntiles entries) in place, per segment, over the
+// whole chip: chunk sums (RSC_TILE entries per workgroup, coalesced), a scan of the chunk sums
+// per segment, then every chunk rescanned from its offset.  (Round 2 scanned a segment in one
+// workgroup, each thread a contiguous run: 2.3 ms for the 3.1M-entry histogram of a 50M-entry
+// ingest sort.)
+#define RSC_T 256
+#define RSC_IT 8
+#define RSC_TILE (RSC_T * RSC_IT)
+
+__global__ __launch_bounds__(RSC_T) void rs_chunk_sums_kernel(const uint32_t* __restrict__ hist,
+                                                              int64_t len, int nchunk,
+                                                              uint32_t* __restrict__ csum) {
+  const int s = blockIdx.y;
+  const uint32_t* hp = hist + (int64_t)s * len;
+  const int64_t base = (int64_t)blockIdx.x * RSC_TILE;
+  uint32_t v = 0;
+#pragma unroll
+  for (int u = 0; u < RSC_IT; ++u) {
+    const int64_t i = base + u * RSC_T + threadIdx.x;
+    v += i < len ? hp[i] : 0u;
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  __shared__ uint32_t ws[RSC_T / 64];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
   __syncthreads();
-  // Hillis-Steele inclusive scan of the 1024 partials
-  for (int off = 1; off < 1024; off <<= 1) {
-    uint32_t v = (threadIdx.x >= off) ? part[threadIdx.x - off] : 0;
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < RSC_T / 64; ++w) t += ws[w];
+    csum[(int64_t)s * nchunk + blockIdx.x] = t;
+  }
+}
+
+// exclusive scan of one segment's chunk sums in place: 1024-entry passes with a carry
+__global__ __launch_bounds__(1024) void rs_chunk_offsets_kernel(uint32_t* __restrict__ csum,
+                                                                int nchunk) {
+  __shared__ uint32_t sh[1024];
+  uint32_t* cp = csum + (int64_t)blockIdx.x * nchunk;
+  uint32_t carry = 0;
+  for (int c0 = 0; c0 < nchunk; c0 += 1024) {
+    const int i = c0 + threadIdx.x;
+    const uint32_t v = i < nchunk ? cp[i] : 0u;
+    sh[threadIdx.x] = v;
     __syncthreads();
-    part[threadIdx.x] += v;
+    for (int off = 1; off < 1024; off <<= 1) {
+      const uint32_t t = threadIdx.x >= off ? sh[threadIdx.x - off] : 0u;
+      __syncthreads();
+      sh[threadIdx.x] += t;
+      __syncthreads();
+    }
+    if (i < nchunk) cp[i] = carry + sh[threadIdx.x] - v;
+    const uint32_t tot = sh[1023];
+    __syncthreads();
+    carry += tot;
+  }
+}
+
+// one chunk rescanned in place from its offset: RSC_IT consecutive entries per thread, a
+// workgroup scan of the thread sums
+__global__ __launch_bounds__(RSC_T) void rs_chunk_write_kernel(uint32_t* __restrict__ hist,
+                                                               int64_t len, int nchunk,
+                                                               const uint32_t* __restrict__ csum) {
+  const int s = blockIdx.y;
+  uint32_t* hp = hist + (int64_t)s * len;
+  const int64_t base = (int64_t)blockIdx.x * RSC_TILE + (int64_t)threadIdx.x * RSC_IT;
+  uint32_t v[RSC_IT];
+  uint32_t t = 0;
+#pragma unroll
+  for (int u = 0; u < RSC_IT; ++u) {
+    v[u] = base + u < len ? hp[base + u] : 0u;
+    t += v[u];
+  }
+  __shared__ uint32_t sh[RSC_T];
+  sh[threadIdx.x] = t;
+  __syncthreads();
+  for (int off = 1; off < RSC_T; off <<= 1) {
+    const uint32_t q = threadIdx.x >= off ? sh[threadIdx.x - off] : 0u;
+    __syncthreads();
+    sh[threadIdx.x] += q;
     __syncthreads();
   }
-  uint32_t run = (threadIdx.x == 0) ? 0 : part[threadIdx.x - 1];
-  for (int64_t i = lo; i < hi; ++i) {
-    const uint32_t v = hp[i];
-    hp[i] = run;
-    run += v;
+  uint32_t run = csum[(int64_t)s * nchunk + blockIdx.x] + sh[threadIdx.x] - t;
+#pragma unroll
+  for (int u = 0; u < RSC_IT; ++u) {
+    if (base + u < len) hp[base + u] = run;
+    run += v[u];
   }
 }
 
@@ -393,6 +453,14 @@ extern "C" hipError_t n2v2r_launch_borda_init(const double* vals, int64_t n, int
 
 extern "C" int n2v2r_radix_tiles(int64_t n) { return (int)((n + RS_TILE - 1) / RS_TILE); }
 
+// uint32 elements of the `hist` buffer a radix pass needs: the [nseg][256][ntiles] histogram
+// plus the chunk sums of its scan
+extern "C" size_t n2v2r_radix_hist_elems(int64_t n, int nseg) {
+  const int64_t len = (int64_t)256 * n2v2r_radix_tiles(n);
+  const int64_t nchunk = (len + RSC_TILE - 1) / RSC_TILE;
+  return (size_t)nseg * (size_t)(len + nchunk);
+}
+
 extern "C" hipError_t n2v2r_launch_radix_pass(const uint64_t* kin, const int32_t* pin,
                                               uint64_t* kout, int32_t* pout, int64_t n, int nseg,
                                               int shift, uint32_t* hist, hipStream_t stream) {
@@ -400,7 +468,14 @@ extern "C" hipError_t n2v2r_launch_radix_pass(const uint64_t* kin, const int32_t
   dim3 grid(ntiles, nseg);
   hipLaunchKernelGGL(radix_hist_kernel, grid, dim3(RS_THREADS), 0, stream, kin, n, shift, ntiles,
                      hist);
-  hipLaunchKernelGGL(radix_scan_kernel, dim3(nseg), dim3(1024), 0, stream, hist, ntiles);
+  const int64_t len = (int64_t)256 * ntiles;
+  const int nchunk = (int)((len + RSC_TILE - 1) / RSC_TILE);
+  uint32_t* csum = hist + (int64_t)nseg * len;  // n2v2r_radix_hist_elems
+  hipLaunchKernelGGL(rs_chunk_sums_kernel, dim3(nchunk, nseg), dim3(RSC_T), 0, stream, hist, len,
+                     nchunk, csum);
+  hipLaunchKernelGGL(rs_chunk_offsets_kernel, dim3(nseg), dim3(1024), 0, stream, csum, nchunk);
+  hipLaunchKernelGGL(rs_chunk_write_kernel, dim3(nchunk, nseg), dim3(RSC_T), 0, stream, hist, len,
+                     nchunk, csum);
   hipLaunchKernelGGL(radix_scatter_kernel, grid, dim3(RS_THREADS), 0, stream, kin, pin, kout, pout,
                      n, shift, ntiles, hist);
   return hipGetLastError();

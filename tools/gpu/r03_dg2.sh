@@ -10,4 +10,5 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_dense.py tests/test_gpu_con
 for v in 1 0; do
   N2V2R_DG_XT=$v timeout -k 10 300 python -u bench.py --config cfg3 --steps 2 --warmup 1 --resident-steps 2 --no-cpu-baseline > gpurun_out/dg2/cfg3_xt$v.json 2> gpurun_out/dg2/cfg3_xt$v.err || { echo bench-fail-$v; exit 1; }
 done
+timeout -k 10 400 python -u tools/probe_block.py --config cfg4 --blocks 8 16 > gpurun_out/dg2/probe_block.jsonl 2> gpurun_out/dg2/probe_block.err || { echo probe-fail; exit 1; }
 echo done
