@@ -106,8 +106,8 @@ typedef struct {
   int spmm_form;             /* SpMM form of the fit: 0 row kernel, 1 row kernel with the layers
                                 split over the XCDs, 2 column blocks + partial reduce, 3 tiled
                                 column blocks (one launch per stage over all layers, row
-                                groups; the default tiled form), 4 dense, 5 tiled column blocks
-                                with packed flat windows (N2V2R_TILE_FLAT=1) */
+                                groups), 4 dense, 5 tiled column blocks with packed flat windows
+                                (the default tiled form) */
 } n2v2r_eig_stats;
 
 /* lifecycle */

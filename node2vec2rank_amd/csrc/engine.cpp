@@ -1435,18 +1435,24 @@ struct Eig {
     if (col_blocks) {
       const char* te = std::getenv("N2V2R_SPMM_TILE");  // read per fit (A/B runs, tests)
       tiled = !(te && te[0] == '0');
-      // tiled: N2V2R_SPMM_TILE_NB column blocks (4, 8, 16 or 32; default 8 -- cfg4 device-
-      // resident step 1848 ms at 8, 2051 at 16, 2726 at 32: every further block adds a row-
-      // pointer pass and a phase of short rows)
-      const char* tn_ = std::getenv("N2V2R_SPMM_TILE_NB");
-      tile_nb = tiled ? (tn_ ? std::atoi(tn_) : 8) : CB_NB;
-      if (tile_nb != 4 && tile_nb != 8 && tile_nb != 16 && tile_nb != 32) tile_nb = 8;
-      // tiled forms: row groups (default; cfg4 0.807 ms per stage launch), packed flat
-      // windows (N2V2R_TILE_FLAT=1: 0.897 ms) or two row groups per wave step at one workgroup
-      // per CU (N2V2R_TILE_PAIR=2: 0.815 ms)
+      // tiled forms: packed flat windows (default), row groups (N2V2R_TILE_FLAT=0) or two row
+      // groups per wave step at one workgroup per CU (N2V2R_TILE_PAIR=2)
       const char* tf = std::getenv("N2V2R_TILE_FLAT");
       const char* tp = std::getenv("N2V2R_TILE_PAIR");
-      tile_form = !tiled ? 0 : (tp && tp[0] == '2') ? 2 : (tf && tf[0] == '1') ? 1 : 0;
+      tile_form = !tiled ? 0 : (tp && tp[0] == '2') ? 2 : (tf && tf[0] == '0') ? 0 : 1;
+      // column blocks (phases) per layer, N2V2R_SPMM_TILE_NB = 4, 8, 16 or 32.  Flat form:
+      // panel blocks of <= 2 MB by default, so a phase's block stays in the XCD's 4 MB L2 beside
+      // the index stream (cfg4: 16 blocks, 0.748 ms per stage launch; 8 blocks 0.896, 32
+      // blocks 0.817; 4 MB blocks left 31 % of the gathers missing L2).  Row-group forms: 8
+      // (their rows get shorter with every block: cfg4 0.807 ms at 8, 0.923 at 16).
+      const char* tn_ = std::getenv("N2V2R_SPMM_TILE_NB");
+      int nb_auto = 8;
+      if (tile_form == 1) {
+        nb_auto = 4;
+        while (nb_auto < 32 && (double)nglob * 32.0 / nb_auto > 2.0 * 1024 * 1024) nb_auto *= 2;
+      }
+      tile_nb = tiled ? (tn_ ? std::atoi(tn_) : nb_auto) : CB_NB;
+      if (tile_nb != 4 && tile_nb != 8 && tile_nb != 16 && tile_nb != 32) tile_nb = nb_auto;
       for (auto& Lp : h->layers)
         col_blocks = ensure_col_blocks(*Lp, nglob, st, tile_nb, tile_form == 1) && col_blocks;
       tiled = tiled && col_blocks;

@@ -653,8 +653,8 @@ extern "C" hipError_t n2v2r_launch_spmm_cb(const SpmmCbArgs& a, hipStream_t stre
 // the LDS read-modify-writes need no barrier or atomic; per row the order is (layer, block,
 // entry) -- deterministic.
 
-// PAIR = 0 (default): one row group per wave step (cb_row_accumulate), 2 workgroups (32 waves)
-// per CU.  PAIR = 2 (N2V2R_TILE_PAIR=2, A/B): two row groups per step with clamped batched loads
+// PAIR = 0 (N2V2R_TILE_FLAT=0; the flat-window kernel below is the default tiled form): one
+// row group per wave step (cb_row_accumulate), 2 workgroups (32 waves) per CU.  PAIR = 2 (N2V2R_TILE_PAIR=2, A/B): two row groups per step with clamped batched loads
 // (two load chains per wave, cb_rows2_accumulate), 1 workgroup (16 waves) per CU with twice the
 // rows: cfg4 0.815 vs 0.795 ms per stage launch.  A one-group clamped form at 32 waves per CU
 // spilled 14-18 VGPRs (64-register cap) and ran 0.995 ms.
@@ -732,10 +732,10 @@ __global__ __launch_bounds__(1024, PAIR == 2 ? 4 : 8) void spmm8_tile_kernel(Spm
 // pointers with one load.  No atomics: one wave owns each window, so every sum has a fixed
 // order (per row: layer, block, entry).  Index words and gathers of up to 4 steps are issued as
 // one batch.  (A first form added every entry with ds_add_f32 into the row accumulators: 4.4 vs
-// 0.8 ms per cfg4 stage launch -- LDS float atomics on shared addresses serialise.)  Measured:
-// 0.897 ms per cfg4 stage launch against 0.807 for the row-group form (N2V2R_TILE_FLAT=1 to
-// select it): full lanes did not raise the gather rate (~124 G entries/s either way), so the
-// 32-B L2 gathers themselves, not idle lanes, bound the SpMM.
+// 0.8 ms per cfg4 stage launch -- LDS float atomics on shared addresses serialise.)  Measured
+// at cfg4: 0.896 ms per stage launch with 8 column blocks (4 MB panel blocks: 31 % of the
+// gathers miss L2), 0.748 ms with 16 (2 MB blocks; the default), against 0.807 / 0.923 ms for
+// the row-group form at 8 / 16 blocks, whose rows get shorter with every block.
 // a wave-uniform pointer loaded from memory, moved to SGPRs and tagged as global: loads through
 // it become global_load with a scalar base (a flat pointer's loads count on lgkmcnt too, so
 // every wait for them would also wait for the LDS traffic)

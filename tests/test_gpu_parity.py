@@ -426,8 +426,8 @@ def test_uase_column_blocks_golden(engine, name, monkeypatch):
 @pytest.mark.parametrize("form", ["flat", "rows", "pair", "partials"])
 def test_uase_column_blocks_er_20k(engine, monkeypatch, form):
     """Column-block SpMM vs the row SpMM on a 20k-node ER graph with a ragged column count
-    (20,003: the last block is short), in every form (tiled with row groups -- the default --,
-    tiled with packed flat windows, tiled with row-group pairs, 8 partials + reduce): same
+    (20,003: the last block is short), in every form (tiled with packed flat windows -- the
+    default --, tiled with row groups, tiled with row-group pairs, 8 partials + reduce): same
     sigma within fp32 tolerance, true residuals, and run-to-run bit-identical embeddings (fixed
     summation order; the flat form's LDS adds of a row all come from one wave)."""
     from node2vec2rank_amd import synthetic
