@@ -10,7 +10,7 @@
 //     across the current round's MFMAs), then stored to LDS (row pitch 68 floats); each lane
 //     reads its row's 16 consecutive k of a group from LDS (lane half h carries k 8h..8h+7, MFMA
 //     m sums k = {m, 8+m}; X's k order is permuted identically).  X staged through LDS 64
-//     k-rows at a time, transposed (XT) so its operands are 16-B reads too.  Split-K over
+//     k-rows at a time.  Split-K over
 //     grid.y when the row tiles alone cannot fill the chip, fp32 partial slabs folded by
 //     dense_fold_kernel.
 //   transpose_kernel       32x32 LDS tiles (A^T of a directed layer, once at ingest).
@@ -58,10 +58,10 @@ __device__ __forceinline__ void dg_store_a(float (*as)[DG_AP], const f32x4 (&v)[
   }
 }
 
-// XT = true (default): X staged transposed, xt[column][k] (pitch DG_AP), so a lane reads its 8
-// consecutive k of a 16-k group as two 16-B LDS reads, like its A operands (4 reads per group
-// instead of 8 one-float reads).  XT = false: xs[k][column], one LDS read per MFMA (A/B,
-// N2V2R_DG_XT=0).
+// XT = false (default): xs[k][column], one LDS read per MFMA.  XT = true (N2V2R_DG_XT=1, A/B):
+// X staged transposed, xs[column][k] (pitch DG_AP), so a lane reads its 8 consecutive k of a
+// 16-k group as two 16-B LDS reads like its A operands -- measured 0.40 vs 0.39 ms per cfg3
+// launch, not kept.
 template <int NT, bool XT>
 __global__ __launch_bounds__(256) void dense_gemm_kernel(const float* __restrict__ A, int64_t lda,
                                                          int64_t rows, int64_t kdim,
@@ -204,9 +204,9 @@ extern "C" hipError_t n2v2r_launch_dense_gemm(const float* A, int64_t lda, int64
   const int64_t ldo = work ? b : ldy;
   const int64_t slab = work ? rows * b : 0;
   const dim3 grid((unsigned)tiles, (unsigned)nsplit);
-  static const bool xt = [] {  // N2V2R_DG_XT=0: X staged k-major, one LDS read per MFMA (A/B)
+  static const bool xt = [] {  // N2V2R_DG_XT=1: X staged transposed (A/B: 0.40 vs 0.39 ms)
     const char* s = getenv("N2V2R_DG_XT");
-    return !(s && s[0] == '0');
+    return s && s[0] == '1';
   }();
 #define DG_LAUNCH(NT, XT)                                                                      \
   hipLaunchKernelGGL((dense_gemm_kernel<NT, XT>), grid, dim3(256), 0, stream, A, lda, rows, kdim, \

@@ -62,6 +62,7 @@ def main():
     ap.add_argument("--stage")
     ap.add_argument("--algo-bytes", type=float, default=None)
     ap.add_argument("--stats")
+    ap.add_argument("--form", type=int, default=None, help="n2v2r_eig_stats.spmm_form profiled")
     a = ap.parse_args()
     rx = re.compile(a.regex)
 
@@ -139,6 +140,8 @@ def main():
                           f"counted), phase 0 of {a.alternate} (stage 1 of each application)")
         if a.algo_bytes:
             rec["algo_bytes_per_launch"] = a.algo_bytes
+        if a.form is not None:
+            rec["spmm_form"] = a.form
         json.dump(rec, open(a.json, "w"), indent=1)
     return out
 
