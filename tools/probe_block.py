@@ -26,12 +26,17 @@ def main():
     ap.add_argument("--blocks", type=int, nargs="+", default=[8, 16])
     ap.add_argument("--keep", type=int, default=0)
     ap.add_argument("--basis", type=int, default=0)
+    ap.add_argument("--sweep", nargs="*", default=[],
+                    help="keep:basis pairs to run at the first block width (0 = default)")
     a = ap.parse_args()
     n, deg, d = CONFIGS[a.config]
     layers = synthetic.er_layers(n, deg, 2, seed_base=1000)
     eng = _lib.Engine(0)
     eng.set_layers(layers)
-    for b in a.blocks:
+    runs = [(b, a.keep, a.basis) for b in a.blocks]
+    runs += [(a.blocks[0], int(x.split(":")[0]), int(x.split(":")[1])) for x in a.sweep]
+    for b, keep, basis in runs:
+        a.keep, a.basis = keep, basis
         eng.uase(d, block=b, seed=42, keep=a.keep, max_basis=a.basis)  # warm (allocations)
         eng.synchronize()
         t0 = time.perf_counter()
@@ -40,7 +45,8 @@ def main():
         wall = time.perf_counter() - t0
         st_t = eng.uase(d, block=b, seed=42, keep=a.keep, max_basis=a.basis,
                         solver_flags=_lib.EIG_TIME_SPMM)
-        print(json.dumps(dict(config=a.config, block=b, wall_ms=round(wall * 1e3, 1),
+        print(json.dumps(dict(config=a.config, block=b, keep=keep, basis=basis,
+                              wall_ms=round(wall * 1e3, 1),
                               restarts=st["restarts"], block_applications=st["block_applications"],
                               vector_applications=st["block_applications"] * b,
                               max_residual=st["max_residual"], converged=st["converged"],
