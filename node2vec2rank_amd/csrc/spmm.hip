@@ -754,7 +754,9 @@ __device__ __forceinline__ int64_t uniform_i64(int64_t v) {
 
 // NS steps of 32 entries of one window: index words and gathers of all NS steps issued as
 // straight-line batches, then per step: stage, and the row owners fold their entries
-template <int NS, bool UNIT>
+// NTL: the index / value stream loaded non-temporally (so it does not displace panel lines in
+// L2; N2V2R_FLAT_NT=1, A/B)
+template <int NS, bool UNIT, bool NTL>
 __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1))) int32_t* ind,
                                            const __attribute__((address_space(1))) float* dat,
                                            int64_t beg, int off, int left,
@@ -768,8 +770,13 @@ __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1)
   for (int u = 0; u < NS; ++u) {
     const int q = u * 32 + pr;
     const int64_t e = beg + off + (q < left ? q : 0);
-    wd[u] = ind[e];
-    v[u] = UNIT ? 1.f : dat[e];
+    if constexpr (NTL) {
+      wd[u] = __builtin_nontemporal_load(ind + e);
+      v[u] = UNIT ? 1.f : __builtin_nontemporal_load(dat + e);
+    } else {
+      wd[u] = ind[e];
+      v[u] = UNIT ? 1.f : dat[e];
+    }
   }
 #pragma unroll
   for (int u = 0; u < NS; ++u)
@@ -785,6 +792,7 @@ __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1)
   }
 }
 
+template <bool NTL>
 __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
   // [tile_rows][8] row accumulators, then a 1-KB staging slot per wave
   extern __shared__ float tacf[];
@@ -834,13 +842,13 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
   for (int off = 0; off < len; off += 128) {                                                   \
     const int left = len - off;                                                                \
     if (left > 96)                                                                             \
-      flat_steps<4, U>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+      flat_steps<4, U, NTL>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
     else if (left > 64)                                                                        \
-      flat_steps<3, U>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+      flat_steps<3, U, NTL>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
     else if (left > 32)                                                                        \
-      flat_steps<2, U>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+      flat_steps<2, U, NTL>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
     else                                                                                       \
-      flat_steps<1, U>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+      flat_steps<1, U, NTL>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
   }
         if (unit) {
           FLAT_STEPS(true)
@@ -883,14 +891,23 @@ extern "C" hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, int rpw, hip
   if (a.form == 1) {  // + a 1-KB staging slot per wave
     const size_t flds = lds + 16 * 1024;
     static const bool fattr = [] {
-      (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel,
+      (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel<false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel<true>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
       (void)hipGetLastError();
       return true;
     }();
     (void)fattr;
+    static const bool ntl = [] {
+      const char* e = getenv("N2V2R_FLAT_NT");
+      return e && e[0] == '1';
+    }();
     if (flds > 80 * 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(spmm8_flat_kernel, dim3(grid), dim3(1024), flds, stream, a);
+    if (ntl)
+      hipLaunchKernelGGL(spmm8_flat_kernel<true>, dim3(grid), dim3(1024), flds, stream, a);
+    else
+      hipLaunchKernelGGL(spmm8_flat_kernel<false>, dim3(grid), dim3(1024), flds, stream, a);
     return hipGetLastError();
   }
   if (lds > 64 * 1024) {

@@ -13,4 +13,5 @@ timeout -k 10 400 python -u bench.py --config cfg3 --steps 3 --warmup 1 > $O/ben
 timeout -k 10 300 python -u bench.py --config cfg1 --steps 20 --warmup 2 --resident-steps 20 > $O/bench_cfg1.json 2> $O/bench_cfg1.err || { echo cfg1-fail; exit 1; }
 timeout -k 10 200 python -u tools/api_wall.py --config cfg2 --reps 3 > $O/api_cfg2.json 2>&1 || { echo api2-fail; exit 1; }
 timeout -k 10 300 python -u tools/api_wall.py --config cfg4 --reps 2 > $O/api_cfg4.json 2>&1 || { echo api4-fail; exit 1; }
+timeout -k 10 400 python -u tools/probe_block.py --config cfg4 --blocks 8 --sweep 144:0 192:0 224:0 160:448 160:384 192:448 > $O/sweep_cfg4.jsonl 2> $O/sweep_cfg4.err || { echo sweep-fail; exit 1; }
 echo done
