@@ -1449,10 +1449,12 @@ struct Eig {
       int nb_auto = 8;
       if (tile_form == 1) {
         nb_auto = 4;
-        while (nb_auto < 32 && (double)nglob * 32.0 / nb_auto > 2.0 * 1024 * 1024) nb_auto *= 2;
+        while (nb_auto < CB_MAX && (double)nglob * 32.0 / nb_auto > 2.0 * 1024 * 1024)
+          nb_auto *= 2;
       }
       tile_nb = tiled ? (tn_ ? std::atoi(tn_) : nb_auto) : CB_NB;
-      if (tile_nb != 4 && tile_nb != 8 && tile_nb != 16 && tile_nb != 32) tile_nb = nb_auto;
+      if (tile_nb != 4 && tile_nb != 8 && tile_nb != 16 && tile_nb != 32 && tile_nb != 64)
+        tile_nb = nb_auto;
       for (auto& Lp : h->layers)
         col_blocks = ensure_col_blocks(*Lp, nglob, st, tile_nb, tile_form == 1) && col_blocks;
       tiled = tiled && col_blocks;
@@ -2007,9 +2009,17 @@ bool col_blocks_wanted(const n2v2r_handle* h, int b) {
   // 0.56 at a 3.2 MB panel (N = 100k: the panel already fits one L2), 1.35 at 9.6 MB,
   // 1.61 at 32 MB, 1.16 at 96 MB, 0.93 at 320 MB (beyond the Infinity Cache the gathers go
   // to HBM either way and the partials only add traffic)
+  // round 3: the flat-window tiled form (the default tiled form) also wins beyond the Infinity
+  // Cache -- each phase gathers from one panel block, which the Infinity Cache holds even when
+  // the whole panel does not (cfg5 on one GPU, 320 MB panel: 9.5 vs 11.5 ms per stage launch)
+  // -- so its window has no upper end; the partials / row-group forms keep 160 MB
+  const char* te = std::getenv("N2V2R_SPMM_TILE");
+  const char* tf = std::getenv("N2V2R_TILE_FLAT");
+  const char* tp = std::getenv("N2V2R_TILE_PAIR");
+  const bool flat = !(te && te[0] == '0') && !(tf && tf[0] == '0') && !(tp && tp[0] == '2');
   const char* m = std::getenv("N2V2R_CB_MIN_MB");
   const char* x = std::getenv("N2V2R_CB_MAX_MB");
-  const double min_mb = m ? atof(m) : 8.0, max_mb = x ? atof(x) : 160.0;
+  const double min_mb = m ? atof(m) : 8.0, max_mb = x ? atof(x) : (flat ? 1e12 : 160.0);
   const double panel = 4.0 * b * (double)h->n;
   return panel > min_mb * 1e6 && panel <= max_mb * 1e6;
 }

@@ -24,7 +24,7 @@ struct SpmmArgs {
 
 // ---- column blocks (b = 8, panels of 8-160 MB) ------------------------------------------------
 #define CB_NB 8      // column blocks of the partials form (one per XCD)
-#define CB_MAX 32    // column blocks of the tiled form (N2V2R_SPMM_TILE_NB)
+#define CB_MAX 64    // column blocks of the tiled form (N2V2R_SPMM_TILE_NB)
 #define CB_WIN 32    // rows per window of the packed tiled form (row-in-window: 5 index bits)
 #define CB_WIN_BITS 5
 
