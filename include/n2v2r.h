@@ -202,6 +202,11 @@ int n2v2r_synchronize(n2v2r_handle* h);
 int n2v2r_probe_spmm_stage2(n2v2r_handle* h, int mode, int reps, double* avg_ms);
 int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, const float* X,
                      float* Y, double* avg_ms, double* algo_bytes);
+/* Diagnostic: the flat-window tiled SpMM of layer k (A_k X, or A_k^T X) at panel width b = 8 or
+ * 16 with nb column blocks (0: panel blocks of <= 2 MB), one-GPU handles; Y (optional, n x b)
+ * receives the product.  N2V2R_ERR_BAD_ARG when the layer cannot take packed blocks. */
+int n2v2r_bench_spmm_tiled(n2v2r_handle* h, int k, int transpose, int b, int nb, int reps,
+                           const float* X, float* Y, double* avg_ms);
 
 /* 1 when UASE (and n2v2r_bench_spmm) use the XCD-local column-block SpMM at panel width b on
  * this handle's layers (b = 8 CSR panels of 8-160 MB: each layer split into 8 column blocks,

@@ -39,7 +39,7 @@ EXPORTED = [
     "n2v2r_get_left_embedding", "n2v2r_get_singular_values", "n2v2r_set_embedding",
     "n2v2r_rank", "n2v2r_get_distances", "n2v2r_get_borda", "n2v2r_rank_timing",
     "n2v2r_pairwise_distances", "n2v2r_borda_columns", "n2v2r_column_sums",
-    "n2v2r_synchronize", "n2v2r_bench_spmm", "n2v2r_spmm_col_blocks",
+    "n2v2r_synchronize", "n2v2r_bench_spmm", "n2v2r_bench_spmm_tiled", "n2v2r_spmm_col_blocks",
     "n2v2r_comm_unique_id", "n2v2r_create_rccl", "n2v2r_simgroup_create",
     "n2v2r_simgroup_destroy", "n2v2r_create_sim", "n2v2r_dist_info", "n2v2r_set_layer_csr_rows",
     "n2v2r_rr_top", "n2v2r_rr_band_top", "n2v2r_set_layer_dense", "n2v2r_project",
@@ -131,6 +131,8 @@ def load(path: str | None = None):
             "n2v2r_bench_spmm": (_i, [_vp, _i, _i, _i, _i, _p(np.float32), _vp,
                                       ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_double)]),
+            "n2v2r_bench_spmm_tiled": (_i, [_vp, _i, _i, _i, _i, _i, _p(np.float32), _vp,
+                                            ctypes.POINTER(ctypes.c_double)]),
             "n2v2r_spmm_col_blocks": (_i, [_vp, _i]),
             "n2v2r_probe_spmm_stage2": (_i, [_vp, _i, _i, ctypes.POINTER(ctypes.c_double)]),
             "n2v2r_rr_top": (_i, [_vp, _i, _p(np.float64), _i, _p(np.float64), _p(np.float32)]),
@@ -450,6 +452,19 @@ class Engine:
                                               int(reps), X, yp, ctypes.byref(ms),
                                               ctypes.byref(by)), "bench_spmm")
         return Y, ms.value, by.value
+
+    def bench_spmm_tiled(self, k: int, X, transpose: bool = False, nb: int = 0, reps: int = 20,
+                         want_y=True):
+        """Time the flat-window tiled SpMM (panel width 8 or 16) of layer k alone."""
+        X = np.ascontiguousarray(X, dtype=np.float32)
+        n, b = X.shape
+        Y = np.empty((self._n_local(), b), dtype=np.float32) if want_y else None
+        ms = ctypes.c_double()
+        yp = Y.ctypes.data_as(ctypes.c_void_p) if want_y else None
+        self._check(self.lib.n2v2r_bench_spmm_tiled(self.h, int(k), int(bool(transpose)), int(b),
+                                                    int(nb), int(reps), X, yp, ctypes.byref(ms)),
+                    "bench_spmm_tiled")
+        return Y, ms.value
 
     def probe_spmm_stage2(self, mode: int, reps: int = 50) -> float:
         """Diagnostic: average ms of the b = 8 second SpMM stage (0 summed, 1 per layer,

@@ -3146,4 +3146,69 @@ int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, con
   });
 }
 
+
+// The flat-window tiled SpMM of one layer at panel width b (8 or 16) with `nb` column blocks
+// (0: the fit's default rule, panel blocks of <= 2 MB), timed alone with HIP events.
+int n2v2r_bench_spmm_tiled(n2v2r_handle* h, int k, int transpose, int b, int nb, int reps,
+                           const float* X, float* Y, double* avg_ms) {
+  return guarded(h, [&]() -> int {
+    if (k < 0 || k >= h->K || !h->layers[k]->loaded || h->layers[k]->dense || (b != 8 && b != 16) ||
+        reps < 1 || !X || h->comm)
+      return N2V2R_ERR_BAD_ARG;
+    if (nb <= 0) {
+      nb = 4;
+      while (nb < CB_MAX && (double)h->n * 4.0 * b / nb > 2.0 * 1024 * 1024) nb *= 2;
+    }
+    if (nb != 4 && nb != 8 && nb != 16 && nb != 32 && nb != 64) return N2V2R_ERR_BAD_ARG;
+    LayerDev& L = *h->layers[k];
+    if (!ensure_col_blocks(L, h->n, h->stream, nb, true)) return N2V2R_ERR_BAD_ARG;
+    const LayerDev::ColBlocks& cbs = (transpose && !L.symmetric) ? L.cb_t : L.cb;
+    if (cbs.cbits == 0) return N2V2R_ERR_BAD_ARG;
+    DevBuf xd, yd, tb;
+    xd.ensure(sizeof(float) * h->n * b);
+    yd.ensure(sizeof(float) * std::max<int64_t>(h->nloc, 1) * b);
+    tb.ensure(sizeof(CsrBlk) * nb);
+    HIPCHK(hipMemcpyAsync(xd.p, X, sizeof(float) * h->n * b, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(tb.p, cbs.blk, sizeof(CsrBlk) * nb, hipMemcpyHostToDevice, h->stream));
+    int ncu = 0;
+    HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
+    SpmmTileArgs a{};
+    a.blk = tb.as<CsrBlk>();
+    a.X[0] = xd.as<float>();
+    a.Y[0] = yd.as<float>();
+    a.ldx = b;
+    a.ldy = b;
+    a.n = h->nloc;
+    a.K = 1;
+    a.nb = nb;
+    a.sum = 0;
+    a.form = 1;
+    a.b = b;
+    a.tile_rows = n2v2r_spmm_tile_rows(h->nloc, ncu, 2);
+    if (b == 16) {
+      const char* tr = std::getenv("N2V2R_T16_ROWS");
+      a.tile_rows = std::min(a.tile_rows, tr ? std::atoi(tr) : 1024);
+      a.tile_rows = std::max(CB_WIN, a.tile_rows / CB_WIN * CB_WIN);
+    }
+    HIPCHK(n2v2r_launch_spmm_tile(a, 0, h->stream));  // warm-up
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, h->stream));
+    for (int r = 0; r < reps; ++r) HIPCHK(n2v2r_launch_spmm_tile(a, 0, h->stream));
+    HIPCHK(hipEventRecord(e1, h->stream));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (avg_ms) *avg_ms = (double)ms / reps;
+    if (Y)
+      HIPCHK(hipMemcpyAsync(Y, yd.p, sizeof(float) * h->nloc * b, hipMemcpyDeviceToHost,
+                            h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return N2V2R_OK;
+  });
+}
+
 }  // extern "C"

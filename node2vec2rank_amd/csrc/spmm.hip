@@ -756,7 +756,7 @@ __device__ __forceinline__ int64_t uniform_i64(int64_t v) {
 // straight-line batches, then per step: stage, and the row owners fold their entries
 // NTL: the index / value stream loaded non-temporally (so it does not displace panel lines in
 // L2; N2V2R_FLAT_NT=1, A/B)
-template <int NS, bool UNIT, bool NTL>
+template <int NS, bool UNIT, bool NTL, bool FOLD = true>
 __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1))) int32_t* ind,
                                            const __attribute__((address_space(1))) float* dat,
                                            int64_t beg, int off, int left,
@@ -785,6 +785,10 @@ __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1)
 #pragma unroll
   for (int u = 0; u < NS; ++u) {
     stage[pr * 2 + sub] = v[u] * x[u];  // entries past the end are never read
+    if constexpr (!FOLD) {  // timing probe (N2V2R_FLAT_NOFOLD=1): wrong sums, no fold loop
+      acc += stage[pr * 2 + sub];
+      continue;
+    }
     const int s0 = off + u * 32;
     const int lo = (rs > s0 ? rs : s0) - s0;
     const int hi = (re < s0 + 32 ? re : s0 + 32) - s0;
@@ -792,10 +796,17 @@ __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1)
   }
 }
 
-template <bool NTL>
+// SCHED (N2V2R_FLAT_SCHED, A/B): bit 0 -- windows handed out per phase from an LDS counter
+// (a wave that finishes early takes the next window instead of idling at the phase barrier);
+// bit 1 -- the next window's row pointers loaded before the current window's entries (one
+// dependent memory round trip less per window).  Each window's entries are folded by one wave
+// in entry order and added to its rows once per phase either way: the sums are bit-identical.
+template <bool NTL, bool FOLD = true, int SCHED = 0>
 __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
+  constexpr bool DYN = (SCHED & 1) != 0, PF = (SCHED & 2) != 0;
   // [tile_rows][8] row accumulators, then a 1-KB staging slot per wave
   extern __shared__ float tacf[];
+  __shared__ int wq[2];  // DYN: per-phase window counters (phase parity)
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nwave = blockDim.x >> 6;
@@ -808,14 +819,19 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
   f32x4* tacc = reinterpret_cast<f32x4*>(tacf);
   f32x4* stage = reinterpret_cast<f32x4*>(tacf + (size_t)a.tile_rows * 8) + wave * 64;
-  // zero / write back by the same window -> wave map as the adds (no barrier needed)
+  // zero / write back by the static window -> wave map (DYN: a barrier before the first phase)
   for (int w = wave; w < nwin; w += nwave) {
     const int lr = w * CB_WIN + pr;
     if (lr < nrows) tacc[lr * 2 + sub] = zero;
   }
+  if constexpr (DYN) {
+    if (threadIdx.x == 0) wq[0] = 0;
+    __syncthreads();
+  }
+  int g = 0;  // phase counter over (layer, block)
   for (int k = 0; k < a.K; ++k) {
     const float* X = a.X[k];
-    for (int p = 0; p < a.nb; ++p) {
+    for (int p = 0; p < a.nb; ++p, ++g) {
       const CsrBlk& A = a.blk[k * a.nb + p];
       const int cbits = __builtin_amdgcn_readfirstlane(A.cbits);
       const int unit = __builtin_amdgcn_readfirstlane(A.unit);
@@ -826,13 +842,43 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
       const int64_t col0 = uniform_i64(A.col0);
       const int32_t cmask = (1 << cbits) - 1;
       const auto Xb = uniform_global(X + col0 * a.ldx);
-      for (int w = wave; w < nwin; w += nwave) {
+      // DYN: the other parity's counter was last used in the previous phase (behind the
+      // barrier) and is next used after the coming one
+      if (DYN && threadIdx.x == 0) wq[(g + 1) & 1] = 0;
+      auto next_window = [&](int cur) -> int {
+        if constexpr (DYN) {
+          int v = 0;
+          if (lane == 0) v = atomicAdd(&wq[g & 1], 1);
+          return __builtin_amdgcn_readfirstlane(v);
+        } else {
+          return cur + nwave;
+        }
+      };
+      // the window's row boundaries: lane pair r holds rows wr + r's [rs, re)
+      auto load_rp = [&](int w, int32_t& ps, int32_t& pe) {
         const int wr = w * CB_WIN;
         const int we = wr + CB_WIN < nrows ? wr + CB_WIN : nrows;
-        // the window's row boundaries: lane pair r holds rows wr + r's [rs, re)
         const int rr = wr + pr < we ? wr + pr : we;
-        const int32_t ps = rp[r0 + rr];
-        const int32_t pe = rp[r0 + (wr + pr < we ? wr + pr + 1 : we)];
+        ps = rp[r0 + rr];
+        pe = rp[r0 + (wr + pr < we ? wr + pr + 1 : we)];
+      };
+      int w = DYN ? next_window(0) : wave;
+      int32_t ps_n = 0, pe_n = 0;
+      if (PF && w < nwin) load_rp(w, ps_n, pe_n);
+      while (w < nwin) {
+        const int cw = w;
+        int32_t ps, pe;
+        if constexpr (PF) {
+          ps = ps_n;
+          pe = pe_n;
+          w = next_window(w);
+          if (w < nwin) load_rp(w, ps_n, pe_n);
+        } else {
+          load_rp(cw, ps, pe);
+          w = next_window(w);
+        }
+        const int wr = cw * CB_WIN;
+        const int we = wr + CB_WIN < nrows ? wr + CB_WIN : nrows;
         const int32_t e0 = __builtin_amdgcn_readfirstlane(ps);
         const int len = __builtin_amdgcn_readlane(pe, 2 * (we - wr - 1)) - e0;
         const int rs = ps - e0, re = pe - e0;
@@ -842,13 +888,13 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
   for (int off = 0; off < len; off += 128) {                                                   \
     const int left = len - off;                                                                \
     if (left > 96)                                                                             \
-      flat_steps<4, U, NTL>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+      flat_steps<4, U, NTL, FOLD>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
     else if (left > 64)                                                                        \
-      flat_steps<3, U, NTL>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+      flat_steps<3, U, NTL, FOLD>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
     else if (left > 32)                                                                        \
-      flat_steps<2, U, NTL>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+      flat_steps<2, U, NTL, FOLD>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
     else                                                                                       \
-      flat_steps<1, U, NTL>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+      flat_steps<1, U, NTL, FOLD>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
   }
         if (unit) {
           FLAT_STEPS(true)
@@ -869,6 +915,136 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
           tacc[lr * 2 + sub] = zero;
         }
       }
+      // DYN: the next layer's first phase may hand these windows to other waves
+      if (DYN && k + 1 < a.K) __syncthreads();
+    }
+  }
+}
+
+// ---- the packed flat-window form at b = 16 ---------------------------------------------------
+// The same windows, column-block phases and packed entries as spmm8_flat_kernel, with 64-B panel
+// rows: a lane quad (q = lane / 4) gathers one entry's row as four 16-B pieces, so a wave step
+// takes 16 entries, and quad q owns window rows q and q + 16 (two register accumulators).  An
+// entry still costs one scattered line access (the bound of the b = 8 form) but
+// carries 16 columns instead of 8, so a vector application costs about half the line accesses.
+template <int NS, bool UNIT>
+__device__ __forceinline__ void flat16_steps(const __attribute__((address_space(1))) int32_t* ind,
+                                             const __attribute__((address_space(1))) float* dat,
+                                             int64_t beg, int off, int left,
+                                             const __attribute__((address_space(1))) float* Xb,
+                                             uint32_t ldx, int32_t cmask, int q, int sub, int rs0,
+                                             int re0, int rs1, int re1, f32x4* stage, f32x4& acc0,
+                                             f32x4& acc1) {
+  int wd[NS];
+  float v[NS];
+  f32x4 x[NS];
+#pragma unroll
+  for (int u = 0; u < NS; ++u) {
+    const int t = u * 16 + q;
+    const int64_t e = beg + off + (t < left ? t : 0);
+    wd[u] = ind[e];
+    v[u] = UNIT ? 1.f : dat[e];
+  }
+#pragma unroll
+  for (int u = 0; u < NS; ++u)
+    x[u] = *reinterpret_cast<const __attribute__((address_space(1))) f32x4*>(
+        Xb + ((uint32_t)(wd[u] & cmask) * ldx + sub * 4));
+#pragma unroll
+  for (int u = 0; u < NS; ++u) {
+    stage[q * 4 + sub] = v[u] * x[u];  // entries past the end are never read
+    const int s0 = off + u * 16;
+    const int lo0 = (rs0 > s0 ? rs0 : s0) - s0, hi0 = (re0 < s0 + 16 ? re0 : s0 + 16) - s0;
+    for (int j = lo0; j < hi0; ++j) acc0 += stage[j * 4 + sub];
+    const int lo1 = (rs1 > s0 ? rs1 : s0) - s0, hi1 = (re1 < s0 + 16 ? re1 : s0 + 16) - s0;
+    for (int j = lo1; j < hi1; ++j) acc1 += stage[j * 4 + sub];
+  }
+}
+
+__global__ __launch_bounds__(1024, 8) void spmm16_flat_kernel(SpmmTileArgs a) {
+  // [tile_rows][16] row accumulators, then a 1-KB staging slot per wave
+  extern __shared__ float tacf[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nwave = blockDim.x >> 6;
+  const int pr = lane >> 1;            // row-pointer lanes: pair pr holds window row pr
+  const int q = lane >> 2, sub = lane & 3;  // entry / row-owner quad, 16-B piece
+  const int64_t r0 = (int64_t)blockIdx.x * a.tile_rows;
+  const int64_t rem = a.n - r0;
+  const int nrows = (int)(rem < a.tile_rows ? rem : a.tile_rows);
+  const int nwin = (nrows + CB_WIN - 1) / CB_WIN;
+  const uint32_t ldx = (uint32_t)a.ldx;
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  f32x4* tacc = reinterpret_cast<f32x4*>(tacf);
+  f32x4* stage = reinterpret_cast<f32x4*>(tacf + (size_t)a.tile_rows * 16) + wave * 64;
+  for (int w = wave; w < nwin; w += nwave) {
+    const int lr = w * CB_WIN + q;
+    if (lr < nrows) tacc[lr * 4 + sub] = zero;
+    if (lr + 16 < nrows) tacc[(lr + 16) * 4 + sub] = zero;
+  }
+  for (int k = 0; k < a.K; ++k) {
+    const float* X = a.X[k];
+    for (int p = 0; p < a.nb; ++p) {
+      const CsrBlk& A = a.blk[k * a.nb + p];
+      const int cbits = __builtin_amdgcn_readfirstlane(A.cbits);
+      const int unit = __builtin_amdgcn_readfirstlane(A.unit);
+      const auto rp = uniform_global(A.rp);
+      const auto ind = uniform_global(A.indices);
+      const auto dat = uniform_global(A.data);
+      const int64_t base = uniform_i64(A.base);
+      const int64_t col0 = uniform_i64(A.col0);
+      const int32_t cmask = (1 << cbits) - 1;
+      const auto Xb = uniform_global(X + col0 * a.ldx);
+      for (int w = wave; w < nwin; w += nwave) {
+        const int wr = w * CB_WIN;
+        const int we = wr + CB_WIN < nrows ? wr + CB_WIN : nrows;
+        const int rr = wr + pr < we ? wr + pr : we;
+        const int32_t ps = rp[r0 + rr];
+        const int32_t pe = rp[r0 + (wr + pr < we ? wr + pr + 1 : we)];
+        const int32_t e0 = __builtin_amdgcn_readfirstlane(ps);
+        const int len = __builtin_amdgcn_readlane(pe, 2 * (we - wr - 1)) - e0;
+        // this quad's rows q and q + 16: their [start, end) from the pointer lanes 2q, 2q + 32
+        const int rs0 = __shfl(ps, 2 * q, 64) - e0, re0 = __shfl(pe, 2 * q, 64) - e0;
+        const int rs1 = __shfl(ps, 2 * q + 32, 64) - e0, re1 = __shfl(pe, 2 * q + 32, 64) - e0;
+        const int64_t beg = base + e0;
+        f32x4 acc0 = zero, acc1 = zero;
+#define FLAT16_STEPS(U)                                                                        \
+  for (int off = 0; off < len; off += 48) {                                                    \
+    const int left = len - off;                                                                \
+    if (left > 32)                                                                             \
+      flat16_steps<3, U>(ind, dat, beg, off, left, Xb, ldx, cmask, q, sub, rs0, re0, rs1, re1, \
+                         stage, acc0, acc1);                                                   \
+    else if (left > 16)                                                                        \
+      flat16_steps<2, U>(ind, dat, beg, off, left, Xb, ldx, cmask, q, sub, rs0, re0, rs1, re1, \
+                         stage, acc0, acc1);                                                   \
+    else                                                                                       \
+      flat16_steps<1, U>(ind, dat, beg, off, left, Xb, ldx, cmask, q, sub, rs0, re0, rs1, re1, \
+                         stage, acc0, acc1);                                                   \
+  }
+        if (unit) {
+          FLAT16_STEPS(true)
+        } else {
+          FLAT16_STEPS(false)
+        }
+#undef FLAT16_STEPS
+        if (wr + q < we) tacc[(wr + q) * 4 + sub] += acc0;
+        if (wr + q + 16 < we) tacc[(wr + q + 16) * 4 + sub] += acc1;
+      }
+      __syncthreads();  // all waves on the same panel block (see spmm8_tile_kernel)
+    }
+    if (!a.sum || k == a.K - 1) {
+      float* Y = a.Y[a.sum ? 0 : k];
+      for (int w = wave; w < nwin; w += nwave) {
+        const int lr = w * CB_WIN + q;
+        if (lr < nrows) {
+          *reinterpret_cast<f32x4*>(Y + (r0 + lr) * a.ldy + sub * 4) = tacc[lr * 4 + sub];
+          tacc[lr * 4 + sub] = zero;
+        }
+        if (lr + 16 < nrows) {
+          *reinterpret_cast<f32x4*>(Y + (r0 + lr + 16) * a.ldy + sub * 4) =
+              tacc[(lr + 16) * 4 + sub];
+          tacc[(lr + 16) * 4 + sub] = zero;
+        }
+      }
     }
   }
 }
@@ -886,6 +1062,20 @@ extern "C" int n2v2r_spmm_tile_rows(int64_t n, int ncu, int wpc) {
 extern "C" hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, int rpw, hipStream_t stream) {
   if (a.K < 1 || a.K > 8 || a.tile_rows < 16 || a.n <= 0) return hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.n + a.tile_rows - 1) / a.tile_rows);
+  if (a.b == 16) {  // 64 B of accumulators per row + a 1-KB staging slot per wave
+    const size_t flds = sizeof(float) * 16 * (size_t)a.tile_rows + 16 * 1024;
+    if (a.form != 1 || a.tile_rows % CB_WIN != 0 || flds > 80 * 1024) return hipErrorInvalidValue;
+    static const bool fattr = [] {
+      (void)hipFuncSetAttribute((const void*)spmm16_flat_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      (void)hipGetLastError();
+      return true;
+    }();
+    (void)fattr;
+    hipLaunchKernelGGL(spmm16_flat_kernel, dim3(grid), dim3(1024), flds, stream, a);
+    return hipGetLastError();
+  }
+  if (a.b != 0 && a.b != 8) return hipErrorInvalidValue;
   const size_t lds = sizeof(float) * 8 * (size_t)a.tile_rows;
   if (a.form < 0 || a.form > 2 || a.tile_rows % CB_WIN != 0) return hipErrorInvalidValue;
   if (a.form == 1) {  // + a 1-KB staging slot per wave
@@ -904,7 +1094,32 @@ extern "C" hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, int rpw, hip
       return e && e[0] == '1';
     }();
     if (flds > 80 * 1024) return hipErrorInvalidValue;
-    if (ntl)
+    static const bool nofold = [] {  // timing probe only: the fold loop skipped, sums wrong
+      const char* e = getenv("N2V2R_FLAT_NOFOLD");
+      if (e && e[0] == '1')
+        (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel<false, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      return e && e[0] == '1';
+    }();
+    static const int sched = [] {  // A/B: 1 windows from a per-phase counter, 2 rp prefetch
+      const char* e = getenv("N2V2R_FLAT_SCHED");
+      const int v = e ? atoi(e) : 0;
+      for (const void* f : {(const void*)spmm8_flat_kernel<false, true, 1>,
+                            (const void*)spmm8_flat_kernel<false, true, 2>,
+                            (const void*)spmm8_flat_kernel<false, true, 3>})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      (void)hipGetLastError();
+      return v >= 0 && v <= 3 ? v : 0;
+    }();
+    if (nofold)
+      hipLaunchKernelGGL((spmm8_flat_kernel<false, false>), dim3(grid), dim3(1024), flds, stream, a);
+    else if (sched == 1)
+      hipLaunchKernelGGL((spmm8_flat_kernel<false, true, 1>), dim3(grid), dim3(1024), flds, stream, a);
+    else if (sched == 2)
+      hipLaunchKernelGGL((spmm8_flat_kernel<false, true, 2>), dim3(grid), dim3(1024), flds, stream, a);
+    else if (sched == 3)
+      hipLaunchKernelGGL((spmm8_flat_kernel<false, true, 3>), dim3(grid), dim3(1024), flds, stream, a);
+    else if (ntl)
       hipLaunchKernelGGL(spmm8_flat_kernel<true>, dim3(grid), dim3(1024), flds, stream, a);
     else
       hipLaunchKernelGGL(spmm8_flat_kernel<false>, dim3(grid), dim3(1024), flds, stream, a);

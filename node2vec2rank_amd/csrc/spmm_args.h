@@ -65,5 +65,6 @@ struct SpmmTileArgs {  // row tiles x column-block phases (spmm8_tile_kernel / _
   int tile_rows;
   int form;            // 0: row groups (guarded loads); 2: two row groups per step;
                        // 1: packed flat windows (spmm8_flat_kernel)
+  int b;               // panel width: 8 (0 means 8) or 16 (flat form only: spmm16_flat_kernel)
 };
 

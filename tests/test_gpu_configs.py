@@ -194,12 +194,17 @@ def test_cfg5_path_w8_one_million(engine):
     assert res_h.max() < 5e-6, res_h
     Y = np.concatenate([r["Y"] for r in res], axis=1).astype(np.float64)
     Yal = orc.align_signs(Y, engine.embedding().astype(np.float64))
-    # both runs stop at residual <= 1e-6 theta_1; a column's deviation is bounded by residual /
-    # gap, so the trailing columns (closest eigenvalues of the ER bulk edge) move the most:
-    # the leading d - 8 columns within 2e-3 of the largest entry, every column within 1e-2
+    # both runs stop at residual <= 1e-6 theta_1, so column j's angle to the other run's column is
+    # at most 2e-6 theta_1 / gap_j (gap_j: distance of theta_j to its nearest computed
+    # neighbour).  The ER bulk edge packs the eigenvalues densely at N = 1M, so the bound per
+    # column is max(2e-3, 4 x that angle) of the largest entry, and never above 1e-2 (a fixed
+    # 2e-3 for the leading columns failed once at 2.0025e-3 on a column whose gap is ~1e-4 theta_1)
+    theta = res[0]["s"].astype(np.float64) ** 2
+    gaps = np.array([np.min(np.abs(np.delete(theta, j) - theta[j])) for j in range(d)])
+    allowed = np.minimum(1e-2, np.maximum(2e-3, 4 * 2e-6 * theta[0] / gaps))
     dev = np.abs(Yal - engine.embedding()).max(axis=(0, 1)) / np.abs(Yal).max()
-    print(f"cfg5 path W=8 N=1M: embedding deviation per column max {dev.max():.2e} "
-          f"(leading {dev[:d - 8].max():.2e})")
-    assert dev[:d - 8].max() <= 2e-3 and dev.max() <= 1e-2, dev
+    print(f"cfg5 path W=8 N=1M: embedding deviation per column max {dev.max():.2e}, "
+          f"max deviation / allowed {np.max(dev / allowed):.2f}")
+    assert np.all(dev <= allowed), (dev, allowed)
     tau = kendalltau(res[0]["B"], engine.borda(0)).statistic
     assert tau > 0.995, tau
