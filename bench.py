@@ -37,6 +37,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -415,18 +416,6 @@ def main():
         except Exception:
             pass
 
-    # N > 1 replicas: the same graph family ALSO as one graph row-partitioned over every rank
-    # (RCCL all-gathers of the panels, all-reduces of the Gram / Rayleigh-Ritz / residual
-    # reductions), strong scaling -- the multi-GPU path SURVEY 8(e) describes, measured beside
-    # the weak-scaling value (N2V2R_BENCH_PARTITIONED=0 skips it)
-    strong = None
-    if (world > 1 and mode == "replicas" and not cfg.get("dense")
-            and os.environ.get("N2V2R_BENCH_PARTITIONED", "1") != "0"):
-        try:
-            strong = strong_scaling(group, cfg, args, local, rank, world)
-        except Exception as e:  # reported in the line; the weak-scaling value stands
-            strong = {"error": repr(e)[:300]}
-
     if mode == "partitioned":
         par = f"row-partitioned x{world} (RCCL)" if world > 1 else "row-partitioned x1"
     else:
@@ -463,7 +452,32 @@ def main():
                 for k, v in (stats or {}).items() if k not in ("ms_spmm", "ms_ortho")},
         "setup_s": round(t_build, 2),
     }
-    if strong is not None:
+    # N > 1 replicas: the same graph family ALSO as one graph row-partitioned over every rank
+    # (RCCL all-gathers of the panels, all-reduces of the Gram / Rayleigh-Ritz / residual
+    # reductions), strong scaling -- the multi-GPU path SURVEY 8(e) describes, measured beside
+    # the weak-scaling value (N2V2R_BENCH_PARTITIONED=0 skips it).  A watchdog guards the
+    # replicas line: if the partitioned leg has not finished in N2V2R_BENCH_PARTITIONED_S
+    # seconds (default 300), rank 0 prints the line with the leg marked as timed out and every
+    # rank exits.
+    if (world > 1 and mode == "replicas" and not cfg.get("dense")
+            and os.environ.get("N2V2R_BENCH_PARTITIONED", "1") != "0"):
+        limit = float(os.environ.get("N2V2R_BENCH_PARTITIONED_S", "300"))
+
+        def _expire():
+            if rank == 0:
+                result["partitioned_same_family"] = {"error": f"timed out after {limit:g} s"}
+                print(json.dumps(result), flush=True)
+            sys.stdout.flush()
+            os._exit(0)
+
+        timer = threading.Timer(limit, _expire)
+        timer.daemon = True
+        timer.start()
+        try:
+            strong = strong_scaling(group, cfg, args, local, rank, world)
+        except Exception as e:  # reported in the line; the weak-scaling value stands
+            strong = {"error": repr(e)[:300]}
+        timer.cancel()
         result["partitioned_same_family"] = strong
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         workers = max(1, min(16, os.cpu_count() or 1))
