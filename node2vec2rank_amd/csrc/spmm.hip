@@ -796,17 +796,10 @@ __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1)
   }
 }
 
-// SCHED (N2V2R_FLAT_SCHED, A/B): bit 0 -- windows handed out per phase from an LDS counter
-// (a wave that finishes early takes the next window instead of idling at the phase barrier);
-// bit 1 -- the next window's row pointers loaded before the current window's entries (one
-// dependent memory round trip less per window).  Each window's entries are folded by one wave
-// in entry order and added to its rows once per phase either way: the sums are bit-identical.
-template <bool NTL, bool FOLD = true, int SCHED = 0>
+template <bool NTL, bool FOLD = true>
 __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
-  constexpr bool DYN = (SCHED & 1) != 0, PF = (SCHED & 2) != 0;
   // [tile_rows][8] row accumulators, then a 1-KB staging slot per wave
   extern __shared__ float tacf[];
-  __shared__ int wq[2];  // DYN: per-phase window counters (phase parity)
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nwave = blockDim.x >> 6;
@@ -819,19 +812,17 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
   f32x4* tacc = reinterpret_cast<f32x4*>(tacf);
   f32x4* stage = reinterpret_cast<f32x4*>(tacf + (size_t)a.tile_rows * 8) + wave * 64;
-  // zero / write back by the static window -> wave map (DYN: a barrier before the first phase)
+  // zero / write back by the same window -> wave map as the adds (no barrier needed).  Measured
+  // and not kept (cfg4 layer launch 0.367 ms): windows handed out per phase from an LDS
+  // counter (0.557 ms), the next window's row pointers loaded before the current window's
+  // entries (0.367 ms, flat)
   for (int w = wave; w < nwin; w += nwave) {
     const int lr = w * CB_WIN + pr;
     if (lr < nrows) tacc[lr * 2 + sub] = zero;
   }
-  if constexpr (DYN) {
-    if (threadIdx.x == 0) wq[0] = 0;
-    __syncthreads();
-  }
-  int g = 0;  // phase counter over (layer, block)
   for (int k = 0; k < a.K; ++k) {
     const float* X = a.X[k];
-    for (int p = 0; p < a.nb; ++p, ++g) {
+    for (int p = 0; p < a.nb; ++p) {
       const CsrBlk& A = a.blk[k * a.nb + p];
       const int cbits = __builtin_amdgcn_readfirstlane(A.cbits);
       const int unit = __builtin_amdgcn_readfirstlane(A.unit);
@@ -842,43 +833,13 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
       const int64_t col0 = uniform_i64(A.col0);
       const int32_t cmask = (1 << cbits) - 1;
       const auto Xb = uniform_global(X + col0 * a.ldx);
-      // DYN: the other parity's counter was last used in the previous phase (behind the
-      // barrier) and is next used after the coming one
-      if (DYN && threadIdx.x == 0) wq[(g + 1) & 1] = 0;
-      auto next_window = [&](int cur) -> int {
-        if constexpr (DYN) {
-          int v = 0;
-          if (lane == 0) v = atomicAdd(&wq[g & 1], 1);
-          return __builtin_amdgcn_readfirstlane(v);
-        } else {
-          return cur + nwave;
-        }
-      };
-      // the window's row boundaries: lane pair r holds rows wr + r's [rs, re)
-      auto load_rp = [&](int w, int32_t& ps, int32_t& pe) {
+      for (int w = wave; w < nwin; w += nwave) {
         const int wr = w * CB_WIN;
         const int we = wr + CB_WIN < nrows ? wr + CB_WIN : nrows;
+        // the window's row boundaries: lane pair r holds rows wr + r's [rs, re)
         const int rr = wr + pr < we ? wr + pr : we;
-        ps = rp[r0 + rr];
-        pe = rp[r0 + (wr + pr < we ? wr + pr + 1 : we)];
-      };
-      int w = DYN ? next_window(0) : wave;
-      int32_t ps_n = 0, pe_n = 0;
-      if (PF && w < nwin) load_rp(w, ps_n, pe_n);
-      while (w < nwin) {
-        const int cw = w;
-        int32_t ps, pe;
-        if constexpr (PF) {
-          ps = ps_n;
-          pe = pe_n;
-          w = next_window(w);
-          if (w < nwin) load_rp(w, ps_n, pe_n);
-        } else {
-          load_rp(cw, ps, pe);
-          w = next_window(w);
-        }
-        const int wr = cw * CB_WIN;
-        const int we = wr + CB_WIN < nrows ? wr + CB_WIN : nrows;
+        const int32_t ps = rp[r0 + rr];
+        const int32_t pe = rp[r0 + (wr + pr < we ? wr + pr + 1 : we)];
         const int32_t e0 = __builtin_amdgcn_readfirstlane(ps);
         const int len = __builtin_amdgcn_readlane(pe, 2 * (we - wr - 1)) - e0;
         const int rs = ps - e0, re = pe - e0;
@@ -915,8 +876,6 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
           tacc[lr * 2 + sub] = zero;
         }
       }
-      // DYN: the next layer's first phase may hand these windows to other waves
-      if (DYN && k + 1 < a.K) __syncthreads();
     }
   }
 }
@@ -1101,24 +1060,8 @@ extern "C" hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, int rpw, hip
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
       return e && e[0] == '1';
     }();
-    static const int sched = [] {  // A/B: 1 windows from a per-phase counter, 2 rp prefetch
-      const char* e = getenv("N2V2R_FLAT_SCHED");
-      const int v = e ? atoi(e) : 0;
-      for (const void* f : {(const void*)spmm8_flat_kernel<false, true, 1>,
-                            (const void*)spmm8_flat_kernel<false, true, 2>,
-                            (const void*)spmm8_flat_kernel<false, true, 3>})
-        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-      (void)hipGetLastError();
-      return v >= 0 && v <= 3 ? v : 0;
-    }();
     if (nofold)
       hipLaunchKernelGGL((spmm8_flat_kernel<false, false>), dim3(grid), dim3(1024), flds, stream, a);
-    else if (sched == 1)
-      hipLaunchKernelGGL((spmm8_flat_kernel<false, true, 1>), dim3(grid), dim3(1024), flds, stream, a);
-    else if (sched == 2)
-      hipLaunchKernelGGL((spmm8_flat_kernel<false, true, 2>), dim3(grid), dim3(1024), flds, stream, a);
-    else if (sched == 3)
-      hipLaunchKernelGGL((spmm8_flat_kernel<false, true, 3>), dim3(grid), dim3(1024), flds, stream, a);
     else if (ntl)
       hipLaunchKernelGGL(spmm8_flat_kernel<true>, dim3(grid), dim3(1024), flds, stream, a);
     else

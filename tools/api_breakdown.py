@@ -1,7 +1,7 @@
 """Where the drop-in API's time goes at a config (GPU): layer conversion + upload + GPU ingest,
 the first fit (column-block build included) vs a refit, ranking, frames, Borda of the frames.
 
-    python tools/api_breakdown.py [--config cfg4|cfg2]
+    python tools/api_breakdown.py [--config cfg4|cfg2|cfg3]
 """
 from __future__ import annotations
 
@@ -22,6 +22,7 @@ from node2vec2rank_amd.model import N2V2R, _as_layer  # noqa: E402
 CONFIGS = {
     "cfg2": dict(n=100_000, avg_deg=20.0, dims=[64]),
     "cfg4": dict(n=1_000_000, avg_deg=50.0, dims=[8, 16, 32, 64, 128]),
+    "cfg3": dict(n=20_000, dense_layers=4, dims=[256]),
 }
 
 
@@ -30,7 +31,10 @@ def main():
     ap.add_argument("--config", default="cfg4", choices=sorted(CONFIGS))
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
-    layers = synthetic.er_layers(cfg["n"], cfg["avg_deg"], 2, seed_base=1000)
+    if cfg.get("dense_layers"):
+        layers = synthetic.corr_layers(cfg["n"], cfg["dense_layers"], seed_base=0)
+    else:
+        layers = synthetic.er_layers(cfg["n"], cfg["avg_deg"], 2, seed_base=1000)
     nodes = [f"n{i}" for i in range(cfg["n"])]
     config = dict(embed_dimensions=cfg["dims"], distance_metrics=["cosine", "euclidean"],
                   comp_strategy="sequential", seed=42, verbose=-1)
@@ -40,6 +44,10 @@ def main():
         t0 = time.perf_counter()
         conv = [_as_layer(g) for g in layers]
         t["as_layer"] = time.perf_counter() - t0
+        if cfg.get("dense_layers"):
+            t0 = time.perf_counter()
+            _lib._denser_than_quarter(np.asarray(conv[0]))
+            t["density_test_one_layer"] = time.perf_counter() - t0
         eng = _lib.Engine(0)
         t0 = time.perf_counter()
         eng.set_layers(conv)
