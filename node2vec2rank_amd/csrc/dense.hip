@@ -708,6 +708,151 @@ extern "C" hipError_t n2v2r_launch_ts_tn_zsum(const BlockList& A, int64_t n, con
   return launch_ts_tn(A, B, n, partial, partial_elems, out, nullptr, &zs, stream);
 }
 
+// ---- paired full passes (deferred reorthogonalisation, engine.cpp Eig::pair_pass) ----------
+// Two right-hand sides in one read of the basis: out = [A]^T [Za Zb] as two Gram arrays,
+// out[r][blk][64] (r = 0: Za, 1: Zb), each block's 8 x 8 in the layout of ts_tn_stream_kernel
+// (row-major (blk * 8 + i, j)).  Same streaming form: one wave per (basis block, row chunk), a
+// lane owns 4 columns of its block over rows rl, rl + 32, ..., fp32 products of at most
+// TS_MAX_CHUNK / 32 rows per lane, then a fixed fp64 reduce-scatter over the 32 row lanes.
+template <int TS_U>
+__global__ __launch_bounds__(256) void ts_tn_stream2_kernel(BlockList A, const float* __restrict__ Za,
+                                                            const float* __restrict__ Zb, int64_t n,
+                                                            int64_t rows_per_chunk,
+                                                            double* __restrict__ partial) {
+  const int lane = threadIdx.x & 63;
+  const int blk = (int)blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (blk >= A.count) return;  // wave-uniform; no block barrier below
+  const int h = lane >> 5, rl = lane & 31;
+  const float* ab = A.blk[blk] + 4 * h;
+  const int64_t c0 = (int64_t)blockIdx.x * rows_per_chunk;
+  int64_t c1 = c0 + rows_per_chunk;
+  if (c1 > n) c1 = n;
+  float acc[4][16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
+  auto fma_row = [&](const f32x4& a, const f32x4& y0, const f32x4& y1, const f32x4& y2,
+                     const f32x4& y3) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[i][j] += a[i] * y0[j];
+        acc[i][4 + j] += a[i] * y1[j];
+        acc[i][8 + j] += a[i] * y2[j];
+        acc[i][12 + j] += a[i] * y3[j];
+      }
+  };
+  int64_t r = c0;
+  for (; r + 32 * TS_U <= c1; r += 32 * TS_U) {
+    f32x4 a[TS_U], y0[TS_U], y1[TS_U], y2[TS_U], y3[TS_U];
+#pragma unroll
+    for (int u = 0; u < TS_U; ++u) {
+      const int64_t rr = r + 32 * u + rl;
+      a[u] = *reinterpret_cast<const f32x4*>(ab + rr * 8);
+      y0[u] = *reinterpret_cast<const f32x4*>(Za + rr * 8);
+      y1[u] = *reinterpret_cast<const f32x4*>(Za + rr * 8 + 4);
+      y2[u] = *reinterpret_cast<const f32x4*>(Zb + rr * 8);
+      y3[u] = *reinterpret_cast<const f32x4*>(Zb + rr * 8 + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < TS_U; ++u) fma_row(a[u], y0[u], y1[u], y2[u], y3[u]);
+  }
+  for (; r < c1; r += 32) {
+    const int64_t rr = r + rl;
+    if (rr < c1) {
+      const f32x4 a1 = *reinterpret_cast<const f32x4*>(ab + rr * 8);
+      fma_row(a1, *reinterpret_cast<const f32x4*>(Za + rr * 8),
+              *reinterpret_cast<const f32x4*>(Za + rr * 8 + 4),
+              *reinterpret_cast<const f32x4*>(Zb + rr * 8),
+              *reinterpret_cast<const f32x4*>(Zb + rr * 8 + 4));
+    }
+  }
+  double v[64];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[i * 16 + j] = (double)acc[i][j];
+  rs_step<0, 32>(v, rl);
+  rs_step<1, 16>(v, rl);
+  rs_step<2, 8>(v, rl);
+  rs_step<3, 4>(v, rl);
+  rs_step<4, 2>(v, rl);
+  // lane rl now holds entries e = (bitrev5(rl) << 1) | t (t = 0, 1) of its column half:
+  // e = i * 16 + j, i = row 4h + i of the block, j < 8: Za column j, else Zb column j - 8
+  const int eb = (((rl & 1) << 4) | ((rl & 2) << 2) | (rl & 4) | ((rl & 8) >> 2) | ((rl & 16) >> 4)) << 1;
+  double* out = partial + (int64_t)blockIdx.x * ((int64_t)A.count * 128);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int e = eb | t, i = e >> 4, j = e & 15;
+    out[((int64_t)(j >> 3) * A.count + blk) * 64 + (4 * h + i) * 8 + (j & 7)] = v[t];
+  }
+}
+
+// out[2][A.count][64] = [A]^T [Za Zb] (fp64, rows over ranks NOT summed here)
+extern "C" hipError_t n2v2r_launch_ts_tn2(const BlockList& A, const float* Za, const float* Zb,
+                                          int64_t n, double* partial, size_t partial_elems,
+                                          double* out, hipStream_t stream) {
+  if (A.width != 8 || A.count < 1 || n < 1) return hipErrorInvalidValue;
+  const int64_t elems = (int64_t)A.count * 128;
+  int64_t s_chunks = (tn_stream_waves() + A.count - 1) / A.count;
+  const int64_t lo = (n + TS_MAX_CHUNK - 1) / TS_MAX_CHUNK,
+                hi = (n + tn_stream_min_rows() - 1) / tn_stream_min_rows();
+  if (s_chunks > hi) s_chunks = hi;
+  if (s_chunks < lo) s_chunks = lo;
+  s_chunks = (s_chunks + 7) & ~(int64_t)7;
+  const int64_t s_rows = ((n + s_chunks - 1) / s_chunks + 31) & ~(int64_t)31;
+  s_chunks = (n + s_rows - 1) / s_rows;
+  if ((size_t)(s_chunks * elems) > partial_elems || s_rows > TS_MAX_CHUNK) return hipErrorNotSupported;
+  const dim3 grid((unsigned)s_chunks, (unsigned)((A.count + 3) / 4));
+  hipLaunchKernelGGL((ts_tn_stream2_kernel<2>), grid, dim3(256), 0, stream, A, Za, Zb, n, s_rows,
+                     partial);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return launch_reduce(partial, s_chunks, elems, out, nullptr, stream);
+}
+
+// The second pass of a pair: Zb's Gram against the CORRECTED Za' = (Za - Q Ca) Ra^{-1} from
+// the pair's Gram, D = Za'^T Zb = Ra^{-T} (Za^T Zb - Ca^T Cb) (Ca, Cb: the old blocks' rows of
+// the two Grams, all of them: rows a selective pass skipped are below its threshold, so their
+// products are below the threshold squared), written over Za's rows of Zb's Gram.  Ra: the
+// first pass's R (rsave; identity when that pass applied nothing) -- reset to the identity here
+// for the next pair.  One 64-thread workgroup, thread = (i, j).
+__global__ __launch_bounds__(64) void pair_fixup_kernel(double* __restrict__ g2, int nblk_all,
+                                                        int nq_old, double* __restrict__ ra) {
+  __shared__ double dr[64], rr[64];
+  const int t = threadIdx.x, i = t >> 3, j = t & 7;
+  const double* ga = g2;                          // [nblk_all][64]: Za's Gram
+  double* gb = g2 + (int64_t)nblk_all * 64;       // Zb's Gram
+  double s = gb[(int64_t)nq_old * 64 + i * 8 + j];  // Za^T Zb (row i of Za, column j of Zb)
+  for (int r = 0; r < nq_old * 8; ++r) s -= ga[(int64_t)r * 8 + i] * gb[(int64_t)r * 8 + j];
+  dr[t] = s;
+  rr[t] = ra[t];
+  __syncthreads();
+  if (t < 8) {  // column t: forward substitution Ra^T d = dr (Ra upper triangular)
+    double d[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      double v = dr[k * 8 + t];
+#pragma unroll
+      for (int m = 0; m < k; ++m) v -= rr[m * 8 + k] * d[m];
+      d[k] = v / rr[k * 8 + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) gb[(int64_t)nq_old * 64 + k * 8 + t] = d[k];
+  }
+  __syncthreads();
+  ra[t] = i == j ? 1.0 : 0.0;
+}
+
+extern "C" hipError_t n2v2r_launch_pair_fixup(double* g2, int nblk_all, int nq_old, double* ra,
+                                              hipStream_t stream) {
+  if (nq_old < 0 || nblk_all < nq_old + 2) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pair_fixup_kernel, dim3(1), dim3(64), 0, stream, g2, nblk_all, nq_old, ra);
+  return hipGetLastError();
+}
+
 // out = sum of `count` partial panels (fixed order), n x 8 fp32
 __global__ void zsum_kernel(ZSum zs, int64_t n) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one half row (16 B)

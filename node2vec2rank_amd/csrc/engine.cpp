@@ -98,6 +98,11 @@ static bool pip_fused() {
   }();
   return v;
 }
+hipError_t n2v2r_launch_ts_tn2(const BlockList& A, const float* Za, const float* Zb, int64_t n,
+                               double* partial, size_t partial_elems, double* out,
+                               hipStream_t stream);
+hipError_t n2v2r_launch_pair_fixup(double* g2, int nblk_all, int nq_old, double* ra,
+                                   hipStream_t stream);
 hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zin, float* Zout,
                                   const double* G, int c, int64_t n, const int* cond, int* flags,
                                   int* any_flag, double* save, int save_row0, int save_rows,
@@ -528,6 +533,7 @@ struct EigWorkspace {
   DevBuf cbpart;                              // [K][CB_NB][npad][8] column-block partials
   DevBuf dbgflag;                             // N2V2R_DEBUG_FINITE result flag
   DevBuf s2part;                              // [K][npad][8] XCD-split second-stage outputs
+  DevBuf g2, pair_ra;                         // paired full passes: the two Grams, R of the first
   DevBuf sturm;                               // Sturm Rayleigh-Ritz: assembled arrow + band
   DevBuf rres;                                // lean images: R of the restart projection
   DevBuf skipc;                               // full passes skipped (selective reorthogonalisation)
@@ -845,6 +851,13 @@ struct Eig {
   // selective reorthogonalisation: a full pass after the local one is skipped (in the fused
   // launch, by every workgroup alike) when max |Q^T z_j| <= reorth_tol ||z_j||
   float reorth_tol = 0.f;
+  // deferred full passes (N2V2R_REORTH_DEFER=1, lazy two-pass mode only): every other Krylov
+  // block goes to its SpMM after the local pass alone and gets its full pass together with the
+  // next block's (a pair shares one read of the old basis once a two-block Gram exists); its
+  // image keeps the uncorrected block, whose components along older blocks are removed from
+  // the next block by that block's full pass.  `deferred`: the block awaiting its full pass.
+  bool defer = false, pair_gram = true;  // N2V2R_REORTH_PAIR=0: the two passes one by one
+  float* deferred = nullptr;
   struct LeanRetry {};
   // Gram scratch of the orthogonalisation passes (the workspace's own, or the spec set while
   // the restart expansion is issued on the spec stream)
@@ -1347,6 +1360,57 @@ struct Eig {
     t_ortho += now_ms() - t0;
   }
 
+  // the deferred block's full pass against the blocks before it (its place in `basis`)
+  void flush_deferred(const std::vector<float*>& basis) {
+    if (!deferred) return;
+    const auto it = std::find(basis.begin(), basis.end(), deferred);
+    if (it == basis.end()) throw StatusFail{N2V2R_ERR_INTERNAL, "deferred block left the basis"};
+    const std::vector<float*> pre(basis.begin(), it);
+    const double t0 = now_ms();
+    if (!pre.empty())
+      pip_pass(deferred, pre, nullptr, flg_p + 64, any_p + 1, nullptr, nullptr, 0, 0, any_p + 3,
+               nullptr, reorth_tol);
+    t_ortho += now_ms() - t0;
+    deferred = nullptr;
+  }
+
+  // The full passes of the deferred block Za (the last block of `basis`) and of the new block
+  // Zb in one read of the old basis Q: G = [Q Za Zb]^T [Za Zb] (ts_tn_stream2), Za's selective
+  // pass against Q (its R kept), Zb's Gram against the corrected Za (pair_fixup), Zb's selective
+  // pass against [Q Za].  false when the two-block Gram does not apply (then the caller runs the
+  // two passes one after the other).
+  bool pair_pass(float* zb, const std::vector<float*>& basis) {
+    if (!deferred || basis.empty() || basis.back() != deferred) return false;
+    const int nq_old = (int)basis.size() - 1;
+    if (nq_old + 2 > N2V2R_MAX_BLOCKS || (nq_old + 1) * 8 > 512) return false;
+    std::vector<float*> all(basis);
+    all.push_back(zb);
+    h->ews.g2.ensure(sizeof(double) * 2 * (size_t)(nq_old + 2) * 64, st);
+    double* g2 = h->ews.g2.as<double>();
+    const double t0 = now_ms();
+    lds_poison();
+    const hipError_t e = n2v2r_launch_ts_tn2(blocks(all, 0, nq_old + 2), deferred, zb, n, part_p,
+                                             part_n, g2, st);
+    if (e == hipErrorNotSupported) return false;
+    if (e != hipSuccess) throw HipFail{e, "n2v2r_launch_ts_tn2"};
+    if (h->comm) h->allreduce_f64(g2, 2 * (size_t)(nq_old + 2) * 64);
+    double* ra = h->ews.pair_ra.as<double>();
+    int* skc = reorth_tol != 0.f ? h->ews.skipc.as<int>() : nullptr;
+    HIPCHK(n2v2r_launch_pip_fused(blocks(basis, 0, nq_old), deferred, deferred, g2, nq_old * b, n,
+                                  nullptr, flg_p + 64, any_p + 1, nullptr, 0, 0, any_p + 3,
+                                  seed ^ (0xABCDull + ++fill_counter), row0, ra, reorth_tol, skc,
+                                  st));
+    HIPCHK(n2v2r_launch_pair_fixup(g2, nq_old + 2, nq_old, ra, st));
+    HIPCHK(n2v2r_launch_pip_fused(blocks(basis, 0, nq_old + 1), zb, zb,
+                                  g2 + (size_t)(nq_old + 2) * 64, (nq_old + 1) * b, n, nullptr,
+                                  flg_p + 64, any_p + 1, nullptr, 0, 0, any_p + 3,
+                                  seed ^ (0xABCDull + ++fill_counter), row0, nullptr, reorth_tol,
+                                  skc, st));
+    t_ortho += now_ms() - t0;
+    deferred = nullptr;
+    return true;
+  }
+
   // blocks M Q[last] couples to: Q[last-1], Q[last]; for the first Krylov block of a cycle
   // (kry0: the start block, or the block E appended at a thick restart) every block before it
   // (the kept Ritz vectors X, whose residuals M X - X Theta lie in span(E))
@@ -1372,7 +1436,31 @@ struct Eig {
     double* save = (save_band && band_rr)
                        ? h->ews.hband.as<double>() + band_off((int)basis.size() - 1)
                        : nullptr;
-    orthonormalize(z, basis, w_from, &loc, save, lazy);  // reads W_from, writes z: no copy
+    if (defer && lazy && !full_first) {
+      // local pass; then either this block waits (its full pass with the next one) or the
+      // waiting block and this one get their full passes
+      const double t0 = now_ms();
+      lds_poison();
+      const bool lp = loc.size() < basis.size();
+      const std::vector<float*>& first = lp ? loc : basis;
+      const int nsave = save ? (int)loc.size() : 0;
+      pip_pass(z, first, nullptr, flg_p, any_p, w_from, nsave ? save : nullptr,
+               ((int)first.size() - nsave) * b, nsave * b);
+      t_ortho += now_ms() - t0;
+      if (deferred && pair_gram && pair_pass(z, basis)) {
+        // (both full passes done)
+      } else if (deferred) {
+        flush_deferred(basis);
+        const double t1 = now_ms();
+        pip_pass(z, basis, nullptr, flg_p + 64, any_p + 1, nullptr, nullptr, 0, 0, any_p + 3,
+                 nullptr, reorth_tol);
+        t_ortho += now_ms() - t1;
+      } else {
+        deferred = z;
+      }
+    } else {
+      orthonormalize(z, basis, w_from, &loc, save, lazy);  // reads W_from, writes z: no copy
+    }
     dbg(z, n * b, false, "orthonormalised Krylov block");
     float* w = take();
     apply_M(z, w);
@@ -1558,6 +1646,22 @@ struct Eig {
       const char* m = std::getenv("N2V2R_REORTH_MODE");  // "whole": all blocks or none
       if (m && m[0] == 'w') reorth_tol = -reorth_tol;
     }
+    {
+      const char* e = std::getenv("N2V2R_REORTH_DEFER");  // read per fit (A/B runs)
+      defer = e && e[0] == '1' && b == 8 && pip_fused();
+      deferred = nullptr;
+      const char* pg = std::getenv("N2V2R_REORTH_PAIR");
+      pair_gram = !(pg && pg[0] == '0');
+      if (defer) {  // R of the pair's first pass: the identity until a pass writes it
+        static const double eye[64] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0,
+                                       0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0,
+                                       0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0,
+                                       0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 1};
+        h->ews.pair_ra.ensure(sizeof(double) * 64, st);
+        HIPCHK(hipMemcpyAsync(h->ews.pair_ra.p, eye, sizeof(eye), hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));
+      }
+    }
     h->ews.skipc.ensure(sizeof(int) * 68);
     HIPCHK(hipMemsetAsync(h->ews.skipc.p, 0, sizeof(int) * 68, st));
     if (lean) h->ews.rres.ensure(sizeof(double) * 64);
@@ -1609,6 +1713,7 @@ struct Eig {
           W[W.size() - 2] = nullptr;
         }
       }
+      flush_deferred(Q);  // (deferred full passes) the cycle's last block
       const int nq = (int)Q.size();
       const int c = nq * b;
       for (int q = 0; q < pb; ++q) {
