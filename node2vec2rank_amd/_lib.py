@@ -535,18 +535,31 @@ def default_engine(device: int = 0) -> Engine:
 
 
 def _denser_than_quarter(a) -> bool:
-    """count_nonzero(a) > a.size // 4, counted in row blocks that stop as soon as the answer is
-    known (a dense co-expression layer is decided after a quarter of its entries)."""
+    """More than a quarter of the entries non-zero (the storage choice of ``set_layers``; dense
+    and CSR storage give the same products).  A strided sample of ~2M entries decides when its
+    density is clearly on one side of 1/4 (a dense co-expression layer: one pass over 1/200 of
+    it instead of a quarter of it, 0.12 s per 20k x 20k layer); otherwise the exact count, in row
+    blocks that stop as soon as the answer is known."""
+    if a.size == 0:
+        return False
     a2 = a.reshape(a.shape[0], -1) if a.ndim > 1 else a.reshape(1, -1)
+    rows, cols = a2.shape
+    stride = max(1, rows // max(1, (1 << 21) // max(1, cols)))
+    if stride > 1:
+        sample = a2[::stride]
+        p = np.count_nonzero(sample) / sample.size
+        if p > 0.3:
+            return True
+        if p < 0.2:
+            return False
     need = a.size // 4
-    rows = a2.shape[0]
-    step = max(1, (1 << 24) // max(1, a2.shape[1]))
+    step = max(1, (1 << 24) // max(1, cols))
     nz = 0
     for r in range(0, rows, step):
         nz += int(np.count_nonzero(a2[r:r + step]))
         if nz > need:
             return True
-        if nz + (rows - r - step) * a2.shape[1] <= need:
+        if nz + (rows - r - step) * cols <= need:
             return False
     return nz > need
 

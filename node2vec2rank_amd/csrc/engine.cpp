@@ -398,12 +398,6 @@ bool ensure_col_blocks(LayerDev& L, int64_t ncols, hipStream_t st, int nb = CB_N
   return L.cb.usable && (L.symmetric || L.cb_t.usable);
 }
 
-// ---- host -> HBM uploads ------------------------------------------------------------------
-#define STAGE_CHUNK (8u << 20)  // bytes per pinned staging buffer
-#define STAGE_WORKERS 8
-void h2d_staged(n2v2r_handle* h, void* dst, size_t dpitch, const void* src, size_t spitch,
-                size_t width, size_t rows, hipStream_t st);
-
 // ---- communicators ----------------------------------------------------------------------
 struct Comm {
   int rank = 0, world = 1;
@@ -563,15 +557,6 @@ struct n2v2r_handle {
     }
     pin_bytes = bytes;
   }
-  // host -> HBM uploads of large layers (h2d_staged): per worker thread two pinned staging
-  // buffers and a stream of its own, allocated on first use and kept with the handle
-  struct Stager {
-    void* buf[2] = {nullptr, nullptr};
-    hipStream_t st = nullptr;
-    hipEvent_t ev[2] = {nullptr, nullptr};
-  };
-  std::vector<Stager> stagers;
-  std::mutex stage_mu;
   std::string err;
   int K = 0;
   int64_t n = 0;        // global nodes
@@ -1648,7 +1633,9 @@ struct Eig {
     }
     {
       const char* e = std::getenv("N2V2R_REORTH_DEFER");  // read per fit (A/B runs)
-      defer = e && e[0] == '1' && b == 8 && pip_fused();
+      // lean images only: with every image kept, the Rayleigh-Ritz and the residuals read the
+      // images themselves, and a deferred block's image is the uncorrected block's
+      defer = e && e[0] == '1' && b == 8 && pip_fused() && lean;
       deferred = nullptr;
       const char* pg = std::getenv("N2V2R_REORTH_PAIR");
       pair_gram = !(pg && pg[0] == '0');
@@ -2230,87 +2217,6 @@ int n2v2r_dist_info(const n2v2r_handle* h, int* rank, int* world, int64_t* row0,
   return N2V2R_OK;
 }
 
-}  // extern "C"
-
-namespace {
-// Host rows (pageable: numpy arrays) -> device rows.  A pageable hipMemcpy runs at ~10 GB/s
-// here (the 6.4 GB of cfg3's dense layers: ~0.6 s of a 1.06 s API step); instead up to
-// STAGE_WORKERS host threads each copy chunks of <= STAGE_CHUNK bytes into their own pinned
-// buffers (two, alternating) and queue the DMA on their own stream, so host copies and
-// transfers of different chunks overlap.  Small uploads take the plain path.  Returns when
-// every byte has landed (the caller's stream `st` is synchronised first, so earlier work
-// reading the destination is done).
-void h2d_staged(n2v2r_handle* h, void* dst, size_t dpitch, const void* src, size_t spitch,
-                size_t width, size_t rows, hipStream_t st) {
-  const size_t total = width * rows;
-  if (total == 0) return;
-  if (rows == 1) dpitch = spitch = width;  // one contiguous range
-  const char* e = std::getenv("N2V2R_H2D_STAGED");
-  const bool off = e && e[0] == '0';
-  if (off || total < 4 * (size_t)STAGE_CHUNK || (rows > 1 && width > STAGE_CHUNK)) {
-    HIPCHK(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, hipMemcpyHostToDevice, st));
-    HIPCHK(hipStreamSynchronize(st));
-    return;
-  }
-  HIPCHK(hipStreamSynchronize(st));
-  // chunks: ranges of <= STAGE_CHUNK bytes (one row) or of whole rows (row-pitched copies)
-  const size_t crow = rows == 1 ? 0 : std::max<size_t>(1, STAGE_CHUNK / width);
-  const size_t nchunks = rows == 1 ? (total + STAGE_CHUNK - 1) / STAGE_CHUNK
-                                   : (rows + crow - 1) / crow;
-  const int nw = (int)std::min<size_t>(STAGE_WORKERS, nchunks);
-  std::lock_guard<std::mutex> lk(h->stage_mu);
-  while ((int)h->stagers.size() < nw) {
-    n2v2r_handle::Stager sg;
-    for (int i = 0; i < 2; ++i) {
-      if (hipHostMalloc(&sg.buf[i], STAGE_CHUNK, hipHostMallocDefault) != hipSuccess) {
-        (void)hipGetLastError();
-        throw std::bad_alloc();
-      }
-      HIPCHK(hipEventCreateWithFlags(&sg.ev[i], hipEventDisableTiming));
-    }
-    HIPCHK(hipStreamCreateWithFlags(&sg.st, hipStreamNonBlocking));
-    h->stagers.push_back(sg);
-  }
-  std::vector<hipError_t> errs(nw, hipSuccess);
-  std::vector<std::thread> th;
-  for (int w = 0; w < nw; ++w) {
-    th.emplace_back([&, w]() {
-      hipError_t r = hipSetDevice(h->device);
-      n2v2r_handle::Stager& sg = h->stagers[w];
-      int slot = 0;
-      for (size_t c = w; c < nchunks && r == hipSuccess; c += nw, slot ^= 1) {
-        // the DMA that last read this buffer must be done before it is refilled
-        r = hipEventSynchronize(sg.ev[slot]);
-        if (r != hipSuccess) break;
-        char* pb = static_cast<char*>(sg.buf[slot]);
-        if (rows == 1) {
-          const size_t b0 = c * (size_t)STAGE_CHUNK, nb = std::min<size_t>(STAGE_CHUNK, total - b0);
-          std::memcpy(pb, static_cast<const char*>(src) + b0, nb);
-          r = hipMemcpyAsync(static_cast<char*>(dst) + b0, pb, nb, hipMemcpyHostToDevice, sg.st);
-        } else {
-          const size_t r0 = c * crow, nr = std::min(crow, rows - r0);
-          const char* sp = static_cast<const char*>(src) + r0 * spitch;
-          if (spitch == width)
-            std::memcpy(pb, sp, nr * width);
-          else
-            for (size_t i = 0; i < nr; ++i) std::memcpy(pb + i * width, sp + i * spitch, width);
-          r = hipMemcpy2DAsync(static_cast<char*>(dst) + r0 * dpitch, dpitch, pb, width, width,
-                               nr, hipMemcpyHostToDevice, sg.st);
-        }
-        if (r == hipSuccess) r = hipEventRecord(sg.ev[slot], sg.st);
-      }
-      if (r == hipSuccess) r = hipStreamSynchronize(sg.st);
-      errs[w] = r;
-    });
-  }
-  for (auto& t : th) t.join();
-  for (hipError_t r : errs)
-    if (r != hipSuccess) throw HipFail{r, "h2d_staged"};
-}
-}  // namespace
-
-extern "C" {
-
 void n2v2r_destroy(n2v2r_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
@@ -2321,14 +2227,6 @@ void n2v2r_destroy(n2v2r_handle* h) {
     if (e) (void)hipEventDestroy(e);
   if (h->side) (void)hipStreamDestroy(h->side);
   if (h->pin) (void)hipHostFree(h->pin);
-  for (auto& sg : h->stagers) {
-    if (sg.st) (void)hipStreamSynchronize(sg.st);
-    for (int i = 0; i < 2; ++i) {
-      if (sg.buf[i]) (void)hipHostFree(sg.buf[i]);
-      if (sg.ev[i]) (void)hipEventDestroy(sg.ev[i]);
-    }
-    if (sg.st) (void)hipStreamDestroy(sg.st);
-  }
   for (hipEvent_t e : h->tev) (void)hipEventDestroy(e);
   if (h->cstream) (void)hipStreamSynchronize(h->cstream);
   for (hipEvent_t& e : h->cev)
@@ -2412,10 +2310,10 @@ int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const in
     dip.ensure(sizeof(int64_t) * (n + 1));
     dix.ensure(sizeof(int32_t) * std::max<int64_t>(nnz, 1));
     ddv.ensure(sizeof(float) * std::max<int64_t>(nnz, 1));
-    h2d_staged(h, dip.p, 0, indptr, 0, sizeof(int64_t) * (n + 1), 1, st);
+    HIPCHK(hipMemcpyAsync(dip.p, indptr, sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, st));
     if (nnz) {
-      h2d_staged(h, dix.p, 0, indices, 0, sizeof(int32_t) * nnz, 1, st);
-      h2d_staged(h, ddv.p, 0, data, 0, sizeof(float) * nnz, 1, st);
+      HIPCHK(hipMemcpyAsync(dix.p, indices, sizeof(int32_t) * nnz, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(ddv.p, data, sizeof(float) * nnz, hipMemcpyHostToDevice, st));
     }
     const bool need_t = symmetric != N2V2R_SYM_YES;
     DevBuf keys[2], pay[2], hist, flag;
@@ -2567,8 +2465,8 @@ int n2v2r_set_layer_dense(n2v2r_handle* h, int k, int64_t n, const float* A, int
     L.lda = (n + 63) / 64 * 64;
     const int64_t nl = std::max<int64_t>(h->nloc, 1);
     L.dA.ensure(sizeof(float) * nl * L.lda);
-    h2d_staged(h, L.dA.p, sizeof(float) * L.lda, A + h->row0 * n, sizeof(float) * n,
-               sizeof(float) * n, h->nloc, h->stream);
+    HIPCHK(hipMemcpy2D(L.dA.p, sizeof(float) * L.lda, A + h->row0 * n, sizeof(float) * n,
+                       sizeof(float) * n, h->nloc, hipMemcpyHostToDevice));
     bool sym = symmetric == N2V2R_SYM_YES;
     if (!sym) {
       // A^T rows [row0, row0 + nloc) = columns of A: a partitioned handle stages all of A once
@@ -2577,8 +2475,8 @@ int n2v2r_set_layer_dense(n2v2r_handle* h, int k, int64_t n, const float* A, int
       const float* src = L.dA.as<float>();
       if (h->comm) {
         full.ensure(sizeof(float) * n * L.lda);
-        h2d_staged(h, full.p, sizeof(float) * L.lda, A, sizeof(float) * n, sizeof(float) * n, n,
-                   h->stream);
+        HIPCHK(hipMemcpy2D(full.p, sizeof(float) * L.lda, A, sizeof(float) * n,
+                           sizeof(float) * n, n, hipMemcpyHostToDevice));
         src = full.as<float>();
       }
       L.dAT.ensure(sizeof(float) * nl * L.lda);
