@@ -818,38 +818,61 @@ extern "C" hipError_t n2v2r_launch_ts_tn2(const BlockList& A, const float* Za, c
 // the two Grams, all of them: rows a selective pass skipped are below its threshold, so their
 // products are below the threshold squared), written over Za's rows of Zb's Gram.  Ra: the
 // first pass's R (rsave; identity when that pass applied nothing) -- reset to the identity here
-// for the next pair.  One 64-thread workgroup, thread = (i, j).
-__global__ __launch_bounds__(64) void pair_fixup_kernel(double* __restrict__ g2, int nblk_all,
-                                                        int nq_old, double* __restrict__ ra) {
-  __shared__ double dr[64], rr[64];
-  const int t = threadIdx.x, i = t >> 3, j = t & 7;
+// for the next pair.  One 256-thread workgroup.
+__global__ __launch_bounds__(256) void pair_fixup_kernel(double* __restrict__ g2, int nblk_all,
+                                                         int nq_old, double* __restrict__ ra) {
+  // LDS: Ca rows | Cb rows (nq_old * 64 fp64 each), staged with all loads of a thread in flight
+  // (a thread-per-entry loop over global rows waited out one load per row: 35 us at cfg2)
+  extern __shared__ double fx[];
+  __shared__ double part[4][64], dr[64], rr[64];
+  const int tid = threadIdx.x;
+  const int nr8 = nq_old * 64;
   const double* ga = g2;                          // [nblk_all][64]: Za's Gram
   double* gb = g2 + (int64_t)nblk_all * 64;       // Zb's Gram
-  double s = gb[(int64_t)nq_old * 64 + i * 8 + j];  // Za^T Zb (row i of Za, column j of Zb)
-  for (int r = 0; r < nq_old * 8; ++r) s -= ga[(int64_t)r * 8 + i] * gb[(int64_t)r * 8 + j];
-  dr[t] = s;
-  rr[t] = ra[t];
+  if (nr8 > 0) {
+    stage_to_lds<256, 16>(fx, ga, nr8, tid);
+    stage_to_lds<256, 16>(fx + nr8, gb, nr8, tid);
+  }
+  if (tid < 64) rr[tid] = ra[tid];
   __syncthreads();
-  if (t < 8) {  // column t: forward substitution Ra^T d = dr (Ra upper triangular)
+  {
+    const int q = tid >> 6, e = tid & 63, i = e >> 3, j = e & 7;
+    double s = 0.0;
+    for (int r = q; r < nq_old * 8; r += 4) s += fx[r * 8 + i] * fx[nr8 + r * 8 + j];
+    part[q][e] = s;
+  }
+  __syncthreads();
+  if (tid < 64)  // Za^T Zb (row i of Za, column j of Zb) - Ca^T Cb, fixed order
+    dr[tid] = gb[(int64_t)nq_old * 64 + tid] - ((part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]));
+  __syncthreads();
+  if (tid < 8) {  // column tid: forward substitution Ra^T d = dr (Ra upper triangular)
     double d[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      double v = dr[k * 8 + t];
+      double v = dr[k * 8 + tid];
 #pragma unroll
       for (int m = 0; m < k; ++m) v -= rr[m * 8 + k] * d[m];
       d[k] = v / rr[k * 8 + k];
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) gb[(int64_t)nq_old * 64 + k * 8 + t] = d[k];
+    for (int k = 0; k < 8; ++k) gb[(int64_t)nq_old * 64 + k * 8 + tid] = d[k];
   }
-  __syncthreads();
-  ra[t] = i == j ? 1.0 : 0.0;
+  if (tid < 64) ra[tid] = (tid >> 3) == (tid & 7) ? 1.0 : 0.0;  // rr holds the copy in use
 }
 
 extern "C" hipError_t n2v2r_launch_pair_fixup(double* g2, int nblk_all, int nq_old, double* ra,
                                               hipStream_t stream) {
   if (nq_old < 0 || nblk_all < nq_old + 2) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pair_fixup_kernel, dim3(1), dim3(64), 0, stream, g2, nblk_all, nq_old, ra);
+  const size_t lds = sizeof(double) * 2 * (size_t)nq_old * 64;
+  if (lds > 120 * 1024) return hipErrorInvalidValue;
+  static const bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)pair_fixup_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
+    (void)hipGetLastError();
+    return true;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL(pair_fixup_kernel, dim3(1), dim3(256), lds, stream, g2, nblk_all, nq_old, ra);
   return hipGetLastError();
 }
 

@@ -836,7 +836,7 @@ struct Eig {
   // selective reorthogonalisation: a full pass after the local one is skipped (in the fused
   // launch, by every workgroup alike) when max |Q^T z_j| <= reorth_tol ||z_j||
   float reorth_tol = 0.f;
-  // deferred full passes (N2V2R_REORTH_DEFER=1, lazy two-pass mode only): every other Krylov
+  // deferred full passes (lean images, lazy two-pass mode; N2V2R_REORTH_DEFER=0: off): every other Krylov
   // block goes to its SpMM after the local pass alone and gets its full pass together with the
   // next block's (a pair shares one read of the old basis once a two-block Gram exists); its
   // image keeps the uncorrected block, whose components along older blocks are removed from
@@ -1635,7 +1635,7 @@ struct Eig {
       const char* e = std::getenv("N2V2R_REORTH_DEFER");  // read per fit (A/B runs)
       // lean images only: with every image kept, the Rayleigh-Ritz and the residuals read the
       // images themselves, and a deferred block's image is the uncorrected block's
-      defer = e && e[0] == '1' && b == 8 && pip_fused() && lean;
+      defer = !(e && e[0] == '0') && b == 8 && pip_fused() && lean;
       deferred = nullptr;
       const char* pg = std::getenv("N2V2R_REORTH_PAIR");
       pair_gram = !(pg && pg[0] == '0');
