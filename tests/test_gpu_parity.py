@@ -405,6 +405,32 @@ def test_uase_residuals_er_20k(engine):
     np.testing.assert_allclose(s, s_ref, rtol=1e-5)
 
 
+@pytest.mark.parametrize("defer", ["1", "0"])
+def test_uase_paired_full_passes(engine, monkeypatch, defer):
+    """Paired full passes (the default with lean images) against one full pass per block
+    (N2V2R_REORTH_DEFER=0): both meet the residual bar recomputed on the host, keep U
+    orthonormal, and agree on sigma; the pairing changes neither the block applications nor the
+    cycles by more than one cycle's worth."""
+    from node2vec2rank_amd import synthetic
+    layers = synthetic.er_layers(30_000, 16, 2, seed_base=31)
+    d = 48
+    engine.set_layers(layers)
+    monkeypatch.setenv("N2V2R_REORTH_DEFER", "0")
+    st0 = engine.uase(d, seed=7)
+    s0 = engine.singular_values()
+    monkeypatch.setenv("N2V2R_REORTH_DEFER", defer)
+    st = engine.uase(d, seed=7)
+    assert st["converged"] == d, st
+    s = engine.singular_values()
+    np.testing.assert_allclose(s, s0, rtol=1e-5)
+    X = engine.left_embedding().astype(np.float64) / np.sqrt(s)[None, :]
+    A = sp.hstack(layers).tocsr().astype(np.float64)
+    res = np.linalg.norm(A @ (A.T @ X) - X * (s ** 2)[None, :], axis=0) / s[0] ** 2
+    assert res.max() < 5e-6, res.max()
+    np.testing.assert_allclose(X.T @ X, np.eye(d), atol=1e-5)
+    assert abs(st["block_applications"] - st0["block_applications"]) <= 48, (st, st0)
+
+
 @pytest.mark.parametrize("name", ["er_cfg1", "directed_weighted", "demo"])
 def test_uase_column_blocks_golden(engine, name, monkeypatch):
     """The XCD-local column-block SpMM (forced on at fixture size; by default it runs for
