@@ -1370,7 +1370,9 @@ struct Eig {
     if (nq_old + 2 > N2V2R_MAX_BLOCKS || (nq_old + 1) * 8 > 512) return false;
     std::vector<float*> all(basis);
     all.push_back(zb);
-    h->ews.g2.ensure(sizeof(double) * 2 * (size_t)(nq_old + 2) * 64, st);
+    // sized for the largest basis when the fit starts (a growing buffer reallocated here cost a
+    // device-wide synchronisation per pair in a fit's first cycle: cfg2 +1.5 ms per fit)
+    if (h->ews.g2.bytes < sizeof(double) * 2 * (size_t)(nq_old + 2) * 64) return false;
     double* g2 = h->ews.g2.as<double>();
     const double t0 = now_ms();
     lds_poison();
@@ -1639,7 +1641,9 @@ struct Eig {
       deferred = nullptr;
       const char* pg = std::getenv("N2V2R_REORTH_PAIR");
       pair_gram = !(pg && pg[0] == '0');
-      if (defer) {  // R of the pair's first pass: the identity until a pass writes it
+      if (defer) {
+        h->ews.g2.ensure(sizeof(double) * 2 * (size_t)(nb_max + 2) * 64, st);
+        // R of the pair's first pass: the identity until a pass writes it
         static const double eye[64] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0,
                                        0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0,
                                        0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0,
