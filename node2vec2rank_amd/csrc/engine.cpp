@@ -844,8 +844,7 @@ struct Eig {
   bool defer = false, pair_gram = true;  // N2V2R_REORTH_PAIR=0: the two passes one by one
   float* deferred = nullptr;
   struct LeanRetry {};
-  // Gram scratch of the orthogonalisation passes (the workspace's own, or the spec set while
-  // the restart expansion is issued on the spec stream)
+  // Gram scratch of the orthogonalisation passes (the workspace's)
   double* part_p = nullptr;
   size_t part_n = 0;
   double* gsm_p = nullptr;
@@ -1612,9 +1611,6 @@ struct Eig {
     gsm_p = h->ews.gsmall.as<double>();
     flg_p = h->ews.flg.as<int>();
     any_p = h->ews.anyflag.as<int>();
-    // the restart expansion (orth(W_last) against the old basis, then its SpMM) needs nothing
-    // from the Rayleigh-Ritz stage: issue it on the spec stream beside the stage (one GPU,
-    // banded Rayleigh-Ritz; N2V2R_RESTART_OVERLAP=0 keeps it in line)
     // Lean images on a partitioned handle too: every quantity they read back (R of the restart
     // projection, the Ritz values and coefficients, the true residuals) is all-reduced first,
     // so every rank takes the same decisions.
