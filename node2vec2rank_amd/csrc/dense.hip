@@ -769,24 +769,24 @@ __global__ __launch_bounds__(256) void ts_tn_stream2_kernel(BlockList A, const f
               *reinterpret_cast<const f32x4*>(Zb + rr * 8 + 4));
     }
   }
-  double v[64];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 16; ++j) v[i * 16 + j] = (double)acc[i][j];
-  rs_step<0, 32>(v, rl);
-  rs_step<1, 16>(v, rl);
-  rs_step<2, 8>(v, rl);
-  rs_step<3, 4>(v, rl);
-  rs_step<4, 2>(v, rl);
-  // lane rl now holds entries e = (bitrev5(rl) << 1) | t (t = 0, 1) of its column half:
-  // e = i * 16 + j, i = row 4h + i of the block, j < 8: Za column j, else Zb column j - 8
-  const int eb = (((rl & 1) << 4) | ((rl & 2) << 2) | (rl & 4) | ((rl & 8) >> 2) | ((rl & 16) >> 4)) << 1;
+  // one right-hand side at a time through the fixed fp64 reduce-scatter (as ts_tn_stream_kernel:
+  // lane rl ends with entry bitrev5(rl) = (i, j) of its column half), so only 32 fp64 values are
+  // live at once (a 64-value fold held 144 VGPRs: 3 waves per SIMD)
+  const int e = ((rl & 1) << 4) | ((rl & 2) << 2) | (rl & 4) | ((rl & 8) >> 2) | ((rl & 16) >> 4);
   double* out = partial + (int64_t)blockIdx.x * ((int64_t)A.count * 128);
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int e = eb | t, i = e >> 4, j = e & 15;
-    out[((int64_t)(j >> 3) * A.count + blk) * 64 + (4 * h + i) * 8 + (j & 7)] = v[t];
+  for (int r = 0; r < 2; ++r) {
+    double v[32];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i * 8 + j] = (double)acc[i][8 * r + j];
+    rs_step<0, 16>(v, rl);
+    rs_step<1, 8>(v, rl);
+    rs_step<2, 4>(v, rl);
+    rs_step<3, 2>(v, rl);
+    rs_step<4, 1>(v, rl);
+    out[((int64_t)r * A.count + blk) * 64 + 32 * h + e] = v[0];
   }
 }
 

@@ -1535,10 +1535,12 @@ struct Eig {
       // blocks 0.817; 4 MB blocks left 31 % of the gathers missing L2).  Row-group forms: 8
       // (their rows get shorter with every block: cfg4 0.807 ms at 8, 0.923 at 16).
       const char* tn_ = std::getenv("N2V2R_SPMM_TILE_NB");
+      // (at most 32 by default: cfg5's 320 MB panel ran 9.47 ms per stage launch at 32 blocks
+      // of 10 MB, 11.53 at 64 of 5 MB -- a window's run per block gets too short)
       int nb_auto = 8;
       if (tile_form == 1) {
         nb_auto = 4;
-        while (nb_auto < CB_MAX && (double)nglob * 32.0 / nb_auto > 2.0 * 1024 * 1024)
+        while (nb_auto < 32 && (double)nglob * 32.0 / nb_auto > 2.0 * 1024 * 1024)
           nb_auto *= 2;
       }
       tile_nb = tiled ? (tn_ ? std::atoi(tn_) : nb_auto) : CB_NB;
@@ -3255,7 +3257,7 @@ int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, con
 
 
 // The flat-window tiled SpMM of one layer at panel width b (8 or 16) with `nb` column blocks
-// (0: the fit's default rule, panel blocks of <= 2 MB), timed alone with HIP events.
+// (0: the fit's default rule, panel blocks of <= 2 MB, at most 32), timed alone with HIP events.
 int n2v2r_bench_spmm_tiled(n2v2r_handle* h, int k, int transpose, int b, int nb, int reps,
                            const float* X, float* Y, double* avg_ms) {
   return guarded(h, [&]() -> int {
@@ -3264,7 +3266,7 @@ int n2v2r_bench_spmm_tiled(n2v2r_handle* h, int k, int transpose, int b, int nb,
       return N2V2R_ERR_BAD_ARG;
     if (nb <= 0) {
       nb = 4;
-      while (nb < CB_MAX && (double)h->n * 4.0 * b / nb > 2.0 * 1024 * 1024) nb *= 2;
+      while (nb < 32 && (double)h->n * 4.0 * b / nb > 2.0 * 1024 * 1024) nb *= 2;
     }
     if (nb != 4 && nb != 8 && nb != 16 && nb != 32 && nb != 64) return N2V2R_ERR_BAD_ARG;
     LayerDev& L = *h->layers[k];
