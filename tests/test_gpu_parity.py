@@ -405,6 +405,28 @@ def test_uase_residuals_er_20k(engine):
     np.testing.assert_allclose(s, s_ref, rtol=1e-5)
 
 
+@pytest.mark.parametrize("b,nb", [(8, 0), (8, 32), (16, 0), (16, 64)])
+def test_spmm_tiled_flat_widths(engine, b, nb):
+    """The flat-window tiled SpMM at panel widths 8 and 16 (the b = 16 form is the probe behind
+    DESIGN §5's width measurement) against scipy, on a directed weighted layer (A and A^T) whose
+    panel spans 4-64 column blocks."""
+    from node2vec2rank_amd import synthetic
+    n = 300_000
+    A = synthetic.er_layers(n, 12, 1, seed_base=91)[0].tocsr().astype(np.float32)
+    rng = np.random.default_rng(3)
+    A = sp.triu(A, k=1, format="csr")                      # directed
+    A.data = rng.uniform(0.5, 2.0, A.nnz).astype(np.float32)  # weighted
+    engine.set_layers([A])
+    X = rng.standard_normal((n, b)).astype(np.float32)
+    rows = rng.choice(n, 3000, replace=False)
+    for tr in (False, True):
+        Y, ms = engine.bench_spmm_tiled(0, X, transpose=tr, nb=nb, reps=2)
+        M = (A.T if tr else A).tocsr()[rows].astype(np.float64)
+        ref = M @ X.astype(np.float64)
+        bound = 1e-5 * (abs(M) @ np.abs(X).astype(np.float64)) + 1e-6
+        assert np.all(np.abs(Y[rows] - ref) <= bound), (b, nb, tr)
+
+
 @pytest.mark.parametrize("defer", ["1", "0"])
 def test_uase_paired_full_passes(engine, monkeypatch, defer):
     """Paired full passes (the default with lean images) against one full pass per block

@@ -8,6 +8,8 @@ mkdir -p $O
 ( while true; do date +%T >> $O/heartbeat.txt; sleep 30; done ) &
 HB=$!
 trap "kill $HB" EXIT
+timeout -k 10 120 ./tools/graph_probe > $O/graph_probe.txt 2>&1 || { echo graph-probe-fail; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -q -rf --timeout 200 --timeout-method thread -p no:cacheprovider -k "tiled_flat_widths or paired" > $O/tests_new.log 2>&1 || { echo new-tests-failed; exit 1; }
 for v in 512 1024 512; do
   N2V2R_FLAT_WG=$v timeout -k 10 300 python -u tools/spmm16_probe.py --widths 8 > $O/probe_$v.$RANDOM.jsonl 2> $O/probe_$v.err || { echo probe-fail-$v; exit 1; }
 done
