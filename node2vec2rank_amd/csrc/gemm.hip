@@ -62,7 +62,7 @@ __device__ __forceinline__ void dg_store_a(float (*as)[DG_AP], const f32x4 (&v)[
 // X staged transposed, xs[column][k] (pitch DG_AP), so a lane reads its 8 consecutive k of a
 // 16-k group as two 16-B LDS reads like its A operands -- measured 0.40 vs 0.39 ms per cfg3
 // launch, not kept.
-template <int NT, bool XT, int PD = 1>
+template <int NT, bool XT>
 __global__ __launch_bounds__(256) void dense_gemm_kernel(const float* __restrict__ A, int64_t lda,
                                                          int64_t rows, int64_t kdim,
                                                          int64_t kper, const float* __restrict__ X,
@@ -143,21 +143,11 @@ __global__ __launch_bounds__(256) void dense_gemm_kernel(const float* __restrict
       }
     }
   };
-  if constexpr (PD == 1) {
-    f32x4 nxt[8];
-    if (k_begin < k_end) dg_load_a(A, lda, rows, tile_r0, k_begin, nxt);
-    for (int64_t k0 = k_begin; k0 < k_end; k0 += DG_KC) round(k0, nxt, k0 + DG_KC);
-  } else {
-    // two A tiles in flight: a round's loads have two rounds of MFMAs to land (one round's
-    // MFMAs, ~2k cycles per wave, is shorter than an HBM round trip under load)
-    f32x4 nb0[8], nb1[8];
-    if (k_begin < k_end) dg_load_a(A, lda, rows, tile_r0, k_begin, nb0);
-    if (k_begin + DG_KC < k_end) dg_load_a(A, lda, rows, tile_r0, k_begin + DG_KC, nb1);
-    for (int64_t k0 = k_begin; k0 < k_end; k0 += 2 * DG_KC) {
-      round(k0, nb0, k0 + 2 * DG_KC);
-      if (k0 + DG_KC < k_end) round(k0 + DG_KC, nb1, k0 + 3 * DG_KC);
-    }
-  }
+  // (two A tiles in flight -- a round's loads with two rounds of MFMAs to land -- measured
+  // 0.395 vs 0.394 ms per cfg3 launch: not kept)
+  f32x4 nxt[8];
+  if (k_begin < k_end) dg_load_a(A, lda, rows, tile_r0, k_begin, nxt);
+  for (int64_t k0 = k_begin; k0 < k_end; k0 += DG_KC) round(k0, nxt, k0 + DG_KC);
   if (r0 >= rows) return;
   float* o = out + (int64_t)blockIdx.y * slab;
 #pragma unroll
@@ -225,15 +215,8 @@ extern "C" hipError_t n2v2r_launch_dense_gemm(const float* A, int64_t lda, int64
 #define DG_LAUNCH(NT, XT)                                                                      \
   hipLaunchKernelGGL((dense_gemm_kernel<NT, XT>), grid, dim3(256), 0, stream, A, lda, rows, kdim, \
                      kper, X, ldx, b, dst, ldo, slab)
-  static const bool pd2 = [] {  // N2V2R_DG_PD=2: two A tiles in flight (A/B)
-    const char* s = getenv("N2V2R_DG_PD");
-    return s && s[0] == '2';
-  }();
   if (b <= 32) {
-    if (pd2)
-      hipLaunchKernelGGL((dense_gemm_kernel<1, false, 2>), grid, dim3(256), 0, stream, A, lda, rows,
-                         kdim, kper, X, ldx, b, dst, ldo, slab);
-    else if (xt) DG_LAUNCH(1, true);
+    if (xt) DG_LAUNCH(1, true);
     else DG_LAUNCH(1, false);
   } else {
     if (xt) DG_LAUNCH(2, true);

@@ -17,7 +17,6 @@
 #include "common.h"
 
 #include <cstdlib>
-#include <cstring>
 
 #include "spmm_args.h"
 
@@ -797,8 +796,8 @@ __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1)
   }
 }
 
-template <bool NTL, bool FOLD = true, int WG = 1024, int MINW = 8>
-__global__ __launch_bounds__(WG, MINW) void spmm8_flat_kernel(SpmmTileArgs a) {
+template <bool NTL, bool FOLD = true>
+__global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
   // [tile_rows][8] row accumulators, then a 1-KB staging slot per wave
   extern __shared__ float tacf[];
   const int lane = threadIdx.x & 63;
@@ -816,7 +815,8 @@ __global__ __launch_bounds__(WG, MINW) void spmm8_flat_kernel(SpmmTileArgs a) {
   // zero / write back by the same window -> wave map as the adds (no barrier needed).  Measured
   // and not kept (cfg4 layer launch 0.367 ms): windows handed out per phase from an LDS
   // counter (0.557 ms), the next window's row pointers loaded before the current window's
-  // entries (0.367 ms, flat)
+  // entries (0.367 ms, flat); 512-thread workgroups with half the tile rows, 4 per CU
+  // (0.448 ms)
   for (int w = wave; w < nwin; w += nwave) {
     const int lr = w * CB_WIN + pr;
     if (lr < nrows) tacc[lr * 2 + sub] = zero;
@@ -1061,27 +1061,6 @@ extern "C" hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, int rpw, hip
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
       return e && e[0] == '1';
     }();
-    // A/B (N2V2R_FLAT_WG=512): 512-thread workgroups with half the tile rows, 4 per CU (the
-    // same waves per CU, half as many behind each phase barrier)
-    static const bool wg512 = [] {
-      const char* e = getenv("N2V2R_FLAT_WG");
-      const bool v = e && strcmp(e, "512") == 0;
-      if (v) {
-        (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel<false, true, 512, 8>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
-        (void)hipGetLastError();
-      }
-      return v;
-    }();
-    if (wg512) {
-      SpmmTileArgs a2 = a;
-      const int tr = a.tile_rows / 2;
-      a2.tile_rows = tr < CB_WIN ? CB_WIN : tr / CB_WIN * CB_WIN;
-      const unsigned g2 = (unsigned)((a.n + a2.tile_rows - 1) / a2.tile_rows);
-      const size_t l2 = sizeof(float) * 8 * (size_t)a2.tile_rows + 8 * 1024;
-      hipLaunchKernelGGL((spmm8_flat_kernel<false, true, 512, 8>), dim3(g2), dim3(512), l2, stream, a2);
-      return hipGetLastError();
-    }
     if (nofold)
       hipLaunchKernelGGL((spmm8_flat_kernel<false, false>), dim3(grid), dim3(1024), flds, stream, a);
     else if (ntl)
