@@ -721,12 +721,17 @@ __global__ __launch_bounds__(256) void ts_tn_stream2_kernel(BlockList A, const f
                                                             double* __restrict__ partial) {
   const int lane = threadIdx.x & 63;
   const int blk = (int)blockIdx.y * 4 + (threadIdx.x >> 6);
-  if (blk >= A.count) return;  // wave-uniform; no block barrier below
+  // the 4 waves of a workgroup read the same rows of Za / Zb for 4 basis blocks: those rows are
+  // staged once through LDS (one 16-B piece per thread per 64 rows, double-buffered, one barrier
+  // per step) instead of every wave loading them (each lane a 64-B Z row per row step: 4x the
+  // block's own bytes through L1).  Waves past the last block stage and wait at the barriers.
+  const bool active = blk < A.count;
   const int h = lane >> 5, rl = lane & 31;
-  const float* ab = A.blk[blk] + 4 * h;
+  const float* ab = A.blk[active ? blk : 0] + 4 * h;
   const int64_t c0 = (int64_t)blockIdx.x * rows_per_chunk;
   int64_t c1 = c0 + rows_per_chunk;
   if (c1 > n) c1 = n;
+  __shared__ f32x4 zst[2][32 * TS_U * 4];
   float acc[4][16];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -744,21 +749,40 @@ __global__ __launch_bounds__(256) void ts_tn_stream2_kernel(BlockList A, const f
         acc[i][12 + j] += a[i] * y3[j];
       }
   };
+  static_assert(32 * TS_U * 4 == 256, "one staged 16-B piece per thread per row step");
   int64_t r = c0;
-  for (; r + 32 * TS_U <= c1; r += 32 * TS_U) {
-    f32x4 a[TS_U], y0[TS_U], y1[TS_U], y2[TS_U], y3[TS_U];
+  const int t = threadIdx.x, zr = t >> 2, zq = t & 3;  // staged row, 16-B quarter
+  const float* zsrc = (zq < 2 ? Za : Zb) + 4 * (zq & 1);
+  int buf = 0;
+  // the next step's A rows and Z piece are loaded before this step's products (one memory round
+  // trip in flight across the barrier and the FMAs)
+  f32x4 an[TS_U], zn = {0.f, 0.f, 0.f, 0.f};
+  auto load_step = [&](int64_t rs) {
+    if (active) {
 #pragma unroll
-    for (int u = 0; u < TS_U; ++u) {
-      const int64_t rr = r + 32 * u + rl;
-      a[u] = *reinterpret_cast<const f32x4*>(ab + rr * 8);
-      y0[u] = *reinterpret_cast<const f32x4*>(Za + rr * 8);
-      y1[u] = *reinterpret_cast<const f32x4*>(Za + rr * 8 + 4);
-      y2[u] = *reinterpret_cast<const f32x4*>(Zb + rr * 8);
-      y3[u] = *reinterpret_cast<const f32x4*>(Zb + rr * 8 + 4);
+      for (int u = 0; u < TS_U; ++u)
+        an[u] = *reinterpret_cast<const f32x4*>(ab + (rs + 32 * u + rl) * 8);
     }
+    zn = *reinterpret_cast<const f32x4*>(zsrc + (rs + zr) * 8);
+  };
+  if (r + 32 * TS_U <= c1) load_step(r);
+  for (; r + 32 * TS_U <= c1; r += 32 * TS_U, buf ^= 1) {
+    f32x4 a[TS_U];
 #pragma unroll
-    for (int u = 0; u < TS_U; ++u) fma_row(a[u], y0[u], y1[u], y2[u], y3[u]);
+    for (int u = 0; u < TS_U; ++u) a[u] = an[u];
+    zst[buf][t] = zn;
+    if (r + 64 * TS_U <= c1) load_step(r + 32 * TS_U);
+    __syncthreads();  // (readers of the other buffer all passed the previous barrier)
+    if (active) {
+#pragma unroll
+      for (int u = 0; u < TS_U; ++u) {
+        const int lr = 32 * u + rl;
+        fma_row(a[u], zst[buf][lr * 4], zst[buf][lr * 4 + 1], zst[buf][lr * 4 + 2],
+                zst[buf][lr * 4 + 3]);
+      }
+    }
   }
+  if (!active) return;  // past the last barrier
   for (; r < c1; r += 32) {
     const int64_t rr = r + rl;
     if (rr < c1) {
