@@ -540,6 +540,98 @@ __global__ __launch_bounds__(256) void ts_tn_stream_kernel(BlockList A, const fl
   out[(int64_t)blk * 64 + 32 * h + e] = v[0];
 }
 
+// The streaming Gram with Z's rows staged once per workgroup through LDS (the 4 waves of a
+// workgroup take 4 basis blocks over the same rows, so each used to load the same 32-B Z row
+// per lane and row step: twice the block's own bytes through L1).  Double-buffered, the next
+// step's A rows and Z piece in flight across the barrier; same products in the same order as
+// ts_tn_stream_kernel<TS_U, false> (bit-identical Grams).  N2V2R_TN_LDS=0: the unstaged form.
+template <int TS_U>
+__global__ __launch_bounds__(256) void ts_tn_stream_lds_kernel(BlockList A, const float* __restrict__ Bz,
+                                                               int64_t n, int64_t rows_per_chunk,
+                                                               double* __restrict__ partial,
+                                                               const int* cond) {
+  if (cond && *cond == 0) return;  // (uniform: before any barrier)
+  static_assert(32 * TS_U * 2 == 256, "one staged 16-B piece per thread per row step");
+  const int lane = threadIdx.x & 63;
+  const int blk = (int)blockIdx.y * 4 + (threadIdx.x >> 6);
+  const bool active = blk < A.count;
+  const int h = lane >> 5, rl = lane & 31;
+  const float* ab = A.blk[active ? blk : 0] + 4 * h;
+  const int64_t c0 = (int64_t)blockIdx.x * rows_per_chunk;
+  int64_t c1 = c0 + rows_per_chunk;
+  if (c1 > n) c1 = n;
+  __shared__ f32x4 zst[2][32 * TS_U * 2];
+  float acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
+  const int t = threadIdx.x, zr = t >> 1, zq = t & 1;
+  f32x4 an[TS_U], zn = {0.f, 0.f, 0.f, 0.f};
+  auto load_step = [&](int64_t rs) {
+    if (active) {
+#pragma unroll
+      for (int u = 0; u < TS_U; ++u)
+        an[u] = *reinterpret_cast<const f32x4*>(ab + (rs + 32 * u + rl) * 8);
+    }
+    zn = *reinterpret_cast<const f32x4*>(Bz + (rs + zr) * 8 + 4 * zq);
+  };
+  int64_t r = c0;
+  int buf = 0;
+  if (r + 32 * TS_U <= c1) load_step(r);
+  for (; r + 32 * TS_U <= c1; r += 32 * TS_U, buf ^= 1) {
+    f32x4 a[TS_U];
+#pragma unroll
+    for (int u = 0; u < TS_U; ++u) a[u] = an[u];
+    zst[buf][t] = zn;
+    if (r + 64 * TS_U <= c1) load_step(r + 32 * TS_U);
+    __syncthreads();  // (readers of the other buffer all passed the previous barrier)
+    if (active) {
+#pragma unroll
+      for (int u = 0; u < TS_U; ++u) {
+        const int lr = 32 * u + rl;
+        const f32x4 z0 = zst[buf][lr * 2], z1 = zst[buf][lr * 2 + 1];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[i][j] += a[u][i] * z0[j];
+            acc[i][4 + j] += a[u][i] * z1[j];
+          }
+      }
+    }
+  }
+  if (!active) return;  // past the last barrier
+  for (; r < c1; r += 32) {
+    const int64_t rr = r + rl;
+    if (rr < c1) {
+      const f32x4 y0 = *reinterpret_cast<const f32x4*>(Bz + rr * 8);
+      const f32x4 y1 = *reinterpret_cast<const f32x4*>(Bz + rr * 8 + 4);
+      const f32x4 a1 = *reinterpret_cast<const f32x4*>(ab + rr * 8);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[i][j] += a1[i] * y0[j];
+          acc[i][4 + j] += a1[i] * y1[j];
+        }
+    }
+  }
+  double v[32];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[i * 8 + j] = (double)acc[i][j];
+  rs_step<0, 16>(v, rl);
+  rs_step<1, 8>(v, rl);
+  rs_step<2, 4>(v, rl);
+  rs_step<3, 2>(v, rl);
+  rs_step<4, 1>(v, rl);
+  const int e = ((rl & 1) << 4) | ((rl & 2) << 2) | (rl & 4) | ((rl & 8) >> 2) | ((rl & 16) >> 4);
+  double* out = partial + (int64_t)blockIdx.x * ((int64_t)A.count * 8) * 8;
+  out[(int64_t)blk * 64 + 32 * h + e] = v[0];
+}
+
 // Gram-kernel selection for 8-wide blocks: streaming form unless N2V2R_TN_FORM=lines;
 // N2V2R_TN_WAVES overrides the streaming form's wave target (tuning runs)
 static bool tn_stream_form() {
@@ -561,6 +653,13 @@ static int64_t tn_stream_min_rows() {  // rows per chunk at least this (N2V2R_TN
     const char* s = getenv("N2V2R_TN_MINROWS");
     const int64_t r = s ? atoll(s) : 256;
     return r < 32 ? (int64_t)32 : (r > TS_MAX_CHUNK ? (int64_t)TS_MAX_CHUNK : r);
+  }();
+  return v;
+}
+static bool tn_lds() {  // N2V2R_TN_LDS=0: the streaming Gram without the LDS-staged Z rows
+  static const bool v = [] {
+    const char* s = getenv("N2V2R_TN_LDS");
+    return !(s && s[0] == '0');
   }();
   return v;
 }
@@ -601,6 +700,9 @@ static hipError_t launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n
     else if (tn_stream_u() == 8)
       hipLaunchKernelGGL((ts_tn_stream_kernel<8, false>), grid, dim3(256), 0, stream, A, B.blk[0],
                          n, rows_per_chunk, partial, cond, none);
+    else if (tn_lds())
+      hipLaunchKernelGGL((ts_tn_stream_lds_kernel<4>), grid, dim3(256), 0, stream, A, B.blk[0],
+                         n, rows_per_chunk, partial, cond);
     else
       hipLaunchKernelGGL((ts_tn_stream_kernel<4, false>), grid, dim3(256), 0, stream, A, B.blk[0],
                          n, rows_per_chunk, partial, cond, none);
