@@ -270,6 +270,26 @@ def roofline_from_stats(st, cfg, b):
     return out
 
 
+def run_guarded(fn, limit_s, on_timeout):
+    """fn() under a watchdog: if it has not returned after limit_s seconds, on_timeout() runs
+    (rank 0 prints the bench line there) and the process exits with status 0, so a stalled
+    optional leg cannot swallow the line already measured."""
+    def _fire():
+        try:
+            on_timeout()
+        finally:
+            sys.stdout.flush()
+            os._exit(0)
+
+    timer = threading.Timer(limit_s, _fire)
+    timer.daemon = True
+    timer.start()
+    try:
+        return fn()
+    finally:
+        timer.cancel()
+
+
 def strong_scaling(group, cfg, args, local, rank, world):
     """One graph of the bench's family row-partitioned over every rank (RCCL), timed like the
     main loop: per step each rank's CSR rows -> HBM, UASE, distances, Borda, tables to host."""
@@ -467,18 +487,14 @@ def main():
             if rank == 0:
                 result["partitioned_same_family"] = {"error": f"timed out after {limit:g} s"}
                 print(json.dumps(result), flush=True)
-            sys.stdout.flush()
-            os._exit(0)
 
-        timer = threading.Timer(limit, _expire)
-        timer.daemon = True
-        timer.start()
-        try:
-            strong = strong_scaling(group, cfg, args, local, rank, world)
-        except Exception as e:  # reported in the line; the weak-scaling value stands
-            strong = {"error": repr(e)[:300]}
-        timer.cancel()
-        result["partitioned_same_family"] = strong
+        def _leg():
+            try:
+                return strong_scaling(group, cfg, args, local, rank, world)
+            except Exception as e:  # reported in the line; the weak-scaling value stands
+                return {"error": repr(e)[:300]}
+
+        result["partitioned_same_family"] = run_guarded(_leg, limit, _expire)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         workers = max(1, min(16, os.cpu_count() or 1))
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample or CPU_SAMPLE[args.config],
