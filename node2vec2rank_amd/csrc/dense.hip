@@ -1930,9 +1930,14 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
   const int lane = tid & 63, h = lane & 1, ro = lane >> 1;
   const int64_t rbase = (int64_t)blockIdx.x * (128 * NU) + (tid >> 6) * (32 * NU) + ro;
   if (rbase >= n) return;
-  const bool ok1 = NU > 1 && rbase + 32 < n;
-  const int64_t rw[2] = {rbase, ok1 ? rbase + 32 : rbase};
-  float acc[2][8];
+  int64_t rw[NU];
+  bool okr[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    okr[u] = rbase + 32 * u < n;
+    rw[u] = okr[u] ? rbase + 32 * u : rbase;  // past the end: row rbase again, not stored
+  }
+  float acc[NU][8];
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
     const f32x4 z = *reinterpret_cast<const f32x4*>(Zin + rw[u] * 8 + 4 * h);
@@ -1944,7 +1949,7 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
   }
   int q = 0;
   for (; q + QB <= napply; q += QB) {  // QB blocks x NU rows (QB NU x 16-B loads) in flight
-    f32x4 a4[QB][2];
+    f32x4 a4[QB][NU];
     int bi[QB];
 #pragma unroll
     for (int b4 = 0; b4 < QB; ++b4) bi[b4] = __builtin_amdgcn_readfirstlane(blist[q + b4]);
@@ -1967,7 +1972,7 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
     }
   }
   for (; q < napply; ++q) {
-    f32x4 a4[2];
+    f32x4 a4[NU];
     const int bq = __builtin_amdgcn_readfirstlane(blist[q]);
 #pragma unroll
     for (int u = 0; u < NU; ++u) a4[u] = *reinterpret_cast<const f32x4*>(Q.blk[bq] + rw[u] * 8 + 4 * h);
@@ -1997,7 +2002,7 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
       for (int j = 0; j < 8; ++j) sum += (j <= jo) ? acc[u][j] * rv[j * 8 + jo] : 0.f;
       o[t] = ((bad >> jo) & 1) ? counter_normal(seed, (uint64_t)(row0 + rw[u]) * 64 + jo) : sum;
     }
-    if (u == 0 || ok1) *reinterpret_cast<f32x4*>(Zout + rw[u] * 8 + 4 * h) = f32x4{o[0], o[1], o[2], o[3]};
+    if (okr[u]) *reinterpret_cast<f32x4*>(Zout + rw[u] * 8 + 4 * h) = f32x4{o[0], o[1], o[2], o[3]};
   }
 }
 
@@ -2016,12 +2021,18 @@ extern "C" hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zi
     const char* s = getenv("N2V2R_PIP_QB");
     return s ? atoi(s) : 4;
   }();
-  // rows per workgroup: 256 (64 per wave); N2V2R_PIP_ROWS=128 halves them (cfg2 flat, cfg4
-  // +20 %: every workgroup stages the (c + 8) x 8 fp64 Gram, 33 KB at c = 512)
-  static const int rows = [] {
+  // rows per workgroup (64 or 128 per wave); 128 rows: cfg2 flat, cfg4 +20 % (every workgroup
+  // stages the (c + 8) x 8 fp64 Gram, 33 KB at c = 512)
+  // 512 rows per workgroup from N = 512k rows on (the per-workgroup prologue -- Gram staging,
+  // selective test, Cholesky -- amortised over twice the rows: cfg4 fit 1,632 vs 1,645 ms; at
+  // cfg2's 100k rows the 196 workgroups leave CUs idle: 34.0 vs 33.1 ms).  N2V2R_PIP_ROWS = 128,
+  // 256 or 512 forces one (A/B)
+  static const int rows_env = [] {
     const char* s = getenv("N2V2R_PIP_ROWS");
-    return (s && atoi(s) == 128) ? 128 : 256;
+    const int v = s ? atoi(s) : 0;
+    return v == 128 || v == 256 || v == 512 ? v : 0;
   }();
+  const int rows = rows_env ? rows_env : (n >= (int64_t)1 << 19 ? 512 : 256);
   static const int pip_stop = [] {  // timing probe only: phases after k skipped
     const char* s = getenv("N2V2R_PIP_STOP");
     return s ? atoi(s) : 0;
@@ -2033,6 +2044,8 @@ extern "C" hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zi
                      seed, row0, rsave, skip_tol, skipped, pip_stop)
   if (rows == 256) {
     if (qb == 8) PIP_LAUNCH(8, 2); else PIP_LAUNCH(4, 2);
+  } else if (rows == 512) {
+    PIP_LAUNCH(2, 4);
   } else {
     if (qb == 4) PIP_LAUNCH(4, 1); else PIP_LAUNCH(8, 1);
   }
