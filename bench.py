@@ -270,16 +270,20 @@ def roofline_from_stats(st, cfg, b):
     return out
 
 
+WATCHDOG_EXIT = 3
+
+
 def run_guarded(fn, limit_s, on_timeout):
     """fn() under a watchdog: if it has not returned after limit_s seconds, on_timeout() runs
-    (rank 0 prints the bench line there) and the process exits with status 0, so a stalled
-    optional leg cannot swallow the line already measured."""
+    (rank 0 prints the bench line there, with the leg marked as timed out) and the process exits
+    with status 3 (WATCHDOG_EXIT), so a stalled optional leg neither swallows the line already
+    measured nor passes for a clean run with callers that check the exit status."""
     def _fire():
         try:
             on_timeout()
         finally:
             sys.stdout.flush()
-            os._exit(0)
+            os._exit(WATCHDOG_EXIT)
 
     timer = threading.Timer(limit_s, _fire)
     timer.daemon = True
@@ -478,7 +482,7 @@ def main():
     # the weak-scaling value (N2V2R_BENCH_PARTITIONED=0 skips it).  A watchdog guards the
     # replicas line: if the partitioned leg has not finished in N2V2R_BENCH_PARTITIONED_S
     # seconds (default 300), rank 0 prints the line with the leg marked as timed out and every
-    # rank exits.
+    # rank exits with status WATCHDOG_EXIT.
     if (world > 1 and mode == "replicas" and not cfg.get("dense")
             and os.environ.get("N2V2R_BENCH_PARTITIONED", "1") != "0"):
         limit = float(os.environ.get("N2V2R_BENCH_PARTITIONED_S", "300"))

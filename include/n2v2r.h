@@ -16,6 +16,7 @@
  *       and borda_aggregate_parallel / _get_ranking           node2vec2rank/model_utils.py:22-36
  *   - n2v2r_pairwise_distances: host-array form of            node2vec2rank/model_utils.py:39
  *   - n2v2r_borda_columns:      host-array form of            node2vec2rank/model_utils.py:28
+ *   - n2v2r_borda_columns_ex:   + the tie order of            node2vec2rank/model.py:173-174
  *   - n2v2r_column_sums:        float32 column sums for       node2vec2rank/model.py:282-311
  */
 #ifndef N2V2R_H
@@ -178,6 +179,22 @@ int n2v2r_pairwise_distances(n2v2r_handle* h, const double* m1, const double* m2
 int n2v2r_borda_columns(n2v2r_handle* h, const double* D /* C*N column-major */, int64_t n,
                         int n_cols, int64_t* borda);
 int n2v2r_column_sums(n2v2r_handle* h, int k, float* out /* N */);
+/* n2v2r_borda_columns with the reference's tie order within the caller's reach
+ * (aggregate_transform, model.py:167-185).  The GPU sort is stable: equal values rank by
+ * ascending node index.  The reference sorts each column with pandas
+ * Series.sort_values(ascending=False) = numpy argsort(kind='quicksort') between two reversals
+ * (model.py:173-174), whose order of EQUAL values is implementation-defined (x86-simd-sort on
+ * AVX-512 hosts); on columns without exact ties every correct descending sort agrees.
+ *   tied (optional, n_cols int32 out): 1 where the column holds two equal non-NaN values
+ *     (-0 == +0), i.e. where its descending order is not unique; 0 elsewhere.
+ *   given_cols / given_orders (optional, n_given columns): columns whose descending order the
+ *     caller supplies (given_orders: n_given x n int32, row g = the node indices of column
+ *     given_cols[g] best first, a permutation of 0..n-1; N2V2R_ERR_BAD_ARG otherwise) instead of
+ *     the stable GPU order.  The Python front-end passes pandas' order for the tied columns only.
+ * n <= 2^31 - 1. */
+int n2v2r_borda_columns_ex(n2v2r_handle* h, const double* D /* C*N column-major */, int64_t n,
+                           int n_cols, const int32_t* given_cols, int n_given,
+                           const int32_t* given_orders, int64_t* borda, int32_t* tied);
 
 /* bipartite projection of a non-square layer (preprocessing_utils.py:16-32): out = W^T W
  * (n x n) when on_columns, else W W^T (m x m), for a host row-major m x n fp64 W; fp64

@@ -38,7 +38,8 @@ EXPORTED = [
     "n2v2r_set_num_layers", "n2v2r_set_layer_csr", "n2v2r_uase", "n2v2r_get_embedding",
     "n2v2r_get_left_embedding", "n2v2r_get_singular_values", "n2v2r_set_embedding",
     "n2v2r_rank", "n2v2r_get_distances", "n2v2r_get_borda", "n2v2r_rank_timing",
-    "n2v2r_pairwise_distances", "n2v2r_borda_columns", "n2v2r_column_sums",
+    "n2v2r_pairwise_distances", "n2v2r_borda_columns", "n2v2r_borda_columns_ex",
+    "n2v2r_column_sums",
     "n2v2r_synchronize", "n2v2r_bench_spmm", "n2v2r_bench_spmm_tiled", "n2v2r_spmm_col_blocks",
     "n2v2r_comm_unique_id", "n2v2r_create_rccl", "n2v2r_simgroup_create",
     "n2v2r_simgroup_destroy", "n2v2r_create_sim", "n2v2r_dist_info", "n2v2r_set_layer_csr_rows",
@@ -126,6 +127,8 @@ def load(path: str | None = None):
             "n2v2r_pairwise_distances": (_i, [_vp, _p(np.float64), _p(np.float64), _i64, _i, _i,
                                               _p(np.float64)]),
             "n2v2r_borda_columns": (_i, [_vp, _p(np.float64), _i64, _i, _p(np.int64)]),
+            "n2v2r_borda_columns_ex": (_i, [_vp, _p(np.float64), _i64, _i, _vp, _i, _vp,
+                                            _p(np.int64), _p(np.int32)]),
             "n2v2r_column_sums": (_i, [_vp, _i, _p(np.float32)]),
             "n2v2r_synchronize": (_i, [_vp]),
             "n2v2r_bench_spmm": (_i, [_vp, _i, _i, _i, _i, _p(np.float32), _vp,
@@ -428,13 +431,33 @@ class Engine:
                     "pairwise_distances")
         return out
 
-    def borda_columns(self, D):
-        """D: N x C float64 (one ranking column per column) -> int64 Borda in row order."""
+    def borda_columns(self, D, tie_order: str = "stable", return_tied: bool = False):
+        """D: N x C float64 (one ranking column per column) -> int64 Borda in row order.
+
+        tie_order "stable": every column sorted on the GPU, equal values by ascending row.
+        "reference": columns holding exact ties (flagged by the GPU) are ordered as the
+        reference orders them, pandas ``Series.sort_values(ascending=False)`` (numpy quicksort,
+        ``model.py:173-174``), whose order of equal values is implementation-defined, and their
+        positions go into the same GPU Borda; tie-free columns (every ER graph of BASELINE) are
+        never touched on the host.  return_tied: also return the per-column tie flags."""
+        if tie_order not in ("stable", "reference"):
+            raise ValueError(f"unknown tie_order {tie_order!r}")
         Dc = np.ascontiguousarray(np.asarray(D, dtype=np.float64).T)
         c, n = Dc.shape
         out = np.empty(n, dtype=np.int64)
-        self._check(self.lib.n2v2r_borda_columns(self.h, Dc, n, c, out), "borda_columns")
-        return out
+        tied = np.zeros(c, dtype=np.int32)
+        self._check(self.lib.n2v2r_borda_columns_ex(self.h, Dc, n, c, None, 0, None, out, tied),
+                    "borda_columns")
+        cols = np.flatnonzero(tied)
+        if tie_order == "reference" and cols.size:
+            orders = np.empty((cols.size, n), dtype=np.int32)
+            for g, j in enumerate(cols):
+                orders[g] = reference_descending_order(Dc[j])
+            gc = np.ascontiguousarray(cols, dtype=np.int32)
+            self._check(self.lib.n2v2r_borda_columns_ex(
+                self.h, Dc, n, c, gc.ctypes.data_as(_vp), int(cols.size),
+                orders.ctypes.data_as(_vp), out, tied), "borda_columns")
+        return (out, tied.astype(bool)) if return_tied else out
 
     def column_sums(self, k: int):
         out = np.empty(self.n, dtype=np.float32)
@@ -520,6 +543,17 @@ class Engine:
 
     def synchronize(self):
         self._check(self.lib.n2v2r_synchronize(self.h), "synchronize")
+
+
+def reference_descending_order(col) -> np.ndarray:
+    """Row indices of one ranking column best first, exactly as the reference sorts it:
+    ``pd.Series(col, index=node_names).sort_values(ascending=False)`` (``model.py:173-174``),
+    i.e. pandas ``nargsort``: reverse, ``argsort(kind='quicksort')``, reverse, NaNs last in row
+    order.  The order of equal values is whatever this host's numpy quicksort gives, as in the
+    reference; only columns the GPU flags as tied come here."""
+    import pandas as pd
+    return pd.Series(np.asarray(col, dtype=np.float64)).sort_values(
+        ascending=False).index.to_numpy(dtype=np.int64)
 
 
 _default = {}

@@ -140,6 +140,8 @@ hipError_t n2v2r_launch_radix_pass(const uint64_t* kin, const int32_t* pin, uint
                                    hipStream_t stream);
 hipError_t n2v2r_launch_borda_finish(const int32_t* sorted_idx, int64_t n, int nseg, int ncols,
                                      int32_t* pos, int64_t* borda, hipStream_t stream);
+hipError_t n2v2r_launch_tie_flags(const uint64_t* sorted_keys, int64_t n, int nseg, int32_t* tied,
+                                  hipStream_t stream);
 hipError_t n2v2r_launch_dense_gemm(const float* A, int64_t lda, int64_t rows, int64_t kdim,
                                    const float* X, int ldx, int b, float* Y, int64_t ldy,
                                    float beta, const float* colscale, float* work,
@@ -2759,8 +2761,16 @@ int n2v2r_set_embedding(n2v2r_handle* h, int num_layers, int64_t n, int d, const
   });
 }
 
+// Borda of nseg descending-sorted columns, ncols per output group.  tied_dev (optional): the
+// per-column exact-tie flags (n2v2r_launch_tie_flags).  given (optional): columns whose order the
+// caller supplies (device int32 permutations, best first) in place of the stable radix order.
+struct GivenOrder {
+  int col;
+  const int32_t* order_dev;
+};
 static void run_borda(n2v2r_handle* h, const double* Ddev, int64_t n, int nseg, int ncols,
-                      int64_t* borda_dev) {
+                      int64_t* borda_dev, int32_t* tied_dev = nullptr,
+                      const std::vector<GivenOrder>* given = nullptr) {
   hipStream_t st = h->stream;
   const size_t tot = (size_t)nseg * n;
   for (int i = 0; i < 2; ++i) {
@@ -2792,6 +2802,11 @@ static void run_borda(n2v2r_handle* h, const double* Ddev, int64_t n, int nseg, 
                                    h->rs_hist.as<uint32_t>(), st));
     cur ^= 1;
   }
+  if (tied_dev) HIPCHK(n2v2r_launch_tie_flags(h->rs_keys[cur].as<uint64_t>(), n, nseg, tied_dev, st));
+  if (given)
+    for (const GivenOrder& g : *given)
+      HIPCHK(hipMemcpyAsync(h->rs_idx[cur].as<int32_t>() + (size_t)g.col * n, g.order_dev,
+                            sizeof(int32_t) * n, hipMemcpyDeviceToDevice, st));
   HIPCHK(n2v2r_launch_borda_finish(h->rs_idx[cur].as<int32_t>(), n, nseg, ncols,
                                    h->rs_pos.as<int32_t>(), borda_dev, st));
 }
@@ -2959,6 +2974,57 @@ int n2v2r_borda_columns(n2v2r_handle* h, const double* D, int64_t n, int n_cols,
     HIPCHK(hipMemcpyAsync(dd.p, D, sizeof(double) * n * n_cols, hipMemcpyHostToDevice, h->stream));
     run_borda(h, dd.as<double>(), n, n_cols, n_cols, bo.as<int64_t>());
     HIPCHK(hipMemcpyAsync(borda, bo.p, sizeof(int64_t) * n, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return N2V2R_OK;
+  });
+}
+
+int n2v2r_borda_columns_ex(n2v2r_handle* h, const double* D, int64_t n, int n_cols,
+                           const int32_t* given_cols, int n_given, const int32_t* given_orders,
+                           int64_t* borda, int32_t* tied) {
+  return guarded(h, [&]() -> int {
+    if (n < 1 || n_cols < 1 || !D || !borda || n_given < 0 || n_given > n_cols ||
+        (n_given > 0 && (!given_cols || !given_orders)) || n > INT32_MAX)
+      return N2V2R_ERR_BAD_ARG;
+    // the caller's orders must be permutations of 0..n-1 of distinct columns (checked here: the
+    // GPU's inverse permutation scatters by them)
+    std::vector<char> seen_col(n_cols, 0), seen((size_t)n);
+    for (int g = 0; g < n_given; ++g) {
+      const int c = given_cols[g];
+      if (c < 0 || c >= n_cols || seen_col[c]) {
+        h->set_err("given column %d out of range or repeated", c);
+        return N2V2R_ERR_BAD_ARG;
+      }
+      seen_col[c] = 1;
+      std::fill(seen.begin(), seen.end(), 0);
+      const int32_t* o = given_orders + (size_t)g * n;
+      for (int64_t i = 0; i < n; ++i) {
+        if (o[i] < 0 || o[i] >= n || seen[o[i]]) {
+          h->set_err("given order of column %d is not a permutation of 0..n-1", c);
+          return N2V2R_ERR_BAD_ARG;
+        }
+        seen[o[i]] = 1;
+      }
+    }
+    DevBuf dd, bo, tf, go;
+    dd.ensure(sizeof(double) * n * n_cols);
+    bo.ensure(sizeof(int64_t) * n);
+    tf.ensure(sizeof(int32_t) * n_cols);
+    HIPCHK(hipMemcpyAsync(dd.p, D, sizeof(double) * n * n_cols, hipMemcpyHostToDevice, h->stream));
+    std::vector<GivenOrder> given;
+    if (n_given > 0) {
+      go.ensure(sizeof(int32_t) * (size_t)n_given * n);
+      HIPCHK(hipMemcpyAsync(go.p, given_orders, sizeof(int32_t) * (size_t)n_given * n,
+                            hipMemcpyHostToDevice, h->stream));
+      for (int g = 0; g < n_given; ++g)
+        given.push_back({given_cols[g], go.as<int32_t>() + (size_t)g * n});
+    }
+    run_borda(h, dd.as<double>(), n, n_cols, n_cols, bo.as<int64_t>(), tf.as<int32_t>(),
+              n_given > 0 ? &given : nullptr);
+    HIPCHK(hipMemcpyAsync(borda, bo.p, sizeof(int64_t) * n, hipMemcpyDeviceToHost, h->stream));
+    if (tied)
+      HIPCHK(hipMemcpyAsync(tied, tf.p, sizeof(int32_t) * n_cols, hipMemcpyDeviceToHost,
+                            h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     return N2V2R_OK;
   });

@@ -481,6 +481,30 @@ extern "C" hipError_t n2v2r_launch_radix_pass(const uint64_t* kin, const int32_t
   return hipGetLastError();
 }
 
+// tied[s] = 1 when the sorted keys of segment s hold two equal non-NaN keys (exact ties,
+// -0 == +0): the segment's descending order is then not unique, and the reference's order for
+// it is numpy quicksort's (model.py:173-174).  Lane 0 of a wave that saw one stores 1 (a plain
+// vector store: every writer stores the same value).
+__global__ __launch_bounds__(256) void tie_flag_kernel(const uint64_t* __restrict__ keys, int64_t n,
+                                                       int32_t* __restrict__ tied) {
+  const int s = blockIdx.y;
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool t = false;
+  if (j + 1 < n) {
+    const uint64_t a = keys[(int64_t)s * n + j];
+    t = a == keys[(int64_t)s * n + j + 1] && a != ~0ull;
+  }
+  if (__ballot(t) != 0ull && (threadIdx.x & 63) == 0) tied[s] = 1;
+}
+
+extern "C" hipError_t n2v2r_launch_tie_flags(const uint64_t* sorted_keys, int64_t n, int nseg,
+                                             int32_t* tied, hipStream_t stream) {
+  (void)hipMemsetAsync(tied, 0, sizeof(int32_t) * nseg, stream);
+  dim3 grid((unsigned)((n + 255) / 256), nseg);
+  hipLaunchKernelGGL(tie_flag_kernel, grid, dim3(256), 0, stream, sorted_keys, n, tied);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t n2v2r_launch_borda_finish(const int32_t* sorted_idx, int64_t n, int nseg,
                                                 int ncols, int32_t* pos, int64_t* borda,
                                                 hipStream_t stream) {

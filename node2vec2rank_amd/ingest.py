@@ -134,10 +134,9 @@ def transform(layer: Layer, threshold=None, top_percent_keep=100, binarize=False
     if m.nnz == 0:
         # the reference takes np.percentile of an empty array here and raises IndexError
         raise IndexError("network_transform: layer has no non-zero entries")
-    if True:
-        cut = _percentile_cut(m.data, 100 - top_percent_keep)
-        m.data[m.data < cut] = 0.0
-        m.eliminate_zeros()
+    cut = _percentile_cut(m.data, 100 - top_percent_keep)
+    m.data[m.data < cut] = 0.0
+    m.eliminate_zeros()
     if binarize:
         m.data[:] = 1.0
     return Layer(m.astype(np.float32), rows, cols)

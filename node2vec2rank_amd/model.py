@@ -8,8 +8,11 @@ embeddings, distances or Borda scores on the host.
 Differences a user can observe (documented in DESIGN.md):
   * embeddings come from a block Krylov-Schur solver instead of ARPACK, so they match the
     reference within the tolerance stated in tests (per-column signs are arbitrary there too);
-  * Borda ties (exactly equal distances) are broken by ascending node index (a stable sort);
-    the reference's order for ties depends on numpy's unstable quicksort.
+  * Borda ties (exactly equal distances): ``aggregate_transform`` orders a column that holds
+    exact ties as the reference does (pandas ``sort_values`` = numpy quicksort, model.py:173-174,
+    an implementation-defined order of equal values); the GPU flags such columns and sums their
+    positions.  ``tie_order="stable"`` (constructor) keeps the GPU's stable order instead:
+    equal values by ascending node index.  Tie-free columns are sorted on the GPU either way.
 """
 from __future__ import annotations
 
@@ -42,7 +45,7 @@ class N2V2R:
     """``N2V2R(graphs, nodes, config)`` (reference ``model.py:18``)."""
 
     def __init__(self, graphs: list, nodes: list, config: dict, device: int = 0,
-                 eig_options: dict | None = None):
+                 eig_options: dict | None = None, tie_order: str = "reference"):
         self.config = config
         self.node_names = nodes
         self.graphs = graphs
@@ -80,6 +83,9 @@ class N2V2R:
         # one engine per device, shared by every model of the process (its allocations and
         # solver workspace are reused across fits); the model that last loaded its layers owns it
         self._device = device
+        if tie_order not in ("reference", "stable"):
+            raise ValueError(f"unknown tie_order {tie_order!r}")
+        self.tie_order = tie_order
         self._eig_options = dict(eig_options or {})
         self._layers_loaded = False
         self._keys = None
@@ -218,7 +224,7 @@ class N2V2R:
             for key, df in self.pairwise_ranks.items():
                 if df.index is not idx and not df.index.equals(idx):
                     df = df.reindex(idx)
-                b = eng.borda_columns(df.to_numpy(dtype=np.float64))
+                b = eng.borda_columns(df.to_numpy(dtype=np.float64), tie_order=self.tie_order)
                 out[key] = pd.DataFrame(b, index=idx, columns=['borda_ranks'])
             self.pairwise_aggregate_ranks = out
             if self.config["verbose"] == 1:

@@ -39,7 +39,14 @@ def borda_aggregate_parallel(rankings: list):
 
 
 def signed_transform_single(ranks: pd.Series, prior_signed_ranks: pd.Series):
+    """``model_utils.py:7-19``: the nodes of ``ranks`` that the prior's index holds, in ``ranks``'
+    order, each rank kept where the prior's value is > 0 and negated otherwise (a NaN prior
+    fails ``> 0``: negated).  Negation, not a multiplication by -1, as the reference (``-rank``,
+    ``model_utils.py:17``): the two differ on a NaN rank's sign bit."""
     keep = ranks.index.isin(prior_signed_ranks.index)
     sub = ranks[keep]
-    sign = np.where(prior_signed_ranks.reindex(sub.index).to_numpy() > 0, 1, -1)
-    return pd.Series(sub.to_numpy() * sign, index=sub.index)
+    if len(sub) == 0:
+        return pd.Series([], index=[])  # the reference's pd.Series([], index=[])
+    pos = prior_signed_ranks.reindex(sub.index).to_numpy() > 0
+    vals = sub.to_numpy()
+    return pd.Series(np.where(pos, vals, -vals), index=sub.index)

@@ -190,6 +190,84 @@ def make_cfg2_env(_N2V2R=None):
     print(f"wrote {path}")
 
 
+def make_cfg4g(N2V2R):
+    """The bench's own grid (BASELINE cfg4: d in {8,16,32,64,128} x {cosine, euclidean}, 10
+    columns, sequential, seed 42) on a cfg4-family graph the reference can finish: 2-layer ER
+    N = 100k, avg-deg 50 (synthetic.er_layers(..., seed_base=1000), the generator bench.py
+    uses).  The reference model.py runs unchanged; the oracle must reproduce it bit-exactly.
+    Stored: sigma (128), the N x 10 distance table with its column names, the reference's
+    Borda (numpy quicksort ties) and the stable-order Borda.  Y and the layers are not stored
+    (the test regenerates the layers and checks the fingerprint)."""
+    import time
+
+    from node2vec2rank_amd import synthetic
+    from oracle import n2v2r_oracle as orc
+    n, deg, seed = 100_000, 50.0, 42
+    dims, metrics = [8, 16, 32, 64, 128], ["cosine", "euclidean"]
+    layers = synthetic.er_layers(n, deg, 2, seed_base=1000)
+    config = dict(embed_dimensions=dims, distance_metrics=metrics, seed=seed,
+                  comp_strategy="sequential", verbose=1, save_dir=None)
+    t0 = time.time()
+    model = N2V2R(graphs=[sp.csr_matrix(a) for a in layers], nodes=list(range(n)), config=config)
+    ranks = model.fit_transform_rank()
+    agg = model.aggregate_transform()
+    print(f"reference fit + rank + Borda: {time.time() - t0:.1f} s")
+    D = ranks["1"].to_numpy(dtype=np.float64)
+    b = agg["1"]["borda_ranks"].to_numpy(dtype=np.int64)
+    Yo, so, _ = orc.uase([sp.csc_matrix(g) for g in layers], 128, seed=seed)
+    assert np.array_equal(Yo, np.asarray(model.node_embeddings)), "cfg4g: oracle UASE differs"
+    oD = orc.rank_distances(Yo, dims, metrics, "sequential", faithful=True)["1"][1]
+    assert np.array_equal(oD, D)
+    assert np.array_equal(orc.borda(D, faithful=True), b), "cfg4g: oracle Borda differs"
+    out = {"n": np.int64(n), "avg_deg": np.float64(deg), "seed_base": np.int64(1000),
+           "num_layers": np.int64(2), "checksum": synthetic.fingerprint(layers),
+           "dims": np.asarray(dims, dtype=np.int64), "metrics": np.asarray(metrics),
+           "strategies": np.asarray(["sequential"]), "seed": np.int64(seed), "sigma": so,
+           "sequential/keys": np.asarray(["1"]), "sequential/1/D": D,
+           "sequential/1/cols": np.asarray(list(ranks["1"].columns)),
+           "sequential/1/borda": b, "sequential/1/borda_stable": orc.borda(D, faithful=False)}
+    path = os.path.join(HERE, "er_cfg4g.npz")
+    np.savez_compressed(path, **out)
+    print(f"wrote {path} ({os.path.getsize(path) / 1024:.0f} KB)")
+
+
+def make_cfg4g_env(_N2V2R=None):
+    """The reference's seed-to-seed envelope on the er_cfg4g graph (as make_cfg2_env): the
+    oracle, bit-exact with the reference there, re-run from the ARPACK start vectors of seeds 43
+    and 44.  No sign alignment anywhere (cosine / euclidean are sign-invariant)."""
+    _envelope("er_cfg4g.npz", (43, 44))
+
+
+def _envelope(fname, seeds):
+    from scipy.stats import kendalltau
+
+    from node2vec2rank_amd import synthetic
+    from oracle import n2v2r_oracle as orc
+    path = os.path.join(HERE, fname)
+    z = np.load(path, allow_pickle=False)
+    out = {k: z[k] for k in z.files}
+    layers = synthetic.er_layers(int(out["n"]), float(out["avg_deg"]), int(out["num_layers"]),
+                                 seed_base=int(out["seed_base"]))
+    dims = [int(x) for x in out["dims"]]
+    metrics = [str(x) for x in out["metrics"]]
+    Dr, br = out["sequential/1/D"], out["sequential/1/borda"]
+    top = lambda b: set(np.argsort(-b, kind="stable")[:100].tolist())  # noqa: E731
+    derr, taus, tops = [], [], []
+    for seed in seeds:
+        Y, _, _ = orc.uase(layers, max(dims), seed=seed)
+        D = orc.rank_distances(Y, dims, metrics, "sequential", faithful=True)["1"][1]
+        b = orc.borda(D, faithful=True)
+        derr.append(np.abs(D - Dr).max(axis=0))
+        taus.append(kendalltau(b, br).statistic)
+        tops.append(len(top(b) & top(br)))
+        print(f"seed {seed}: distance diff {derr[-1]}, tau {taus[-1]:.6f}, top-100 {tops[-1]}")
+    out["env_distance_per_col"] = np.max(np.asarray(derr), axis=0)
+    out["env_tau"] = np.float64(min(taus))
+    out["env_top100"] = np.int64(min(tops))
+    np.savez_compressed(path, **out)
+    print(f"wrote {path}")
+
+
 def make_writer(N2V2R):
     """The reference's output files (model.py:40-48 config.json, :142-145 {key}.tsv,
     :193-196 {key}_agg.tsv, :306-309 {key}_degDif.tsv, :269-278 {key}_signed.tsv and
@@ -231,6 +309,7 @@ def main():
     if only:
         for name in only:
             {"er_cfg2": make_cfg2, "er_cfg2_env": make_cfg2_env,
+             "er_cfg4g": make_cfg4g, "er_cfg4g_env": make_cfg4g_env,
              "writer": make_writer}[name](N2V2R)
         return
 

@@ -1,5 +1,6 @@
 """bench.py's watchdog around the optional row-partitioned leg (CPU): a leg that returns in time
-gives its value; a stalled one lets the line print and the process exit with status 0."""
+gives its value; a stalled one lets the line print and the process exit with status 3
+(bench.WATCHDOG_EXIT), not 0, so a hang is visible to whoever checks the exit status."""
 import os
 import subprocess
 import sys
@@ -18,5 +19,5 @@ def test_run_guarded_timeout_prints_and_exits():
             "bench.run_guarded(lambda: time.sleep(60), 0.5, lambda: print('LINE', flush=True)); "
             "print('NOT REACHED')" % REPO)
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
-    assert p.returncode == 0
+    assert p.returncode == 3, (p.returncode, p.stderr)
     assert "LINE" in p.stdout and "NOT REACHED" not in p.stdout

@@ -93,3 +93,24 @@ def test_engine_pool_reuse_and_takeover(monkeypatch):
     t.join(30)
     assert not t.is_alive(), "acquire_engine deadlocked"
     assert out == dict(distinct=_lib.POOL_MAX, takeover=True, owner=True, reuse=True), out
+
+
+def test_reference_descending_order_is_the_references():
+    """The host half of the reference tie order (_lib.reference_descending_order, used only for
+    the columns the GPU flags as tied) reproduces the reference's Borda on every fixture column
+    set, ties included (model.py:173-174 + model_utils.py:22-34)."""
+    import numpy as np
+    from conftest import FIXTURES, load_fixture
+    from node2vec2rank_amd import _lib
+    for name in FIXTURES:
+        fx = load_fixture(name)
+        for strategy in [str(x) for x in fx["strategies"]]:
+            for key in [str(k) for k in fx[f"{strategy}/keys"]]:
+                D = fx[f"{strategy}/{key}/D"]
+                n = D.shape[0]
+                score = np.zeros(n, dtype=np.int64)
+                for c in D.T:
+                    pos = np.empty(n, dtype=np.int64)
+                    pos[_lib.reference_descending_order(c)] = np.arange(n)
+                    score += n - pos
+                np.testing.assert_array_equal(score, fx[f"{strategy}/{key}/borda"])

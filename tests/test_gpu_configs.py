@@ -4,13 +4,18 @@
   own outputs (tests/golden/er_cfg2.npz, made by running the reference model.py on the same
   regenerated graph): singular values, distances, and the integer ranks by SURVEY 8(c)(4)'s
   bar (Kendall tau >= 0.998, identical top-100 set).
+* cfg4's grid (d = 128, 10 columns) on an N=100k, avg-deg 50 graph against the reference's
+  own outputs (tests/golden/er_cfg4g.npz), with the cfg2 bar.
 * cfg4 (2-layer ER N=1M, avg-deg 50, dims {8..128} x {cos, euc}): the full fit; host fp64
   true residuals and orthonormality of the returned vectors, distances vs the oracle from the
   returned embedding, Borda bit-exact vs the stable oracle.
 * cfg3 (4 dense |corrcoef| layers, N=20k, d=256, MFMA path): the full fit; host residuals and
   orthonormality, ranking consistency.
-* cfg5's code path (row partition over W ranks): W = 8 ranks of the thread communicator at
-  N = 1M (cfg5's degree 30), each ingesting only its own rows, vs the single-GPU engine.
+* cfg5 (2-layer ER N=10M, avg-deg 30, d=128) at its own size through the row-partitioned code
+  on an RCCL world-1 communicator: host fp64 residuals, orthonormality, distances vs the oracle
+  fed the returned embedding, Borda given them.
+* cfg5's code path at W > 1: W = 8 ranks of the thread communicator at N = 1M (cfg5's degree
+  30), each ingesting only its own rows, vs the single-GPU engine and an RCCL world-1 handle.
 The reference itself cannot run at cfg3/cfg4 sizes (svds alone exceeded 55 min at cfg4,
 BASELINE.md 2), so those are checked through size-independent properties.
 """
@@ -75,6 +80,50 @@ def test_cfg2_end_to_end_vs_reference():
           f"(reference envelope {float(fx['env_tau']):.6f}), top-100 overlap {top}")
     assert np.all(derr <= np.maximum(1e-4, env)), (derr, env)
     assert tau >= 0.998, tau        # SURVEY 8(c)(4); the reference's own tau is 0.99926
+    assert top == 100, top
+
+
+def test_cfg4_grid_vs_reference():
+    """The bench's own grid (BASELINE cfg4: d = 128, dims {8,16,32,64,128} x {cosine,
+    euclidean}, 10 columns, sequential, seed 42) on a cfg4-family graph the reference finishes
+    (2-layer ER N = 100k, avg-deg 50; tests/golden/er_cfg4g.npz, made by the reference model.py
+    itself, make_golden.py er_cfg4g): singular values, the column order and names (dims outer,
+    metrics inner, model.py:73-93), the prefix slicing [:, :, :dim] (each dim's columns against
+    the reference's), per-column distance error within max(1e-4, the reference's own
+    seed-to-seed envelope), and the integer ranks by SURVEY 8(c)(4)'s bar (Kendall tau >= 0.998,
+    identical top-100 set) (model.py:57-96, 149-185)."""
+    from node2vec2rank_amd import synthetic
+    from node2vec2rank_amd.model import N2V2R
+    fx = load_fixture("er_cfg4g")
+    n = int(fx["n"])
+    layers = synthetic.er_layers(n, float(fx["avg_deg"]), int(fx["num_layers"]),
+                                 seed_base=int(fx["seed_base"]))
+    np.testing.assert_array_equal(synthetic.fingerprint(layers), fx["checksum"])
+    dims = [int(x) for x in fx["dims"]]
+    metrics = [str(x) for x in fx["metrics"]]
+    cfg = dict(embed_dimensions=dims, distance_metrics=metrics, seed=int(fx["seed"]),
+               comp_strategy="sequential", verbose=-1, save_dir=None)
+    m = N2V2R(layers, list(range(n)), cfg)
+    ranks = m.fit_transform_rank()
+    agg = m.aggregate_transform()
+    assert m.eig_stats["converged"] == 128, m.eig_stats
+    np.testing.assert_allclose(m._engine.singular_values(), fx["sigma"], rtol=2e-5)
+    assert list(ranks) == ["1"] and list(agg) == ["1"]
+    cols = [str(c) for c in fx["sequential/1/cols"]]
+    assert list(ranks["1"].columns) == cols
+    assert cols == [f"dim-{d}_distance-{mm}" for d in dims for mm in metrics]
+    D = ranks["1"].to_numpy()
+    derr = np.abs(D - fx["sequential/1/D"]).max(axis=0)
+    env = fx["env_distance_per_col"]
+    b = agg["1"]["borda_ranks"].to_numpy()
+    ref = fx["sequential/1/borda"]
+    tau = kendalltau(b, ref).statistic
+    top = len(_top(b, 100) & _top(ref, 100))
+    print(f"cfg4 grid at N=100k: distance err per column {derr} (reference envelope {env}), "
+          f"Kendall tau {tau:.6f} (reference envelope {float(fx['env_tau']):.6f}), top-100 "
+          f"overlap {top}, bit-exact {np.array_equal(b, ref)}")
+    assert np.all(derr <= np.maximum(1e-4, env)), (derr, env)
+    assert tau >= 0.998, tau
     assert top == 100, top
 
 
@@ -156,6 +205,76 @@ def test_cfg3_dense_full_size(engine):
         np.testing.assert_array_equal(engine.borda(c), orc.borda(D))
 
 
+def _chunked_gram(U, rows=1 << 20):
+    """U^T U in fp64, accumulated over row chunks (U is 5 GB at cfg5)."""
+    G = np.zeros((U.shape[1], U.shape[1]), dtype=np.float64)
+    for r in range(0, U.shape[0], rows):
+        u = U[r:r + rows].astype(np.float64)
+        G += u.T @ u
+    return G
+
+
+def test_cfg5_full_size_rccl():
+    """BASELINE cfg5 at its own size: 2-layer ER N = 10M, avg-deg 30, d = 128, through the
+    row-partitioned code on an RCCL communicator (world 1, so every panel gather, Gram /
+    Rayleigh-Ritz / residual all-reduce and distance-column gather is an RCCL call), the layers
+    ingested as the rank's own rows (set_layer_csr_rows), exactly as bench.py --config cfg5.
+    Checked: convergence, host fp64 true residuals of 5 columns (first, last, the bulk edge),
+    orthonormality of all 128 left vectors, distances vs the oracle fed the returned embedding,
+    Borda bit-exact given them (reference model.py:51-96)."""
+    import time
+
+    from node2vec2rank_amd import _lib, synthetic
+    n, deg, d = 10_000_000, 30.0, 128
+    dims, metrics = [128], ["cosine", "euclidean"]
+    t0 = time.time()
+    layers = [synthetic.er_layer_rows(n, deg, 2000 + k, 0, n) for k in range(2)]
+    print(f"cfg5: layers built in {time.time() - t0:.1f} s, nnz {[a.nnz for a in layers]}",
+          flush=True)
+    eng = _lib.Engine.rccl(0, 0, 1, _lib.comm_unique_id())
+    try:
+        eng.set_layer_rows(n, 2, [])
+        assert eng.dist_info() == (0, 1, 0, n)
+        t0 = time.time()
+        eng.set_layer_rows(n, 2, layers)
+        st = eng.uase(d, seed=42)
+        eng.rank("sequential", dims, metrics)
+        print(f"cfg5: fit + rank {time.time() - t0:.1f} s, {st['restarts']} cycles, "
+              f"{st['block_applications']} block applications, max residual "
+              f"{st['max_residual']:.2e}", flush=True)
+        assert st["converged"] == d and st["max_residual"] <= 1e-6, st
+        s = eng.singular_values()
+        X = eng.left_embedding()
+        Y = eng.embedding()
+        D = eng.distances(0)
+        B = eng.borda(0)
+    finally:
+        eng.close()
+    assert np.all(np.diff(s) <= 0) and np.all(s > 0)
+    theta = s.astype(np.float64) ** 2
+    U = X / np.sqrt(s)[None, :].astype(np.float32)
+    del X
+    G = _chunked_gram(U)
+    orth = np.abs(G - np.eye(d)).max()
+    cols = [0, 1, 64, 126, 127]
+    res = _host_residuals(layers, U, theta, cols)
+    print(f"cfg5: |U^T U - I| {orth:.2e}, host residuals {res}", flush=True)
+    assert orth < 1e-5, orth
+    assert res.max() < 5e-6, res
+    del U
+    # distances from the returned embedding, fp64 on both sides, in row chunks (Y is 10 GB)
+    names = [name for _, _, name in orc.column_names(dims, metrics)]
+    assert D.shape == (n, len(names))
+    step = 1 << 21
+    for r in range(0, n, step):
+        e1, e2 = Y[0, r:r + step, :128], Y[1, r:r + step, :128]
+        for c, m in enumerate(metrics):
+            np.testing.assert_allclose(D[r:r + step, c], orc.distances_fast(e1, e2, m),
+                                       rtol=0, atol=1e-9)
+    del Y
+    np.testing.assert_array_equal(B, orc.borda(D))
+
+
 def test_cfg5_path_w8_one_million(engine):
     """cfg5's row-partitioned path at >= 1M nodes: 8 ranks (thread communicator, one GPU), each
     ingesting only its own rows of the counter-based ER layers bench.py's cfg5 uses, vs the
@@ -187,6 +306,18 @@ def test_cfg5_path_w8_one_million(engine):
     engine.rank("sequential", dims, metrics)
     s1 = engine.singular_values()
     np.testing.assert_allclose(res[0]["s"], s1, rtol=1e-5)
+    # the partitioned code on an RCCL world-1 communicator agrees with the plain engine too
+    from node2vec2rank_amd import _lib
+    reng = _lib.Engine.rccl(0, 0, 1, _lib.comm_unique_id())
+    try:
+        reng.set_layer_rows(n, 2, [])
+        reng.set_layer_rows(n, 2, full)
+        st_r = reng.uase(d, seed=9)
+        s_r = reng.singular_values()
+    finally:
+        reng.close()
+    assert st_r["converged"] == d or st_r["stagnated"] == 1, st_r
+    np.testing.assert_allclose(s_r, s1, rtol=1e-5)
     X = np.concatenate([r["X"] for r in res], axis=0)
     U = X / np.sqrt(res[0]["s"])[None, :].astype(np.float32)
     res_h = _host_residuals(full, U, res[0]["s"] ** 2, [0, 1, 31, 62, 63])

@@ -154,6 +154,28 @@ def _tau_envelope(Y_other, fx, strategy, key):
     return kendalltau(orc.borda(Da), orc.borda(Db)).statistic
 
 
+ENV_SEEDS = 4
+
+
+def _tau_envelope_unaligned(layers, fx, strategy):
+    """The reference's envelope as a sign-arbitrary method sees it: Kendall tau between the
+    reference's own Borda (quicksort ties, fx) and the reference's algorithm re-run from the
+    ARPACK start vectors of seeds seed+1 .. seed+ENV_SEEDS with NO sign alignment (correlation
+    distances depend on the per-column signs ARPACK leaves to its start vector), the minimum
+    over those runs per comparison key."""
+    from scipy.stats import kendalltau
+    dims = [int(x) for x in fx["dims"]]
+    metrics = [str(x) for x in fx["metrics"]]
+    seed = int(fx["seed"])
+    out = {}
+    for s in range(seed + 1, seed + 1 + ENV_SEEDS):
+        Y, _, _ = orc.uase(layers, max(dims), seed=s)
+        for key, (_, D) in orc.rank_distances(Y, dims, metrics, strategy, faithful=True).items():
+            t = kendalltau(orc.borda(D, faithful=True), fx[f"{strategy}/{key}/borda"]).statistic
+            out[key] = min(out.get(key, 1.0), t)
+    return out
+
+
 @pytest.mark.parametrize("name", FIXTURES)
 def test_uase_matches_reference(engine, name):
     fx = load_fixture(name)
@@ -233,17 +255,70 @@ def test_pairwise_seam(engine):
 
 
 # ----------------------------------------------------------------------------- Borda
+def _has_ties(c):
+    v = c[~np.isnan(c)]
+    v = np.where(v == 0.0, 0.0, v)  # -0 == +0
+    return len(np.unique(v)) < len(v)
+
+
 @pytest.mark.parametrize("name", FIXTURES)
 def test_borda_bit_exact_given_reference_distances(engine, name):
+    """Given the reference's distance table: the stable GPU order equals the stable oracle, and
+    the reference tie order (GPU tie flags + pandas' order for the tied columns,
+    model.py:173-174) equals the REFERENCE's own Borda bit for bit, ties included."""
     fx = load_fixture(name)
+    n_tied = 0
     for strategy in [str(x) for x in fx["strategies"]]:
         for key in [str(k) for k in fx[f"{strategy}/keys"]]:
             D = fx[f"{strategy}/{key}/D"]
-            got = engine.borda_columns(D)
+            got, tied = engine.borda_columns(D, return_tied=True)
             np.testing.assert_array_equal(got, fx[f"{strategy}/{key}/borda_stable"])
-            tie_free = all(len(np.unique(c[~np.isnan(c)])) == (~np.isnan(c)).sum() for c in D.T)
-            if tie_free:
-                np.testing.assert_array_equal(got, fx[f"{strategy}/{key}/borda"])
+            np.testing.assert_array_equal(tied, [_has_ties(c) for c in D.T])
+            n_tied += int(tied.sum())
+            ref = engine.borda_columns(D, tie_order="reference")
+            # this host's numpy must order ties as the one that made the fixture (else the
+            # comparison below is between two numpy builds, not between us and the reference)
+            np.testing.assert_array_equal(orc.borda(D, faithful=True),
+                                          fx[f"{strategy}/{key}/borda"])
+            np.testing.assert_array_equal(ref, fx[f"{strategy}/{key}/borda"])
+    print(f"{name}: {n_tied} tied columns")
+    if name in ("demo", "ties_nan", "k4_strategies"):
+        assert n_tied > 0  # the fixtures that hold exact ties exercise the tied path
+
+
+def test_borda_given_orders_validated(engine):
+    """n2v2r_borda_columns_ex refuses a given order that is not a permutation (the GPU scatters
+    by it) and sums a valid one exactly."""
+    import ctypes
+    from node2vec2rank_amd import _lib
+    rng = np.random.default_rng(2)
+    n = 1000
+    D = np.round(rng.random((n, 3)) * 20)  # heavy ties
+    Dc = np.ascontiguousarray(D.T)
+    out = np.empty(n, dtype=np.int64)
+    tied = np.empty(3, dtype=np.int32)
+    cols = np.array([1], dtype=np.int32)
+    perm = rng.permutation(n).astype(np.int32)[None, :]
+    lib = engine.lib
+    st = lib.n2v2r_borda_columns_ex(engine.h, Dc, n, 3, cols.ctypes.data_as(ctypes.c_void_p), 1,
+                                    perm.ctypes.data_as(ctypes.c_void_p), out, tied)
+    assert st == _lib.OK
+    pos = np.empty(n, dtype=np.int64)
+    pos[perm[0]] = np.arange(n)
+    stable = [orc._descending_order_pandas(D[:, j], "stable") for j in (0, 2)]
+    want = n - pos
+    for o in stable:
+        p = np.empty(n, dtype=np.int64)
+        p[o] = np.arange(n)
+        want += n - p
+    np.testing.assert_array_equal(out, want)
+    assert tied.tolist() == [1, 1, 1]
+    bad = perm.copy()
+    bad[0, 5] = bad[0, 6]
+    for b, c in ((bad, cols), (perm, np.array([3], dtype=np.int32))):
+        st = lib.n2v2r_borda_columns_ex(engine.h, Dc, n, 3, c.ctypes.data_as(ctypes.c_void_p), 1,
+                                        b.ctypes.data_as(ctypes.c_void_p), out, tied)
+        assert st == _lib.ERR_BAD_ARG
 
 
 def test_borda_large_with_ties_nans_and_negzero(engine):
@@ -258,6 +333,9 @@ def test_borda_large_with_ties_nans_and_negzero(engine):
     got = engine.borda_columns(D)
     np.testing.assert_array_equal(got, orc.borda(D, faithful=False))
     assert got.sum() == c * n * (n + 1) // 2   # every column is a permutation
+    # the reference's tie order (pandas / numpy quicksort, model.py:173-174) on every column
+    np.testing.assert_array_equal(engine.borda_columns(D, tie_order="reference"),
+                                  orc.borda(D, faithful=True))
 
 
 def test_borda_label_seam():
@@ -288,9 +366,12 @@ def test_model_end_to_end(name):
     nodes = [str(x) for x in fx["nodes"]]
     d = int(fx["dims"].max())
     env, Y_other = _envelope(layers, d, int(fx["seed"]))
+    env_unaligned = {}
+    if name not in END_TO_END_STRICT:
+        env_unaligned = {s: _tau_envelope_unaligned(layers, fx, s)
+                         for s in [str(x) for x in fx["strategies"]]}
     for strategy in [str(x) for x in fx["strategies"]]:
-        model = N2V2R(graphs=layers, nodes=nodes, config=_cfg(fx, strategy),
-                      )
+        model = N2V2R(graphs=layers, nodes=nodes, config=_cfg(fx, strategy))
         ranks = model.fit_transform_rank()
         agg = model.aggregate_transform()
         keys = [str(k) for k in fx[f"{strategy}/keys"]]
@@ -316,28 +397,39 @@ def test_model_end_to_end(name):
             assert derr <= max(1e-4, 20 * env), (name, strategy, key, derr, env)
             b = agg[key]["borda_ranks"].to_numpy()
             assert agg[key]["borda_ranks"].dtype == np.int64
-            # exact ties (e.g. 2-d correlation is always 0 or 2) are ordered by node index on
-            # the GPU; the reference's quicksort order for them is implementation-defined, so
-            # the rank comparison uses the stable order of the reference's distances
-            ref_b = orc.borda(Dref)
-            if not corr.any():
-                np.testing.assert_array_equal(ref_b, fx[f"{strategy}/{key}/borda_stable"])
+            # aggregate_transform orders tied columns as the reference (pandas quicksort), so
+            # the integer ranks compare with the reference's own Borda; correlation columns
+            # against the reference's distances re-signed to ours, in the reference's order
+            ref_b = (orc.borda(Dref, faithful=True) if corr.any()
+                     else fx[f"{strategy}/{key}/borda"])
             tau = kendalltau(b, ref_b).statistic
             k = min(100, len(nodes) // 10)
             top = len(set(np.argsort(-b, kind="stable")[:k]) &
                       set(np.argsort(-ref_b, kind="stable")[:k]))
-            tau_env = _tau_envelope(Y_other, fx, strategy, key)
-            print(f"{name}/{strategy}/{key}: Kendall tau {tau:.6f} (reference envelope "
-                  f"{tau_env:.6f}), top-{k} overlap {top}")
+            exact = bool(np.array_equal(b, ref_b))
+            print(f"{name}/{strategy}/{key}: Kendall tau {tau:.6f}, top-{k} overlap {top}, "
+                  f"bit-exact {exact}")
             if name in END_TO_END_STRICT:
                 # tau >= 0.998 and the identical top-100 set (top N/10 below
-                # 1000 nodes); measured 0.99995-1.0 on these fixtures
+                # 1000 nodes)
                 assert tau >= 0.998 and top == k, (name, strategy, key, tau, top)
             else:
                 # k4_strategies (400-node SBM, dims 1..6, correlation columns): near-tied
-                # distances make its ranks noise-level even for the reference, whose own
-                # seed-to-seed tau is 0.966-0.998 here: the bar is that envelope minus 0.02
-                assert tau >= min(0.998, tau_env - 0.02), (name, strategy, key, tau, tau_env)
+                # distances make its ranks noise-level even for the reference.  Correlation
+                # distances depend on the SVD's per-column signs, which the reference leaves to
+                # ARPACK's start vector and the engine fixes (svd_flip), so no sign-arbitrary
+                # method can match them; the bar is the reference's own envelope as such a
+                # method sees it: tau of the reference's Borda against the reference re-run from
+                # other start vectors, without sign alignment, the minimum over ENV_SEEDS runs
+                # (and against the drop-in's own correlation-free-of-sign comparison above)
+                tau_ref = kendalltau(b, fx[f"{strategy}/{key}/borda"]).statistic
+                env_al = _tau_envelope(Y_other, fx, strategy, key)
+                env_un = env_unaligned[strategy][key]
+                print(f"    vs the reference's Borda as is: tau {tau_ref:.6f}; reference "
+                      f"envelope aligned {env_al:.6f}, unaligned (min of {ENV_SEEDS}) "
+                      f"{env_un:.6f}")
+                assert tau_ref >= min(0.998, env_un), (name, strategy, key, tau_ref, env_un)
+                assert tau >= min(0.998, env_al - 0.02), (name, strategy, key, tau, env_al)
         Y = model.node_embeddings
         assert Y.shape == fx["Y"].shape
 

@@ -102,3 +102,27 @@ def test_signed_ranks_needs_prior(tmp_path, monkeypatch):
     m, _, _ = _model(tmp_path, monkeypatch)
     with pytest.raises(ValueError):
         m.signed_ranks_transform()
+
+
+def test_signed_transform_single_seam():
+    """node2vec2rank_amd.model_utils.signed_transform_single (the seam of model_utils.py:7-19)
+    vs the literal restatement: order, kept nodes, values and the sign bit of NaN / 0 ranks."""
+    from node2vec2rank_amd import model_utils as mu
+    rng = np.random.default_rng(8)
+    names = [f"g{i}" for i in range(500)]
+    vals = rng.standard_normal(500)
+    vals[::40] = np.nan
+    vals[::55] = 0.0
+    ranks = pd.Series(vals, index=names)
+    pick = rng.permutation(500)[:320]
+    prior = pd.Series(rng.integers(-2, 3, 320).astype(np.float32), index=[names[i] for i in pick])
+    prior.iloc[::17] = np.nan
+    for r in (ranks, pd.Series(rng.integers(1, 900, 500), index=names)):
+        got = mu.signed_transform_single(r, prior)
+        ref = orc.signed_transform_single(r, prior)
+        assert list(got.index) == list(ref.index)
+        np.testing.assert_array_equal(got.to_numpy(), ref.to_numpy())
+        np.testing.assert_array_equal(np.signbit(got.to_numpy()), np.signbit(ref.to_numpy()))
+        assert got.dtype == ref.dtype
+    empty = mu.signed_transform_single(ranks, pd.Series([1.0], index=["absent"]))
+    assert len(empty) == 0
