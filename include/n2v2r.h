@@ -136,11 +136,16 @@ void n2v2r_simgroup_destroy(n2v2r_simgroup* g);
 int n2v2r_create_sim(int device, n2v2r_simgroup* g, int rank, n2v2r_handle** out);
 int n2v2r_dist_info(const n2v2r_handle* h, int* rank, int* world, int64_t* row0, int64_t* n_local);
 
-/* graph layers: K layers over the same N nodes.  CSR is copied to HBM (int64 row pointers are
- * accepted; int32 column indices; fp32 values).  The column-index range check, the transpose
- * (stable LSD radix sort of the entries by column on the GPU) and symmetric = N2V2R_SYM_DETECT
- * (A compared with A^T entry by entry on the GPU) run on the device.  Non-symmetric layers also
- * keep A^T. */
+/* graph layers: K layers over the same N nodes.  CSR is copied to HBM (int64 row pointers;
+ * int32 column indices; fp32 values).  The column-index range check, the transpose (stable LSD
+ * radix sort of the entries by column on the GPU) and symmetric = N2V2R_SYM_DETECT (A compared
+ * with A^T entry by entry on the GPU) run on the device.  Non-symmetric layers also keep A^T.
+ * The transpose sorts int32 entry indices: a layer with more than 2^31 - 1 entries needs
+ * symmetric = N2V2R_SYM_YES (N2V2R_ERR_BAD_ARG otherwise).
+ * Memory: on a partitioned handle this call still uploads the WHOLE layer to every rank (and,
+ * unless N2V2R_SYM_YES, sorts its transpose there, ~40 B per global entry at the peak) before
+ * keeping the rank's rows; n2v2r_set_layer_csr_rows is the ingest whose memory scales with the
+ * row partition. */
 int n2v2r_set_num_layers(n2v2r_handle* h, int num_layers, int64_t n);
 int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const int64_t* indptr,
                         const int32_t* indices, const float* data, int symmetric);
@@ -205,47 +210,8 @@ int n2v2r_project(n2v2r_handle* h, int64_t m, int64_t n, const double* W, int on
 /* device sync */
 int n2v2r_synchronize(n2v2r_handle* h);
 
-/* SpMM kernel alone (tests + roofline): Y = A_k X (transpose = 0) or A_k^T X (1) for a host
- * N x b panel X (b = 8, 16, 32 or 64), timed with HIP events on the engine stream over `reps`
- * launches after one warm-up.  avg_ms = mean launch duration; algo_bytes = SURVEY 8(d) bytes
- * per launch (8 nnz + 4 (N+1) + 8 N b).  On a partitioned handle A_k means this rank's rows:
- * X is the global N x b panel, Y its n_local x b rows, bytes 8 nnz_loc + 4 (n_loc+1) +
- * 4 (N + n_loc) b.  Y may be NULL. */
-/* Diagnostic: time the b = 8 second SpMM stage W = sum_k A_k Z_k on the loaded layers with
- * random panels; mode 0 = one summed output (the solver's form), 1 = one output per layer
- * (grid.y = layer), 2 = one output per layer with the layers split over the XCDs; 3 and 4 =
- * modes 1 and 2 with one panel shared by all layers (the first stage's form).  Returns the
- * average launch time in ms. */
-int n2v2r_probe_spmm_stage2(n2v2r_handle* h, int mode, int reps, double* avg_ms);
-int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, const float* X,
-                     float* Y, double* avg_ms, double* algo_bytes);
-/* Diagnostic: the flat-window tiled SpMM of layer k (A_k X, or A_k^T X) at panel width b = 8 or
- * 16 with nb column blocks (0: panel blocks of <= 2 MB), one-GPU handles; Y (optional, n x b)
- * receives the product.  N2V2R_ERR_BAD_ARG when the layer cannot take packed blocks. */
-int n2v2r_bench_spmm_tiled(n2v2r_handle* h, int k, int transpose, int b, int nb, int reps,
-                           const float* X, float* Y, double* avg_ms);
-
-/* 1 when UASE (and n2v2r_bench_spmm) use the XCD-local column-block SpMM at panel width b on
- * this handle's layers (b = 8 CSR panels of 8-160 MB: each layer split into 8 column blocks,
- * workgroup i mod 8 on XCD i mod 8 gathers only from block i mod 8, fixed-order reduce of the
- * 8 partials; env N2V2R_SPMM_CB=1/0 forces it), else 0.  Then bench_spmm times the block
- * launch plus the reduce. */
-int n2v2r_spmm_col_blocks(const n2v2r_handle* h, int b);
-
-/* Rayleigh-Ritz stage alone (tests): top-p eigenpairs of a host symmetric c x c fp64 matrix H
- * (3 <= c <= 768) through UASE's own path, all on the GPU (Householder tridiagonalisation,
- * bisection + inverse iteration on the tridiagonal, compact-WY back-transform).  w: p eigenvalues, descending; S: c x p
- * row-major fp32 eigenvectors (the Ritz coefficients UASE consumes). */
-int n2v2r_rr_top(n2v2r_handle* h, int c, const double* H, int p, double* w, float* S);
-
-/* Banded Rayleigh-Ritz stage alone (tests; block width 8, c <= 512, kp + 8 <= 192): the
- * projected matrix of a Krylov-Schur cycle given as UASE keeps it.  Basis order [X (kp
- * columns, diagonal theta_prev), E, Z_2, ...] in 8-wide blocks; hband holds band column
- * j0 = kp/8 ([X E]^T M E, (kp+8) x 8 row-major) at offset 0, then for every later block j the
- * 16 x 8 matrix [Q_{j-1} Q_j]^T M Q_j.  Entries outside the band (half-bandwidth 8) are taken
- * as zero.  Same outputs as n2v2r_rr_top. */
-int n2v2r_rr_band_top(n2v2r_handle* h, int c, int kp, const double* hband, int64_t hband_len,
-                      const double* theta_prev, int p, double* w, float* S);
+/* Diagnostic entry points (kernel timings, single stages for tests) are declared in
+ * n2v2r_diag.h: they are not part of the drop-in API. */
 
 #ifdef __cplusplus
 }

@@ -32,7 +32,7 @@ STRATEGY = {"sequential": 0, "one_vs_before": 1, "one_vs_rest": 2}
 METRIC = {"cosine": 0, "euclidean": 1, "correlation": 2}
 SYM_DETECT, SYM_NO, SYM_YES = -1, 0, 1
 
-# every symbol include/n2v2r.h declares (checked by tests/test_capi.py)
+# every symbol include/n2v2r.h and include/n2v2r_diag.h declare (checked by tests/test_capi.py)
 EXPORTED = [
     "n2v2r_create", "n2v2r_destroy", "n2v2r_last_error", "n2v2r_version",
     "n2v2r_set_num_layers", "n2v2r_set_layer_csr", "n2v2r_uase", "n2v2r_get_embedding",
@@ -44,7 +44,6 @@ EXPORTED = [
     "n2v2r_comm_unique_id", "n2v2r_create_rccl", "n2v2r_simgroup_create",
     "n2v2r_simgroup_destroy", "n2v2r_create_sim", "n2v2r_dist_info", "n2v2r_set_layer_csr_rows",
     "n2v2r_rr_top", "n2v2r_rr_band_top", "n2v2r_set_layer_dense", "n2v2r_project",
-    "n2v2r_probe_spmm_stage2",
 ]
 UNIQUE_ID_BYTES = 128
 
@@ -137,7 +136,6 @@ def load(path: str | None = None):
             "n2v2r_bench_spmm_tiled": (_i, [_vp, _i, _i, _i, _i, _i, _p(np.float32), _vp,
                                             ctypes.POINTER(ctypes.c_double)]),
             "n2v2r_spmm_col_blocks": (_i, [_vp, _i]),
-            "n2v2r_probe_spmm_stage2": (_i, [_vp, _i, _i, ctypes.POINTER(ctypes.c_double)]),
             "n2v2r_rr_top": (_i, [_vp, _i, _p(np.float64), _i, _p(np.float64), _p(np.float32)]),
             "n2v2r_rr_band_top": (_i, [_vp, _i, _i, _p(np.float64), ctypes.c_int64, _vp, _i,
                                        _p(np.float64), _p(np.float32)]),
@@ -478,7 +476,7 @@ class Engine:
 
     def bench_spmm_tiled(self, k: int, X, transpose: bool = False, nb: int = 0, reps: int = 20,
                          want_y=True):
-        """Time the flat-window tiled SpMM (panel width 8 or 16) of layer k alone."""
+        """Time the flat-window tiled SpMM (panel width 8) of layer k alone."""
         X = np.ascontiguousarray(X, dtype=np.float32)
         n, b = X.shape
         Y = np.empty((self._n_local(), b), dtype=np.float32) if want_y else None
@@ -488,14 +486,6 @@ class Engine:
                                                     int(nb), int(reps), X, yp, ctypes.byref(ms)),
                     "bench_spmm_tiled")
         return Y, ms.value
-
-    def probe_spmm_stage2(self, mode: int, reps: int = 50) -> float:
-        """Diagnostic: average ms of the b = 8 second SpMM stage (0 summed, 1 per layer,
-        2 per layer split over the XCDs) on the loaded layers."""
-        ms = ctypes.c_double(0)
-        self._check(self.lib.n2v2r_probe_spmm_stage2(self.h, int(mode), int(reps),
-                                                      ctypes.byref(ms)), "probe_spmm_stage2")
-        return ms.value
 
     def spmm_col_blocks(self, b: int = 8) -> bool:
         """True when the SpMM at panel width b runs the XCD-local column-block form."""

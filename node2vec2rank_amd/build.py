@@ -18,7 +18,8 @@ OBJ_DIR = os.path.join(OUT_DIR, "obj")
 HIP_SOURCES = ["spmm.hip", "dense.hip", "gemm.hip", "rank.hip", "rr.hip", "rr_band.hip",
                "rr_sturm.hip", "ingest.hip", "engine.cpp"]
 HOST_SOURCES: list = []
-HEADERS = ["common.h", "spmm_args.h", os.path.join("..", "..", "include", "n2v2r.h")]
+HEADERS = ["common.h", "spmm_args.h", os.path.join("..", "..", "include", "n2v2r.h"),
+           os.path.join("..", "..", "include", "n2v2r_diag.h")]
 ARCH = os.environ.get("N2V2R_OFFLOAD_ARCH", "gfx950")
 
 

@@ -1600,13 +1600,59 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
       for (int sl = 0; sl < 16; ++sl) s -= part[sl][tid];
       R[i][j] = s;
     }
-  } else {
+  } else if (stage) {
     for (int e = tid; e < bb; e += nt) {
       const int i = e / b, j = e % b;
       double s = 0.5 * (Gs[(int64_t)(c + i) * b + j] + Gs[(int64_t)(c + j) * b + i]);
       for (int k = 0; k < c; ++k) s -= Gs[(int64_t)k * b + i] * Gs[(int64_t)k * b + j];
       R[i][j] = s;
     }
+  } else {
+    // G beyond the staging size (b = 32 / 64 blocks, long bases: cfg3): C = Q^T Z goes through
+    // LDS 4096 / b rows at a time (X's storage, not yet in use), every thread's loads of a chunk
+    // in flight together, and each entry of C^T C accumulates from LDS (was: c dependent L2
+    // loads per entry, ~170 us per call at c = 768, b = 32)
+    double* cst = &X[0][0];
+    const int rows = 4096 / b;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};  // entries tid + nt u, bb <= 4096
+    for (int k0 = 0; k0 < c; k0 += rows) {
+      const int kr = min(rows, c - k0);
+      const int tot = kr * b;
+      __syncthreads();
+      for (int q0 = tid; q0 < tot; q0 += nt * 4) {
+        double t4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) t4[u] = G[(int64_t)k0 * b + min(q0 + nt * u, tot - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) cst[min(q0 + nt * u, tot - 1)] = t4[u];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = tid + nt * u;
+        if (e < bb) {
+          const int i = e / b, j = e % b;
+          double a0 = 0.0, a1 = 0.0;
+          int k = 0;
+          for (; k + 1 < kr; k += 2) {
+            a0 += cst[k * b + i] * cst[k * b + j];
+            a1 += cst[(k + 1) * b + i] * cst[(k + 1) * b + j];
+          }
+          if (k < kr) a0 += cst[k * b + i] * cst[k * b + j];
+          acc[u] += a0 + a1;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + nt * u;
+      if (e < bb) {
+        const int i = e / b, j = e % b;
+        R[i][j] = 0.5 * (G[(int64_t)(c + i) * b + j] + G[(int64_t)(c + j) * b + i]) - acc[u];
+      }
+    }
+    __syncthreads();
   }
   for (int e = tid; e < bb; e += nt) X[e / b][e % b] = (e / b == e % b) ? 1.0 : 0.0;
   if (tid < 64) bad[tid] = 0;
@@ -1671,7 +1717,38 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
     }
   }
   __syncthreads();
-  if (fout) {  // every thread: F[k][j] = -sum_{m <= j} C[k][m] X[m][j]; F[c + i][j] = X[i][j]
+  if (fout && !stage && bb > 64) {
+    // the same F with C through LDS in chunks (R's storage: R is spent once xinv is out)
+    double* cst = &R[0][0];
+    const int rows = 4096 / b;
+    for (int k0 = 0; k0 < c; k0 += rows) {
+      const int kr = min(rows, c - k0);
+      const int tot = kr * b;
+      __syncthreads();
+      for (int q0 = tid; q0 < tot; q0 += nt * 4) {
+        double t4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) t4[u] = G[(int64_t)k0 * b + min(q0 + nt * u, tot - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) cst[min(q0 + nt * u, tot - 1)] = t4[u];
+      }
+      __syncthreads();
+      for (int e = tid; e < tot; e += nt) {
+        const int kk = e / b, j = e % b;
+        float v = 0.f;
+        if (!bad[j]) {
+          double sacc = 0.0;
+          for (int m = 0; m <= j; ++m) sacc -= cst[kk * b + m] * X[m][j];
+          v = (float)sacc;
+        }
+        fout[(int64_t)k0 * b + e] = v;
+      }
+    }
+    for (int e = tid; e < bb; e += nt) {
+      const int i = e / b, j = e % b;
+      fout[(int64_t)(c + i) * b + j] = bad[j] ? 0.f : (float)X[i][j];
+    }
+  } else if (fout) {  // every thread: F[k][j] = -sum_{m <= j} C[k][m] X[m][j]; F[c + i][j] = X[i][j]
     for (int e = tid; e < (c + b) * b; e += nt) {
       const int k = e / b, j = e % b;
       float v = 0.f;

@@ -43,6 +43,7 @@
 #include <vector>
 
 #include "../../include/n2v2r.h"
+#include "../../include/n2v2r_diag.h"
 #include "common.h"
 
 // ---- kernel launchers (spmm.hip, dense.hip, rank.hip) ------------------------------------
@@ -58,12 +59,8 @@ struct DistPlan {
 extern "C" {
 hipError_t n2v2r_launch_spmm(const SpmmArgs& args, int B, hipStream_t stream);
 hipError_t n2v2r_launch_row_sums(const CsrDev& A, float* out, hipStream_t stream);
-hipError_t n2v2r_launch_spmm_cb(const SpmmCbArgs& a, hipStream_t stream);
-hipError_t n2v2r_launch_cb_reduce(const float* P, int nparts, int64_t pstride, int64_t n,
-                                  float* out, int64_t ldo, hipStream_t stream);
-hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, int rpw, hipStream_t stream);
+hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, hipStream_t stream);
 int n2v2r_spmm_tile_rows(int64_t n, int ncu, int wpc);
-int n2v2r_cb_rpw(const CsrBlk* A, int nb, int64_t n);
 hipError_t n2v2r_launch_cb_count(const CsrDev& A, int64_t cw, int nb, int32_t* cnt,
                                  hipStream_t stream);
 hipError_t n2v2r_launch_cb_rowptrs(const int32_t* cnt, int64_t n, int nb, int64_t nnz,
@@ -153,7 +150,8 @@ hipError_t n2v2r_launch_transpose(const float* in, int64_t ldi, int64_t rows, in
 hipError_t n2v2r_launch_mismatch(const float* a, const float* b, int64_t ld, int64_t rows,
                                  int64_t cols, unsigned long long* count, hipStream_t stream);
 hipError_t n2v2r_launch_rr_tridiag(double* A, int c, double* d, double* e, double* tau, double* V,
-                                   hipStream_t stream);
+                                   void* scratch, hipStream_t stream);
+size_t n2v2r_rr_tridiag_scratch_bytes(int c);
 hipError_t n2v2r_launch_rr_tri_eig(const double* d, const double* e, int c, int p, double* w,
                                    double* Y, double* scratch, hipStream_t stream);
 hipError_t n2v2r_launch_rr_backtransform(const double* V, const double* tau, int c,
@@ -318,7 +316,7 @@ struct LayerDev {
   struct ColBlocks {
     DevBuf rp, idx, dat;   // [nb][n_rows + 1] int32 row pointers (relative); entries; values
     CsrBlk blk[CB_MAX];
-    int nb = 0;            // blocks (CB_NB = 8 for the partials form; 4-32 tiled)
+    int nb = 0;            // blocks (4-64; phases of the flat tiled SpMM)
     int cbits = 0;         // packed entries for the flat tiled form (0: global columns)
     bool packed = false;   // built packed (requested and the column bits fit)
     int64_t ncols = 0;     // column count the blocks were cut for
@@ -326,13 +324,26 @@ struct LayerDev {
     bool usable = false;   // every block under 2^31 entries (int32 row pointers)
   };
   ColBlocks cb, cb_t;
-  void drop_col_blocks() {
+  // partitioned handles, reduce-scatter form: this rank's columns of A, A[:, own rows], as a CSR
+  // over the world x npad padded global rows with local column indices (built on first use)
+  DevBuf c_indptr, c_indices, c_data;
+  int64_t c_nnz = 0, c_rows = 0;
+  bool c_built = false;
+  CsrDev csr_c() const {
+    return CsrDev{c_indptr.as<int64_t>(), c_indices.as<int32_t>(), c_data.as<float>(), c_rows,
+                  c_nnz, (symmetric ? unit : t_unit) ? 1 : 0};
+  }
+  void drop_col_blocks() {  // (and every other derived form of the layer)
     for (ColBlocks* c : {&cb, &cb_t}) {
       c->rp.release();
       c->idx.release();
       c->dat.release();
       c->built = false;
     }
+    c_indptr.release();
+    c_indices.release();
+    c_data.release();
+    c_built = false;
   }
 };
 
@@ -400,6 +411,54 @@ bool ensure_col_blocks(LayerDev& L, int64_t ncols, hipStream_t st, int nb = CB_N
   return L.cb.usable && (L.symmetric || L.cb_t.usable);
 }
 
+// A[:, own rows] of a partitioned layer as a CSR over rows_out (>= N) global rows, columns local:
+// the transpose of the rank's rows of A^T (A's own columns), by the ingest's GPU transpose (the
+// stable LSD radix sort of col << 32 | row keys over the column digits).  Stage 2 of the
+// reduce-scatter form gathers from this rank's Z rows only.  One-off per layer.
+void ensure_colcsr(LayerDev& L, int64_t ncols, int64_t rows_out, hipStream_t st) {
+  if (L.c_built && L.c_rows == rows_out) return;
+  const CsrDev s = L.csr_t();
+  const int64_t nnz = s.nnz;
+  if (nnz > (int64_t)INT32_MAX)
+    throw StatusFail{N2V2R_ERR_BAD_ARG, "a rank's layer block over 2^31 - 1 entries"};
+  L.c_indptr.ensure(sizeof(int64_t) * (rows_out + 1));
+  L.c_indices.ensure(sizeof(int32_t) * std::max<int64_t>(nnz, 1));
+  if (!s.unit) L.c_data.ensure(sizeof(float) * std::max<int64_t>(nnz, 1));
+  if (nnz == 0) {
+    HIPCHK(n2v2r_launch_csr_from_sorted(nullptr, nullptr, nullptr, 0, rows_out,
+                                        L.c_indptr.as<int64_t>(), nullptr, nullptr, st));
+  } else {
+    DevBuf keys[2], pay[2], hist, flag;
+    for (int i = 0; i < 2; ++i) {
+      keys[i].ensure(sizeof(uint64_t) * nnz);
+      pay[i].ensure(sizeof(int32_t) * nnz);
+    }
+    flag.ensure(sizeof(unsigned) * 4, st);
+    HIPCHK(hipMemsetAsync(flag.p, 0, sizeof(unsigned) * 4, st));
+    HIPCHK(n2v2r_launch_csr_scan(s.indptr, s.indices, s.data, s.n_rows, ncols,
+                                 keys[0].as<uint64_t>(), pay[0].as<int32_t>(),
+                                 flag.as<unsigned>(), st));
+    hist.ensure(sizeof(uint32_t) * n2v2r_radix_hist_elems(nnz, 1));
+    int bits = 1;
+    while (bits < 31 && ((int64_t)1 << bits) < ncols) ++bits;
+    int cur = 0;
+    for (int sh = 32; sh < 32 + bits; sh += 8) {
+      HIPCHK(n2v2r_launch_radix_pass(keys[cur].as<uint64_t>(), pay[cur].as<int32_t>(),
+                                     keys[cur ^ 1].as<uint64_t>(), pay[cur ^ 1].as<int32_t>(),
+                                     nnz, 1, sh, hist.as<uint32_t>(), st));
+      cur ^= 1;
+    }
+    HIPCHK(n2v2r_launch_csr_from_sorted(keys[cur].as<uint64_t>(), pay[cur].as<int32_t>(), s.data,
+                                        nnz, rows_out, L.c_indptr.as<int64_t>(),
+                                        L.c_indices.as<int32_t>(),
+                                        s.unit ? nullptr : L.c_data.as<float>(), st));
+    HIPCHK(hipStreamSynchronize(st));  // the sort scratch dies here
+  }
+  L.c_nnz = nnz;
+  L.c_rows = rows_out;
+  L.c_built = true;
+}
+
 // ---- communicators ----------------------------------------------------------------------
 struct Comm {
   int rank = 0, world = 1;
@@ -409,6 +468,9 @@ struct Comm {
   virtual void allreduce_sum_f64(double* buf, size_t count, hipStream_t st) = 0;
   virtual void allreduce_max_u64(unsigned long long* buf, size_t count, hipStream_t st) = 0;
   virtual void allreduce_sum_f32(float* buf, size_t count, hipStream_t st) = 0;
+  // recv (count floats) = sum over ranks of their send[rank * count .. (rank + 1) * count)
+  virtual void reduce_scatter_sum_f32(const float* send, float* recv, size_t count,
+                                      hipStream_t st) = 0;
   virtual const char* kind() const = 0;
 };
 
@@ -438,6 +500,10 @@ struct RcclComm : Comm {
   }
   void allreduce_sum_f32(float* buf, size_t count, hipStream_t st) override {
     NCCLCHK(ncclAllReduce(buf, buf, count, ncclFloat, ncclSum, c, st));
+  }
+  void reduce_scatter_sum_f32(const float* send, float* recv, size_t count,
+                              hipStream_t st) override {
+    NCCLCHK(ncclReduceScatter(send, recv, count, ncclFloat, ncclSum, c, st));
   }
   const char* kind() const override { return "rccl"; }
 };
@@ -508,6 +574,27 @@ struct ThreadComm : Comm {
   void allreduce_sum_f32(float* buf, size_t count, hipStream_t st) override {
     allreduce(buf, count, st, [](float a, float b) { return a + b; });
   }
+  // fixed rank order, on the device (every rank's send buffer is on this one device)
+  void reduce_scatter_sum_f32(const float* send, float* recv, size_t count,
+                              hipStream_t st) override {
+    HIPCHK(hipStreamSynchronize(st));
+    g->ptrs[rank] = send;
+    g->barrier();
+    const int64_t rows8 = (int64_t)(count / 8);  // count is a multiple of 8 (b = 8..64 panels)
+    int r = 0;
+    bool first = true;
+    while (r < world) {  // 8 ranks, then the running sum + 7 more at a time
+      const float* parts[8];
+      int np = 0;
+      if (!first) parts[np++] = recv;
+      while (r < world && np < 8)
+        parts[np++] = static_cast<const float*>(g->ptrs[r++]) + (size_t)rank * count;
+      HIPCHK(n2v2r_launch_zsum(parts, np, recv, rows8, st));
+      first = false;
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    g->barrier();  // no rank rewrites its send buffer while another still reads it
+  }
   const char* kind() const override { return "thread"; }
 };
 
@@ -524,9 +611,9 @@ struct EigWorkspace {
   DevBuf rinv, flg, anyflag, gsmall, csmall;
   DevBuf rback;  // the per-cycle read-back, packed on the device before one copy to the host
   DevBuf tri, refl, ytri, tscr;               // GPU Rayleigh-Ritz: [d|e|tau], reflectors, Y_T
+  DevBuf trcoop;                              // multi-workgroup tridiagonalisation scratch
   DevBuf hband, band, varr, taua, rrerr;      // banded RR: band columns, band matrix, arrow
   DevBuf fcoef;                               // fp32 [-C R^-1; R^-1] of the apply pass
-  DevBuf cbpart;                              // [K][CB_NB][npad][8] column-block partials
   DevBuf dbgflag;                             // N2V2R_DEBUG_FINITE result flag
   DevBuf s2part;                              // [K][npad][8] XCD-split second-stage outputs
   DevBuf g2, pair_ra;                         // paired full passes: the two Grams, R of the first
@@ -771,9 +858,8 @@ double spmm_algo_bytes(int64_t nnz, bool unit, int64_t rows, int64_t panel_rows,
          4.0 * (double)(panel_rows + rows) * b;
 }
 
-// XCD-local column-block SpMM: b = 8 CSR panels of (N2V2R_CB_MIN_MB, N2V2R_CB_MAX_MB] (default
-// 8-160 MB: several XCD L2s' worth, inside the Infinity Cache); N2V2R_SPMM_CB=1 / 0 forces it
-// on / off (tests, A/B runs).
+// The column-block SpMM (the flat-window tiled form): b = 8 CSR panels beyond N2V2R_CB_MIN_MB
+// (default 8 MB: beyond one XCD's L2); N2V2R_SPMM_CB=1 / 0 forces it on / off (tests, A/B runs).
 // Read on every call, so a test can switch it between fits.
 bool col_blocks_wanted(const n2v2r_handle* h, int b);
 
@@ -818,11 +904,13 @@ struct Eig {
   int kry0 = 0;             // index of the first Krylov block of the current cycle
   bool full_first = false;  // N2V2R_EIG_FULL_FIRST_PASS
   bool band_rr = false;     // banded Rayleigh-Ritz (b = 8, c <= 512), else dense
-  bool col_blocks = false;  // XCD-local column-block SpMM (b = 8, large panels)
-  // column blocks as row tiles x block phases with LDS accumulators (no partials, no reduce;
-  // N2V2R_SPMM_TILE=0: the partial + reduce form)
-  bool tiled = false;
-  int tile_rows = 0, tile_rpw[2] = {0, 0}, tile_nb = CB_NB, tile_form = 0;
+  // the flat-window tiled column-block SpMM (b = 8, panels beyond 8 MB): row tiles with LDS
+  // accumulators walking tile_nb column-block phases, one launch per stage
+  bool col_blocks = false;
+  int tile_rows = 0, tile_nb = CB_NB;
+  // partitioned CSR handles: stage 2 as a reduce-scatter of this rank's column share (default)
+  // instead of all-gathers of every layer's stage-1 panel (N2V2R_DIST_STAGE2=gather)
+  bool rs_form = false;
   // XCD-split second SpMM stage (b = 8, one GPU): A_k Z_k lands in per-layer partials on the
   // XCDs of layer k; the image W = sum_k of them is stored by the next Gram pass that reads it
   // (the local first pass of the next expansion), or by materialize() before any other use
@@ -920,7 +1008,7 @@ struct Eig {
     EigWorkspace& w = h->ews;
     for (DevBuf* d : {&w.rinv, &w.flg, &w.anyflag, &w.gsmall, &w.csmall, &w.tri, &w.refl,
                       &w.ytri, &w.tscr, &w.hband, &w.band, &w.varr, &w.taua, &w.rrerr, &w.fcoef,
-                      &w.cbpart, &h->partial, &h->theta, &h->resid})
+                      &h->partial, &h->theta, &h->resid})
       if (d->p) HIPCHK(hipMemsetAsync(d->p, 0xFF, d->bytes, st));
     for (auto& d : w.pool) HIPCHK(hipMemsetAsync(d->p, 0xFF, d->bytes, st));
     for (auto& d : w.zk) HIPCHK(hipMemsetAsync(d->p, 0xFF, d->bytes, st));
@@ -984,6 +1072,64 @@ struct Eig {
       h->allreduce_f64(out, (size_t)A.count * A.width * B.count * B.width);
   }
 
+  // Partitioned CSR handles, reduce-scatter form (the default at W > 1):
+  // stage 1 as the gather form on the all-gathered X, then this rank's column share of stage 2,
+  // P = sum_k A_k[:, own rows] Z_k[own rows] over all (padded) global rows -- gathered from the
+  // rank's own Z rows only -- and ONE reduce-scatter of P into W's own rows: one all-gather + one
+  // reduce-scatter per application instead of K + 1 all-gathers.
+  void apply_M_rs(const float* xg, float* Wout) {
+    const int64_t ng = (int64_t)h->world * npad;
+    float* P = h->ews.zg.as<float>();  // the gather form's Z panels' buffer (>= ng x b)
+    double b0 = 0.0, b1 = 0.0;
+    for (int k = 0; k < K; ++k) b0 += layer_bytes(k, true);
+    int te;
+    if (col_blocks) {
+      SpmmTileArgs a{};
+      a.blk = h->ews.tblk.as<CsrBlk>();
+      a.ldx = a.ldy = 8;
+      a.n = n;
+      a.K = K;
+      a.nb = tile_nb;
+      a.sum = 0;
+      a.tile_rows = tile_rows;
+      for (int k = 0; k < K; ++k) {
+        a.X[k] = xg;
+        a.Y[k] = h->ews.zk[k]->as<float>();
+      }
+      te = tbeg();
+      HIPCHK(n2v2r_launch_spmm_tile(a, st));
+    } else {
+      SpmmArgs a{};
+      a.K = K;
+      a.ldx = a.ldy = b;
+      for (int k = 0; k < K; ++k) {
+        a.A[k] = h->layers[k]->csr_t();
+        a.X[k] = xg;
+        a.Y[k] = h->ews.zk[k]->as<float>();
+      }
+      te = tbeg();
+      HIPCHK(n2v2r_launch_spmm(a, b, st));
+    }
+    tend(te, 0, b0);
+    SpmmArgs s2{};
+    s2.K = K;
+    s2.sum = 1;
+    s2.ldx = s2.ldy = b;
+    for (int k = 0; k < K; ++k) {
+      const LayerDev& L = *h->layers[k];
+      s2.A[k] = L.csr_c();
+      s2.X[k] = h->ews.zk[k]->as<float>();
+      b1 += spmm_algo_bytes(L.c_nnz, s2.A[k].unit != 0, ng, npad, b);
+    }
+    s2.Y[0] = P;
+    te = tbeg();
+    HIPCHK(n2v2r_launch_spmm(s2, b, st));
+    tend(te, 1, b1);
+    h->comm->reduce_scatter_sum_f32(P, Wout, (size_t)npad * b, st);
+    algo_bytes += b0 + b1;
+    launches += 2;
+  }
+
   // W = M X = sum_k A_k (A_k^T X); X, W local, gathered panels for the column side
   void apply_M(const float* X, float* Wout) {
     const double t0 = now_ms();
@@ -1022,13 +1168,13 @@ struct Eig {
       t_spmm += now_ms() - t0;
       return;
     }
-    if (col_blocks && tiled) {
-      apply_M_tiled(xg, Wout, ng);
+    if (rs_form) {
+      apply_M_rs(xg, Wout);
       t_spmm += now_ms() - t0;
       return;
     }
     if (col_blocks) {
-      apply_M_cb(xg, Wout, ng);
+      apply_M_tiled(xg, Wout, ng);
       t_spmm += now_ms() - t0;
       return;
     }
@@ -1121,7 +1267,6 @@ struct Eig {
     a.nb = tile_nb;
     a.sum = 0;
     a.tile_rows = tile_rows;
-    a.form = tile_form;
     double b0 = 0.0, b1 = 0.0;
     for (int k = 0; k < K; ++k) {
       a.X[k] = xg;
@@ -1140,7 +1285,7 @@ struct Eig {
         a1.X[0] = xg;
         a1.Y[0] = a.Y[k];
         te = tbeg();
-        HIPCHK(n2v2r_launch_spmm_tile(a1, tile_rpw[0], st));
+        HIPCHK(n2v2r_launch_spmm_tile(a1, st));
         tend(te, 0, layer_bytes(k, true));
         h->gather_panel_async(h->ews.zk[k]->as<float>(),
                               h->ews.zg.as<float>() + (size_t)k * ng * b, b, k);
@@ -1148,7 +1293,7 @@ struct Eig {
       for (int k = 0; k < K; ++k) h->gather_wait(k);
     } else {
       te = tbeg();
-      HIPCHK(n2v2r_launch_spmm_tile(a, tile_rpw[0], st));
+      HIPCHK(n2v2r_launch_spmm_tile(a, st));
       tend(te, 0, b0);
     }
     SpmmTileArgs s2 = a;
@@ -1165,106 +1310,10 @@ struct Eig {
     }
     s2.Y[0] = Wout;
     te = tbeg();
-    HIPCHK(n2v2r_launch_spmm_tile(s2, tile_rpw[1], st));
+    HIPCHK(n2v2r_launch_spmm_tile(s2, st));
     tend(te, 1, b1);
     algo_bytes += b0 + b1;
     launches += 2;
-  }
-
-  // apply_M with the column-block SpMM (spmm.hip): per layer one launch per stage writing
-  // CB_NB partials, reduced in fixed (layer, block) order.
-  void apply_M_cb(const float* xg, float* Wout, int64_t ng) {
-    const int64_t pst = npad * 8;
-    float* part = h->ews.cbpart.as<float>();
-    static const bool overlap = [] {  // measured: cfg4 fit 2240 -> 2221 ms; =0 disables
-      const char* e = std::getenv("N2V2R_CB_OVERLAP");
-      return !(e && e[0] == '0');
-    }();
-    if (overlap && !h->comm) {
-      // stage-1 reduce of layer k on the side stream, beside the block launch of layer k + 1
-      // (and the stage-2 launch of layer k - 1); the same kernels and order of sums
-      if (!h->side) {
-        HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
-        for (hipEvent_t& e : h->cb_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      }
-      for (int k = 0; k < K; ++k) {
-        LayerDev& L = *h->layers[k];
-        SpmmCbArgs a{};
-        for (int j = 0; j < CB_NB; ++j) a.A[j] = (L.symmetric ? L.cb : L.cb_t).blk[j];
-        a.X = xg;
-        a.ldx = 8;
-        a.P = part + (size_t)k * CB_NB * pst;
-        a.pstride = pst;
-        const int te = tbeg();
-        HIPCHK(n2v2r_launch_spmm_cb(a, st));
-        tend(te, 0, layer_bytes(k, true));
-        HIPCHK(hipEventRecord(h->cb_ev[k], st));
-        HIPCHK(hipStreamWaitEvent(h->side, h->cb_ev[k], 0));
-        HIPCHK(n2v2r_launch_cb_reduce(a.P, CB_NB, pst, n, h->ews.zk[k]->as<float>(), 8, h->side));
-        HIPCHK(hipEventRecord(h->cb_ev[SPMM_MAX_LAYERS + k], h->side));
-      }
-      for (int k = 0; k < K; ++k) {
-        LayerDev& L = *h->layers[k];
-        HIPCHK(hipStreamWaitEvent(st, h->cb_ev[SPMM_MAX_LAYERS + k], 0));
-        SpmmCbArgs a{};
-        for (int j = 0; j < CB_NB; ++j) a.A[j] = L.cb.blk[j];
-        a.X = h->ews.zk[k]->as<float>();
-        a.ldx = 8;
-        a.P = part + (size_t)k * CB_NB * pst;
-        a.pstride = pst;
-        const int te = tbeg();
-        HIPCHK(n2v2r_launch_spmm_cb(a, st));
-        tend(te, 1, layer_bytes(k, false));
-      }
-      HIPCHK(n2v2r_launch_cb_reduce(part, K * CB_NB, pst, n, Wout, 8, st));
-      for (int k = 0; k < K; ++k) {
-        const LayerDev& L = *h->layers[k];
-        algo_bytes += spmm_algo_bytes(L.nnz, L.unit, n, n, b) +
-                      spmm_algo_bytes(L.symmetric ? L.nnz : L.t_nnz,
-                                      L.symmetric ? L.unit : L.t_unit, n, n, b);
-      }
-      launches += 2 * K + K + 1;
-      return;
-    }
-    for (int k = 0; k < K; ++k) {
-      LayerDev& L = *h->layers[k];
-      SpmmCbArgs a{};
-      for (int j = 0; j < CB_NB; ++j) a.A[j] = (L.symmetric ? L.cb : L.cb_t).blk[j];
-      a.X = xg;
-      a.ldx = 8;
-      a.P = part + (size_t)k * CB_NB * pst;
-      a.pstride = pst;
-      const int te = tbeg();
-      HIPCHK(n2v2r_launch_spmm_cb(a, st));
-      tend(te, 0, layer_bytes(k, true));
-      HIPCHK(n2v2r_launch_cb_reduce(a.P, CB_NB, pst, n, h->ews.zk[k]->as<float>(), 8, st));
-    }
-    for (int k = 0; k < K; ++k) {
-      LayerDev& L = *h->layers[k];
-      const float* zin = h->ews.zk[k]->as<float>();
-      if (h->comm) {
-        float* zgk = h->ews.zg.as<float>() + (size_t)k * ng * b;
-        h->gather_panel(h->ews.zk[k]->as<float>(), zgk, b);
-        zin = zgk;
-      }
-      SpmmCbArgs a{};
-      for (int j = 0; j < CB_NB; ++j) a.A[j] = L.cb.blk[j];
-      a.X = zin;
-      a.ldx = 8;
-      a.P = part + (size_t)k * CB_NB * pst;
-      a.pstride = pst;
-      const int te = tbeg();
-      HIPCHK(n2v2r_launch_spmm_cb(a, st));
-      tend(te, 1, layer_bytes(k, false));
-    }
-    HIPCHK(n2v2r_launch_cb_reduce(part, K * CB_NB, pst, n, Wout, 8, st));
-    for (int k = 0; k < K; ++k) {
-      const LayerDev& L = *h->layers[k];
-      algo_bytes += spmm_algo_bytes(L.nnz, L.unit, n, n, b) +
-                    spmm_algo_bytes(L.symmetric ? L.nnz : L.t_nnz,
-                                    L.symmetric ? L.unit : L.t_unit, n, n, b);
-    }
-    launches += 2 * K + K + 1;
   }
 
   // One fused BCGS + CholQR pass: G = [Q Z]^T Z -> R^{-1} -> Z <- [Q Z] [-C R^{-1}; R^{-1}],
@@ -1524,42 +1573,28 @@ struct Eig {
     }
     col_blocks = col_blocks_wanted(h, b);
     if (col_blocks) {
-      const char* te = std::getenv("N2V2R_SPMM_TILE");  // read per fit (A/B runs, tests)
-      tiled = !(te && te[0] == '0');
-      // tiled forms: packed flat windows (default), row groups (N2V2R_TILE_FLAT=0) or two row
-      // groups per wave step at one workgroup per CU (N2V2R_TILE_PAIR=2)
-      const char* tf = std::getenv("N2V2R_TILE_FLAT");
-      const char* tp = std::getenv("N2V2R_TILE_PAIR");
-      tile_form = !tiled ? 0 : (tp && tp[0] == '2') ? 2 : (tf && tf[0] == '0') ? 0 : 1;
-      // column blocks (phases) per layer, N2V2R_SPMM_TILE_NB = 4, 8, 16 or 32.  Flat form:
-      // panel blocks of <= 2 MB by default, so a phase's block stays in the XCD's 4 MB L2 beside
-      // the index stream (cfg4: 16 blocks, 0.748 ms per stage launch; 8 blocks 0.896, 32
-      // blocks 0.817; 4 MB blocks left 31 % of the gathers missing L2).  Row-group forms: 8
-      // (their rows get shorter with every block: cfg4 0.807 ms at 8, 0.923 at 16).
+      // the flat-window tiled SpMM: column blocks (phases) per layer of <= 2 MB of panel, so a
+      // phase's block stays in the XCD's 4 MB L2 beside the index stream (cfg4: 16 blocks,
+      // 0.748 ms per stage launch; 8 blocks 0.896, 32 blocks 0.817: 4 MB blocks left 31 % of
+      // the gathers missing L2), at most 32 (cfg5's 320 MB panel: 9.47 ms per stage launch at 32
+      // blocks of 10 MB, 11.53 at 64 of 5 MB -- a window's run per block gets too short).
+      // N2V2R_SPMM_TILE_NB = 4..64 overrides (read per fit).
+      int nb_auto = 4;
+      while (nb_auto < 32 && (double)nglob * 32.0 / nb_auto > 2.0 * 1024 * 1024) nb_auto *= 2;
       const char* tn_ = std::getenv("N2V2R_SPMM_TILE_NB");
-      // (at most 32 by default: cfg5's 320 MB panel ran 9.47 ms per stage launch at 32 blocks
-      // of 10 MB, 11.53 at 64 of 5 MB -- a window's run per block gets too short)
-      int nb_auto = 8;
-      if (tile_form == 1) {
-        nb_auto = 4;
-        while (nb_auto < 32 && (double)nglob * 32.0 / nb_auto > 2.0 * 1024 * 1024)
-          nb_auto *= 2;
-      }
-      tile_nb = tiled ? (tn_ ? std::atoi(tn_) : nb_auto) : CB_NB;
+      tile_nb = tn_ ? std::atoi(tn_) : nb_auto;
       if (tile_nb != 4 && tile_nb != 8 && tile_nb != 16 && tile_nb != 32 && tile_nb != 64)
         tile_nb = nb_auto;
       for (auto& Lp : h->layers)
-        col_blocks = ensure_col_blocks(*Lp, nglob, st, tile_nb, tile_form == 1) && col_blocks;
-      tiled = tiled && col_blocks;
-      if (tile_form == 1)  // packed only where the column bits fit (else plain columns)
-        for (auto& Lp : h->layers)
-          if (Lp->cb.cbits == 0 || (!Lp->symmetric && Lp->cb_t.cbits == 0)) tile_form = 0;
-      if (col_blocks && !tiled)
-        h->ews.cbpart.ensure(sizeof(float) * (size_t)K * CB_NB * npad * 8);
-      if (tiled) {
+        col_blocks = ensure_col_blocks(*Lp, nglob, st, tile_nb, true) && col_blocks;
+      // packed entries need the in-block column bits to fit beside the 5 row bits (always, for
+      // N < 2^27 per block); otherwise the row kernel runs
+      for (auto& Lp : h->layers)
+        if (Lp->cb.cbits == 0 || (!Lp->symmetric && Lp->cb_t.cbits == 0)) col_blocks = false;
+      if (col_blocks) {
         int ncu = 0;
         HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
-        tile_rows = n2v2r_spmm_tile_rows(n, ncu, tile_form == 2 ? 1 : 2);
+        tile_rows = n2v2r_spmm_tile_rows(n, ncu, 2);
         const int nb = tile_nb;
         std::vector<CsrBlk> hb((size_t)2 * K * nb);
         for (int k = 0; k < K; ++k) {
@@ -1569,13 +1604,18 @@ struct Eig {
             hb[(size_t)(K + k) * nb + j] = L.cb.blk[j];
           }
         }
-        tile_rpw[0] = n2v2r_cb_rpw(hb.data(), nb, n);
-        tile_rpw[1] = n2v2r_cb_rpw(hb.data() + (size_t)K * nb, nb, n);
         h->ews.tblk.ensure(sizeof(CsrBlk) * hb.size());
         HIPCHK(hipMemcpyAsync(h->ews.tblk.p, hb.data(), sizeof(CsrBlk) * hb.size(),
                               hipMemcpyHostToDevice, st));
         HIPCHK(hipStreamSynchronize(st));  // hb dies here
       }
+    }
+    rs_form = false;
+    if (h->comm && !h->dense_layers()) {
+      const char* e = std::getenv("N2V2R_DIST_STAGE2");  // read per fit (tests, A/B runs)
+      rs_form = !(e && std::strcmp(e, "gather") == 0);
+      if (rs_form)
+        for (auto& Lp : h->layers) ensure_colcsr(*Lp, nglob, (int64_t)h->world * npad, st);
     }
     split2 = split2_wanted(h, b) && !col_blocks;
     pending = nullptr;
@@ -1593,6 +1633,7 @@ struct Eig {
                                                         (size_t)c_max * (c_max / 8 + 2) * 9));
     h->ews.ytri.ensure(sizeof(double) * (size_t)c_max * keep);
     h->ews.tscr.ensure(sizeof(double) * 6 * (size_t)((keep + 63) / 64 * 64) * c_max);
+    h->ews.trcoop.ensure(n2v2r_rr_tridiag_scratch_bytes(c_max));
     h->ews.rinv.ensure(sizeof(double) * 64 * 64);
     h->ews.fcoef.ensure(sizeof(float) * (size_t)(c_max + 64) * 64);
     h->ews.flg.ensure(sizeof(int) * 256);
@@ -1754,8 +1795,12 @@ struct Eig {
         tn(blocks(Q, 0, nq), blocks(W, 0, nq), h->ews.gsmall.as<double>(), nullptr);
         dbg(h->ews.gsmall.p, (int64_t)c * c, true, "projected matrix H = Q^T W");
         lds_poison();
+        // thread-communicator ranks share one device: their concurrent launches of the
+        // multi-workgroup form could not all be resident, so they keep the one-workgroup kernel
+        const bool shared_device = h->comm && std::strcmp(h->comm->kind(), "thread") == 0;
         HIPCHK(n2v2r_launch_rr_tridiag(h->ews.gsmall.as<double>(), c, trid, trid + c_max,
-                                       trid + 2 * c_max, h->ews.refl.as<double>(), st));
+                                       trid + 2 * c_max, h->ews.refl.as<double>(),
+                                       shared_device ? nullptr : h->ews.trcoop.p, st));
         dbg(trid, c, true, "tridiagonal diagonal");
         dbg(trid + c_max, c - 1, true, "tridiagonal off-diagonal");
         lds_poison();
@@ -2082,10 +2127,7 @@ struct Eig {
       stats->est_scale = est_scale;
       stats->lean_checks = lean_checks;
       stats->pool_blocks = (int)h->ews.pool.size();
-      stats->spmm_form = h->dense_layers() ? 4
-                         : (col_blocks && tiled) ? (tile_form == 1 ? 5 : 3)
-                         : col_blocks ? 2
-                         : split2 ? 1 : 0;
+      stats->spmm_form = h->dense_layers() ? 4 : col_blocks ? 5 : split2 ? 1 : 0;
       tsum(stats);
     }
     return (conv == d || stagnated) ? N2V2R_OK : N2V2R_ERR_NO_CONVERGENCE;
@@ -2120,19 +2162,14 @@ bool col_blocks_wanted(const n2v2r_handle* h, int b) {
   // 0.56 at a 3.2 MB panel (N = 100k: the panel already fits one L2), 1.35 at 9.6 MB,
   // 1.61 at 32 MB, 1.16 at 96 MB, 0.93 at 320 MB (beyond the Infinity Cache the gathers go
   // to HBM either way and the partials only add traffic)
-  // round 3: the flat-window tiled form (the default tiled form) also wins beyond the Infinity
-  // Cache -- each phase gathers from one panel block, which the Infinity Cache holds even when
-  // the whole panel does not (cfg5 on one GPU, 320 MB panel: 9.5 vs 11.5 ms per stage launch)
-  // -- so its window has no upper end; the partials / row-group forms keep 160 MB
-  const char* te = std::getenv("N2V2R_SPMM_TILE");
-  const char* tf = std::getenv("N2V2R_TILE_FLAT");
-  const char* tp = std::getenv("N2V2R_TILE_PAIR");
-  const bool flat = !(te && te[0] == '0') && !(tf && tf[0] == '0') && !(tp && tp[0] == '2');
+  // round 3: the flat-window tiled form also wins beyond the Infinity Cache -- each phase
+  // gathers from one panel block, which the Infinity Cache holds even when the whole panel does
+  // not (cfg5 on one GPU, 320 MB panel: 9.5 vs 11.5 ms per stage launch) -- so the window has no
+  // upper end
   const char* m = std::getenv("N2V2R_CB_MIN_MB");
-  const char* x = std::getenv("N2V2R_CB_MAX_MB");
-  const double min_mb = m ? atof(m) : 8.0, max_mb = x ? atof(x) : (flat ? 1e12 : 160.0);
+  const double min_mb = m ? atof(m) : 8.0;
   const double panel = 4.0 * b * (double)h->n;
-  return panel > min_mb * 1e6 && panel <= max_mb * 1e6;
+  return panel > min_mb * 1e6;
 }
 }  // namespace
 
@@ -2284,8 +2321,11 @@ int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const in
       h->set_err("layer %d: indptr must start at 0 and end at nnz", k);
       return N2V2R_ERR_BAD_ARG;
     }
-    if (nnz > (int64_t)INT32_MAX) {  // the transpose sort's payload is an int32 entry index
-      h->set_err("layer %d: more than 2^31 - 1 entries", k);
+    // the GPU transpose (and the symmetry test built on it) sorts int32 entry indices: a layer
+    // that needs it is limited to 2^31 - 1 entries; N2V2R_SYM_YES layers are not
+    if (symmetric != N2V2R_SYM_YES && nnz > (int64_t)INT32_MAX) {
+      h->set_err("layer %d: more than 2^31 - 1 entries need symmetric = N2V2R_SYM_YES (the GPU "
+                 "transpose / symmetry test sorts int32 entry indices)", k);
       return N2V2R_ERR_BAD_ARG;
     }
     for (int64_t r = 0; r < n; ++r)
@@ -2570,7 +2610,7 @@ int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_sta
     int st = 0, b = 0;
     // the fit's tiled column-block configuration, reused for the embedding images below
     bool ytile = false;
-    int ytile_rows = 0, ytile_nb = 0, ytile_form = 0, ytile_rpw = 0;
+    int ytile_rows = 0, ytile_nb = 0;
     for (int attempt = 0;; ++attempt) {
       Eig eig{};
       eig.h = h;
@@ -2590,11 +2630,9 @@ int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_sta
         continue;
       }
       b = eig.b;
-      ytile = eig.col_blocks && eig.tiled && eig.b == 8;
+      ytile = eig.col_blocks && eig.b == 8;
       ytile_rows = eig.tile_rows;
       ytile_nb = eig.tile_nb;
-      ytile_form = eig.tile_form;
-      ytile_rpw = eig.tile_rpw[0];
       break;
     }
     // deterministic signs: largest-magnitude entry of every column of U positive
@@ -2657,7 +2695,6 @@ int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_sta
       a.nb = ytile_nb;
       a.sum = 0;
       a.tile_rows = ytile_rows;
-      a.form = ytile_form;
       for (int q = 0; q * 8 < ldu; ++q) {
         HIPCHK(hipMemcpy2DAsync(panel.p, sizeof(float) * 8, ug + q * 8, sizeof(float) * ldu,
                                 sizeof(float) * 8, ng, hipMemcpyDeviceToDevice, h->stream));
@@ -2665,7 +2702,7 @@ int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_sta
           a.X[k] = panel.as<float>();
           a.Y[k] = h->Y.as<float>() + (size_t)k * h->npad * ldu + q * 8;
         }
-        HIPCHK(n2v2r_launch_spmm_tile(a, ytile_rpw, h->stream));
+        HIPCHK(n2v2r_launch_spmm_tile(a, h->stream));
       }
       for (int k = 0; k < h->K; ++k)
         HIPCHK(n2v2r_launch_scale_cols(h->Y.as<float>() + (size_t)k * h->npad * ldu, ldu,
@@ -3094,8 +3131,10 @@ int n2v2r_rr_top(n2v2r_handle* h, int c, const double* H, int p, double* w, floa
     HIPCHK(hipMemcpyAsync(a.p, H, sizeof(double) * c * c, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));  // pageable source: complete before the kernel
     double* t = tri.as<double>();
+    DevBuf trs;
+    trs.ensure(n2v2r_rr_tridiag_scratch_bytes(c));
     HIPCHK(n2v2r_launch_rr_tridiag(a.as<double>(), c, t, t + c, t + 2 * c, refl.as<double>(),
-                                   h->stream));
+                                   trs.p, h->stream));
     DevBuf wd, scr;
     wd.ensure(sizeof(double) * p);
     scr.ensure(sizeof(double) * 6 * (size_t)((p + 63) / 64 * 64) * c);
@@ -3175,43 +3214,51 @@ int n2v2r_spmm_col_blocks(const n2v2r_handle* h, int b) {
   return col_blocks_wanted(h, b) ? 1 : 0;
 }
 
-int n2v2r_probe_spmm_stage2(n2v2r_handle* h, int mode, int reps, double* avg_ms) {
-  return guarded(h, [&]() -> int {
-    if (h->K < 1 || h->K > 8 || h->comm || h->dense_layers() || reps < 1 || !avg_ms ||
-        mode < 0 || mode > 4)
-      return N2V2R_ERR_BAD_ARG;
-    for (auto& L : h->layers)
-      if (!L->loaded) return N2V2R_ERR_BAD_ARG;
-    const int64_t n = h->n;
-    DevBuf z, y;
-    z.ensure(sizeof(float) * n * 8 * h->K, h->stream);
-    y.ensure(sizeof(float) * n * 8 * h->K, h->stream);
-    HIPCHK(n2v2r_launch_fill_normal(z.as<float>(), 8, n * h->K, 7, nullptr, nullptr, 0, h->stream));
-    SpmmArgs s{};
-    s.K = h->K;
-    s.sum = mode == 0 ? 1 : 0;
-    s.split = (mode == 2 || mode == 4) ? 1 : 0;
-    s.ldx = s.ldy = 8;
-    for (int k = 0; k < h->K; ++k) {
-      s.A[k] = h->layers[k]->csr();
-      s.X[k] = z.as<float>() + (size_t)(mode >= 3 ? 0 : k) * n * 8;  // 3, 4: one shared panel
-      s.Y[k] = y.as<float>() + (size_t)(mode == 0 ? 0 : k) * n * 8;
-    }
-    HIPCHK(n2v2r_launch_spmm(s, 8, h->stream));
-    hipEvent_t e0, e1;
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipEventCreate(&e1));
-    HIPCHK(hipEventRecord(e0, h->stream));
-    for (int r = 0; r < reps; ++r) HIPCHK(n2v2r_launch_spmm(s, 8, h->stream));
-    HIPCHK(hipEventRecord(e1, h->stream));
-    HIPCHK(hipEventSynchronize(e1));
-    float ms = 0.f;
-    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    *avg_ms = (double)ms / reps;
-    return N2V2R_OK;
-  });
+// The flat-window tiled SpMM of layer k (A_k X, or A_k^T X) with `nb` column blocks (0: the fit's
+// rule, panel blocks of <= 2 MB, at most 32) from device panels, timed with HIP events over `reps`
+// launches after a warm-up.  N2V2R_ERR_BAD_ARG when the layer cannot take packed blocks.
+static int time_tiled(n2v2r_handle* h, int k, int transpose, int nb, const float* xd, float* yd,
+                      int reps, double* avg_ms) {
+  if (nb <= 0) {
+    nb = 4;
+    while (nb < 32 && (double)h->n * 32.0 / nb > 2.0 * 1024 * 1024) nb *= 2;
+  }
+  if (nb != 4 && nb != 8 && nb != 16 && nb != 32 && nb != 64) return N2V2R_ERR_BAD_ARG;
+  LayerDev& L = *h->layers[k];
+  if (!ensure_col_blocks(L, h->n, h->stream, nb, true)) return N2V2R_ERR_BAD_ARG;
+  const LayerDev::ColBlocks& cbs = (transpose && !L.symmetric) ? L.cb_t : L.cb;
+  if (cbs.cbits == 0) return N2V2R_ERR_BAD_ARG;
+  DevBuf tb;
+  tb.ensure(sizeof(CsrBlk) * nb);
+  HIPCHK(hipMemcpyAsync(tb.p, cbs.blk, sizeof(CsrBlk) * nb, hipMemcpyHostToDevice, h->stream));
+  int ncu = 0;
+  HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
+  SpmmTileArgs a{};
+  a.blk = tb.as<CsrBlk>();
+  a.X[0] = xd;
+  a.Y[0] = yd;
+  a.ldx = 8;
+  a.ldy = 8;
+  a.n = h->nloc;
+  a.K = 1;
+  a.nb = nb;
+  a.sum = 0;
+  a.tile_rows = n2v2r_spmm_tile_rows(h->nloc, ncu, 2);
+  HIPCHK(n2v2r_launch_spmm_tile(a, h->stream));  // warm-up
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  HIPCHK(hipEventRecord(e0, h->stream));
+  for (int r = 0; r < reps; ++r) HIPCHK(n2v2r_launch_spmm_tile(a, h->stream));
+  HIPCHK(hipEventRecord(e1, h->stream));
+  HIPCHK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (avg_ms) *avg_ms = (double)ms / reps;
+  HIPCHK(hipStreamSynchronize(h->stream));  // tb dies here
+  return N2V2R_OK;
 }
 
 int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, const float* X,
@@ -3250,44 +3297,20 @@ int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, con
       HIPCHK(hipStreamSynchronize(h->stream));
       return N2V2R_OK;
     }
-    if (col_blocks_wanted(h, b) && ensure_col_blocks(*h->layers[k], h->n, h->stream)) {
-      // column-block SpMM of one layer: the block launch + the fixed-order partial reduce,
-      // timed together (the same algorithmic bytes as the row kernel; the partials are extra)
-      LayerDev& Lm = *h->layers[k];
-      const int64_t pst = std::max<int64_t>(h->nloc, 1) * 8;
-      DevBuf part;
-      part.ensure(sizeof(float) * CB_NB * pst, h->stream);
-      SpmmCbArgs a{};
-      const LayerDev::ColBlocks& cbs = (transpose && !Lm.symmetric) ? Lm.cb_t : Lm.cb;
-      for (int j = 0; j < CB_NB; ++j) a.A[j] = cbs.blk[j];
-      a.X = xd.as<float>();
-      a.ldx = 8;
-      a.P = part.as<float>();
-      a.pstride = pst;
-      auto once = [&]() {
-        HIPCHK(n2v2r_launch_spmm_cb(a, h->stream));
-        HIPCHK(n2v2r_launch_cb_reduce(a.P, CB_NB, pst, h->nloc, yd.as<float>(), 8, h->stream));
-      };
-      once();  // warm-up
-      hipEvent_t e0, e1;
-      HIPCHK(hipEventCreate(&e0));
-      HIPCHK(hipEventCreate(&e1));
-      HIPCHK(hipEventRecord(e0, h->stream));
-      for (int r = 0; r < reps; ++r) once();
-      HIPCHK(hipEventRecord(e1, h->stream));
-      HIPCHK(hipEventSynchronize(e1));
-      float ms = 0.f;
-      HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-      (void)hipEventDestroy(e0);
-      (void)hipEventDestroy(e1);
-      if (avg_ms) *avg_ms = (double)ms / reps;
-      const CsrDev c0 = transpose ? Lm.csr_t() : Lm.csr();
-      if (algo_bytes) *algo_bytes = spmm_algo_bytes(c0.nnz, c0.unit != 0, h->nloc, h->n, b);
-      if (Y)
-        HIPCHK(hipMemcpyAsync(Y, yd.p, sizeof(float) * h->nloc * b, hipMemcpyDeviceToHost,
-                              h->stream));
-      HIPCHK(hipStreamSynchronize(h->stream));
-      return N2V2R_OK;
+    if (col_blocks_wanted(h, b)) {
+      // the flat-window tiled SpMM of one layer (the fit's form at this panel size)
+      double ms = 0.0;
+      const int st_ = time_tiled(h, k, transpose, 0, xd.as<float>(), yd.as<float>(), reps, &ms);
+      if (st_ == N2V2R_OK) {
+        const CsrDev c0 = transpose ? L.csr_t() : L.csr();
+        if (avg_ms) *avg_ms = ms;
+        if (algo_bytes) *algo_bytes = spmm_algo_bytes(c0.nnz, c0.unit != 0, h->nloc, h->n, b);
+        if (Y)
+          HIPCHK(hipMemcpyAsync(Y, yd.p, sizeof(float) * h->nloc * b, hipMemcpyDeviceToHost,
+                                h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        return N2V2R_OK;
+      }
     }
     SpmmArgs a{};
     a.K = 1;
@@ -3322,62 +3345,18 @@ int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, con
 }
 
 
-// The flat-window tiled SpMM of one layer at panel width b (8 or 16) with `nb` column blocks
-// (0: the fit's default rule, panel blocks of <= 2 MB, at most 32), timed alone with HIP events.
 int n2v2r_bench_spmm_tiled(n2v2r_handle* h, int k, int transpose, int b, int nb, int reps,
                            const float* X, float* Y, double* avg_ms) {
   return guarded(h, [&]() -> int {
-    if (k < 0 || k >= h->K || !h->layers[k]->loaded || h->layers[k]->dense || (b != 8 && b != 16) ||
+    if (k < 0 || k >= h->K || !h->layers[k]->loaded || h->layers[k]->dense || b != 8 ||
         reps < 1 || !X || h->comm)
       return N2V2R_ERR_BAD_ARG;
-    if (nb <= 0) {
-      nb = 4;
-      while (nb < 32 && (double)h->n * 4.0 * b / nb > 2.0 * 1024 * 1024) nb *= 2;
-    }
-    if (nb != 4 && nb != 8 && nb != 16 && nb != 32 && nb != 64) return N2V2R_ERR_BAD_ARG;
-    LayerDev& L = *h->layers[k];
-    if (!ensure_col_blocks(L, h->n, h->stream, nb, true)) return N2V2R_ERR_BAD_ARG;
-    const LayerDev::ColBlocks& cbs = (transpose && !L.symmetric) ? L.cb_t : L.cb;
-    if (cbs.cbits == 0) return N2V2R_ERR_BAD_ARG;
-    DevBuf xd, yd, tb;
+    DevBuf xd, yd;
     xd.ensure(sizeof(float) * h->n * b);
     yd.ensure(sizeof(float) * std::max<int64_t>(h->nloc, 1) * b);
-    tb.ensure(sizeof(CsrBlk) * nb);
     HIPCHK(hipMemcpyAsync(xd.p, X, sizeof(float) * h->n * b, hipMemcpyHostToDevice, h->stream));
-    HIPCHK(hipMemcpyAsync(tb.p, cbs.blk, sizeof(CsrBlk) * nb, hipMemcpyHostToDevice, h->stream));
-    int ncu = 0;
-    HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
-    SpmmTileArgs a{};
-    a.blk = tb.as<CsrBlk>();
-    a.X[0] = xd.as<float>();
-    a.Y[0] = yd.as<float>();
-    a.ldx = b;
-    a.ldy = b;
-    a.n = h->nloc;
-    a.K = 1;
-    a.nb = nb;
-    a.sum = 0;
-    a.form = 1;
-    a.b = b;
-    a.tile_rows = n2v2r_spmm_tile_rows(h->nloc, ncu, 2);
-    if (b == 16) {
-      const char* tr = std::getenv("N2V2R_T16_ROWS");
-      a.tile_rows = std::min(a.tile_rows, tr ? std::atoi(tr) : 1024);
-      a.tile_rows = std::max(CB_WIN, a.tile_rows / CB_WIN * CB_WIN);
-    }
-    HIPCHK(n2v2r_launch_spmm_tile(a, 0, h->stream));  // warm-up
-    hipEvent_t e0, e1;
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipEventCreate(&e1));
-    HIPCHK(hipEventRecord(e0, h->stream));
-    for (int r = 0; r < reps; ++r) HIPCHK(n2v2r_launch_spmm_tile(a, 0, h->stream));
-    HIPCHK(hipEventRecord(e1, h->stream));
-    HIPCHK(hipEventSynchronize(e1));
-    float ms = 0.f;
-    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    if (avg_ms) *avg_ms = (double)ms / reps;
+    const int st_ = time_tiled(h, k, transpose, nb, xd.as<float>(), yd.as<float>(), reps, avg_ms);
+    if (st_ != N2V2R_OK) return st_;
     if (Y)
       HIPCHK(hipMemcpyAsync(Y, yd.p, sizeof(float) * h->nloc * b, hipMemcpyDeviceToHost,
                             h->stream));

@@ -14,7 +14,9 @@
 //                        (c x ld) the NN kernels consume.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -246,6 +248,217 @@ __global__ __launch_bounds__(NT) void rr_tridiag_kernel(double* __restrict__ A, 
     t = tn;
     m = mn;
   }
+}
+
+// ---- the same reduction spread over G = PR x nt workgroups (one per CU) ---------------------
+// The c x c matrix is cut into 32 x 32 tiles (nt per dimension) that stay in LDS for the whole
+// launch: workgroup (pr, pc) owns the column tile pc and the row tiles pr, pr + PR, ...
+// (block-cyclic, so the active trailing block stays spread as it shrinks), i.e. up to
+// ceil(nt / PR) tiles (12 at c = 768, PR = 2: 99 KB).  Each step k (pivot o = k + 1):
+//   every workgroup, redundantly and bit-identically, forms p = t sum_pr part[pr] (the previous
+//   pass's column partials, fixed order), w = p - (t/2)(p.v) v, the updated pivot row
+//   (published by its owners) -> d[o] and the next reflector vn;
+//   then updates its own tiles B -= v w^T + w v^T on rows/columns >= o+1 and accumulates the
+//   column partials of the next matvec B' vn, which it publishes with the new pivot row o+1.
+// One grid barrier per step.  Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first
+// row of the sc1 table): every published double is an agent-scope relaxed atomic store
+// (global_store sc1), every storing wave waits vmcnt(0), a workgroup barrier, then ONE lane
+// adds to the monotonic counter; the poller reads it with sc1 loads, the workgroup barrier
+// releases the other waves, and every load of published data is an sc1 load.  Partials and the
+// pivot row are double-buffered by step parity (a buffer is rewritten only two barriers after
+// it was read).  The spin is bounded: a workgroup that waits ~seconds gives up, sets *err and
+// writes NaN to d[0] (the caller's Ritz values then fail), so the launch always drains.
+#define TRC_TS 32
+#define TRC_LD 33
+#define TRC_NT 256
+
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __longlong_as_double(__hip_atomic_load(reinterpret_cast<const long long*>(p),
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1(double* p, double x) {
+  __hip_atomic_store(reinterpret_cast<long long*>(p), __double_as_longlong(x), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// returns true when the wait timed out
+__device__ __forceinline__ bool trc_grid_barrier(unsigned* ctr, unsigned target, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int f = 0;
+    long it = 0;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (++it > (1l << 24)) {
+        f = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    *flag = f;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+__global__ __launch_bounds__(TRC_NT) void rr_tridiag_coop_kernel(
+    const double* __restrict__ A, int c, int PR, double* __restrict__ dd, double* __restrict__ ee,
+    double* __restrict__ tau, double* __restrict__ V, double* part /* [2][PR][c] */,
+    double* rowbuf /* [2][c] */, unsigned* ctr, int* err) {
+  constexpr int NW = TRC_NT / 64;
+  extern __shared__ double lds[];
+  const int nt = (c + TRC_TS - 1) / TRC_TS;
+  const int G = gridDim.x;
+  const int pc = blockIdx.x % nt, pr = blockIdx.x / nt;
+  const int ntr = (nt - pr + PR - 1) / PR;  // row tiles pr + PR q, q < ntr
+  double* T = lds;                                   // [ntr][32][33]
+  double* v = T + (size_t)ntr * TRC_TS * TRC_LD;     // [c], global indices
+  double* w = v + c;
+  double* vn = w + c;
+  double* p = vn + c;
+  double* row = p + c;
+  double* accs = row + c;                            // [8][32]
+  __shared__ double red[NW];
+  __shared__ int flag;
+  const int tid = threadIdx.x, tx = tid & 31, ty = tid >> 5;
+  const int J = TRC_TS * pc + tx;  // this thread's column
+  const bool lead = blockIdx.x == 0;
+
+  auto bsum = [&](double x) -> double {
+    x = wave_sum(x);
+    __syncthreads();
+    if ((tid & 63) == 0) red[tid >> 6] = x;
+    __syncthreads();
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) s += red[q];
+    return s;
+  };
+  // reflector from x[lo..c) in place (x[lo] = 1 after), row k of V (the leader writes it)
+  auto make_reflector = [&](double* x, int lo, int k) -> double {
+    double part2 = 0.0;
+    for (int i = lo + 1 + tid; i < c; i += TRC_NT) part2 += x[i] * x[i];
+    const double x0 = x[lo];
+    const double sig = bsum(part2);
+    double t = 0.0, beta = x0, scale = 0.0;
+    if (sig != 0.0) {
+      const double nrm = sqrt(x0 * x0 + sig);
+      beta = (x0 >= 0) ? -nrm : nrm;
+      t = (beta - x0) / beta;
+      scale = 1.0 / (x0 - beta);
+    }
+    double* vk = V + (int64_t)k * c - lo;
+    for (int i = lo + tid; i < c; i += TRC_NT) {
+      const double vi = (i == lo) ? 1.0 : x[i] * scale;
+      x[i] = vi;
+      if (lead) vk[i] = vi;
+    }
+    if (lead && tid == 0) {
+      ee[k] = beta;
+      tau[k] = t;
+    }
+    __syncthreads();
+    return t;
+  };
+  // the WG's tiles on rows / columns >= lo: optional rank-2 update (v, w), column partials of
+  // the product with mv, published to part[par][pr][.], and the pivot row lo to rowbuf[par]
+  auto pass = [&](int lo, bool upd, const double* mv, int par) {
+    const bool jok = J >= lo && J < c;
+    const double vJ = (upd && jok) ? v[J] : 0.0, wJ = (upd && jok) ? w[J] : 0.0;
+    const int rlo = lo & (TRC_TS - 1), blo = lo / TRC_TS;
+    double acc = 0.0;
+    for (int q = 0; q < ntr; ++q) {
+      const int bi = pr + PR * q;
+      if (bi < blo) continue;
+      double* tile = T + (size_t)q * TRC_TS * TRC_LD;
+#pragma unroll
+      for (int u = 0; u < TRC_TS / 8; ++u) {
+        const int rr = ty + 8 * u, R = TRC_TS * bi + rr;
+        if (R >= lo && R < c && jok) {
+          double a = tile[rr * TRC_LD + tx];
+          if (upd) {
+            a -= v[R] * wJ + w[R] * vJ;
+            tile[rr * TRC_LD + tx] = a;
+          }
+          acc += a * mv[R];
+          if (R == lo) st_sc1(rowbuf + (size_t)par * c + J, a);
+        }
+      }
+    }
+    accs[ty * TRC_TS + tx] = acc;
+    __syncthreads();
+    if (ty == 0 && J < c) {
+      double sacc = 0.0;
+#pragma unroll
+      for (int y = 0; y < 8; ++y) sacc += accs[y * TRC_TS + tx];
+      st_sc1(part + ((size_t)par * PR + pr) * c + J, sacc);
+    }
+  };
+
+  // tiles in: symmetrised as the one-workgroup kernel does
+  for (int q = 0; q < ntr; ++q) {
+    const int bi = pr + PR * q;
+    double* tile = T + (size_t)q * TRC_TS * TRC_LD;
+    for (int rr = ty; rr < TRC_TS; rr += 8) {
+      const int R = TRC_TS * bi + rr;
+      tile[rr * TRC_LD + tx] =
+          (R < c && J < c) ? 0.5 * (A[(int64_t)R * c + J] + A[(int64_t)J * c + R]) : 0.0;
+    }
+  }
+  // reflector 0 from row 0, then the first matvec (no update)
+  for (int i = 1 + tid; i < c; i += TRC_NT) v[i] = 0.5 * (A[i] + A[(int64_t)i * c]);
+  if (lead && tid == 0) dd[0] = A[0];
+  __syncthreads();
+  double t = make_reflector(v, 1, 0);
+  pass(1, false, v, 0);
+  unsigned nbar = 1;
+  bool failed = trc_grid_barrier(ctr, (unsigned)G * nbar, &flag);
+  for (int k = 0; !failed; ++k) {
+    const int o = k + 1, par = k & 1;
+    for (int i = o + tid; i < c; i += TRC_NT) {
+      double sp = 0.0;
+      for (int q = 0; q < PR; ++q) sp += ld_sc1(part + ((size_t)par * PR + q) * c + i);
+      p[i] = t * sp;
+      row[i] = ld_sc1(rowbuf + (size_t)par * c + i);
+    }
+    __syncthreads();
+    double pp = 0.0;
+    for (int i = o + tid; i < c; i += TRC_NT) pp += p[i] * v[i];
+    const double half = 0.5 * t * bsum(pp);
+    for (int i = o + tid; i < c; i += TRC_NT) w[i] = p[i] - half * v[i];
+    __syncthreads();
+    const double vo = v[o], wo = w[o];
+    if (lead && tid == 0) dd[o] = row[o] - 2.0 * vo * wo;
+    for (int i = o + 1 + tid; i < c; i += TRC_NT) vn[i] = row[i] - vo * w[i] - wo * v[i];
+    __syncthreads();
+    if (c - o == 2) {  // the last 2 x 2 block
+      if (lead && tid == 0) {
+        ee[o] = vn[o + 1];
+        tau[o] = 0.0;
+      }
+      const int R = c - 1, bi = R / TRC_TS;
+      if (pc == bi && bi % PR == pr && tx == (R & 31) && ty == ((R & 31) & 7)) {
+        const double b11 = T[((size_t)((bi - pr) / PR) * TRC_TS + (R & 31)) * TRC_LD + tx];
+        dd[R] = b11 - 2.0 * v[R] * w[R];
+      }
+      break;
+    }
+    const double tn = make_reflector(vn, o + 1, o);
+    pass(o + 1, true, vn, par ^ 1);
+    // every read of v in the pass precedes the partials' barrier inside it
+    for (int i = o + 1 + tid; i < c; i += TRC_NT) v[i] = vn[i];
+    t = tn;
+    failed = trc_grid_barrier(ctr, (unsigned)G * ++nbar, &flag);
+  }
+  if (failed && tid == 0) {
+    __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st_sc1(dd, __builtin_nan(""));
+  }
+}
+
+extern "C" size_t n2v2r_rr_tridiag_scratch_bytes(int c) {
+  return sizeof(double) * ((size_t)2 * 4 * c + (size_t)2 * c) + 64;
 }
 
 // Y: p eigenvectors of T, column-major (vector j at Y[j * c]).  S[i * lds + j] = (P Y)[i][j],
@@ -766,9 +979,46 @@ extern "C" hipError_t n2v2r_launch_rr_tri_inviter(const double* d, const double*
   return hipGetLastError();
 }
 
+// scratch (device, >= n2v2r_rr_tridiag_scratch_bytes(c)): the multi-workgroup form
+// (rr_tridiag_coop_kernel); NULL: the one-workgroup kernel (handles whose ranks share one device
+// pass NULL: their concurrent launches could not all be resident).  N2V2R_RR_TRI=1
+// forces the one-workgroup kernel, N2V2R_RR_TRI_PR the row-residue count (1..4) of the
+// multi-workgroup one.
+static hipError_t launch_rr_tridiag_coop(double* A, int c, double* d, double* e, double* tau,
+                                         double* V, void* scratch, hipStream_t stream) {
+  const int nt = (c + TRC_TS - 1) / TRC_TS;
+  int PR = nt > 12 ? 2 : 1;  // <= 12 row tiles per workgroup: <= 99 KB of tiles in LDS
+  if (const char* ev = std::getenv("N2V2R_RR_TRI_PR")) PR = std::max(1, std::min(4, std::atoi(ev)));
+  const int ntr = (nt + PR - 1) / PR;
+  const size_t shmem = sizeof(double) * ((size_t)ntr * TRC_TS * TRC_LD + 5 * (size_t)c + 8 * TRC_TS);
+  if (shmem > 150 * 1024) return hipErrorInvalidValue;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)rr_tridiag_coop_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    (void)hipGetLastError();
+    attr_set = true;
+  }
+  double* part = static_cast<double*>(scratch);
+  double* rowbuf = part + (size_t)2 * 4 * c;
+  unsigned* ctr = reinterpret_cast<unsigned*>(rowbuf + (size_t)2 * c);
+  int* err = reinterpret_cast<int*>(ctr + 1);  // 1 after a timed-out grid barrier
+  hipError_t er = hipMemsetAsync(ctr, 0, 2 * sizeof(unsigned), stream);
+  if (er != hipSuccess) return er;
+  void* args[] = {&A, &c, &PR, &d, &e, &tau, &V, &part, &rowbuf, &ctr, &err};
+  return hipLaunchCooperativeKernel((const void*)rr_tridiag_coop_kernel, dim3((unsigned)(PR * nt)),
+                                    dim3(TRC_NT), args, (unsigned)shmem, stream);
+}
+
 extern "C" hipError_t n2v2r_launch_rr_tridiag(double* A, int c, double* d, double* e, double* tau,
-                                              double* V, hipStream_t stream) {
+                                              double* V, void* scratch, hipStream_t stream) {
   if (c < 3 || c > RR_MAXC) return hipErrorInvalidValue;
+  const char* ev = std::getenv("N2V2R_RR_TRI");  // read per call (tests switch it)
+  const bool force_one = ev && std::atoi(ev) == 1;
+  if (scratch && !force_one) {
+    const hipError_t er = launch_rr_tridiag_coop(A, c, d, e, tau, V, scratch, stream);
+    if (er != hipErrorInvalidValue) return er;
+  }
   // 1024 threads up to c = 512; 512 threads (twice the registers per lane) beyond.  Even c
   // (every UASE basis: c = blocks x b): 16-B column-pair accesses.
   static bool attr_set = false;

@@ -263,97 +263,6 @@ __global__ __launch_bounds__(256) void spmm8_pipe_kernel(SpmmArgs args) {
   }
 }
 
-// B = 8, one lane per entry: lane li of a row's L-lane group takes entries li, li + L, ... and
-// gathers the whole 32-B panel row itself (two 16-B loads), so a wave-instruction serves 64
-// entries (the two-lanes-per-row form serves 32) and no index / value shuffles are needed.
-// Two group-widths per step keep 4 loads per lane in flight; entries past the row end read
-// panel row 0 and multiply by 0 (clamped addresses: the loads issue as one batch).  The L
-// partial sums of a row are folded by an xor butterfly.
-template <int RPW>
-__global__ __launch_bounds__(256) void spmm8_lane_kernel(SpmmArgs args) {
-  constexpr int L = 64 / RPW;
-  const int lane = threadIdx.x & 63;
-  const int g = lane / L, li = lane % L;
-  const int K = args.sum ? args.K : 1;
-  const int kfix = args.sum ? 0 : (int)blockIdx.y;
-  const int64_t n = args.A[kfix].n_rows;
-  const int64_t ngroups = (n + RPW - 1) / RPW;
-  const int64_t gstride = (int64_t)gridDim.x * (blockDim.x / 64);
-  for (int64_t grp = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); grp < ngroups;
-       grp += gstride) {
-    const int64_t row = grp * RPW + g;
-    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < K; ++k) {
-      const CsrDev& A = args.A[kfix + k];
-      const float* X = args.X[kfix + k];
-      int64_t beg = 0, len = 0;
-      if (row < n) {
-        beg = A.indptr[row];
-        len = A.indptr[row + 1] - beg;
-      }
-      int64_t maxlen = len;
-#pragma unroll
-      for (int m = L; m < 64; m <<= 1) {
-        const int64_t o = __shfl_xor(maxlen, m, 64);
-        maxlen = o > maxlen ? o : maxlen;
-      }
-      for (int64_t off = 0; off < maxlen; off += 2 * L) {
-        const bool in0 = off + li < len, in1 = off + L + li < len;
-        const int c0 = in0 ? A.indices[beg + off + li] : 0;
-        const int c1 = in1 ? A.indices[beg + off + L + li] : 0;
-        float v0 = in0 ? 1.f : 0.f, v1 = in1 ? 1.f : 0.f;
-        if (!A.unit) {
-          v0 = in0 ? A.data[beg + off + li] : 0.f;
-          v1 = in1 ? A.data[beg + off + L + li] : 0.f;
-        }
-        const float* x0 = X + (int64_t)c0 * args.ldx;
-        const float* x1 = X + (int64_t)c1 * args.ldx;
-        const f32x4 x00 = *reinterpret_cast<const f32x4*>(x0);
-        const f32x4 x01 = *reinterpret_cast<const f32x4*>(x0 + 4);
-        const f32x4 x10 = *reinterpret_cast<const f32x4*>(x1);
-        const f32x4 x11 = *reinterpret_cast<const f32x4*>(x1 + 4);
-        a0 += v0 * x00;
-        a1 += v0 * x01;
-        a0 += v1 * x10;
-        a1 += v1 * x11;
-      }
-    }
-#pragma unroll
-    for (int m = 1; m < L; m <<= 1) {
-      a0.x += __shfl_xor(a0.x, m, 64);
-      a0.y += __shfl_xor(a0.y, m, 64);
-      a0.z += __shfl_xor(a0.z, m, 64);
-      a0.w += __shfl_xor(a0.w, m, 64);
-      a1.x += __shfl_xor(a1.x, m, 64);
-      a1.y += __shfl_xor(a1.y, m, 64);
-      a1.z += __shfl_xor(a1.z, m, 64);
-      a1.w += __shfl_xor(a1.w, m, 64);
-    }
-    if (row < n && li < 2) {
-      f32x4 o = li ? a1 : a0;
-      if (args.colscale) o *= *reinterpret_cast<const f32x4*>(args.colscale + li * 4);
-      *reinterpret_cast<f32x4*>(args.Y[kfix] + row * args.ldy + li * 4) = o;
-    }
-  }
-}
-
-static int spmm8_form() {  // N2V2R_SPMM8=lane: the one-lane-per-entry kernel (A/B runs)
-  static const int v = [] {
-    const char* s = getenv("N2V2R_SPMM8");
-    return (s && s[0] == 'l') ? 1 : 0;
-  }();
-  return v;
-}
-
-// B = 8 uses the pipelined kernel unless N2V2R_SPMM_PIPE=0 (A/B runs)
-static bool spmm8_pipelined() {
-  static const bool v = [] {
-    const char* s = getenv("N2V2R_SPMM_PIPE");
-    return !(s && s[0] == '0');
-  }();
-  return v;
-}
-
 template <int B, int RPW>
 static void launch_spmm_t(const SpmmArgs& args, hipStream_t stream) {
   const int64_t n = args.A[0].n_rows;
@@ -362,20 +271,16 @@ static void launch_spmm_t(const SpmmArgs& args, hipStream_t stream) {
   const int64_t cap = (int64_t)N2V2R_SPMM_WGS / (args.sum ? 1 : args.K);
   if (wgs > cap) wgs = cap;
   dim3 grid((unsigned)wgs, args.sum ? 1 : args.K);
-  if (args.split) grid = dim3((unsigned)N2V2R_SPMM_WGS, 1);
-  if constexpr (B == 8) {
-    if (spmm8_form() == 1) {
-      hipLaunchKernelGGL((spmm8_lane_kernel<RPW>), grid, dim3(256), 0, stream, args);
-      return;
-    }
-  }
   if constexpr (B == 8 && RPW >= 2) {
-    if (spmm8_pipelined()) {
-      hipLaunchKernelGGL((spmm8_pipe_kernel<RPW>), grid, dim3(256), 0, stream, args);
-      return;
-    }
+    if (args.split) grid = dim3((unsigned)N2V2R_SPMM_WGS, 1);
+    hipLaunchKernelGGL((spmm8_pipe_kernel<RPW>), grid, dim3(256), 0, stream, args);
+  } else {
+    // the XCD split lives in the pipelined kernel; here the same per-layer outputs come from
+    // grid.y = layer
+    SpmmArgs a = args;
+    a.split = 0;
+    hipLaunchKernelGGL((spmm_csr_panel_kernel<B, RPW>), grid, dim3(256), 0, stream, a);
   }
-  hipLaunchKernelGGL((spmm_csr_panel_kernel<B, RPW>), grid, dim3(256), 0, stream, args);
 }
 
 // rows per wave from the mean row length: a row group of L lanes gathers L / (B/4) panel rows
@@ -390,11 +295,6 @@ static void launch_spmm_b(const SpmmArgs& args, hipStream_t stream) {
   const double want_l = LPN * avg / 3.5;
   int rpw = 1;
   while (rpw < 8 && 64 / (rpw * 2) >= LPN && 64.0 / (rpw * 2) >= want_l) rpw *= 2;
-  static const int rpw_env = [] {  // N2V2R_SPMM_RPW: rows per wave override (tuning runs)
-    const char* s = getenv("N2V2R_SPMM_RPW");
-    return s ? atoi(s) : 0;
-  }();
-  if (rpw_env == 1 || rpw_env == 2 || rpw_env == 4 || rpw_env == 8) rpw = rpw_env;
   switch (rpw) {
     case 8: if constexpr (64 / 8 >= LPN) { launch_spmm_t<B, 8>(args, stream); break; } [[fallthrough]];
     case 4: if constexpr (64 / 4 >= LPN) { launch_spmm_t<B, 4>(args, stream); break; } [[fallthrough]];
@@ -405,10 +305,7 @@ static void launch_spmm_b(const SpmmArgs& args, hipStream_t stream) {
 
 extern "C" hipError_t n2v2r_launch_spmm(const SpmmArgs& args_in, int B, hipStream_t stream) {
   if (args_in.split && (B != 8 || args_in.sum || args_in.K > 8)) return hipErrorInvalidValue;
-  SpmmArgs args = args_in;
-  // the XCD split lives in the pipelined kernel; other b = 8 forms (A/B switches) write the
-  // same per-layer outputs with grid.y = layer
-  if (args.split && (!spmm8_pipelined() || spmm8_form() != 0)) args.split = 0;
+  const SpmmArgs& args = args_in;
   if (B == 8)
     launch_spmm_b<8>(args, stream);
   else if (B == 16)
@@ -422,305 +319,18 @@ extern "C" hipError_t n2v2r_launch_spmm(const SpmmArgs& args_in, int B, hipStrea
   return hipGetLastError();
 }
 
-// ---- XCD-local column blocks (b = 8, panels larger than the L2s) -------------------------
-// At N = 1M a b = 8 panel is 32 MB: it lives in the Infinity Cache, and every 32-B gather
-// pulls a whole line over the fabric, so the gathers run at Infinity-Cache line bandwidth.
-// The column-block form splits each layer's columns into CB_NB = 8 equal ranges and keeps one
-// CSR per range (same row order, entries of a row in their original order).  Workgroup i runs
-// on XCD i mod 8 (round-robin dispatch), so XCD j only gathers from panel rows of column block
-// j (N/8 x 32 B = 4 MB at N = 1M): the gathers hit that XCD's L2.  Each block writes its own
-// partial output (N x 8 fp32); cb_reduce sums the partials in fixed block order (then layer
-// order), so the result is deterministic.  Extra traffic: 2 x 8 x N x 32 B of partials per
-// layer launch.
-// b = 8 row accumulation for the column blocks: block rows are short (N avg-deg / 8 entries),
-// so the index loads of two group-widths are issued together before the gathers (one
-// index -> gather latency per 2L entries instead of per L).  Same per-lane entry order as
-// spmm_row_accumulate<8, RPW>.
-template <int RPW>
-__device__ __forceinline__ void cb_row_accumulate(const CsrBlk& A, const float* __restrict__ X,
-                                                  int64_t ldx, int64_t row, bool row_ok,
-                                                  int lane, f32x4& acc) {
-  constexpr int L = 64 / RPW;
-  constexpr int NPS = L / 2;  // panel rows per step (2 lanes per 32-B panel row)
-  const int g = lane / L;
-  const int li = lane % L;
-  const int sub = li & 1;
-  const int srcbase = g * L + (li >> 1);
-  int64_t beg = 0, end = 0;
-  if (row_ok) {
-    beg = A.base + A.rp[row];
-    end = A.base + A.rp[row + 1];
-  }
-  const int64_t len = end - beg;
-  int64_t maxlen = len;
-#pragma unroll
-  for (int m = L; m < 64; m <<= 1) {
-    const int64_t o = __shfl_xor(maxlen, m, 64);
-    maxlen = o > maxlen ? o : maxlen;
-  }
-  for (int64_t off = 0; off < maxlen; off += 2 * L) {
-    int cv[2] = {0, 0};
-    float vv[2] = {0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int64_t p = off + u * L + li;
-      if (p < len) {
-        cv[u] = A.indices[beg + p];
-        vv[u] = A.unit ? 1.f : A.data[beg + p];
-      }
-    }
-    const int64_t rem = maxlen - off;
-    const int nn = (int)(rem < 2 * L ? rem : 2 * L);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      if (s * NPS >= nn) break;
-      const int u = s >> 1;  // L / NPS = 2 steps per group-width
-      const int c0 = __shfl(cv[u], srcbase + (s & 1) * NPS, 64);
-      const float v0 = __shfl(vv[u], srcbase + (s & 1) * NPS, 64);
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(X + (int64_t)c0 * ldx + sub * 4);
-      acc += v0 * x0;
-    }
-  }
-}
-
-// Two row groups of one column block at once (the tiled kernel): both groups' row pointers,
-// then both groups' first two group-widths of column indices, then all their gathers, issued
-// as batches -- clamped addresses and zero weights instead of guarded loads, so no load waits
-// behind a branch (entries past a row's end gather panel row `beg` or 0 with weight 0: the
-// sums are bit-identical).  Rows longer than 2L entries finish in a plain loop.
-template <int RPW>
-__device__ __forceinline__ void cb_rows2_accumulate(const CsrBlk& A, const float* __restrict__ X,
-                                                    int64_t ldx, int64_t rowA, bool okA,
-                                                    int64_t rowB, bool okB, int lane,
-                                                    f32x4& accA, f32x4& accB) {
-  constexpr int L = 64 / RPW;
-  constexpr int NPS = L / 2;
-  const int g = lane / L;
-  const int li = lane % L;
-  const int sub = li & 1;
-  const int srcbase = g * L + (li >> 1);
-  const int64_t rA = okA ? rowA : 0, rB = okB ? rowB : 0;
-  const int32_t a0 = A.rp[rA], a1 = A.rp[rA + 1], b0 = A.rp[rB], b1 = A.rp[rB + 1];
-  const int64_t begA = A.base + a0, begB = A.base + b0;
-  const int64_t lenA = okA ? (int64_t)(a1 - a0) : 0, lenB = okB ? (int64_t)(b1 - b0) : 0;
-  int64_t mx = lenA > lenB ? lenA : lenB;
-#pragma unroll
-  for (int m = L; m < 64; m <<= 1) {
-    const int64_t o = __shfl_xor(mx, m, 64);
-    mx = o > mx ? o : mx;
-  }
-  // first 2L entries of both rows, unconditionally (index 0 of the block's entries when past
-  // the end; A.nnz >= 1 whenever any row of the block has an entry, else mx == 0 below)
-  int cA[2], cB[2];
-  float vA[2], vB[2];
-  if (mx > 0) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int64_t p = u * L + li;
-      const int64_t qa = p < lenA ? begA + p : A.base;
-      const int64_t qb = p < lenB ? begB + p : A.base;
-      cA[u] = A.indices[qa];
-      cB[u] = A.indices[qb];
-      vA[u] = p < lenA ? (A.unit ? 1.f : A.data[qa]) : 0.f;
-      vB[u] = p < lenB ? (A.unit ? 1.f : A.data[qb]) : 0.f;
-    }
-    f32x4 xa[4], xb[4];
-    float wa[4], wb[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int u = s >> 1;
-      const int src = srcbase + (s & 1) * NPS;
-      const int ca = __shfl(cA[u], src, 64), cb = __shfl(cB[u], src, 64);
-      wa[s] = __shfl(vA[u], src, 64);
-      wb[s] = __shfl(vB[u], src, 64);
-      xa[s] = *reinterpret_cast<const f32x4*>(X + (int64_t)ca * ldx + sub * 4);
-      xb[s] = *reinterpret_cast<const f32x4*>(X + (int64_t)cb * ldx + sub * 4);
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      accA += wa[s] * xa[s];
-      accB += wb[s] * xb[s];
-    }
-  }
-  // long rows: the rest one group-width at a time
-  for (int64_t off = 2 * L; off < mx; off += L) {
-    const int64_t p = off + li;
-    const int ca = p < lenA ? A.indices[begA + p] : 0;
-    const float va = p < lenA ? (A.unit ? 1.f : A.data[begA + p]) : 0.f;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int src = srcbase + s * NPS;
-      const int c0 = __shfl(ca, src, 64);
-      const float w0 = __shfl(va, src, 64);
-      accA += w0 * *reinterpret_cast<const f32x4*>(X + (int64_t)c0 * ldx + sub * 4);
-    }
-    const int cb = p < lenB ? A.indices[begB + p] : 0;
-    const float vb = p < lenB ? (A.unit ? 1.f : A.data[begB + p]) : 0.f;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int src = srcbase + s * NPS;
-      const int c1 = __shfl(cb, src, 64);
-      const float w1 = __shfl(vb, src, 64);
-      accB += w1 * *reinterpret_cast<const f32x4*>(X + (int64_t)c1 * ldx + sub * 4);
-    }
-  }
-}
-
-template <int RPW>
-__global__ __launch_bounds__(256) void spmm8_cb_kernel(SpmmCbArgs a) {
-  constexpr int L = 64 / RPW;
-  const int lane = threadIdx.x & 63;
-  const int j = blockIdx.x & (CB_NB - 1);
-  const int64_t t = blockIdx.x / CB_NB;
-  const int64_t nwg = gridDim.x / CB_NB;
-  const CsrBlk& A = a.A[j];
-  const int64_t n = A.n_rows;
-  const int li = lane % L;
-  float* __restrict__ P = a.P + (int64_t)j * a.pstride;
-  const int64_t nw = nwg * (blockDim.x / 64);
-  for (int64_t wid = t * (blockDim.x / 64) + (threadIdx.x >> 6); wid * RPW < n; wid += nw) {
-    const int64_t row = wid * RPW + lane / L;
-    const bool row_ok = row < n;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    cb_row_accumulate<RPW>(A, a.X, a.ldx, row, row_ok, lane, acc);
-#pragma unroll
-    for (int m = 2; m < L; m <<= 1) {
-      acc.x += __shfl_xor(acc.x, m, 64);
-      acc.y += __shfl_xor(acc.y, m, 64);
-      acc.z += __shfl_xor(acc.z, m, 64);
-      acc.w += __shfl_xor(acc.w, m, 64);
-    }
-    if (row_ok && li < 2) *reinterpret_cast<f32x4*>(P + row * 8 + li * 4) = acc;
-  }
-}
-
-// rows per wave of the column-block kernels from the mean entries per block row (largest
-// block): aim for ~3-4 gather steps of L/2 panel rows per row group
-extern "C" int n2v2r_cb_rpw(const CsrBlk* A, int nb, int64_t n) {
-  double avg = 0.0;
-  for (int j = 0; j < nb; ++j) {
-    const double m = (double)A[j].nnz / (double)(n > 0 ? n : 1);
-    avg = m > avg ? m : avg;
-  }
-  int rpw = 1;
-  while (rpw < 16 && 64.0 / (rpw * 2) / 2.0 * 3.5 >= avg) rpw *= 2;
-  return rpw;
-}
-
-extern "C" hipError_t n2v2r_launch_spmm_cb(const SpmmCbArgs& a, hipStream_t stream) {
-  const int64_t n = a.A[0].n_rows;
-  int rpw = n2v2r_cb_rpw(a.A, CB_NB, n);
-  static const int rpw_env = [] {  // N2V2R_CB_RPW / N2V2R_CB_WGS: tuning runs
-    const char* s = getenv("N2V2R_CB_RPW");
-    return s ? atoi(s) : 0;
-  }();
-  static const int wgs_env = [] {
-    const char* s = getenv("N2V2R_CB_WGS");
-    return s ? atoi(s) : 0;
-  }();
-  if (rpw_env == 1 || rpw_env == 2 || rpw_env == 4 || rpw_env == 8 || rpw_env == 16 ||
-      rpw_env == 32)
-    rpw = rpw_env;
-  const int64_t waves = (n + rpw - 1) / rpw;
-  int64_t per = (waves + 3) / 4;  // workgroups per block
-  const int64_t cap = (wgs_env >= CB_NB ? wgs_env : N2V2R_SPMM_WGS) / CB_NB;
-  if (per > cap) per = cap;
-  if (per < 1) per = 1;
-  dim3 grid((unsigned)(per * CB_NB));
-#define CB_LAUNCH(R) hipLaunchKernelGGL((spmm8_cb_kernel<R>), grid, dim3(256), 0, stream, a)
-  switch (rpw) {
-    case 32: CB_LAUNCH(32); break;
-    case 16: CB_LAUNCH(16); break;
-    case 8: CB_LAUNCH(8); break;
-    case 4: CB_LAUNCH(4); break;
-    case 2: CB_LAUNCH(2); break;
-    default: CB_LAUNCH(1); break;
-  }
-#undef CB_LAUNCH
-  return hipGetLastError();
-}
-
-// ---- row tiles x column-block phases (b = 8, panels of 8-160 MB) ---------------------------
-// The column-block SpMM above writes 8 partial outputs per layer launch (2 x 8 x 32 B per row
-// of extra HBM traffic, then a reduce launch).  Here every workgroup owns a tile of rows whose
-// accumulators stay in LDS (tile x 32 B: 62.5 KB at N = 1M with 2 workgroups per CU) and walks
-// the column blocks in a fixed order 0..7 (the phases), gathering only from panel block p in
-// phase p.  All workgroups start together and their rows carry equal work (ER / uniform
-// graphs), so at any time the chip gathers from one 4 MB panel block, which every XCD's L2
-// holds: the gathers hit L2 as in the column-block form, and each output row is written once.
+// ---- row tiles x column-block phases (b = 8, panels beyond an XCD's L2) -------------------
+// Every workgroup owns a tile of rows whose accumulators stay in LDS (tile x 32 B) and walks each
+// layer's column blocks in a fixed order (the phases), gathering only from panel block p in
+// phase p.  All workgroups start together and their rows carry equal work (ER / uniform graphs),
+// so at any time the chip gathers from one panel block of <= 2 MB, which every XCD's L2 holds.
 // Sum mode (stage 2) accumulates the K layers into one output; otherwise (stage 1) each layer's
-// output is written after its 8 phases.  Each row belongs to one wave (fixed row groups), so
-// the LDS read-modify-writes need no barrier or atomic; per row the order is (layer, block,
-// entry) -- deterministic.
+// output is written after its phases.  Per row the order is (layer, block, entry): deterministic.
+// (Round 2-3 forms measured against it and removed in round 4: 8 partial outputs per layer + a
+// reduce launch, 2.2 s per cfg4 step; row groups per wave, 0.807 ms per stage launch at 8
+// blocks; two row groups per step at one workgroup per CU, 0.815 ms)
 
-// PAIR = 0 (N2V2R_TILE_FLAT=0; the flat-window kernel below is the default tiled form): one
-// row group per wave step (cb_row_accumulate), 2 workgroups (32 waves) per CU.  PAIR = 2 (N2V2R_TILE_PAIR=2, A/B): two row groups per step with clamped batched loads
-// (two load chains per wave, cb_rows2_accumulate), 1 workgroup (16 waves) per CU with twice the
-// rows: cfg4 0.815 vs 0.795 ms per stage launch.  A one-group clamped form at 32 waves per CU
-// spilled 14-18 VGPRs (64-register cap) and ran 0.995 ms.
-template <int RPW, int PAIR>
-__global__ __launch_bounds__(1024, PAIR == 2 ? 4 : 8) void spmm8_tile_kernel(SpmmTileArgs a) {
-  constexpr int L = 64 / RPW;
-  extern __shared__ f32x4 tacc[];  // [tile_rows][2]
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int nwave = blockDim.x >> 6;
-  const int li = lane % L;
-  const int64_t r0 = (int64_t)blockIdx.x * a.tile_rows;
-  const int64_t rem = a.n - r0;
-  const int nrows = (int)(rem < a.tile_rows ? rem : a.tile_rows);
-  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-  for (int grp = wave; grp * RPW < nrows; grp += nwave) {
-    const int lr = grp * RPW + lane / L;
-    if (lr < nrows && li < 2) tacc[lr * 2 + li] = zero;
-  }
-  for (int k = 0; k < a.K; ++k) {
-    const float* X = a.X[k];
-    for (int p = 0; p < a.nb; ++p) {
-      const CsrBlk A = a.blk[k * a.nb + p];
-      // PAIR row groups per step (grp, grp + nwave): PAIR independent load chains per wave
-      for (int grp = wave; grp * RPW < nrows; grp += (PAIR == 2 ? 2 : 1) * nwave) {
-        const int lrA = grp * RPW + lane / L, lrB = lrA + nwave * RPW;
-        const bool okA = lrA < nrows, okB = PAIR == 2 && lrB < nrows;
-        f32x4 accA = zero, accB = zero;
-        if constexpr (PAIR == 0)
-          cb_row_accumulate<RPW>(A, X, a.ldx, r0 + lrA, okA, lane, accA);
-        else
-          cb_rows2_accumulate<RPW>(A, X, a.ldx, r0 + lrA, okA, r0 + lrB, okB, lane, accA, accB);
-#pragma unroll
-        for (int m = 2; m < L; m <<= 1) {
-          accA.x += __shfl_xor(accA.x, m, 64);
-          accA.y += __shfl_xor(accA.y, m, 64);
-          accA.z += __shfl_xor(accA.z, m, 64);
-          accA.w += __shfl_xor(accA.w, m, 64);
-          if constexpr (PAIR == 2) {
-            accB.x += __shfl_xor(accB.x, m, 64);
-            accB.y += __shfl_xor(accB.y, m, 64);
-            accB.z += __shfl_xor(accB.z, m, 64);
-            accB.w += __shfl_xor(accB.w, m, 64);
-          }
-        }
-        if (okA && li < 2) tacc[lrA * 2 + li] += accA;
-        if (PAIR == 2 && okB && li < 2) tacc[lrB * 2 + li] += accB;
-      }
-      // the workgroup's waves move to the next panel block together (drifting waves would
-      // want several blocks in L2 at once); each wave only touches its own rows' LDS entries
-      __syncthreads();
-    }
-    if (!a.sum || k == a.K - 1) {
-      float* Y = a.Y[a.sum ? 0 : k];
-      for (int grp = wave; grp * RPW < nrows; grp += nwave) {
-        const int lr = grp * RPW + lane / L;
-        if (lr < nrows && li < 2) {
-          *reinterpret_cast<f32x4*>(Y + (r0 + lr) * a.ldy + li * 4) = tacc[lr * 2 + li];
-          tacc[lr * 2 + li] = zero;
-        }
-      }
-    }
-  }
-}
-
-// Packed flat windows (form 1): a wave owns windows of CB_WIN = 32 rows of the tile; a window's
+// Packed flat windows: a wave owns windows of CB_WIN = 32 rows of the tile; a window's
 // entries in column block p are one contiguous run of the block's index array (rows are in
 // order), so the wave walks that run 32 entries per step -- lane pair i takes entry i, reads its
 // packed word (row in window, column in block), gathers the 32-B panel row as two 16-B halves
@@ -753,10 +363,9 @@ __device__ __forceinline__ int64_t uniform_i64(int64_t v) {
 }
 
 // NS steps of 32 entries of one window: index words and gathers of all NS steps issued as
-// straight-line batches, then per step: stage, and the row owners fold their entries
-// NTL: the index / value stream loaded non-temporally (so it does not displace panel lines in
-// L2; N2V2R_FLAT_NT=1, A/B)
-template <int NS, bool UNIT, bool NTL, bool FOLD = true>
+// straight-line batches, then per step: stage, and the row owners fold their entries (the fold is
+// ~5 % of the launch at cfg4: the gathers are the cost)
+template <int NS, bool UNIT>
 __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1))) int32_t* ind,
                                            const __attribute__((address_space(1))) float* dat,
                                            int64_t beg, int off, int left,
@@ -770,13 +379,8 @@ __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1)
   for (int u = 0; u < NS; ++u) {
     const int q = u * 32 + pr;
     const int64_t e = beg + off + (q < left ? q : 0);
-    if constexpr (NTL) {
-      wd[u] = __builtin_nontemporal_load(ind + e);
-      v[u] = UNIT ? 1.f : __builtin_nontemporal_load(dat + e);
-    } else {
-      wd[u] = ind[e];
-      v[u] = UNIT ? 1.f : dat[e];
-    }
+    wd[u] = ind[e];
+    v[u] = UNIT ? 1.f : dat[e];
   }
 #pragma unroll
   for (int u = 0; u < NS; ++u)
@@ -785,10 +389,6 @@ __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1)
 #pragma unroll
   for (int u = 0; u < NS; ++u) {
     stage[pr * 2 + sub] = v[u] * x[u];  // entries past the end are never read
-    if constexpr (!FOLD) {  // timing probe (N2V2R_FLAT_NOFOLD=1): wrong sums, no fold loop
-      acc += stage[pr * 2 + sub];
-      continue;
-    }
     const int s0 = off + u * 32;
     const int lo = (rs > s0 ? rs : s0) - s0;
     const int hi = (re < s0 + 32 ? re : s0 + 32) - s0;
@@ -796,7 +396,6 @@ __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1)
   }
 }
 
-template <bool NTL, bool FOLD = true>
 __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
   // [tile_rows][8] row accumulators, then a 1-KB staging slot per wave
   extern __shared__ float tacf[];
@@ -850,13 +449,13 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
   for (int off = 0; off < len; off += 128) {                                                   \
     const int left = len - off;                                                                \
     if (left > 96)                                                                             \
-      flat_steps<4, U, NTL, FOLD>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+      flat_steps<4, U>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
     else if (left > 64)                                                                        \
-      flat_steps<3, U, NTL, FOLD>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+      flat_steps<3, U>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
     else if (left > 32)                                                                        \
-      flat_steps<2, U, NTL, FOLD>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+      flat_steps<2, U>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
     else                                                                                       \
-      flat_steps<1, U, NTL, FOLD>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+      flat_steps<1, U>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
   }
         if (unit) {
           FLAT_STEPS(true)
@@ -866,7 +465,7 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
 #undef FLAT_STEPS
         if (wr + pr < we) tacc[(wr + pr) * 2 + sub] += acc;
       }
-      __syncthreads();  // all waves on the same panel block (see spmm8_tile_kernel)
+      __syncthreads();  // the workgroup's waves move to the next panel block together
     }
     if (!a.sum || k == a.K - 1) {
       float* Y = a.Y[a.sum ? 0 : k];
@@ -875,134 +474,6 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
         if (lr < nrows) {
           *reinterpret_cast<f32x4*>(Y + (r0 + lr) * a.ldy + sub * 4) = tacc[lr * 2 + sub];
           tacc[lr * 2 + sub] = zero;
-        }
-      }
-    }
-  }
-}
-
-// ---- the packed flat-window form at b = 16 ---------------------------------------------------
-// The same windows, column-block phases and packed entries as spmm8_flat_kernel, with 64-B panel
-// rows: a lane quad (q = lane / 4) gathers one entry's row as four 16-B pieces, so a wave step
-// takes 16 entries, and quad q owns window rows q and q + 16 (two register accumulators).  An
-// entry still costs one scattered line access (the bound of the b = 8 form) but
-// carries 16 columns instead of 8, so a vector application costs about half the line accesses.
-template <int NS, bool UNIT>
-__device__ __forceinline__ void flat16_steps(const __attribute__((address_space(1))) int32_t* ind,
-                                             const __attribute__((address_space(1))) float* dat,
-                                             int64_t beg, int off, int left,
-                                             const __attribute__((address_space(1))) float* Xb,
-                                             uint32_t ldx, int32_t cmask, int q, int sub, int rs0,
-                                             int re0, int rs1, int re1, f32x4* stage, f32x4& acc0,
-                                             f32x4& acc1) {
-  int wd[NS];
-  float v[NS];
-  f32x4 x[NS];
-#pragma unroll
-  for (int u = 0; u < NS; ++u) {
-    const int t = u * 16 + q;
-    const int64_t e = beg + off + (t < left ? t : 0);
-    wd[u] = ind[e];
-    v[u] = UNIT ? 1.f : dat[e];
-  }
-#pragma unroll
-  for (int u = 0; u < NS; ++u)
-    x[u] = *reinterpret_cast<const __attribute__((address_space(1))) f32x4*>(
-        Xb + ((uint32_t)(wd[u] & cmask) * ldx + sub * 4));
-#pragma unroll
-  for (int u = 0; u < NS; ++u) {
-    stage[q * 4 + sub] = v[u] * x[u];  // entries past the end are never read
-    const int s0 = off + u * 16;
-    const int lo0 = (rs0 > s0 ? rs0 : s0) - s0, hi0 = (re0 < s0 + 16 ? re0 : s0 + 16) - s0;
-    for (int j = lo0; j < hi0; ++j) acc0 += stage[j * 4 + sub];
-    const int lo1 = (rs1 > s0 ? rs1 : s0) - s0, hi1 = (re1 < s0 + 16 ? re1 : s0 + 16) - s0;
-    for (int j = lo1; j < hi1; ++j) acc1 += stage[j * 4 + sub];
-  }
-}
-
-__global__ __launch_bounds__(1024, 8) void spmm16_flat_kernel(SpmmTileArgs a) {
-  // [tile_rows][16] row accumulators, then a 1-KB staging slot per wave
-  extern __shared__ float tacf[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nwave = blockDim.x >> 6;
-  const int pr = lane >> 1;            // row-pointer lanes: pair pr holds window row pr
-  const int q = lane >> 2, sub = lane & 3;  // entry / row-owner quad, 16-B piece
-  const int64_t r0 = (int64_t)blockIdx.x * a.tile_rows;
-  const int64_t rem = a.n - r0;
-  const int nrows = (int)(rem < a.tile_rows ? rem : a.tile_rows);
-  const int nwin = (nrows + CB_WIN - 1) / CB_WIN;
-  const uint32_t ldx = (uint32_t)a.ldx;
-  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-  f32x4* tacc = reinterpret_cast<f32x4*>(tacf);
-  f32x4* stage = reinterpret_cast<f32x4*>(tacf + (size_t)a.tile_rows * 16) + wave * 64;
-  for (int w = wave; w < nwin; w += nwave) {
-    const int lr = w * CB_WIN + q;
-    if (lr < nrows) tacc[lr * 4 + sub] = zero;
-    if (lr + 16 < nrows) tacc[(lr + 16) * 4 + sub] = zero;
-  }
-  for (int k = 0; k < a.K; ++k) {
-    const float* X = a.X[k];
-    for (int p = 0; p < a.nb; ++p) {
-      const CsrBlk& A = a.blk[k * a.nb + p];
-      const int cbits = __builtin_amdgcn_readfirstlane(A.cbits);
-      const int unit = __builtin_amdgcn_readfirstlane(A.unit);
-      const auto rp = uniform_global(A.rp);
-      const auto ind = uniform_global(A.indices);
-      const auto dat = uniform_global(A.data);
-      const int64_t base = uniform_i64(A.base);
-      const int64_t col0 = uniform_i64(A.col0);
-      const int32_t cmask = (1 << cbits) - 1;
-      const auto Xb = uniform_global(X + col0 * a.ldx);
-      for (int w = wave; w < nwin; w += nwave) {
-        const int wr = w * CB_WIN;
-        const int we = wr + CB_WIN < nrows ? wr + CB_WIN : nrows;
-        const int rr = wr + pr < we ? wr + pr : we;
-        const int32_t ps = rp[r0 + rr];
-        const int32_t pe = rp[r0 + (wr + pr < we ? wr + pr + 1 : we)];
-        const int32_t e0 = __builtin_amdgcn_readfirstlane(ps);
-        const int len = __builtin_amdgcn_readlane(pe, 2 * (we - wr - 1)) - e0;
-        // this quad's rows q and q + 16: their [start, end) from the pointer lanes 2q, 2q + 32
-        const int rs0 = __shfl(ps, 2 * q, 64) - e0, re0 = __shfl(pe, 2 * q, 64) - e0;
-        const int rs1 = __shfl(ps, 2 * q + 32, 64) - e0, re1 = __shfl(pe, 2 * q + 32, 64) - e0;
-        const int64_t beg = base + e0;
-        f32x4 acc0 = zero, acc1 = zero;
-#define FLAT16_STEPS(U)                                                                        \
-  for (int off = 0; off < len; off += 48) {                                                    \
-    const int left = len - off;                                                                \
-    if (left > 32)                                                                             \
-      flat16_steps<3, U>(ind, dat, beg, off, left, Xb, ldx, cmask, q, sub, rs0, re0, rs1, re1, \
-                         stage, acc0, acc1);                                                   \
-    else if (left > 16)                                                                        \
-      flat16_steps<2, U>(ind, dat, beg, off, left, Xb, ldx, cmask, q, sub, rs0, re0, rs1, re1, \
-                         stage, acc0, acc1);                                                   \
-    else                                                                                       \
-      flat16_steps<1, U>(ind, dat, beg, off, left, Xb, ldx, cmask, q, sub, rs0, re0, rs1, re1, \
-                         stage, acc0, acc1);                                                   \
-  }
-        if (unit) {
-          FLAT16_STEPS(true)
-        } else {
-          FLAT16_STEPS(false)
-        }
-#undef FLAT16_STEPS
-        if (wr + q < we) tacc[(wr + q) * 4 + sub] += acc0;
-        if (wr + q + 16 < we) tacc[(wr + q + 16) * 4 + sub] += acc1;
-      }
-      __syncthreads();  // all waves on the same panel block (see spmm8_tile_kernel)
-    }
-    if (!a.sum || k == a.K - 1) {
-      float* Y = a.Y[a.sum ? 0 : k];
-      for (int w = wave; w < nwin; w += nwave) {
-        const int lr = w * CB_WIN + q;
-        if (lr < nrows) {
-          *reinterpret_cast<f32x4*>(Y + (r0 + lr) * a.ldy + sub * 4) = tacc[lr * 4 + sub];
-          tacc[lr * 4 + sub] = zero;
-        }
-        if (lr + 16 < nrows) {
-          *reinterpret_cast<f32x4*>(Y + (r0 + lr + 16) * a.ldy + sub * 4) =
-              tacc[(lr + 16) * 4 + sub];
-          tacc[(lr + 16) * 4 + sub] = zero;
         }
       }
     }
@@ -1019,137 +490,21 @@ extern "C" int n2v2r_spmm_tile_rows(int64_t n, int ncu, int wpc) {
   return (int)t;
 }
 
-extern "C" hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, int rpw, hipStream_t stream) {
-  if (a.K < 1 || a.K > 8 || a.tile_rows < 16 || a.n <= 0) return hipErrorInvalidValue;
+extern "C" hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, hipStream_t stream) {
+  if (a.K < 1 || a.K > 8 || a.tile_rows < 16 || a.n <= 0 || a.tile_rows % CB_WIN != 0)
+    return hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.n + a.tile_rows - 1) / a.tile_rows);
-  if (a.b == 16) {  // 64 B of accumulators per row + a 1-KB staging slot per wave
-    const size_t flds = sizeof(float) * 16 * (size_t)a.tile_rows + 16 * 1024;
-    if (a.form != 1 || a.tile_rows % CB_WIN != 0 || flds > 80 * 1024) return hipErrorInvalidValue;
-    static const bool fattr = [] {
-      (void)hipFuncSetAttribute((const void*)spmm16_flat_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-      (void)hipGetLastError();
-      return true;
-    }();
-    (void)fattr;
-    hipLaunchKernelGGL(spmm16_flat_kernel, dim3(grid), dim3(1024), flds, stream, a);
-    return hipGetLastError();
-  }
-  if (a.b != 0 && a.b != 8) return hipErrorInvalidValue;
-  const size_t lds = sizeof(float) * 8 * (size_t)a.tile_rows;
-  if (a.form < 0 || a.form > 2 || a.tile_rows % CB_WIN != 0) return hipErrorInvalidValue;
-  if (a.form == 1) {  // + a 1-KB staging slot per wave
-    const size_t flds = lds + 16 * 1024;
-    static const bool fattr = [] {
-      (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel<false>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-      (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel<true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-      (void)hipGetLastError();
-      return true;
-    }();
-    (void)fattr;
-    static const bool ntl = [] {
-      const char* e = getenv("N2V2R_FLAT_NT");
-      return e && e[0] == '1';
-    }();
-    if (flds > 80 * 1024) return hipErrorInvalidValue;
-    static const bool nofold = [] {  // timing probe only: the fold loop skipped, sums wrong
-      const char* e = getenv("N2V2R_FLAT_NOFOLD");
-      if (e && e[0] == '1')
-        (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel<false, false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-      return e && e[0] == '1';
-    }();
-    if (nofold)
-      hipLaunchKernelGGL((spmm8_flat_kernel<false, false>), dim3(grid), dim3(1024), flds, stream, a);
-    else if (ntl)
-      hipLaunchKernelGGL(spmm8_flat_kernel<true>, dim3(grid), dim3(1024), flds, stream, a);
-    else
-      hipLaunchKernelGGL(spmm8_flat_kernel<false>, dim3(grid), dim3(1024), flds, stream, a);
-    return hipGetLastError();
-  }
-  if (lds > 64 * 1024) {
-    static bool attr = false;
-    if (!attr) {
-      for (const void* f : {(const void*)spmm8_tile_kernel<32, 2>, (const void*)spmm8_tile_kernel<16, 2>,
-                            (const void*)spmm8_tile_kernel<8, 2>, (const void*)spmm8_tile_kernel<4, 2>,
-                            (const void*)spmm8_tile_kernel<2, 2>})
-        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipGetLastError();
-      attr = true;
-    }
-  }
-#define TILE_LAUNCH(R)                                                                     \
-  if (a.form == 2)                                                                         \
-    hipLaunchKernelGGL((spmm8_tile_kernel<R, 2>), dim3(grid), dim3(1024), lds, stream, a); \
-  else                                                                                     \
-    hipLaunchKernelGGL((spmm8_tile_kernel<R, 0>), dim3(grid), dim3(1024), lds, stream, a)
-  switch (rpw) {
-    case 32: TILE_LAUNCH(32); break;
-    case 16: TILE_LAUNCH(16); break;
-    case 8: TILE_LAUNCH(8); break;
-    case 4: TILE_LAUNCH(4); break;
-    default: TILE_LAUNCH(2); break;
-  }
-#undef TILE_LAUNCH
-  return hipGetLastError();
-}
-
-// out[r] = colscale .* sum_{p < nparts} P[p][r] (rows of 8 fp32, fixed part order)
-// out row r = sum_p P[p] row r, p in order (the fixed order keeps results bit-identical to the
-// column-block partials' summation in every form).  NP > 0: all NP loads of a thread issued
-// before the first add (the runtime-count loop waited out one memory round trip per partial:
-// ~1.2 TB/s at N = 1M); NP = 0: any count.
-template <int NP>
-__global__ __launch_bounds__(256) void cb_reduce_kernel(const float* __restrict__ P, int nparts,
-                                                        int64_t pstride, int64_t n,
-                                                        float* __restrict__ out, int64_t ldo) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one float4 each
-  if (i >= n * 2) return;
-  const int64_t r = i >> 1;
-  const int h = (int)(i & 1);
-  const float* src = P + r * 8 + h * 4;
-  f32x4 s;
-  if constexpr (NP > 0) {
-    f32x4 v[NP];
-#pragma unroll
-    for (int p = 0; p < NP; ++p) v[p] = *reinterpret_cast<const f32x4*>(src + p * pstride);
-    s = v[0];
-#pragma unroll
-    for (int p = 1; p < NP; ++p) s += v[p];
-  } else {
-    s = *reinterpret_cast<const f32x4*>(src);
-    for (int p = 1; p < nparts; ++p) s += *reinterpret_cast<const f32x4*>(src + p * pstride);
-  }
-  *reinterpret_cast<f32x4*>(out + r * ldo + h * 4) = s;
-}
-
-extern "C" hipError_t n2v2r_launch_cb_reduce(const float* P, int nparts, int64_t pstride,
-                                             int64_t n, float* out, int64_t ldo,
-                                             hipStream_t stream) {
-  if (n <= 0) return hipSuccess;
-  const int64_t thr = n * 2;
-  const dim3 g((unsigned)((thr + 255) / 256));
-  // the runtime-count loop by default: the stage-1 reduces run beside the next layer's block
-  // launch, where the unrolled form's burst of loads slowed that launch more than it saved
-  // (cfg4 2353 vs 2205 ms per step); unrolled for the stage-2 sum only: 2209 vs 2206.
-  // N2V2R_CB_REDUCE_UNROLL=1 / 2: always / stage-2 sums (K x 8 partials) only (A/B).
-  static const int unroll_mode = [] {
-    const char* e = getenv("N2V2R_CB_REDUCE_UNROLL");
-    return e ? atoi(e) : 0;
+  // 32 B of accumulators per row + a 1-KB staging slot per wave
+  const size_t flds = sizeof(float) * 8 * (size_t)a.tile_rows + 16 * 1024;
+  if (flds > 80 * 1024) return hipErrorInvalidValue;
+  static const bool fattr = [] {
+    (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    (void)hipGetLastError();
+    return true;
   }();
-  const bool unrolled = unroll_mode == 1 || (unroll_mode == 2 && nparts >= 16);
-  if (!unrolled)
-    hipLaunchKernelGGL(cb_reduce_kernel<0>, g, dim3(256), 0, stream, P, nparts, pstride, n, out, ldo);
-  else if (nparts == 8)
-    hipLaunchKernelGGL(cb_reduce_kernel<8>, g, dim3(256), 0, stream, P, nparts, pstride, n, out, ldo);
-  else if (nparts == 16)
-    hipLaunchKernelGGL(cb_reduce_kernel<16>, g, dim3(256), 0, stream, P, nparts, pstride, n, out, ldo);
-  else if (nparts == 24)
-    hipLaunchKernelGGL(cb_reduce_kernel<24>, g, dim3(256), 0, stream, P, nparts, pstride, n, out, ldo);
-  else
-    hipLaunchKernelGGL(cb_reduce_kernel<0>, g, dim3(256), 0, stream, P, nparts, pstride, n, out, ldo);
+  (void)fattr;
+  hipLaunchKernelGGL(spmm8_flat_kernel, dim3(grid), dim3(1024), flds, stream, a);
   return hipGetLastError();
 }
 

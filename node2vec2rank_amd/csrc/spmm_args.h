@@ -22,17 +22,17 @@ struct SpmmArgs {
                          // so each XCD's L2 holds one layer's panel
 };
 
-// ---- column blocks (b = 8, panels of 8-160 MB) ------------------------------------------------
-#define CB_NB 8      // column blocks of the partials form (one per XCD)
-#define CB_MAX 64    // column blocks of the tiled form (N2V2R_SPMM_TILE_NB)
+// ---- column blocks (b = 8 panels beyond 8 MB: the flat-window tiled SpMM) --------------------
+#define CB_NB 8      // default column blocks when a caller names none (the fit picks 4-32)
+#define CB_MAX 64    // column blocks per layer at most (N2V2R_SPMM_TILE_NB)
 #define CB_WIN 32    // rows per window of the packed tiled form (row-in-window: 5 index bits)
 #define CB_WIN_BITS 5
 
 // One column block: int32 row pointers relative to `base` (the block's first entry in the
 // shared index / value arrays; half the row-pointer bytes of int64).  cbits = 0: `indices`
-// hold global column indices.  cbits > 0 (packed, tiled form only): entry = (row % CB_WIN)
-// << cbits | (column - col0), so a wave walking a window of CB_WIN rows reads its entries as
-// one flat run and each entry names its own row.
+// hold global column indices.  cbits > 0 (packed): entry = (row % CB_WIN) << cbits | (column -
+// col0), so a wave walking a window of CB_WIN rows reads its entries as one flat run and each
+// entry names its own row.
 struct CsrBlk {
   const int32_t* rp;       // n_rows + 1
   const int32_t* indices;  // shared by the blocks of a layer
@@ -45,15 +45,7 @@ struct CsrBlk {
   int64_t col0;            // first column of the block
 };
 
-struct SpmmCbArgs {  // column block j of one layer, partial j at P + j * pstride
-  CsrBlk A[CB_NB];
-  const float* X;    // gathered panel, global column index = panel row
-  int64_t ldx;
-  float* P;          // rows of 8 fp32
-  int64_t pstride;
-};
-
-struct SpmmTileArgs {  // row tiles x column-block phases (spmm8_tile_kernel / _flat_)
+struct SpmmTileArgs {  // row tiles x column-block phases (spmm8_flat_kernel)
   const CsrBlk* blk;   // device array [K][nb]
   const float* X[SPMM_MAX_LAYERS];  // panel per layer (gathered, global rows)
   float* Y[SPMM_MAX_LAYERS];        // output per layer (sum: Y[0])
@@ -63,8 +55,4 @@ struct SpmmTileArgs {  // row tiles x column-block phases (spmm8_tile_kernel / _
   int nb;              // column blocks (phases) per layer
   int sum;
   int tile_rows;
-  int form;            // 0: row groups (guarded loads); 2: two row groups per step;
-                       // 1: packed flat windows (spmm8_flat_kernel)
-  int b;               // panel width: 8 (0 means 8) or 16 (flat form only: spmm16_flat_kernel)
 };
-

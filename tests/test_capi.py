@@ -1,4 +1,4 @@
-"""C-ABI library: loads, exports every symbol include/n2v2r.h declares, host-side pieces.
+"""C-ABI library: loads, exports every symbol include/*.h declares, host-side pieces.
 CPU only (no compute calls need a GPU)."""
 import ctypes
 import os
@@ -11,7 +11,8 @@ from conftest import REPO
 
 
 def _header_symbols():
-    txt = open(os.path.join(REPO, "include", "n2v2r.h")).read()
+    txt = "".join(open(os.path.join(REPO, "include", h)).read()
+                  for h in ("n2v2r.h", "n2v2r_diag.h"))
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return sorted(set(re.findall(r"\b(n2v2r_[a-z_0-9]+)\s*\(", txt)))
 

@@ -79,9 +79,17 @@ def _concat(res):
     return Y, X
 
 
+@pytest.fixture(params=["rs", "gather"])
+def stage2(request, monkeypatch):
+    """Stage 2 of a partitioned application: the rank's column share reduce-scattered (the
+    default) or every layer's stage-1 panel all-gathered (N2V2R_DIST_STAGE2=gather)."""
+    monkeypatch.setenv("N2V2R_DIST_STAGE2", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("name", ["er_cfg1", "k4_strategies", "directed_weighted"])
-def test_partitioned_matches_reference(engine, name, world):
+def test_partitioned_matches_reference(engine, name, world, stage2):
     fx = load_fixture(name)
     layers = fixture_layers(fx)
     n = layers[0].shape[0]
@@ -127,11 +135,11 @@ def test_partitioned_matches_reference(engine, name, world):
 
 
 @pytest.mark.parametrize("name", ["er_cfg1", "directed_weighted"])
-def test_partitioned_column_blocks(engine, name, monkeypatch):
-    """Row partition + the XCD-local column-block SpMM (forced on): column blocks are cut over
-    the global column range of the gathered panel."""
+def test_partitioned_column_blocks(engine, name, monkeypatch, stage2):
+    """Row partition + the tiled column-block SpMM (forced on): column blocks are cut over the
+    global column range of the gathered panel."""
     monkeypatch.setenv("N2V2R_SPMM_CB", "1")
-    test_partitioned_matches_reference(engine, name, 2)
+    test_partitioned_matches_reference(engine, name, 2, stage2)
 
 
 def test_partitioned_er_large_rows_ingest(engine):
@@ -157,9 +165,10 @@ def test_partitioned_er_large_rows_ingest(engine):
     assert kendalltau(res[0]["B"][0], one["B"][0]).statistic > 0.99
 
 
-def test_rccl_world1(engine):
+def test_rccl_world1(engine, stage2):
     """Every collective routed through RCCL at world size 1 (init, all-gather of panels and of
-    the distance columns, all-reduces of Gram / residual / sign keys)."""
+    the distance columns, all-reduces of Gram / residual / sign keys, and the reduce-scatter of
+    stage 2 in the default form)."""
     from node2vec2rank_amd import _lib
     fx = load_fixture("er_cfg1")
     layers = fixture_layers(fx)

@@ -33,7 +33,7 @@ def test_spmm_matches_scipy(engine, name, b):
 
 @pytest.mark.parametrize("name", ["er_cfg1", "directed_weighted", "demo"])
 def test_spmm_column_blocks_matches_scipy(engine, name, monkeypatch):
-    """The column-block SpMM (block launch + fixed-order reduce of the 8 partials), forced on."""
+    """The column-block SpMM (the flat-window tiled form), forced on, through n2v2r_bench_spmm."""
     monkeypatch.setenv("N2V2R_SPMM_CB", "1")
     fx = load_fixture(name)
     layers = fixture_layers(fx)
@@ -497,11 +497,11 @@ def test_uase_residuals_er_20k(engine):
     np.testing.assert_allclose(s, s_ref, rtol=1e-5)
 
 
-@pytest.mark.parametrize("b,nb", [(8, 0), (8, 32), (16, 0), (16, 64)])
-def test_spmm_tiled_flat_widths(engine, b, nb):
-    """The flat-window tiled SpMM at panel widths 8 and 16 (the b = 16 form is the probe behind
-    DESIGN §5's width measurement) against scipy, on a directed weighted layer (A and A^T) whose
-    panel spans 4-64 column blocks."""
+@pytest.mark.parametrize("nb", [0, 4, 32, 64])
+def test_spmm_tiled_flat_blocks(engine, nb):
+    """The flat-window tiled SpMM (b = 8) against scipy, on a directed weighted layer (A and A^T)
+    whose panel spans 4-64 column blocks (0: the fit's rule)."""
+    b = 8
     from node2vec2rank_amd import synthetic
     n = 300_000
     A = synthetic.er_layers(n, 12, 1, seed_base=91)[0].tocsr().astype(np.float32)
@@ -516,7 +516,7 @@ def test_spmm_tiled_flat_widths(engine, b, nb):
         M = (A.T if tr else A).tocsr()[rows].astype(np.float64)
         ref = M @ X.astype(np.float64)
         bound = 1e-5 * (abs(M) @ np.abs(X).astype(np.float64)) + 1e-6
-        assert np.all(np.abs(Y[rows] - ref) <= bound), (b, nb, tr)
+        assert np.all(np.abs(Y[rows] - ref) <= bound), (nb, tr)
 
 
 @pytest.mark.parametrize("defer", ["1", "0"])
@@ -547,9 +547,9 @@ def test_uase_paired_full_passes(engine, monkeypatch, defer):
 
 @pytest.mark.parametrize("name", ["er_cfg1", "directed_weighted", "demo"])
 def test_uase_column_blocks_golden(engine, name, monkeypatch):
-    """The XCD-local column-block SpMM (forced on at fixture size; by default it runs for
-    panels of 8-160 MB) reproduces the reference embedding: symmetric, directed (A^T split) and
-    weighted layers."""
+    """The flat-window tiled column-block SpMM (forced on at fixture size; by default it runs
+    for b = 8 panels beyond 8 MB) reproduces the reference embedding: symmetric, directed (A^T
+    split) and weighted layers."""
     monkeypatch.setenv("N2V2R_SPMM_CB", "1")
     fx = load_fixture(name)
     layers = fixture_layers(fx)
@@ -563,20 +563,18 @@ def test_uase_column_blocks_golden(engine, name, monkeypatch):
     assert err <= max(5e-4, 3 * env), (name, err, env)
 
 
-@pytest.mark.parametrize("form", ["flat", "rows", "pair", "partials"])
-def test_uase_column_blocks_er_20k(engine, monkeypatch, form):
-    """Column-block SpMM vs the row SpMM on a 20k-node ER graph with a ragged column count
-    (20,003: the last block is short), in every form (tiled with packed flat windows -- the
-    default --, tiled with row groups, tiled with row-group pairs, 8 partials + reduce): same
-    sigma within fp32 tolerance, true residuals, and run-to-run bit-identical embeddings (fixed
-    summation order; the flat form's LDS adds of a row all come from one wave)."""
+@pytest.mark.parametrize("nb", ["", "4", "64"])
+def test_uase_column_blocks_er_20k(engine, monkeypatch, nb):
+    """The flat-window tiled column-block SpMM vs the row SpMM on a 20k-node ER graph with a
+    ragged column count (20,003: the last block is short), at the fit's block count and at 4 and
+    64 blocks: same sigma within fp32 tolerance, true residuals, and run-to-run bit-identical
+    embeddings (fixed summation order; the LDS adds of a row all come from one wave)."""
     from node2vec2rank_amd import synthetic
     layers = synthetic.er_layers(20_003, 20, 2)
     d = 32
     engine.set_layers(layers)
-    monkeypatch.setenv("N2V2R_SPMM_TILE", "0" if form == "partials" else "1")
-    monkeypatch.setenv("N2V2R_TILE_FLAT", "1" if form == "flat" else "0")
-    monkeypatch.setenv("N2V2R_TILE_PAIR", "2" if form == "pair" else "0")
+    if nb:
+        monkeypatch.setenv("N2V2R_SPMM_TILE_NB", nb)
     monkeypatch.setenv("N2V2R_SPMM_CB", "0")
     engine.uase(d, seed=42)
     s_row = engine.singular_values().copy()
@@ -596,8 +594,7 @@ def test_uase_column_blocks_er_20k(engine, monkeypatch, form):
         assert np.abs(Y1[k] - Yk).max() <= 1e-5 * np.abs(Yk).max(), k
     engine.uase(d, seed=42)
     assert np.array_equal(engine.embedding(), Y1)
-    if form in ("flat", "rows"):
-        assert st["spmm_form"] == (5 if form == "flat" else 3), st["spmm_form"]
+    assert st["spmm_form"] == 5, st["spmm_form"]
 
 
 @pytest.mark.parametrize("layers_k", [2, 3])
@@ -724,10 +721,18 @@ def test_uase_block_widths(engine, name, block):
 
 
 # ----------------------------------------------------------------------------- Rayleigh-Ritz
-@pytest.mark.parametrize("c,p", [(40, 12), (256, 80), (300, 100), (512, 160), (600, 150), (768, 200)])
-def test_rayleigh_ritz_stage(engine, c, p):
-    """GPU tridiagonalisation + host tridiagonal solve + GPU back-transform vs numpy eigh,
-    including a tight cluster (gaps 1e-9 relative) and an exactly repeated eigenvalue."""
+@pytest.mark.parametrize("form", ["multi", "multi-pr4", "one"])
+@pytest.mark.parametrize("c,p", [(40, 12), (256, 80), (300, 100), (512, 160), (600, 150),
+                                 (737, 64), (768, 200)])
+def test_rayleigh_ritz_stage(engine, monkeypatch, c, p, form):
+    """GPU tridiagonalisation (the multi-workgroup form: 32 x 32 tiles in the LDS of PR x nt
+    workgroups, one grid barrier per step; and the one-workgroup kernel, N2V2R_RR_TRI=1) +
+    tridiagonal bisection / inverse iteration + GPU back-transform vs numpy eigh, including a
+    tight cluster (gaps 1e-9 relative) and an exactly repeated eigenvalue."""
+    if form == "one":
+        monkeypatch.setenv("N2V2R_RR_TRI", "1")
+    elif form == "multi-pr4":
+        monkeypatch.setenv("N2V2R_RR_TRI_PR", "4")
     rng = np.random.default_rng(c)
     ev = np.sort(rng.random(c))[::-1] * 100.0
     ev[3:8] = ev[3] - 1e-7 * np.arange(5)
