@@ -1005,9 +1005,12 @@ static hipError_t launch_rr_tridiag_coop(double* A, int c, double* d, double* e,
   int* err = reinterpret_cast<int*>(ctr + 1);  // 1 after a timed-out grid barrier
   hipError_t er = hipMemsetAsync(ctr, 0, 2 * sizeof(unsigned), stream);
   if (er != hipSuccess) return er;
-  void* args[] = {&A, &c, &PR, &d, &e, &tau, &V, &part, &rowbuf, &ctr, &err};
-  return hipLaunchCooperativeKernel((const void*)rr_tridiag_coop_kernel, dim3((unsigned)(PR * nt)),
-                                    dim3(TRC_NT), args, (unsigned)shmem, stream);
+  // a plain launch: PR x nt <= 4 x 24 workgroups of one CU each are resident on the 256 CUs
+  // (the cooperative launch would only add its occupancy check, +15-19 us of host time; the
+  // bounded spin ends the launch even if a workgroup were held back)
+  hipLaunchKernelGGL(rr_tridiag_coop_kernel, dim3((unsigned)(PR * nt)), dim3(TRC_NT), shmem, stream,
+                     A, c, PR, d, e, tau, V, part, rowbuf, ctr, err);
+  return hipGetLastError();
 }
 
 extern "C" hipError_t n2v2r_launch_rr_tridiag(double* A, int c, double* d, double* e, double* tau,
