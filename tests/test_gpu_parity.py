@@ -357,6 +357,11 @@ def _cfg(fx, strategy):
                 comp_strategy=strategy, verbose=-1, save_dir=None)
 
 
+def eng_stable_borda(df):
+    from node2vec2rank_amd import _lib
+    return _lib.default_engine().borda_columns(df.to_numpy(dtype=np.float64), tie_order="stable")
+
+
 @pytest.mark.parametrize("name", FIXTURES)
 def test_model_end_to_end(name):
     from node2vec2rank_amd.model import N2V2R
@@ -422,14 +427,19 @@ def test_model_end_to_end(name):
                 # method sees it: tau of the reference's Borda against the reference re-run from
                 # other start vectors, without sign alignment, the minimum over ENV_SEEDS runs
                 # (and against the drop-in's own correlation-free-of-sign comparison above)
+                # (a) the drop-in's output against the reference's output as they are
                 tau_ref = kendalltau(b, fx[f"{strategy}/{key}/borda"]).statistic
-                env_al = _tau_envelope(Y_other, fx, strategy, key)
                 env_un = env_unaligned[strategy][key]
-                print(f"    vs the reference's Borda as is: tau {tau_ref:.6f}; reference "
-                      f"envelope aligned {env_al:.6f}, unaligned (min of {ENV_SEEDS}) "
-                      f"{env_un:.6f}")
+                # (b) with the signs aligned and both sides in the stable tie order (numpy
+                # quicksort's order of the 0 / 2 ties of the 2-d correlation column changes with
+                # any perturbation of the column, so only the stable order compares ties)
+                tau_st = kendalltau(eng_stable_borda(df), orc.borda(Dref)).statistic
+                env_al = _tau_envelope(Y_other, fx, strategy, key)
+                print(f"    vs the reference's Borda as is: tau {tau_ref:.6f} (reference "
+                      f"envelope, unaligned, min of {ENV_SEEDS}: {env_un:.6f}); signs aligned, "
+                      f"stable ties: tau {tau_st:.6f} (envelope {env_al:.6f})")
                 assert tau_ref >= min(0.998, env_un), (name, strategy, key, tau_ref, env_un)
-                assert tau >= min(0.998, env_al - 0.02), (name, strategy, key, tau, env_al)
+                assert tau_st >= min(0.998, env_al - 0.02), (name, strategy, key, tau_st, env_al)
         Y = model.node_embeddings
         assert Y.shape == fx["Y"].shape
 
