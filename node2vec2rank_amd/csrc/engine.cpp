@@ -1698,6 +1698,7 @@ struct Eig {
     HIPCHK(hipMemsetAsync(h->ews.skipc.p, 0, sizeof(int) * 68, st));
     if (lean) h->ews.rres.ensure(sizeof(double) * 64);
     double est_scale = 1.0;  // lean: true / estimated residual seen at a failed final check
+    double last_true = 1e300;  // lean: the worst true residual of the previous check
     bool rr_armed = false;   // the Rayleigh-Ritz error words zeroed (then by every read-back)
     int lean_checks = 0;
     // pinned read-back per cycle: residuals, Ritz values (keep each), flags, R (8 x 8), S's last rows
@@ -2042,15 +2043,19 @@ struct Eig {
                               hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         for (float* p : MV) give(p);
-        double worst = 0.0, ratio = 0.0;
+        double worst = 0.0, est_max = 0.0;
         int tconv = 0;
         for (int j = 0; j < d; ++j) {
           const double r = std::sqrt(std::max(pres[j], 0.0)) / th1;
           const double e = std::sqrt(std::max(res2[j], 0.0)) / th1;
           worst = std::max(worst, r);
+          est_max = std::max(est_max, e);
           if (r <= tol) ++tconv;
-          if (e > 0.0) ratio = std::max(ratio, r / e);
         }
+        // the scale that brings the worst estimate to the worst true residual (a ratio taken
+        // vector by vector blew up on estimates at the fp32 noise level: 1e-12 against a true
+        // 1e-7 gave a scale of 1e5, and the scaled estimates never came back below tol)
+        const double ratio = est_max > 0.0 ? worst / est_max : 0.0;
         if (trace)
           fprintf(stderr, "[n2v2r] cycle %d: true max_res %.3e converged %d/%d (estimate %.3e)\n",
                   cycle, worst, tconv, d, maxres);
@@ -2058,17 +2063,21 @@ struct Eig {
         conv = tconv;
         stagnated = 0;
         if (conv < d && cycle + 1 < max_restarts) {
-          // at the fp32 floor the true residual stops falling: finish within 100x tol
-          if (lean_checks >= 4 && worst <= 100.0 * tol) {
+          // at the fp32 floor the true residual stops falling: finish within 100x tol once a
+          // check shows no 10 % gain over the previous one (or after 4 checks)
+          const bool flat = lean_checks >= 2 && worst > 0.9 * last_true;
+          if ((flat || lean_checks >= 4) && worst <= 100.0 * tol) {
             stagnated = 1;
           } else {
             done = false;
             // the estimates (already scaled) trail the true residual by `ratio`: rescale from
-            // this check (it may also shrink back towards 1 after a pessimistic one)
-            if (ratio > 0.0) est_scale = std::max(1.0, est_scale * 1.25 * ratio);
+            // this check (it may also shrink back towards 1 after a pessimistic one), at most
+            // by 1e3 in all
+            if (ratio > 0.0) est_scale = std::min(1e3, std::max(1.0, est_scale * 1.25 * ratio));
             hist_res.clear();
           }
         }
+        last_true = worst;
       }
       if (done) {
         give(E_lean);

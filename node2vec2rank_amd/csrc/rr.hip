@@ -260,38 +260,60 @@ __global__ __launch_bounds__(NT) void rr_tridiag_kernel(double* __restrict__ A, 
 //   (published by its owners) -> d[o] and the next reflector vn;
 //   then updates its own tiles B -= v w^T + w v^T on rows/columns >= o+1 and accumulates the
 //   column partials of the next matvec B' vn, which it publishes with the new pivot row o+1.
-// No grid barrier: every published double travels as two data-tagged 8-B granules {32 bits of
-// the value, the step's tag} (MI355X_MICROARCH.md, persistent-kernel price list: handoff-1to1),
-// each written by one agent-scope relaxed atomic store (global_store_dwordx2 sc1) and read by
-// sc1 loads until both tags equal the step's; a naturally aligned 8-B access is single-copy
-// atomic, so a granule is either the old one or the new one.  Partials and pivot rows are
-// double-buffered by step parity: a workgroup rewrites a slot two steps after it was read,
-// having consumed the intermediate step's data from every workgroup, each of which published it
-// only after reading that slot.  (The first form, a monotonic counter barrier per step -- sc1
-// payload stores, vmcnt(0), one atomic add, an sc1 poll -- ran 6.5 ms per call at c = 768.)
-// The spin is bounded: a workgroup that waits ~seconds gives up, sets *err and writes NaN to
-// d[0] (the caller's Ritz values then fail), so the launch always drains.
+// One grid barrier per step.  Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first
+// row of the sc1 table): every published double is an agent-scope relaxed atomic store
+// (global_store sc1), every storing wave waits vmcnt(0), a workgroup barrier, then ONE lane
+// adds to the monotonic counter; the poller reads it with sc1 loads, the workgroup barrier
+// releases the other waves, and every load of published data is an sc1 load.  Partials and the
+// pivot row are double-buffered by step parity (a buffer is rewritten only two barriers after
+// it was read).  The spin is bounded: a workgroup that waits ~seconds gives up, sets *err and
+// writes NaN to d[0] (the caller's Ritz values then fail), so the launch always drains.
+// (Measured and dropped: data-tagged 8-B granules polled by every thread instead of the
+// counter -- no barrier, but 96 workgroups x 256 threads polling the same lines starved the
+// producers' stores: one c = 768 call at PR = 4 timed out; the counter poll is one lane per
+// workgroup.)
 #define TRC_TS 32
 #define TRC_LD 33
 #define TRC_NT 256
 
-typedef unsigned long long u64;
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __longlong_as_double(__hip_atomic_load(reinterpret_cast<const long long*>(p),
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1(double* p, double x) {
+  __hip_atomic_store(reinterpret_cast<long long*>(p), __double_as_longlong(x), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
 
-__device__ __forceinline__ void st_gran(u64* g, double x, unsigned tag) {
-  const u64 b = (u64)__double_as_longlong(x);
-  __hip_atomic_store(g, ((u64)tag << 32) | (b & 0xFFFFFFFFull), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(g + 1, ((u64)tag << 32) | (b >> 32), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
+// returns true when the wait timed out
+__device__ __forceinline__ bool trc_grid_barrier(unsigned* ctr, unsigned target, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int f = 0;
+    long it = 0;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (++it > (1l << 24)) {
+        f = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    *flag = f;
+  }
+  __syncthreads();
+  return *flag != 0;
 }
 
 __global__ __launch_bounds__(TRC_NT) void rr_tridiag_coop_kernel(
     const double* __restrict__ A, int c, int PR, double* __restrict__ dd, double* __restrict__ ee,
-    double* __restrict__ tau, double* __restrict__ V, u64* part /* [2][PR][c][2] granules */,
-    u64* rowbuf /* [2][c][2] granules */, int* err) {
+    double* __restrict__ tau, double* __restrict__ V, double* part /* [2][PR][c] */,
+    double* rowbuf /* [2][c] */, unsigned* ctr, int* err) {
   constexpr int NW = TRC_NT / 64;
   extern __shared__ double lds[];
   const int nt = (c + TRC_TS - 1) / TRC_TS;
+  const int G = gridDim.x;
   const int pc = blockIdx.x % nt, pr = blockIdx.x / nt;
   const int ntr = (nt - pr + PR - 1) / PR;  // row tiles pr + PR q, q < ntr
   double* T = lds;                                   // [ntr][32][33]
@@ -302,7 +324,7 @@ __global__ __launch_bounds__(TRC_NT) void rr_tridiag_coop_kernel(
   double* row = p + c;
   double* accs = row + c;                            // [8][32]
   __shared__ double red[NW];
-  __shared__ int flag;  // a timed-out wait (set by any thread, read after a barrier)
+  __shared__ int flag;
   const int tid = threadIdx.x, tx = tid & 31, ty = tid >> 5;
   const int J = TRC_TS * pc + tx;  // this thread's column
   const bool lead = blockIdx.x == 0;
@@ -344,9 +366,8 @@ __global__ __launch_bounds__(TRC_NT) void rr_tridiag_coop_kernel(
     return t;
   };
   // the WG's tiles on rows / columns >= lo: optional rank-2 update (v, w), column partials of
-  // the product with mv, published to part[par][pr][.], and the pivot row lo to rowbuf[par],
-  // tagged `tag`
-  auto pass = [&](int lo, bool upd, const double* mv, int par, unsigned tag) {
+  // the product with mv, published to part[par][pr][.], and the pivot row lo to rowbuf[par]
+  auto pass = [&](int lo, bool upd, const double* mv, int par) {
     const bool jok = J >= lo && J < c;
     const double vJ = (upd && jok) ? v[J] : 0.0, wJ = (upd && jok) ? w[J] : 0.0;
     const int rlo = lo & (TRC_TS - 1), blo = lo / TRC_TS;
@@ -365,7 +386,7 @@ __global__ __launch_bounds__(TRC_NT) void rr_tridiag_coop_kernel(
             tile[rr * TRC_LD + tx] = a;
           }
           acc += a * mv[R];
-          if (R == lo) st_gran(rowbuf + ((size_t)par * c + J) * 2, a, tag);
+          if (R == lo) st_sc1(rowbuf + (size_t)par * c + J, a);
         }
       }
     }
@@ -375,11 +396,10 @@ __global__ __launch_bounds__(TRC_NT) void rr_tridiag_coop_kernel(
       double sacc = 0.0;
 #pragma unroll
       for (int y = 0; y < 8; ++y) sacc += accs[y * TRC_TS + tx];
-      st_gran(part + (((size_t)par * PR + pr) * c + J) * 2, sacc, tag);
+      st_sc1(part + ((size_t)par * PR + pr) * c + J, sacc);
     }
   };
 
-  if (tid == 0) flag = 0;  // (read only after the barriers below)
   // tiles in: symmetrised as the one-workgroup kernel does
   for (int q = 0; q < ntr; ++q) {
     const int bi = pr + PR * q;
@@ -395,60 +415,18 @@ __global__ __launch_bounds__(TRC_NT) void rr_tridiag_coop_kernel(
   if (lead && tid == 0) dd[0] = A[0];
   __syncthreads();
   double t = make_reflector(v, 1, 0);
-  pass(1, false, v, 0, 1u);
-  bool failed = false;
-  for (int k = 0;; ++k) {
+  pass(1, false, v, 0);
+  unsigned nbar = 1;
+  bool failed = trc_grid_barrier(ctr, (unsigned)G * nbar, &flag);
+  for (int k = 0; !failed; ++k) {
     const int o = k + 1, par = k & 1;
-    const unsigned want = (unsigned)(k + 1);
-    // this thread's entries i = o + tid + 256 j (j < 3: c <= 768) of the PR partials and of the
-    // pivot row: every granule pair loaded, the tags checked, the stale ones loaded again
-    {
-      double val[3][5];
-      unsigned need = 0;
-#pragma unroll
-      for (int j = 0; j < 3; ++j)
-        for (int q = 0; q <= PR; ++q)
-          if (o + tid + TRC_NT * j < c) need |= 1u << (j * 5 + q);
-      long spins = 0;
-      while (need) {
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-#pragma unroll
-          for (int q = 0; q < 5; ++q) {
-            if (!(need >> (j * 5 + q) & 1u)) continue;
-            const int i = o + tid + TRC_NT * j;
-            const u64* g = q < PR ? part + (((size_t)par * PR + q) * c + i) * 2
-                                  : rowbuf + ((size_t)par * c + i) * 2;
-            const u64 lo = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const u64 hi = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((unsigned)(lo >> 32) == want && (unsigned)(hi >> 32) == want) {
-              val[j][q] = __longlong_as_double((long long)((hi << 32) | (lo & 0xFFFFFFFFull)));
-              need &= ~(1u << (j * 5 + q));
-            }
-          }
-        }
-        if (need) {
-          if (++spins > (1l << 22)) break;
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-      if (need) flag = 1;  // (several threads may store it: the same value)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int i = o + tid + TRC_NT * j;
-        if (i < c && !need) {
-          double sp = 0.0;
-          for (int q = 0; q < PR; ++q) sp += val[j][q];
-          p[i] = t * sp;
-          row[i] = val[j][PR];
-        }
-      }
+    for (int i = o + tid; i < c; i += TRC_NT) {
+      double sp = 0.0;
+      for (int q = 0; q < PR; ++q) sp += ld_sc1(part + ((size_t)par * PR + q) * c + i);
+      p[i] = t * sp;
+      row[i] = ld_sc1(rowbuf + (size_t)par * c + i);
     }
     __syncthreads();
-    if (flag) {
-      failed = true;
-      break;
-    }
     double pp = 0.0;
     for (int i = o + tid; i < c; i += TRC_NT) pp += p[i] * v[i];
     const double half = 0.5 * t * bsum(pp);
@@ -471,20 +449,20 @@ __global__ __launch_bounds__(TRC_NT) void rr_tridiag_coop_kernel(
       break;
     }
     const double tn = make_reflector(vn, o + 1, o);
-    pass(o + 1, true, vn, par ^ 1, want + 1);
-    // every read of v in the pass precedes the workgroup barrier inside it
+    pass(o + 1, true, vn, par ^ 1);
+    // every read of v in the pass precedes the partials' barrier inside it
     for (int i = o + 1 + tid; i < c; i += TRC_NT) v[i] = vn[i];
     t = tn;
+    failed = trc_grid_barrier(ctr, (unsigned)G * ++nbar, &flag);
   }
   if (failed && tid == 0) {
     __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    dd[0] = __builtin_nan("");
+    st_sc1(dd, __builtin_nan(""));
   }
 }
 
-// [2][PR <= 4][c][2] partial granules, [2][c][2] pivot-row granules, an error word
 extern "C" size_t n2v2r_rr_tridiag_scratch_bytes(int c) {
-  return sizeof(u64) * ((size_t)2 * 4 * c * 2 + (size_t)2 * c * 2) + 64;
+  return sizeof(double) * ((size_t)2 * 4 * c + (size_t)2 * c) + 64;
 }
 
 // Y: p eigenvectors of T, column-major (vector j at Y[j * c]).  S[i * lds + j] = (P Y)[i][j],
@@ -1025,17 +1003,17 @@ static hipError_t launch_rr_tridiag_coop(double* A, int c, double* d, double* e,
     (void)hipGetLastError();
     attr_set = true;
   }
-  u64* part = static_cast<u64*>(scratch);
-  u64* rowbuf = part + (size_t)2 * 4 * c * 2;
-  int* err = reinterpret_cast<int*>(rowbuf + (size_t)2 * c * 2);  // 1 after a timed-out wait
-  // tags start at 1: zeroed granules never match
-  hipError_t er = hipMemsetAsync(scratch, 0, n2v2r_rr_tridiag_scratch_bytes(c), stream);
+  double* part = static_cast<double*>(scratch);
+  double* rowbuf = part + (size_t)2 * 4 * c;
+  unsigned* ctr = reinterpret_cast<unsigned*>(rowbuf + (size_t)2 * c);
+  int* err = reinterpret_cast<int*>(ctr + 1);  // 1 after a timed-out grid barrier
+  hipError_t er = hipMemsetAsync(ctr, 0, 2 * sizeof(unsigned), stream);
   if (er != hipSuccess) return er;
   // a plain launch: PR x nt <= 4 x 24 workgroups of one CU each are resident on the 256 CUs
   // (the cooperative launch would only add its occupancy check, +15-19 us of host time; the
   // bounded spin ends the launch even if a workgroup were held back)
   hipLaunchKernelGGL(rr_tridiag_coop_kernel, dim3((unsigned)(PR * nt)), dim3(TRC_NT), shmem, stream,
-                     A, c, PR, d, e, tau, V, part, rowbuf, err);
+                     A, c, PR, d, e, tau, V, part, rowbuf, ctr, err);
   return hipGetLastError();
 }
 

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 N2V2R_TRACE=1 timeout -k 10 200 python -u tools/trace_fit.py 100000 50 128 > gpurun_out/r04_trace_cfg4g.json 2> gpurun_out/r04_trace_cfg4g.err
 rc=$?; tail -3 gpurun_out/r04_trace_cfg4g.err; cut -c1-400 gpurun_out/r04_trace_cfg4g.json; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python -u -m pytest tests -m gpu -v -s --maxfail=5 --timeout 400 \
-  --timeout-method thread -p no:cacheprovider -k "rayleigh_ritz_stage or cfg3 or end_to_end or large_dimension or block_widths" \
+  --timeout-method thread -p no:cacheprovider -k "rayleigh_ritz_stage or cfg3 or end_to_end or large_dimension or block_widths or cfg4_grid or lean or uase_residuals" \
   > gpurun_out/r04_c_tests.log 2>&1
 rc=$?; tail -5 gpurun_out/r04_c_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 180 tools/gather_ceiling 100 20 > gpurun_out/r04_gather_ceiling.jsonl 2>&1
