@@ -17,6 +17,7 @@
 //           random values by fill_flagged so the next CGS pass can orthogonalise them.
 #include "common.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -1549,12 +1550,18 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
                                                         double* __restrict__ save, int save_row0,
                                                         int save_rows, float* __restrict__ fout,
                                                         int stage, int* sticky) {
+  // grid.x > 1 (wide blocks, long bases): every workgroup forms P and factors it (redundant,
+  // bit-identical), workgroup g writes rows [g, g + 1) * ceil((c + b) / grid.x) of F, and
+  // workgroup 0 alone the other outputs
+  const bool lead = blockIdx.x == 0;
   if (cond && *cond == 0) {
-    if (threadIdx.x < b) flags[threadIdx.x] = 0;
-    if (threadIdx.x == 0) *any_flag = 0;
+    if (lead && threadIdx.x < b) flags[threadIdx.x] = 0;
+    if (lead && threadIdx.x == 0) *any_flag = 0;
     return;
   }
-  if (save)
+  const int fper = (c + b + gridDim.x - 1) / gridDim.x;
+  const int fbeg = blockIdx.x * fper, fend = min(c + b, fbeg + fper);
+  if (save && lead)
     for (int e = threadIdx.x; e < save_rows * b; e += blockDim.x)
       save[e] = G[(int64_t)save_row0 * b + e];
   // G staged through LDS when it fits (b = 8: (c + 8) x 8 doubles <= 50 KB): the P and F loops
@@ -1704,12 +1711,13 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
       PIP_WSYNC();
     }
 #undef PIP_WSYNC
-    for (int e = tid; e < bb; e += nw) {
-      const int r = e / b, cc = e % b;
-      xinv[e] = bad[cc] ? 0.0 : X[r][cc];
-    }
-    if (tid < b) flags[tid] = bad[tid];
-    if (tid == 0) {
+    if (lead)
+      for (int e = tid; e < bb; e += nw) {
+        const int r = e / b, cc = e % b;
+        xinv[e] = bad[cc] ? 0.0 : X[r][cc];
+      }
+    if (lead && tid < b) flags[tid] = bad[tid];
+    if (lead && tid == 0) {
       int any = 0;
       for (int j = 0; j < b; ++j) any |= bad[j];
       *any_flag = any;
@@ -1718,11 +1726,13 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
   }
   __syncthreads();
   if (fout && !stage && bb > 64) {
-    // the same F with C through LDS in chunks (R's storage: R is spent once xinv is out)
+    // the same F with C through LDS in chunks (R's storage: R is spent once xinv is out), this
+    // workgroup's rows [fbeg, fend) only
     double* cst = &R[0][0];
     const int rows = 4096 / b;
-    for (int k0 = 0; k0 < c; k0 += rows) {
-      const int kr = min(rows, c - k0);
+    const int cend = min(c, fend);
+    for (int k0 = fbeg; k0 < cend; k0 += rows) {
+      const int kr = min(rows, cend - k0);
       const int tot = kr * b;
       __syncthreads();
       for (int q0 = tid; q0 < tot; q0 += nt * 4) {
@@ -1746,10 +1756,11 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
     }
     for (int e = tid; e < bb; e += nt) {
       const int i = e / b, j = e % b;
-      fout[(int64_t)(c + i) * b + j] = bad[j] ? 0.f : (float)X[i][j];
+      if (c + i >= fbeg && c + i < fend)
+        fout[(int64_t)(c + i) * b + j] = bad[j] ? 0.f : (float)X[i][j];
     }
   } else if (fout) {  // every thread: F[k][j] = -sum_{m <= j} C[k][m] X[m][j]; F[c + i][j] = X[i][j]
-    for (int e = tid; e < (c + b) * b; e += nt) {
+    for (int e = tid + fbeg * b; e < fend * b; e += nt) {
       const int k = e / b, j = e % b;
       float v = 0.f;
       if (!bad[j]) {
@@ -1774,7 +1785,9 @@ extern "C" hipError_t n2v2r_launch_pip_chol(const double* G, int c, int b, doubl
   if (b > 64) return hipErrorInvalidValue;
   const size_t gbytes = sizeof(double) * (size_t)(c + b) * b;
   const int stage = gbytes <= 56 * 1024 ? 1 : 0;
-  hipLaunchKernelGGL(pip_chol_kernel, dim3(1), dim3(1024), stage ? gbytes : 0, stream, G, c, b,
+  // wide blocks with F wanted: F's rows over up to 8 workgroups (each factors P itself)
+  const int nwg = (fout && b > 8) ? std::min(8, (c + b + 127) / 128) : 1;
+  hipLaunchKernelGGL(pip_chol_kernel, dim3(nwg), dim3(1024), stage ? gbytes : 0, stream, G, c, b,
                      xinv, flags, any_flag, cond, save, save_row0, save_rows, fout, stage, sticky);
   return hipGetLastError();
 }

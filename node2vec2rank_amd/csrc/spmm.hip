@@ -415,7 +415,10 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
   // and not kept (cfg4 layer launch 0.367 ms): windows handed out per phase from an LDS
   // counter (0.557 ms), the next window's row pointers loaded before the current window's
   // entries (0.367 ms, flat); 512-thread workgroups with half the tile rows, 4 per CU
-  // (0.448 ms)
+  // (0.448 ms); round 4: a wave owning one contiguous span of 4 windows walked as one run (no
+  // partial step per window; the row sums folded by a per-lane row cursor): 0.393 vs 0.368 ms,
+  // fit 1,682 vs 1,613 ms, bit-identical sums (profiles/r04_span_ab.jsonl) -- the partial steps
+  // are not what the launch waits on
   for (int w = wave; w < nwin; w += nwave) {
     const int lr = w * CB_WIN + pr;
     if (lr < nrows) tacc[lr * 2 + sub] = zero;
