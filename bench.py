@@ -264,13 +264,15 @@ def roofline_from_stats(st, cfg, b):
            "fit_spmm_gpu_ms": [round(x, 2) for x in ms], "fit_spmm_launches": [int(c) for c in cnt]}
     if cfg.get("dense"):
         flops = 2.0 * cfg["n"] * cfg["n"] * b  # one layer's GEMM per launch
-        out["kernel"] = "dense_gemm_kernel (A_k X, MFMA f32 32x32x2)"
+        out["kernel"] = ("dense_tn_kernel (A_k X as (B^T X), B streamed from HBM into the MFMA "
+                         "B operand, f32 32x32x2)")
         out["mfma_tflops"] = round(flops / (t * 1e-3) / 1e12, 2)
         out["mfma_frac"] = round(flops / (t * 1e-3) / 1e12 / MFMA_F32_PEAK_TFLOPS, 4)
     return out
 
 
 WATCHDOG_EXIT = 3
+GATHER_CEILING_G = 182.1  # G entries/s, profiles/r04_gather_ceiling.jsonl (stream+gather, 2 MB)
 
 
 def run_guarded(fn, limit_s, on_timeout):
@@ -416,18 +418,29 @@ def main():
         form = int(st_t.get("spmm_form", 0))
         roof["kernel"] = {0: "spmm8_pipe_kernel (b = 8)",
                           1: "spmm8_pipe_kernel (b = 8, layers split over the XCDs)",
-                          2: "spmm8_cb_kernel (XCD-local column blocks; + cb_reduce)",
-                          3: "spmm8_tile_kernel (row tiles x column-block phases, LDS "
-                             "accumulators)",
                           5: "spmm8_flat_kernel (row tiles x column-block phases, packed flat "
-                             "windows, LDS accumulators)"}.get(form, str(form))
+                             "windows, LDS accumulators, non-temporal index stream)"
+                          }.get(form, str(form))
         # one 32-B panel row gathered per stored entry (served by L2 / Infinity Cache): the
-        # line-access rate, reported beside the HBM roofline.  Entries per launch: every
-        # layer's (row kernel, tiled), one layer's (column blocks + partials)
+        # line-access rate, reported beside the HBM roofline
         nnz_launch = float(sum(nnz)) / (world if mode == "partitioned" else 1)
-        ent = nnz_launch / len(nnz) if form == 2 else nnz_launch
+        ent = nnz_launch
         roof["gathered_entries_per_launch"] = ent
         roof["gather_G_entries_per_s"] = round(ent / (roof["avg_launch_ms"] * 1e-3) / 1e9, 1)
+        # the same launch against the measured gather ceiling (tools/gather_ceiling.hip, 32-B
+        # rows from a 2 MB L2-resident panel with the 4-B index stream:
+        # profiles/r04_gather_ceiling.jsonl)
+        roof["gather_ceiling_G_entries_per_s"] = GATHER_CEILING_G
+        roof["gather_ceiling_frac"] = round(roof["gather_G_entries_per_s"] / GATHER_CEILING_G, 3)
+        # SURVEY 8(d)'s bytes as written (a value stream even for unweighted layers, 4-B row
+        # pointers, panel + output): 8 nnz + 4 (N + 1) + 8 N b per layer
+        n_launch = cfg["n"] / (world if mode == "partitioned" else 1)
+        lit = sum(8.0 * z / (world if mode == "partitioned" else 1) for z in nnz) + \
+            len(nnz) * (4.0 * (n_launch + 1) + 8.0 * n_launch * b)
+        roof["literal_8d"] = {"bytes_per_launch": lit,
+                              "achieved": round(lit / (roof["avg_launch_ms"] * 1e-3) / 1e9, 1),
+                              "frac": round(lit / (roof["avg_launch_ms"] * 1e-3) / 1e9
+                                            / HBM_PEAK_GBPS, 4)}
     tpath = os.path.join(REPO, "profiles", "spmm_traffic.json")
     if roof is not None and os.path.exists(tpath) and world == 1:
         try:

@@ -1664,10 +1664,51 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
   for (int e = tid; e < bb; e += nt) X[e / b][e % b] = (e / b == e % b) ? 1.0 : 0.0;
   if (tid < 64) bad[tid] = 0;
   __syncthreads();
-  // O(b^3), b <= 64: wave 0 alone, synchronised as a wave (LDS executes a wave's accesses in
-  // order; the waits only keep the compiler from reordering), the other waves wait at the
-  // barrier below -- no block-wide barrier per elimination step
-  if (tid < 64) {
+  if (b > 8 && bb <= nt) {
+    // 8 < b <= 32: one thread per entry of the b x b matrix, the upper triangle in registers,
+    // one workgroup barrier per elimination step and per substitution step (the wave-0 form
+    // below serialises ~b^3 / 64 dependent LDS updates: ~110 us per call at b = 32)
+    const int ei = tid / b, ej = tid % b;
+    const bool own = tid < bb;
+    if (tid < 64) {
+      double m = (tid < b) ? R[tid][tid] : 0.0;
+      for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+      if (tid == 0) dmax = m;
+    }
+    double v = own ? R[ei][ej] : 0.0;
+    __syncthreads();
+    const double tiny = 1e-10 * dmax;
+    for (int k = 0; k < b; ++k) {
+      // row k of R in LDS holds its values after step k - 1 (written before the barrier)
+      const double d = R[k][k];
+      const bool isbad = !(d > tiny);
+      const double pk = isbad ? 1.0 : sqrt(d);
+      if (own && ei == k) {
+        v = isbad ? (ej == k ? 1.0 : 0.0) : (ej == k ? pk : v / pk);
+      } else if (own && ei > k && ej >= ei && !isbad) {
+        v -= (R[k][ei] / pk) * (R[k][ej] / pk);
+      }
+      if (tid == 0) bad[k] = isbad ? 1 : 0;
+      if (own && ei == k + 1) R[k + 1][ej] = v;  // the next pivot row (no reader this step)
+      __syncthreads();
+    }
+    if (own && ej >= ei) R[ei][ej] = v;  // final R (upper triangle)
+    __syncthreads();
+    // X = R^{-1} (upper triangular) by back substitution, x = X[ei][ej] in a register: step j
+    // finishes row j (scaled by 1 / R[j][j], published), then every row above subtracts it
+    double x = (own && ei == ej) ? 1.0 : 0.0;
+    for (int j = b - 1; j >= 0; --j) {
+      if (own && ei == j) {
+        x *= 1.0 / R[j][j];
+        X[j][ej] = x;
+      }
+      __syncthreads();
+      if (own && ei < j) x -= R[ei][j] * X[j][ej];
+    }
+  } else if (tid < 64) {
+    // O(b^3), b <= 64: wave 0 alone, synchronised as a wave (LDS executes a wave's accesses in
+    // order; the waits only keep the compiler from reordering), the other waves wait at the
+    // barrier below -- no block-wide barrier per elimination step
     const int nw = 64;
 #define PIP_WSYNC() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
     {
@@ -1711,20 +1752,20 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
       PIP_WSYNC();
     }
 #undef PIP_WSYNC
-    if (lead)
-      for (int e = tid; e < bb; e += nw) {
-        const int r = e / b, cc = e % b;
-        xinv[e] = bad[cc] ? 0.0 : X[r][cc];
-      }
-    if (lead && tid < b) flags[tid] = bad[tid];
-    if (lead && tid == 0) {
-      int any = 0;
-      for (int j = 0; j < b; ++j) any |= bad[j];
-      *any_flag = any;
-      if (any && sticky) *sticky = 1;
-    }
   }
   __syncthreads();
+  if (lead)
+    for (int e = tid; e < bb; e += nt) {
+      const int r = e / b, cc = e % b;
+      xinv[e] = bad[cc] ? 0.0 : X[r][cc];
+    }
+  if (lead && tid < b) flags[tid] = bad[tid];
+  if (lead && tid == 0) {
+    int any = 0;
+    for (int j = 0; j < b; ++j) any |= bad[j];
+    *any_flag = any;
+    if (any && sticky) *sticky = 1;
+  }
   if (fout && !stage && bb > 64) {
     // the same F with C through LDS in chunks (R's storage: R is spent once xinv is out), this
     // workgroup's rows [fbeg, fend) only

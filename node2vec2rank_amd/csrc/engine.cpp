@@ -139,6 +139,10 @@ hipError_t n2v2r_launch_borda_finish(const int32_t* sorted_idx, int64_t n, int n
                                      int32_t* pos, int64_t* borda, hipStream_t stream);
 hipError_t n2v2r_launch_tie_flags(const uint64_t* sorted_keys, int64_t n, int nseg, int32_t* tied,
                                   hipStream_t stream);
+hipError_t n2v2r_launch_dense_tn(const float* B, int64_t ldb, int64_t ncols, int64_t kdim,
+                                 const float* X, int ldx, int b, float* Y, int64_t ldy, float beta,
+                                 const float* colscale, float* work, size_t work_elems,
+                                 hipStream_t stream);
 hipError_t n2v2r_launch_dense_gemm(const float* A, int64_t lda, int64_t rows, int64_t kdim,
                                    const float* X, int ldx, int b, float* Y, int64_t ldy,
                                    float beta, const float* colscale, float* work,
@@ -686,13 +690,24 @@ struct n2v2r_handle {
   DevBuf dense_work;        // split-K slabs of the dense GEMM
   size_t dense_work_elems = 0;
   bool dense_layers() const { return !layers.empty() && layers[0]->dense; }
-  // Y (nloc x b, ld ldy) = beta Y + colscale .* (A_loc X_global) for dense layer rows
+  // Y (nloc x b, ld ldy) = beta Y + colscale .* (A_loc X_global) for dense layer rows.
+  // Bt (optional, unpartitioned handles): the stored matrix whose TRANSPOSE is A (A itself when
+  // symmetric, the other copy when directed): then Y = Bt^T X by dense_tn_kernel, B streaming
+  // from HBM into the MFMA operands (N2V2R_DENSE_TN=0, read per call: the LDS-staged kernel)
   void dense_apply(const float* Aloc, int64_t lda, const float* X, int ldx, int b, float* Y,
-                   int64_t ldy, float beta, const float* colscale) {
-    const size_t need = (size_t)std::max<int64_t>(nloc, 1) * b * 8;
+                   int64_t ldy, float beta, const float* colscale, const float* Bt = nullptr) {
+    const size_t need = (size_t)std::max<int64_t>(nloc, 1) * b * 16;
     if (dense_work_elems < need) {
       dense_work.ensure(sizeof(float) * need);
       dense_work_elems = need;
+    }
+    const char* tn = std::getenv("N2V2R_DENSE_TN");
+    if (Bt && nloc == n && !(tn && tn[0] == '0')) {
+      const hipError_t e = n2v2r_launch_dense_tn(Bt, lda, nloc, n, X, ldx, b, Y, ldy, beta,
+                                                 colscale, dense_work.as<float>(),
+                                                 dense_work_elems, stream);
+      if (e == hipSuccess) return;
+      if (e != hipErrorNotSupported) throw HipFail{e, "n2v2r_launch_dense_tn"};
     }
     HIPCHK(n2v2r_launch_dense_gemm(Aloc, lda, nloc, n, X, ldx, b, Y, ldy, beta, colscale,
                                    dense_work.as<float>(), dense_work_elems, stream));
@@ -908,8 +923,8 @@ struct Eig {
   // accumulators walking tile_nb column-block phases, one launch per stage
   bool col_blocks = false;
   int tile_rows = 0, tile_nb = CB_NB;
-  // partitioned CSR handles: stage 2 as a reduce-scatter of this rank's column share (default)
-  // instead of all-gathers of every layer's stage-1 panel (N2V2R_DIST_STAGE2=gather)
+  // partitioned CSR handles: stage 2 as a reduce-scatter of this rank's column share (default
+  // at W > 1) instead of all-gathers of every layer's stage-1 panel (N2V2R_DIST_STAGE2=gather)
   bool rs_form = false;
   // XCD-split second SpMM stage (b = 8, one GPU): A_k Z_k lands in per-layer partials on the
   // XCDs of layer k; the image W = sum_k of them is stored by the next Gram pass that reads it
@@ -1148,7 +1163,8 @@ struct Eig {
       for (int k = 0; k < K; ++k) {
         const LayerDev& L = *h->layers[k];
         const int te = tbeg();
-        h->dense_apply(L.dense_at(), L.lda, xg, b, b, h->ews.zk[k]->as<float>(), b, 0.f, nullptr);
+        h->dense_apply(L.dense_at(), L.lda, xg, b, b, h->ews.zk[k]->as<float>(), b, 0.f, nullptr,
+                       h->comm ? nullptr : L.dense_a());
         tend(te, 0, gb);
       }
       for (int k = 0; k < K; ++k) {
@@ -1160,7 +1176,8 @@ struct Eig {
           zin = zgk;
         }
         const int te = tbeg();
-        h->dense_apply(L.dense_a(), L.lda, zin, b, b, Wout, b, k == 0 ? 0.f : 1.f, nullptr);
+        h->dense_apply(L.dense_a(), L.lda, zin, b, b, Wout, b, k == 0 ? 0.f : 1.f, nullptr,
+                       h->comm ? nullptr : L.dense_at());
         tend(te, 1, gb);
         algo_bytes += 2.0 * gb;
       }
@@ -1612,8 +1629,13 @@ struct Eig {
     }
     rs_form = false;
     if (h->comm && !h->dense_layers()) {
-      const char* e = std::getenv("N2V2R_DIST_STAGE2");  // read per fit (tests, A/B runs)
-      rs_form = !(e && std::strcmp(e, "gather") == 0);
+      // read per fit (tests, A/B runs): "rs" / "gather" force a form; unset: the reduce-scatter
+      // when there is more than one rank (one rank's "column share" is every row: its stage 2
+      // would gather from the whole Z with the row kernel, slower than the tiled gather form)
+      const char* e = std::getenv("N2V2R_DIST_STAGE2");
+      rs_form = e && std::strcmp(e, "rs") == 0 ? true
+                : e && std::strcmp(e, "gather") == 0 ? false
+                : h->world > 1;
       if (rs_form)
         for (auto& Lp : h->layers) ensure_colcsr(*Lp, nglob, (int64_t)h->world * npad, st);
     }
@@ -3284,13 +3306,14 @@ int n2v2r_bench_spmm(n2v2r_handle* h, int k, int transpose, int b, int reps, con
     if (L.dense) {
       // dense layer: the GEMM Y = A_k X (or A_k^T X) over this rank's rows
       const float* am = transpose ? L.dense_at() : L.dense_a();
-      h->dense_apply(am, L.lda, xd.as<float>(), b, b, yd.as<float>(), b, 0.f, nullptr);
+      const float* bt = h->comm ? nullptr : (transpose ? L.dense_a() : L.dense_at());
+      h->dense_apply(am, L.lda, xd.as<float>(), b, b, yd.as<float>(), b, 0.f, nullptr, bt);
       hipEvent_t e0, e1;
       HIPCHK(hipEventCreate(&e0));
       HIPCHK(hipEventCreate(&e1));
       HIPCHK(hipEventRecord(e0, h->stream));
       for (int r = 0; r < reps; ++r)
-        h->dense_apply(am, L.lda, xd.as<float>(), b, b, yd.as<float>(), b, 0.f, nullptr);
+        h->dense_apply(am, L.lda, xd.as<float>(), b, b, yd.as<float>(), b, 0.f, nullptr, bt);
       HIPCHK(hipEventRecord(e1, h->stream));
       HIPCHK(hipEventSynchronize(e1));
       float ms = 0.f;

@@ -58,6 +58,9 @@ __device__ __forceinline__ void dg_store_a(float (*as)[DG_AP], const f32x4 (&v)[
   }
 }
 
+// (Round 4, measured and not kept: X rows loaded a round ahead with the A tile and each 16-k
+// group's LDS operands read before the previous group's MFMAs: 0.447 vs 0.407 ms per cfg3
+// launch, profiles/r04_dense_forms.jsonl.)
 // XT = false (default): xs[k][column], one LDS read per MFMA.  XT = true (N2V2R_DG_XT=1, A/B):
 // X staged transposed, xs[column][k] (pitch DG_AP), so a lane reads its 8 consecutive k of a
 // 16-k group as two 16-B LDS reads like its A operands -- measured 0.40 vs 0.39 ms per cfg3
@@ -228,6 +231,159 @@ extern "C" hipError_t n2v2r_launch_dense_gemm(const float* A, int64_t lda, int64
   const int64_t elems = rows * b;
   hipLaunchKernelGGL(dense_fold_kernel, dim3((unsigned)((elems + 255) / 256)), dim3(256), 0, stream,
                      work, (int)nsplit, slab, rows, b, Y, ldy, beta, colscale);
+  return hipGetLastError();
+}
+
+// ---- Y = B^T X with B row-major (round 4): the stored matrix is the MFMA's B operand ---------
+// Y[n][j] = sum_k B[k][n] X[k][j] (j < b <= 32).  For a symmetric layer B = A (Y = A X); for a
+// directed one the engine passes the other stored copy (A X = (A^T)^T X).  Computed as
+// Y^T = X^T B: v_mfma_f32_32x32x2_f32 takes X^T as its A operand (lane l: X[k0 + l/32][l%32],
+// one 4-B load per k pair shared by 4 MFMAs) and B in its natural row-major layout as the B
+// operand: lane l loads B[k0 + l/32][n0 + 4 (l%32) .. + 3] with ONE 16-B load (lanes 0-31 one
+// 512-B run of row k, lanes 32-63 of row k + 1) and feeds element q to MFMA q, whose output
+// column c stands for n = n0 + 4c + q.  No LDS on the way in: A streams from HBM straight into
+// the MFMA operands, D k pairs per stage, double-buffered (the next stage's loads in flight
+// across this stage's 4 D MFMAs).  A wave owns 128 n x 32 j (4 accumulators) over a quarter of
+// its workgroup's k range; the 4 quarters are summed in LDS in fixed order, split-K slabs over
+// grid.y are folded by dense_fold_kernel (deterministic).  dense_gemm_kernel above stages A
+// through LDS as the A operand: 0.39 ms per cfg3 launch (0.50 of HBM, MFMA busy 0.45).
+template <int DT_D, int OCC>
+__global__ __launch_bounds__(256, OCC) void dense_tn_kernel(const float* __restrict__ B, int64_t ldb,
+                                                          int64_t ncols, int64_t kdim, int64_t kper,
+                                                          const float* __restrict__ X, int ldx,
+                                                          int b, float* __restrict__ out,
+                                                          int64_t ldo, int64_t slab) {
+  extern __shared__ float red[];  // [128 n][33]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: scalar bases
+  const int c = lane & 31, h = lane >> 5;
+  const int64_t n0 = (int64_t)blockIdx.x * 128;
+  const int64_t wk0 = (int64_t)blockIdx.y * kper;
+  int64_t wk1 = wk0 + kper;
+  if (wk1 > kdim) wk1 = kdim;
+  // this wave's quarter of the workgroup's k range, in k pairs
+  const int64_t npair_wg = (wk1 - wk0 + 1) / 2;
+  const int64_t qp = (npair_wg + 3) / 4;
+  const int64_t kb = wk0 + 2 * qp * wave;
+  int64_t ke = kb + 2 * qp;
+  if (ke > wk1) ke = wk1;
+  const int64_t npair = ke > kb ? (ke - kb + 1) / 2 : 0;
+  // column of this lane's 16-B B load (clamped into the row: ldb % 4 == 0, ldb >= ncols)
+  int64_t nc = n0 + 4 * c;
+  if (nc > ldb - 4) nc = ldb - 4;
+  const int jc = c < b ? c : b - 1;
+  // wave-uniform bases (scalar registers) + 32-bit per-lane element offsets: one VGPR per load
+  // address instead of a 64-bit pair (the host checks (kper + 1) * ldb < 2^32)
+  const float* Bw = B + kb * ldb + n0;  // (kb, n0: wave-uniform)
+  const float* Xw = X + kb * ldx;
+  const uint32_t ncl = (uint32_t)(nc - n0);
+  const int krel_max = (int)(ke - kb) - 1;
+  const uint32_t lb = (uint32_t)ldb, lx = (uint32_t)ldx;
+  f32x16 acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = f32x16{0.f};
+  f32x4 bb0[DT_D], bb1[DT_D];
+  float xb0[DT_D], xb1[DT_D];
+  auto load = [&](f32x4 (&bb)[DT_D], float (&xb)[DT_D], int64_t p0) {
+#pragma unroll
+    for (int u = 0; u < DT_D; ++u) {
+      const int kr = (int)(2 * (p0 + u)) + h;
+      const uint32_t krc = (uint32_t)(kr < krel_max ? kr : krel_max);  // clamped: one batch
+      bb[u] = *reinterpret_cast<const f32x4*>(Bw + (krc * lb + ncl));
+      xb[u] = Xw[krc * lx + (uint32_t)jc];  // raw: masked at the use (a select here becomes a
+                                            // branch with a wait; a multiply, a wait per load)
+    }
+  };
+  auto compute = [&](const f32x4 (&bb)[DT_D], const float (&xb)[DT_D], int64_t p0) {
+#pragma unroll
+    for (int u = 0; u < DT_D; ++u) {
+      // X is finite (clamped loads of valid rows): 0 * x = 0 past the range
+      const float xm = xb[u] * ((kb + 2 * (p0 + u) + h < ke && c < b) ? 1.f : 0.f);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(xm, bb[u][q], acc[q], 0, 0, 0);
+    }
+  };
+  // sched_barrier(0) after each batch of loads: without it the scheduler sinks every load to
+  // just before its MFMAs (load, wait vmcnt(0), 4 MFMAs: no load in flight across MFMAs)
+  // No early exit between the two halves: a conditional use lets the optimiser sink the next
+  // half's loads below this half's MFMAs; past npair the k pairs are masked to zero instead
+  // (at most DT_D wasted k pairs per wave).
+  if (npair > 0) {
+    load(bb0, xb0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    for (int64_t p0 = 0; p0 < npair; p0 += 2 * DT_D) {
+      load(bb1, xb1, p0 + DT_D);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(bb0, xb0, p0);
+      load(bb0, xb0, p0 + 2 * DT_D);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(bb1, xb1, p0 + DT_D);
+    }
+  }
+  // acc[q][r] at lane l: Y^T[j][c] with j = (r & 3) + 8 (r >> 2) + 4 h, n = n0 + 4 c + q.
+  // The 4 waves' tiles summed in wave order through ONE 128 x 33 LDS buffer (17 KB: the LDS
+  // does not cap the workgroups per CU)
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float& dst = red[(4 * c + q) * 33 + (r & 3) + 8 * (r >> 2) + 4 * h];
+          dst = w == 0 ? acc[q][r] : dst + acc[q][r];
+        }
+    }
+    __syncthreads();
+  }
+  float* o = out + (int64_t)blockIdx.y * slab;
+  for (int e = threadIdx.x; e < 128 * 32; e += 256) {
+    const int nl = e >> 5, j = e & 31;
+    const int64_t n = n0 + nl;
+    if (n < ncols && j < b) o[n * ldo + j] = red[nl * 33 + j];
+  }
+}
+
+// Y (ncols x b, ld ldy) = beta * Y + colscale .* (B[kdim x ncols]^T X[kdim x b]), b <= 32;
+// `work` holds the split-K slabs (nsplit * ncols * b floats).  hipErrorNotSupported when the
+// form does not apply (the caller then takes n2v2r_launch_dense_gemm on the other copy).
+extern "C" hipError_t n2v2r_launch_dense_tn(const float* B, int64_t ldb, int64_t ncols,
+                                           int64_t kdim, const float* X, int ldx, int b, float* Y,
+                                           int64_t ldy, float beta, const float* colscale,
+                                           float* work, size_t work_elems, hipStream_t stream) {
+  if (ncols <= 0) return hipSuccess;
+  if (b < 1 || b > 32 || !work || ldb % 4 != 0 || ldb < ncols || ((uintptr_t)B & 15) != 0 ||
+      kdim < 2 || (double)(kdim + 1) * (double)(ldb > ldx ? ldb : ldx) >= 4294967296.0)
+    return hipErrorNotSupported;  // (32-bit element offsets inside a wave's k range)
+  const int64_t tiles = (ncols + 127) / 128;
+  // ~2048 workgroups (4 rounds of 2 per CU), at least 512 k per workgroup, slabs within work.
+  // (Measured and not kept: 16 / 24 k pairs per stage at one workgroup per CU, 512 VGPRs:
+  // 0.38 ms vs 0.36 per cfg3 launch, profiles/r04_dense_forms.jsonl.)
+  int64_t nsplit = (2048 + tiles / 2) / tiles;
+  const int64_t kmax = kdim / 512;
+  if (nsplit > kmax) nsplit = kmax;
+  if (nsplit < 1) nsplit = 1;
+  const int64_t cap = (int64_t)(work_elems / (size_t)(ncols * b));
+  if (nsplit > cap) nsplit = cap;
+  if (nsplit < 1) return hipErrorNotSupported;
+  int64_t kper = (kdim + nsplit - 1) / nsplit;
+  kper = (kper + 7) & ~(int64_t)7;
+  nsplit = (kdim + kper - 1) / kper;
+  static const bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)dense_tn_kernel<8, 2>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 33 * 4);
+    (void)hipGetLastError();
+    return true;
+  }();
+  (void)attr;
+  const dim3 grid((unsigned)tiles, (unsigned)nsplit);
+  hipLaunchKernelGGL((dense_tn_kernel<8, 2>), grid, dim3(256), 128 * 33 * sizeof(float),
+                     stream, B, ldb, ncols, kdim, kper, X, ldx, b, work, (int64_t)b, ncols * b);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int64_t elems = ncols * b;
+  hipLaunchKernelGGL(dense_fold_kernel, dim3((unsigned)((elems + 255) / 256)), dim3(256), 0, stream,
+                     work, (int)nsplit, ncols * b, ncols, b, Y, ldy, beta, colscale);
   return hipGetLastError();
 }
 

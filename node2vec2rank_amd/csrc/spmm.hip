@@ -365,7 +365,7 @@ __device__ __forceinline__ int64_t uniform_i64(int64_t v) {
 // NS steps of 32 entries of one window: index words and gathers of all NS steps issued as
 // straight-line batches, then per step: stage, and the row owners fold their entries (the fold is
 // ~5 % of the launch at cfg4: the gathers are the cost)
-template <int NS, bool UNIT>
+template <int NS, bool UNIT, bool NT>
 __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1))) int32_t* ind,
                                            const __attribute__((address_space(1))) float* dat,
                                            int64_t beg, int off, int left,
@@ -379,8 +379,8 @@ __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1)
   for (int u = 0; u < NS; ++u) {
     const int q = u * 32 + pr;
     const int64_t e = beg + off + (q < left ? q : 0);
-    wd[u] = ind[e];
-    v[u] = UNIT ? 1.f : dat[e];
+    wd[u] = NT ? __builtin_nontemporal_load(ind + e) : ind[e];
+    v[u] = UNIT ? 1.f : (NT ? __builtin_nontemporal_load(dat + e) : dat[e]);
   }
 #pragma unroll
   for (int u = 0; u < NS; ++u)
@@ -396,6 +396,7 @@ __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1)
   }
 }
 
+template <bool NT, bool BAR>
 __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
   // [tile_rows][8] row accumulators, then a 1-KB staging slot per wave
   extern __shared__ float tacf[];
@@ -452,13 +453,13 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
   for (int off = 0; off < len; off += 128) {                                                   \
     const int left = len - off;                                                                \
     if (left > 96)                                                                             \
-      flat_steps<4, U>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+      flat_steps<4, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
     else if (left > 64)                                                                        \
-      flat_steps<3, U>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+      flat_steps<3, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
     else if (left > 32)                                                                        \
-      flat_steps<2, U>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+      flat_steps<2, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
     else                                                                                       \
-      flat_steps<1, U>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+      flat_steps<1, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
   }
         if (unit) {
           FLAT_STEPS(true)
@@ -468,7 +469,7 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
 #undef FLAT_STEPS
         if (wr + pr < we) tacc[(wr + pr) * 2 + sub] += acc;
       }
-      __syncthreads();  // the workgroup's waves move to the next panel block together
+      if (BAR) __syncthreads();  // the workgroup's waves move to the next panel block together
     }
     if (!a.sum || k == a.K - 1) {
       float* Y = a.Y[a.sum ? 0 : k];
@@ -501,13 +502,30 @@ extern "C" hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, hipStream_t 
   const size_t flds = sizeof(float) * 8 * (size_t)a.tile_rows + 16 * 1024;
   if (flds > 80 * 1024) return hipErrorInvalidValue;
   static const bool fattr = [] {
-    (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel,
+    (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel<false, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel<true, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel<true, false>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
     (void)hipGetLastError();
     return true;
   }();
   (void)fattr;
-  hipLaunchKernelGGL(spmm8_flat_kernel, dim3(grid), dim3(1024), flds, stream, a);
+  // Non-temporal index / value loads (the stream is read once; the panel gathers keep L2):
+  // cfg4 layer launch 0.354 vs 0.363 ms, fit 1,599 vs 1,609 ms (profiles/r04_flat_nt.jsonl;
+  // N2V2R_FLAT_NT=0 for the plain loads).  N2V2R_FLAT_BAR=0 (A/B): no barrier between phases.
+  // Both read per launch.
+  const char* ntv = getenv("N2V2R_FLAT_NT");
+  const char* bav = getenv("N2V2R_FLAT_BAR");
+  const bool nt = !(ntv && ntv[0] == '0');
+  const bool bar = !(bav && bav[0] == '0');
+  if (!nt)
+    hipLaunchKernelGGL((spmm8_flat_kernel<false, true>), dim3(grid), dim3(1024), flds, stream, a);
+  else if (bar)
+    hipLaunchKernelGGL((spmm8_flat_kernel<true, true>), dim3(grid), dim3(1024), flds, stream, a);
+  else
+    hipLaunchKernelGGL((spmm8_flat_kernel<true, false>), dim3(grid), dim3(1024), flds, stream, a);
   return hipGetLastError();
 }
 

@@ -10,9 +10,14 @@ from oracle import n2v2r_oracle as orc
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("form", ["tn", "lds"])
 @pytest.mark.parametrize("b", [8, 16, 32, 64])
-@pytest.mark.parametrize("n", [1000, 1037])
-def test_dense_gemm_matches_numpy(engine, n, b):
+@pytest.mark.parametrize("n", [1000, 1037, 2501])
+def test_dense_gemm_matches_numpy(engine, n, b, form, monkeypatch):
+    """Both dense GEMM kernels (b <= 32: the B-operand streaming dense_tn_kernel by default,
+    N2V2R_DENSE_TN=0 the LDS-staged dense_gemm_kernel; b = 64 always the latter) against an
+    fp64 product, for A and A^T of a directed layer."""
+    monkeypatch.setenv("N2V2R_DENSE_TN", "1" if form == "tn" else "0")
     rng = np.random.default_rng(n + b)
     A = rng.standard_normal((n, n)).astype(np.float32)
     engine.set_layers([A, A.T.copy()], storage="dense", symmetric=-1)

@@ -82,7 +82,8 @@ def _concat(res):
 @pytest.fixture(params=["rs", "gather"])
 def stage2(request, monkeypatch):
     """Stage 2 of a partitioned application: the rank's column share reduce-scattered (the
-    default) or every layer's stage-1 panel all-gathered (N2V2R_DIST_STAGE2=gather)."""
+    default at W > 1; forced here at any W) or every layer's stage-1 panel all-gathered
+    (N2V2R_DIST_STAGE2=gather, the default at W = 1)."""
     monkeypatch.setenv("N2V2R_DIST_STAGE2", request.param)
     return request.param
 

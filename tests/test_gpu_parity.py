@@ -439,7 +439,7 @@ def test_model_end_to_end(name):
                       f"envelope, unaligned, min of {ENV_SEEDS}: {env_un:.6f}); signs aligned, "
                       f"stable ties: tau {tau_st:.6f} (envelope {env_al:.6f})")
                 assert tau_ref >= min(0.998, env_un), (name, strategy, key, tau_ref, env_un)
-                assert tau_st >= min(0.998, env_al - 0.02), (name, strategy, key, tau_st, env_al)
+                assert tau_st >= min(0.998, env_al - 0.01), (name, strategy, key, tau_st, env_al)
         Y = model.node_embeddings
         assert Y.shape == fx["Y"].shape
 

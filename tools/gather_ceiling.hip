@@ -12,6 +12,7 @@
 //   stream+gather : index words from HBM, then the gathers (the flat kernel's memory work)
 //   gather only   : indices from a counter hash (no index stream): the pure gather rate
 //   stream only   : the index words alone (no gathers)
+//   nt-stream+gather : stream + gather with non-temporal index loads (kept out of L2's way?)
 // Also at 64-B rows (b = 16 panels: a lane quad per entry).  Prints one JSON line per (form, row
 // bytes, panel size): G entries/s and the index-stream GB/s.
 #include <hip/hip_runtime.h>
@@ -44,16 +45,24 @@ __global__ void fill_idx(int32_t* idx, int64_t e, uint32_t rows) {
   if (i < e) idx[i] = (int32_t)(((uint64_t)hash32((uint64_t)i * 7919u) * rows) >> 32);
 }
 
+__global__ void narrow_idx(const int32_t* idx, uint16_t* idx16, int64_t e) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < e) idx16[i] = (uint16_t)idx[i];
+}
+
 __global__ void fill_x(float* x, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[i] = (float)(i & 1023) * 1e-3f;
 }
 
-// MODE 0: stream + gather, 1: gather only (hashed indices), 2: stream only.  W: panel width in
+// MODE 0: stream + gather, 1: gather only (hashed indices), 2: stream only, 3: stream with
+// non-temporal index loads + gather, 4: 2-B index words (non-temporal) + gather (rows < 65536:
+// a column block's offsets), 5: 2-B index words alone.  W: panel width in
 // floats (8: 32-B rows, a lane pair per entry, 32 entries per wave step; 16: 64-B rows, a lane
 // quad per entry, 16 entries per step)
 template <int MODE, int W>
 __global__ __launch_bounds__(1024, 8) void gather_kernel(const int32_t* __restrict__ idx,
+                                                         const uint16_t* __restrict__ idx16,
                                                          int64_t e, const float* __restrict__ X,
                                                          uint32_t rows, float* __restrict__ out) {
   constexpr int G = W / 4;       // lanes per entry
@@ -74,10 +83,14 @@ __global__ __launch_bounds__(1024, 8) void gather_kernel(const int32_t* __restri
       const int64_t qc = q < end ? q : end - 1;
       if (MODE == 1)
         wd[u] = (int)(((uint64_t)hash32((uint64_t)qc * 7919u) * rows) >> 32);
+      else if (MODE == 3)
+        wd[u] = __builtin_nontemporal_load(idx + qc);
+      else if (MODE == 4 || MODE == 5)
+        wd[u] = __builtin_nontemporal_load(idx16 + qc);
       else
         wd[u] = idx[qc];
     }
-    if (MODE == 2) {
+    if (MODE == 2 || MODE == 5) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[u] += (float)wd[u];
       continue;
@@ -93,17 +106,17 @@ __global__ __launch_bounds__(1024, 8) void gather_kernel(const int32_t* __restri
 }
 
 template <int MODE, int W>
-static double run(const int32_t* idx, int64_t e, const float* X, uint32_t rows, float* out,
-                  int reps, int ncu) {
+static double run(const int32_t* idx, const uint16_t* idx16, int64_t e, const float* X,
+                  uint32_t rows, float* out, int reps, int ncu) {
   const dim3 grid((unsigned)(2 * ncu)), block(1024);
-  hipLaunchKernelGGL((gather_kernel<MODE, W>), grid, block, 0, 0, idx, e, X, rows, out);
+  hipLaunchKernelGGL((gather_kernel<MODE, W>), grid, block, 0, 0, idx, idx16, e, X, rows, out);
   CHK(hipDeviceSynchronize());
   hipEvent_t a, b;
   CHK(hipEventCreate(&a));
   CHK(hipEventCreate(&b));
   CHK(hipEventRecord(a, 0));
   for (int r = 0; r < reps; ++r)
-    hipLaunchKernelGGL((gather_kernel<MODE, W>), grid, block, 0, 0, idx, e, X, rows, out);
+    hipLaunchKernelGGL((gather_kernel<MODE, W>), grid, block, 0, 0, idx, idx16, e, X, rows, out);
   CHK(hipEventRecord(b, 0));
   CHK(hipEventSynchronize(b));
   float ms = 0.f;
@@ -122,6 +135,8 @@ int main(int argc, char** argv) {
   const uint32_t max_rows = (uint32_t)(mb.back() * 1024 * 1024 / 32);  // 32-B rows (floats: x8)
   float *X, *out;
   int32_t* idx;
+  uint16_t* idx16;
+  CHK(hipMalloc(&idx16, (size_t)e * 2));
   CHK(hipMalloc(&X, (size_t)max_rows * 32));
   CHK(hipMalloc(&out, 4096));
   CHK(hipMalloc(&idx, (size_t)e * 4));
@@ -133,24 +148,32 @@ int main(int argc, char** argv) {
       const uint32_t rows = (uint32_t)(m * 1024 * 1024 / (4 * W));
       hipLaunchKernelGGL(fill_idx, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, 0, idx, e,
                          rows);
+      hipLaunchKernelGGL(narrow_idx, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, 0, idx,
+                         idx16, e);
       CHK(hipDeviceSynchronize());
-      double ts[3];
+      double ts[6] = {-1.0, -1.0, -1.0, -1.0, -1.0, -1.0};
+      const bool narrow = rows <= 65536;
       if (W == 8) {
-        ts[0] = run<0, 8>(idx, e, X, rows, out, reps, ncu);
-        ts[1] = run<1, 8>(idx, e, X, rows, out, reps, ncu);
-        ts[2] = run<2, 8>(idx, e, X, rows, out, reps, ncu);
+        ts[0] = run<0, 8>(idx, idx16, e, X, rows, out, reps, ncu);
+        ts[1] = run<1, 8>(idx, idx16, e, X, rows, out, reps, ncu);
+        ts[2] = run<2, 8>(idx, idx16, e, X, rows, out, reps, ncu);
+        ts[3] = run<3, 8>(idx, idx16, e, X, rows, out, reps, ncu);
+        if (narrow) {
+          ts[4] = run<4, 8>(idx, idx16, e, X, rows, out, reps, ncu);
+          ts[5] = run<5, 8>(idx, idx16, e, X, rows, out, reps, ncu);
+        }
       } else {
-        ts[0] = run<0, 16>(idx, e, X, rows, out, reps, ncu);
-        ts[1] = run<1, 16>(idx, e, X, rows, out, reps, ncu);
-        ts[2] = -1.0;
+        ts[0] = run<0, 16>(idx, idx16, e, X, rows, out, reps, ncu);
+        ts[1] = run<1, 16>(idx, idx16, e, X, rows, out, reps, ncu);
       }
-      const char* names[3] = {"stream+gather", "gather only", "stream only"};
-      for (int f = 0; f < 3; ++f) {
+      const char* names[6] = {"stream+gather", "gather only", "stream only",
+                              "nt-stream+gather", "u16-stream+gather", "u16-stream only"};
+      for (int f = 0; f < 6; ++f) {
         if (ts[f] < 0) continue;
         printf("{\"form\": \"%s\", \"row_bytes\": %d, \"panel_MB\": %g, \"entries\": %lld, "
                "\"ms\": %.4f, \"G_entries_per_s\": %.1f, \"index_GB_per_s\": %.0f}\n",
                names[f], 4 * W, m, (long long)e, ts[f], e / (ts[f] * 1e-3) / 1e9,
-               f == 1 ? 0.0 : 4.0 * e / (ts[f] * 1e-3) / 1e9);
+               f == 1 ? 0.0 : (f >= 4 ? 2.0 : 4.0) * e / (ts[f] * 1e-3) / 1e9);
         fflush(stdout);
       }
     }
@@ -158,5 +181,6 @@ int main(int argc, char** argv) {
   CHK(hipFree(X));
   CHK(hipFree(out));
   CHK(hipFree(idx));
+  CHK(hipFree(idx16));
   return 0;
 }

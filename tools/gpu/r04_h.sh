@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 4: dense_tn_kernel (B-operand streaming GEMM for the dense layers) -- the dense tests,
+# the tn / lds A/B at cfg3 size, the RR tests, then the cfg3 bench
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests -m gpu -v -s --maxfail=3 --timeout 300 \
+  --timeout-method thread -p no:cacheprovider -k "dense or cfg3" \
+  > gpurun_out/r04_h_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/r04_h_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python -u tools/dense_tn_probe.py --fits 0 > gpurun_out/r04_dense_tn.jsonl 2> gpurun_out/r04_dense_tn.err
+rc=$?; cat gpurun_out/r04_dense_tn.jsonl; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u bench.py --config cfg3 --steps 3 --warmup 1 --no-cpu-baseline \
+  > gpurun_out/r04_bench_cfg3_h.json 2> gpurun_out/r04_bench_cfg3_h.err
+rc=$?; cut -c1-300 gpurun_out/r04_bench_cfg3_h.json; exit $rc
