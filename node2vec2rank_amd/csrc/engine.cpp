@@ -287,6 +287,20 @@ struct DevBuf {
     if (e != hipSuccess) throw HipFail{e, "hipMemset"};
     bytes = b;
   }
+  // scratch that every use overwrites before reading it: no zero fill, no device sync; kept
+  // (and grown) across calls when owned by the handle
+  void ensure_raw(size_t b) {
+    if (bytes >= b && p) return;
+    if (b == 0) b = 16;
+    if (debug_poison()) return ensure(b);
+    release();
+    if (hipMalloc(&p, b) != hipSuccess) {
+      p = nullptr;
+      throw StatusFail{N2V2R_ERR_OUT_OF_MEMORY,
+                       "hipMalloc of " + std::to_string(b) + " bytes failed"};
+    }
+    bytes = b;
+  }
   template <class T>
   T* as() const {
     return static_cast<T*>(p);
@@ -713,6 +727,11 @@ struct n2v2r_handle {
                                    dense_work.as<float>(), dense_work_elems, stream));
   }
   DevBuf rs_keys[2], rs_idx[2], rs_pos, rs_hist, rs_or, rs_and;
+  // ingest scratch (n2v2r_set_layer_csr: radix keys / payloads of the transpose, histogram,
+  // flags) and the embedding's panel slice, kept across calls (a per-call hipMalloc + zero
+  // fill + device sync + hipFree each time otherwise)
+  DevBuf ing_keys[2], ing_pay[2], ing_hist, ing_flag;
+  DevBuf ypanel;
 
 
   void set_err(const char* fmt, ...) {
@@ -1549,8 +1568,12 @@ struct Eig {
     const int64_t nglob = h->n;
     // small graphs: shrink the block until the Krylov space fits well inside R^n
     int keep = 0, maxc = 0;
+    // dense layers (b = 32): keep d + b, basis <= 704 -- on three cfg3-family graphs 61 block
+    // applications and 215-218 ms per fit against 66 and 236-240 ms with the general rule's
+    // keep 5d/4 = 320 and basis 768 (profiles/r04_cfg3_sweep*.jsonl)
+    const bool dense_rule = h->dense_layers() && !o.block;
     for (;; b /= 2) {
-      keep = o.keep ? o.keep : std::max(d + 16, (d * 5) / 4);
+      keep = o.keep ? o.keep : (dense_rule ? d + b : std::max(d + 16, (d * 5) / 4));
       keep = ((keep + b - 1) / b) * b;
       // default basis: 3.2 keep for the dense Rayleigh-Ritz (its cost grows as c^3); 4.8 keep
       // (<= 512) for the banded one (b = 8), where fewer, longer cycles win (cfg2: 14 cycles
@@ -1565,6 +1588,7 @@ struct Eig {
           (int)std::min<int64_t>((nglob / 2) / b * b, (int64_t)(N2V2R_MAX_BLOCKS - 1) * b);
       if (maxc > cap) maxc = cap;
       if (maxc > 768) maxc = 768 / b * b;  // Rayleigh-Ritz kernels: c <= 768
+      if (dense_rule && !o.max_basis && maxc > 704) maxc = 704 / b * b;
       if (maxc >= keep + b) break;
       if (b == 8)
         throw StatusFail{N2V2R_ERR_BAD_ARG,
@@ -2391,12 +2415,15 @@ int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const in
       HIPCHK(hipMemcpyAsync(ddv.p, data, sizeof(float) * nnz, hipMemcpyHostToDevice, st));
     }
     const bool need_t = symmetric != N2V2R_SYM_YES;
-    DevBuf keys[2], pay[2], hist, flag;
-    flag.ensure(sizeof(unsigned) * 4, st);
-    HIPCHK(hipMemsetAsync(flag.p, 0, sizeof(unsigned) * 4, st));  // (N2V2R_POISON fills 0xFF)
+    DevBuf* keys = h->ing_keys;
+    DevBuf* pay = h->ing_pay;
+    DevBuf& hist = h->ing_hist;
+    DevBuf& flag = h->ing_flag;
+    flag.ensure_raw(sizeof(unsigned) * 4);
+    HIPCHK(hipMemsetAsync(flag.p, 0, sizeof(unsigned) * 4, st));
     if (need_t && nnz) {
-      keys[0].ensure(sizeof(uint64_t) * nnz);
-      pay[0].ensure(sizeof(int32_t) * nnz);
+      keys[0].ensure_raw(sizeof(uint64_t) * nnz);
+      pay[0].ensure_raw(sizeof(int32_t) * nnz);
     }
     HIPCHK(n2v2r_launch_csr_scan(dip.as<int64_t>(), dix.as<int32_t>(), ddv.as<float>(), n, n,
                                  need_t && nnz ? keys[0].as<uint64_t>() : nullptr,
@@ -2422,14 +2449,14 @@ int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const in
                                             nullptr, nullptr, st));
         return;
       }
-      keys[0].ensure(sizeof(uint64_t) * nnz);
-      pay[0].ensure(sizeof(int32_t) * nnz);
-      keys[1].ensure(sizeof(uint64_t) * nnz);
-      pay[1].ensure(sizeof(int32_t) * nnz);
+      keys[0].ensure_raw(sizeof(uint64_t) * nnz);
+      pay[0].ensure_raw(sizeof(int32_t) * nnz);
+      keys[1].ensure_raw(sizeof(uint64_t) * nnz);
+      pay[1].ensure_raw(sizeof(int32_t) * nnz);
       if (!have_keys)
         HIPCHK(n2v2r_launch_csr_scan(ip_, ix_, dv_, n, n, keys[0].as<uint64_t>(),
                                      pay[0].as<int32_t>(), flag.as<unsigned>() + 1, st));
-      hist.ensure(sizeof(uint32_t) * n2v2r_radix_hist_elems(nnz, 1));
+      hist.ensure_raw(sizeof(uint32_t) * n2v2r_radix_hist_elems(nnz, 1));
       int bits = 1;
       while (bits < 31 && ((int64_t)1 << bits) < n) ++bits;
       int cur = 0;
@@ -2715,8 +2742,8 @@ int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_sta
       // contiguous panel, then one column scaling of every Y_k (the row kernel below gathers
       // 32 B out of each 512-B row of U -- a 512 MB panel at cfg4 -- and scales in-kernel)
       const int64_t ng = h->comm ? (int64_t)h->world * h->npad : h->npad;
-      DevBuf panel;
-      panel.ensure(sizeof(float) * ng * 8);
+      DevBuf& panel = h->ypanel;
+      panel.ensure_raw(sizeof(float) * ng * 8);
       SpmmTileArgs a{};
       a.blk = h->ews.tblk.as<CsrBlk>();
       a.ldx = 8;

@@ -469,7 +469,11 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
 #undef FLAT_STEPS
         if (wr + pr < we) tacc[(wr + pr) * 2 + sub] += acc;
       }
-      if (BAR) __syncthreads();  // the workgroup's waves move to the next panel block together
+      // the workgroup's waves move to the next panel block together.  (No barrier: 0.57 vs
+      // 0.36 ms per cfg4 layer launch; a bounded skew -- a wave starts phase g once all have
+      // finished g - 2, LDS counters -- 0.393 vs 0.354 ms, fit 1,714 vs 1,603 ms,
+      // profiles/r04_flat_sync.jsonl: the L2 locality of lockstep phases is worth the idling)
+      if (BAR) __syncthreads();
     }
     if (!a.sum || k == a.K - 1) {
       float* Y = a.Y[a.sum ? 0 : k];

@@ -1,6 +1,7 @@
 """Flat tiled SpMM knobs A/B on a cfg4-sized ER graph (read per launch by the library):
-N2V2R_FLAT_NT (non-temporal index / value loads, default on) and N2V2R_FLAT_BAR (barrier between
-column-block phases, default on).  One-layer launches, then whole fits, alternating in one
+N2V2R_FLAT_NT (non-temporal index / value loads, default on) and N2V2R_FLAT_BAR (the barrier
+between column-block phases, default on).  (profiles/r04_flat_sync.jsonl came from a bounded-skew
+variant, N2V2R_FLAT_SYNC=2, since dropped.)  One-layer launches, then whole fits, alternating in one
 process.
 
     python tools/flat_knob_probe.py [--n 1000000] [--deg 50] [--reps 20] [--fits 1] [--d 128]
