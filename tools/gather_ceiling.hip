@@ -1,7 +1,7 @@
 // Calibration of the b = 8 SpMM gather ceiling on MI355X.
 //
 //   hipcc --offload-arch=gfx950 -O3 -o tools/gather_ceiling tools/gather_ceiling.hip
-//   tools/gather_ceiling [entries_millions=100] [reps=20]
+//   tools/gather_ceiling [entries_millions=100] [reps=20] [panel_MB=all] [row_bytes=all]
 //
 // What spmm8_flat_kernel does per stored entry, without its row structure, LDS staging and
 // per-row fold: a lane pair reads the entry's 4-B column word from a streamed index array and
@@ -129,6 +129,8 @@ static double run(const int32_t* idx, const uint16_t* idx16, int64_t e, const fl
 int main(int argc, char** argv) {
   const int64_t e = (int64_t)(argc > 1 ? atof(argv[1]) : 100.0) * 1000000;
   const int reps = argc > 2 ? atoi(argv[2]) : 20;
+  const double only_mb = argc > 3 ? atof(argv[3]) : 0.0;  // one panel size (PMC runs)
+  const int only_rb = argc > 4 ? atoi(argv[4]) : 0;       // one row width in bytes
   int ncu = 0;
   CHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
   const std::vector<double> mb = {1, 2, 4, 8, 32, 160, 320};
@@ -144,7 +146,9 @@ int main(int argc, char** argv) {
                      0, X, (int64_t)max_rows * 8);
   for (int wsel = 0; wsel < 2; ++wsel) {
     const int W = wsel ? 16 : 8;
+    if (only_rb && only_rb != 4 * W) continue;
     for (double m : mb) {
+      if (only_mb > 0.0 && m != only_mb) continue;
       const uint32_t rows = (uint32_t)(m * 1024 * 1024 / (4 * W));
       hipLaunchKernelGGL(fill_idx, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, 0, idx, e,
                          rows);
