@@ -159,8 +159,9 @@ size_t n2v2r_rr_tridiag_scratch_bytes(int c);
 hipError_t n2v2r_launch_rr_tri_eig(const double* d, const double* e, int c, int p, double* w,
                                    double* Y, double* scratch, hipStream_t stream);
 hipError_t n2v2r_launch_rr_backtransform(const double* V, const double* tau, int c,
-                                         const double* Y, int p, float* S, int lds,
+                                         const double* Y, int p, float* S, int lds, double* tfac,
                                          hipStream_t stream);
+size_t n2v2r_rr_bt_scratch_bytes(int c);
 hipError_t n2v2r_launch_lds_poison(hipStream_t stream);
 hipError_t n2v2r_launch_nonfinite(const void* p, int64_t count, int f64, int* flag,
                                   hipStream_t stream);
@@ -630,6 +631,7 @@ struct EigWorkspace {
   DevBuf rback;  // the per-cycle read-back, packed on the device before one copy to the host
   DevBuf tri, refl, ytri, tscr;               // GPU Rayleigh-Ritz: [d|e|tau], reflectors, Y_T
   DevBuf trcoop;                              // multi-workgroup tridiagonalisation scratch
+  DevBuf btf;                                 // Rayleigh-Ritz back-transform: blocks' T factors
   DevBuf hband, band, varr, taua, rrerr;      // banded RR: band columns, band matrix, arrow
   DevBuf fcoef;                               // fp32 [-C R^-1; R^-1] of the apply pass
   DevBuf dbgflag;                             // N2V2R_DEBUG_FINITE result flag
@@ -1680,6 +1682,7 @@ struct Eig {
     h->ews.ytri.ensure(sizeof(double) * (size_t)c_max * keep);
     h->ews.tscr.ensure(sizeof(double) * 6 * (size_t)((keep + 63) / 64 * 64) * c_max);
     h->ews.trcoop.ensure(n2v2r_rr_tridiag_scratch_bytes(c_max));
+    h->ews.btf.ensure(n2v2r_rr_bt_scratch_bytes(c_max));
     h->ews.rinv.ensure(sizeof(double) * 64 * 64);
     h->ews.fcoef.ensure(sizeof(float) * (size_t)(c_max + 64) * 64);
     h->ews.flg.ensure(sizeof(int) * 256);
@@ -1858,7 +1861,8 @@ struct Eig {
         lds_poison();
         HIPCHK(n2v2r_launch_rr_backtransform(h->ews.refl.as<double>(), trid + 2 * c_max, c,
                                              h->ews.ytri.as<double>(), keep,
-                                             h->ews.csmall.as<float>(), keep, st));
+                                             h->ews.csmall.as<float>(), keep,
+                                             h->ews.btf.as<double>(), st));
       }
       dbg(h->theta.p, keep, true, "Ritz values");
       dbg(h->ews.csmall.p, (int64_t)c * keep, false, "Ritz coefficients S");
@@ -3199,8 +3203,10 @@ int n2v2r_rr_top(n2v2r_handle* h, int c, const double* H, int p, double* w, floa
     HIPCHK(n2v2r_launch_rr_tri_eig(t, t + c, c, p, wd.as<double>(), y.as<double>(),
                                    scr.as<double>(), h->stream));
     HIPCHK(hipMemcpyAsync(w, wd.p, sizeof(double) * p, hipMemcpyDeviceToHost, h->stream));
+    DevBuf btf;
+    btf.ensure(n2v2r_rr_bt_scratch_bytes(c));
     HIPCHK(n2v2r_launch_rr_backtransform(refl.as<double>(), t + 2 * c, c, y.as<double>(), p,
-                                         s.as<float>(), p, h->stream));
+                                         s.as<float>(), p, btf.as<double>(), h->stream));
     HIPCHK(hipMemcpyAsync(S, s.p, sizeof(float) * c * p, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     return N2V2R_OK;

@@ -469,32 +469,25 @@ extern "C" size_t n2v2r_rr_tridiag_scratch_bytes(int c) {
 // P = H_0 H_1 ... H_{c-3}.  Blocked (compact WY): the reflectors are taken BT_NB at a time,
 // last block first; for the block H_k0 ... H_k1-1 = I - W T W^T (T upper triangular, the
 // forward column-wise LAPACK larft recurrence, built from the block's Gram matrix W^T W) the
-// update is z <- z - W (T (W^T z)).  One workgroup per RR_BT_COLS columns keeps its columns in
-// LDS; about 4 barriers per block instead of 2 per reflector.
+// update is z <- z - W (T (W^T z)).
+//   rr_bt_tfactor_kernel: the T factors of all blocks at once, one workgroup per block (they
+//     depend on the reflectors alone).  Round 4: moved out of the column workgroups, which each
+//     rebuilt every block's Gram and ran the serial larft rows between two barriers (1.39 ms per
+//     cfg3 call, 24 blocks x ~58 us on the critical path).
+//   rr_backtransform_kernel: one workgroup per RR_BT_COLS columns keeps its columns in LDS and
+//     walks the blocks with the precomputed T: W^T z, U = T (W^T z), z -= W U.
+// Bit-identical to the former single kernel: the same partial sums in the same order.
 #define BT_NB 32
 #define BT_CH 128
-__global__ __launch_bounds__(256) void rr_backtransform_kernel(const double* __restrict__ V,
-                                                               const double* __restrict__ tau,
-                                                               int c, const double* __restrict__ Y,
-                                                               int p, float* __restrict__ S,
-                                                               int lds) {
-  __shared__ double z[RR_BT_COLS][RR_MAXC + 1];  // +1: the 8 columns fall in distinct banks
-  __shared__ double Wc[BT_NB][BT_CH + 1];         // staged rows of the block's reflectors
+
+__global__ __launch_bounds__(256) void rr_bt_tfactor_kernel(const double* __restrict__ V,
+                                                            const double* __restrict__ tau, int c,
+                                                            double* __restrict__ Tg) {
+  __shared__ double Wc[BT_NB][BT_CH + 1];
   __shared__ double G[BT_NB][BT_NB + 1];
   __shared__ double T[BT_NB][BT_NB + 1];
-  __shared__ double WZ[BT_NB][RR_BT_COLS];
-  __shared__ double U[BT_NB][RR_BT_COLS];
   const int tid = threadIdx.x;
-  const int j0 = blockIdx.x * RR_BT_COLS;
-  const int nj = (p - j0) < RR_BT_COLS ? (p - j0) : RR_BT_COLS;
-  for (int q = tid; q < RR_BT_COLS * c; q += 256) {
-    const int jj = q / c, i = q % c;
-    z[jj][i] = (jj < nj) ? Y[(int64_t)(j0 + jj) * c + i] : 0.0;
-  }
-  __syncthreads();
-  // thread roles in the dot phase: (a, jj) = (tid / 8, tid % 8) for W^T z; Gram pairs
-  // (a, bb), bb < a, enumerated e = tid and tid + 256
-  const int wa = tid / RR_BT_COLS, wj = tid % RR_BT_COLS;
+  // Gram pairs (a, bb), bb < a, enumerated e = tid and tid + 256
   int ga[2], gb[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -507,9 +500,97 @@ __global__ __launch_bounds__(256) void rr_backtransform_kernel(const double* __r
     gb[h] = e;
   }
   const int nref = c - 2;  // reflectors 0 .. c-3 (v_k acts on indices k+1 .. c-1)
+  const int kb = blockIdx.x * BT_NB;
+  const int nb = (nref - kb) < BT_NB ? (nref - kb) : BT_NB;
+  double g0 = 0.0, g1 = 0.0;
+  for (int ich = kb + 1; ich < c; ich += BT_CH) {
+    const int len = (c - ich) < BT_CH ? (c - ich) : BT_CH;
+#pragma unroll 8
+    for (int it = 0; it < BT_NB * BT_CH / 256; ++it) {
+      const int q = tid + 256 * it;
+      const int a = q / BT_CH, ii = q % BT_CH;
+      const int k = kb + a, i = ich + ii;
+      const bool ok = a < nb && ii < len && i >= k + 1;
+      const double x = V[ok ? (int64_t)k * c + (i - k - 1) : 0];
+      Wc[a][ii] = ok ? x : 0.0;
+    }
+    __syncthreads();
+    {
+      const double* a0 = Wc[ga[0] < nb ? ga[0] : 0];
+      const double* b0 = Wc[gb[0]];
+      const double* a1 = Wc[ga[1] < nb ? ga[1] : 0];
+      const double* b1 = Wc[gb[1] < BT_NB ? gb[1] : 0];
+      double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+      const int len4 = len & ~3;
+      for (int ii = 0; ii < len4; ii += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          s1[u] += a0[ii + u] * b0[ii + u];
+          s2[u] += a1[ii + u] * b1[ii + u];
+        }
+      }
+      for (int ii = len4; ii < len; ++ii) {
+        s1[0] += a0[ii] * b0[ii];
+        s2[0] += a1[ii] * b1[ii];
+      }
+      if (ga[0] < nb) g0 += (s1[0] + s1[1]) + (s1[2] + s1[3]);
+      if (ga[1] < nb) g1 += (s2[0] + s2[1]) + (s2[2] + s2[3]);
+    }
+    __syncthreads();
+  }
+  if (ga[0] < nb) G[gb[0]][ga[0]] = g0;
+  if (ga[1] < nb) G[gb[1]][ga[1]] = g1;
+  for (int q = tid; q < BT_NB * (BT_NB + 1); q += 256) (&T[0][0])[q] = 0.0;
+  __syncthreads();
+  // T (forward larft): lane r builds row r alone (its own LDS row, 4 partial sums),
+  // T[r][i] = -tau_i sum_{q=r}^{i-1} T[r][q] G[q][i]
+  if (tid < nb) {
+    const int r = tid;
+    T[r][r] = tau[kb + r];
+    for (int i = r + 1; i < nb; ++i) {
+      double sa[4] = {0.0, 0.0, 0.0, 0.0};
+      int q = r;
+      for (; q + 4 <= i; q += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sa[u] += T[r][q + u] * G[q + u][i];
+      }
+      for (; q < i; ++q) sa[0] += T[r][q] * G[q][i];
+      T[r][i] = -tau[kb + i] * ((sa[0] + sa[1]) + (sa[2] + sa[3]));
+    }
+  }
+  __syncthreads();
+  double* out = Tg + (size_t)blockIdx.x * BT_NB * BT_NB;
+  for (int q = tid; q < BT_NB * BT_NB; q += 256) out[q] = T[q / BT_NB][q % BT_NB];
+}
+
+__global__ __launch_bounds__(256) void rr_backtransform_kernel(const double* __restrict__ V,
+                                                               const double* __restrict__ Tg,
+                                                               int c, const double* __restrict__ Y,
+                                                               int p, float* __restrict__ S,
+                                                               int lds) {
+  __shared__ double z[RR_BT_COLS][RR_MAXC + 1];  // +1: the 8 columns fall in distinct banks
+  __shared__ double Wc[BT_NB][BT_CH + 1];         // staged rows of the block's reflectors
+  __shared__ double T[BT_NB][BT_NB + 1];
+  __shared__ double WZ[BT_NB][RR_BT_COLS];
+  __shared__ double U[BT_NB][RR_BT_COLS];
+  const int tid = threadIdx.x;
+  const int j0 = blockIdx.x * RR_BT_COLS;
+  const int nj = (p - j0) < RR_BT_COLS ? (p - j0) : RR_BT_COLS;
+  for (int q = tid; q < RR_BT_COLS * c; q += 256) {
+    const int jj = q / c, i = q % c;
+    z[jj][i] = (jj < nj) ? Y[(int64_t)(j0 + jj) * c + i] : 0.0;
+  }
+  __syncthreads();
+  // thread role in the dot phase: (a, jj) = (tid / 8, tid % 8) for W^T z
+  const int wa = tid / RR_BT_COLS, wj = tid % RR_BT_COLS;
+  const int nref = c - 2;
   for (int kb = ((nref - 1) / BT_NB) * BT_NB; kb >= 0; kb -= BT_NB) {
     const int nb = (nref - kb) < BT_NB ? (nref - kb) : BT_NB;
-    double wz = 0.0, g0 = 0.0, g1 = 0.0;
+    {  // this block's T (zero past nb), read before the first barrier below
+      const double* tg = Tg + (size_t)(kb / BT_NB) * BT_NB * BT_NB;
+      for (int q = tid; q < BT_NB * BT_NB; q += 256) T[q / BT_NB][q % BT_NB] = tg[q];
+    }
+    double wz = 0.0;
     for (int ich = kb + 1; ich < c; ich += BT_CH) {
       const int len = (c - ich) < BT_CH ? (c - ich) : BT_CH;
       // fixed trip count, unrolled: all 16 loads of a thread are in flight together
@@ -524,58 +605,21 @@ __global__ __launch_bounds__(256) void rr_backtransform_kernel(const double* __r
         Wc[a][ii] = ok ? x : 0.0;
       }
       __syncthreads();
-      // three independent dot products per thread, each split over 4 accumulators, so the
-      // LDS loads of successive terms overlap instead of forming one dependent chain
-      // (Wc is zero past len, z is read only below c)
-      {
+      {  // (Wc is zero past len, z is read only below c)
         const double* wr = Wc[wa < nb ? wa : 0];
         const double* zr = &z[wj][ich];
-        const double* a0 = Wc[ga[0] < nb ? ga[0] : 0];
-        const double* b0 = Wc[gb[0]];
-        const double* a1 = Wc[ga[1] < nb ? ga[1] : 0];
-        const double* b1 = Wc[gb[1] < BT_NB ? gb[1] : 0];
-        double s0[4] = {0.0, 0.0, 0.0, 0.0}, s1[4] = {0.0, 0.0, 0.0, 0.0};
-        double s2[4] = {0.0, 0.0, 0.0, 0.0};
+        double s0[4] = {0.0, 0.0, 0.0, 0.0};
         const int len4 = len & ~3;
         for (int ii = 0; ii < len4; ii += 4) {
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            s0[u] += wr[ii + u] * zr[ii + u];
-            s1[u] += a0[ii + u] * b0[ii + u];
-            s2[u] += a1[ii + u] * b1[ii + u];
-          }
+          for (int u = 0; u < 4; ++u) s0[u] += wr[ii + u] * zr[ii + u];
         }
-        for (int ii = len4; ii < len; ++ii) {
-          s0[0] += wr[ii] * zr[ii];
-          s1[0] += a0[ii] * b0[ii];
-          s2[0] += a1[ii] * b1[ii];
-        }
+        for (int ii = len4; ii < len; ++ii) s0[0] += wr[ii] * zr[ii];
         if (wa < nb) wz += (s0[0] + s0[1]) + (s0[2] + s0[3]);
-        if (ga[0] < nb) g0 += (s1[0] + s1[1]) + (s1[2] + s1[3]);
-        if (ga[1] < nb) g1 += (s2[0] + s2[1]) + (s2[2] + s2[3]);
       }
       __syncthreads();
     }
     if (wa < nb) WZ[wa][wj] = wz;
-    if (ga[0] < nb) G[gb[0]][ga[0]] = g0;
-    if (ga[1] < nb) G[gb[1]][ga[1]] = g1;
-    __syncthreads();
-    // T (forward larft): lane r builds row r alone (its own LDS row, 4 partial sums),
-    // T[r][i] = -tau_i sum_{q=r}^{i-1} T[r][q] G[q][i]
-    if (tid < nb) {
-      const int r = tid;
-      T[r][r] = tau[kb + r];
-      for (int i = r + 1; i < nb; ++i) {
-        double sa[4] = {0.0, 0.0, 0.0, 0.0};
-        int q = r;
-        for (; q + 4 <= i; q += 4) {
-#pragma unroll
-          for (int u = 0; u < 4; ++u) sa[u] += T[r][q + u] * G[q + u][i];
-        }
-        for (; q < i; ++q) sa[0] += T[r][q] * G[q][i];
-        T[r][i] = -tau[kb + i] * ((sa[0] + sa[1]) + (sa[2] + sa[3]));
-      }
-    }
     __syncthreads();
     {
       // every row of U is written: rows a >= nb (the partial block, processed first) are
@@ -1062,11 +1106,18 @@ extern "C" hipError_t n2v2r_launch_rr_tridiag(double* A, int c, double* d, doubl
   return hipGetLastError();
 }
 
+extern "C" size_t n2v2r_rr_bt_scratch_bytes(int c) {
+  return sizeof(double) * (size_t)((c - 2 + BT_NB - 1) / BT_NB) * BT_NB * BT_NB;
+}
+
+// tfac: n2v2r_rr_bt_scratch_bytes(c) of device scratch (the blocks' T factors)
 extern "C" hipError_t n2v2r_launch_rr_backtransform(const double* V, const double* tau, int c,
                                                     const double* Y, int p, float* S, int lds,
-                                                    hipStream_t stream) {
-  if (c < 3 || c > RR_MAXC || p < 1 || p > c) return hipErrorInvalidValue;
+                                                    double* tfac, hipStream_t stream) {
+  if (c < 3 || c > RR_MAXC || p < 1 || p > c || !tfac) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rr_bt_tfactor_kernel, dim3((unsigned)((c - 2 + BT_NB - 1) / BT_NB)),
+                     dim3(256), 0, stream, V, tau, c, tfac);
   hipLaunchKernelGGL(rr_backtransform_kernel, dim3((unsigned)((p + RR_BT_COLS - 1) / RR_BT_COLS)),
-                     dim3(256), 0, stream, V, tau, c, Y, p, S, lds);
+                     dim3(256), 0, stream, V, tfac, c, Y, p, S, lds);
   return hipGetLastError();
 }

@@ -13,6 +13,7 @@
 //   gather only   : indices from a counter hash (no index stream): the pure gather rate
 //   stream only   : the index words alone (no gathers)
 //   nt-stream+gather : stream + gather with non-temporal index loads (kept out of L2's way?)
+//   ..., indices 1 / 2 batches ahead : the nt stream software-pipelined against the gathers
 // Also at 64-B rows (b = 16 panels: a lane quad per entry).  Prints one JSON line per (form, row
 // bytes, panel size): G entries/s and the index-stream GB/s.
 #include <hip/hip_runtime.h>
@@ -105,6 +106,144 @@ __global__ __launch_bounds__(1024, 8) void gather_kernel(const int32_t* __restri
   if (acc[0] == 12345.f) out[threadIdx.x] = acc[1] + acc[2] + acc[3];  // keeps the loads alive
 }
 
+// Software-pipelined stream + gather: the index words of batch i + PD are issued right after
+// batch i's gathers, so a wave waits on one memory latency per batch (the gathers) instead of
+// two in series (index word -> gather).  PD = 1 or 2 batches ahead; non-temporal index loads.
+template <int PD>
+__global__ __launch_bounds__(1024, 8) void gather_pipe_kernel(const int32_t* __restrict__ idx,
+                                                              int64_t e,
+                                                              const float* __restrict__ X,
+                                                              float* __restrict__ out) {
+  constexpr int EPS = 32;
+  const int lane = threadIdx.x & 63;
+  const int pr = lane >> 1, sub = lane & 1;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t w0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t per = (e / nw + 4 * EPS - 1) / (4 * EPS) * (4 * EPS);
+  const int64_t beg = w0 * per;
+  const int64_t end = beg + per < e ? beg + per : e;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  int wd[PD][4];
+#pragma unroll
+  for (int d = 0; d < PD; ++d)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t q = beg + d * 4 * EPS + u * EPS + pr;
+      wd[d][u] = __builtin_nontemporal_load(idx + (q < end ? q : end - 1));
+    }
+  for (int64_t off = beg; off < end; off += 4 * EPS) {
+    f32x4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      x[u] = *reinterpret_cast<const f32x4*>(X + (uint32_t)wd[0][u] * 8u + sub * 4);
+#pragma unroll
+    for (int d = 0; d + 1 < PD; ++d)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) wd[d][u] = wd[d + 1][u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t q = off + PD * 4 * EPS + u * EPS + pr;
+      wd[PD - 1][u] = __builtin_nontemporal_load(idx + (q < end ? q : (end > beg ? end - 1 : beg)));
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc += x[u];
+  }
+  if (acc[0] == 12345.f) out[threadIdx.x] = acc[1] + acc[2] + acc[3];
+}
+
+// Fewer index instructions: the plain form loads each entry's word in both lanes of its pair
+// (64 lane addresses for 32 words per instruction, one instruction per step).  FORM 0: a dword
+// of a distinct entry per lane (one instruction per 2 steps), handed to the pairs by
+// ds_bpermute; FORM 1: a dwordx2 per lane (one instruction per 4 steps), likewise.  Non-temporal.
+template <int FORM>
+__global__ __launch_bounds__(1024, 8) void gather_wide_kernel(const int32_t* __restrict__ idx,
+                                                              int64_t e,
+                                                              const float* __restrict__ X,
+                                                              float* __restrict__ out) {
+  constexpr int EPS = 32;
+  const int lane = threadIdx.x & 63;
+  const int pr = lane >> 1, sub = lane & 1;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t w0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t per = (e / nw + 4 * EPS - 1) / (4 * EPS) * (4 * EPS);
+  const int64_t beg = w0 * per;
+  const int64_t end = beg + per < e ? beg + per : e;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t off = beg; off < end; off += 4 * EPS) {
+    int wd[4];
+    if (FORM == 0) {
+      int w[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int64_t q = off + i * 64 + lane;
+        w[i] = __builtin_nontemporal_load(idx + (q < end ? q : end - 1));
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) wd[u] = __shfl(w[u >> 1], (u & 1) * 32 + pr, 64);
+    } else {
+      const int64_t q = off + 2 * lane;
+      typedef int i32x2 __attribute__((ext_vector_type(2)));
+      const i32x2 w = __builtin_nontemporal_load(
+          reinterpret_cast<const i32x2*>(idx + (q + 1 < end ? q : end - 2)));
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int src = (u * 32 + pr) >> 1;
+        const int a = __shfl(w.x, src, 64), b = __shfl(w.y, src, 64);
+        wd[u] = (pr & 1) ? b : a;
+      }
+    }
+    f32x4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      x[u] = *reinterpret_cast<const f32x4*>(X + (uint32_t)wd[u] * 8u + sub * 4);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc += x[u];
+  }
+  if (acc[0] == 12345.f) out[threadIdx.x] = acc[1] + acc[2] + acc[3];
+}
+
+template <int FORM>
+static double run_wide(const int32_t* idx, int64_t e, const float* X, float* out, int reps,
+                       int ncu) {
+  const dim3 grid((unsigned)(2 * ncu)), block(1024);
+  hipLaunchKernelGGL((gather_wide_kernel<FORM>), grid, block, 0, 0, idx, e, X, out);
+  CHK(hipDeviceSynchronize());
+  hipEvent_t a, b;
+  CHK(hipEventCreate(&a));
+  CHK(hipEventCreate(&b));
+  CHK(hipEventRecord(a, 0));
+  for (int r = 0; r < reps; ++r)
+    hipLaunchKernelGGL((gather_wide_kernel<FORM>), grid, block, 0, 0, idx, e, X, out);
+  CHK(hipEventRecord(b, 0));
+  CHK(hipEventSynchronize(b));
+  float ms = 0.f;
+  CHK(hipEventElapsedTime(&ms, a, b));
+  CHK(hipEventDestroy(a));
+  CHK(hipEventDestroy(b));
+  return ms / reps;
+}
+
+template <int PD>
+static double run_pipe(const int32_t* idx, int64_t e, const float* X, float* out, int reps,
+                       int ncu) {
+  const dim3 grid((unsigned)(2 * ncu)), block(1024);
+  hipLaunchKernelGGL((gather_pipe_kernel<PD>), grid, block, 0, 0, idx, e, X, out);
+  CHK(hipDeviceSynchronize());
+  hipEvent_t a, b;
+  CHK(hipEventCreate(&a));
+  CHK(hipEventCreate(&b));
+  CHK(hipEventRecord(a, 0));
+  for (int r = 0; r < reps; ++r)
+    hipLaunchKernelGGL((gather_pipe_kernel<PD>), grid, block, 0, 0, idx, e, X, out);
+  CHK(hipEventRecord(b, 0));
+  CHK(hipEventSynchronize(b));
+  float ms = 0.f;
+  CHK(hipEventElapsedTime(&ms, a, b));
+  CHK(hipEventDestroy(a));
+  CHK(hipEventDestroy(b));
+  return ms / reps;
+}
+
 template <int MODE, int W>
 static double run(const int32_t* idx, const uint16_t* idx16, int64_t e, const float* X,
                   uint32_t rows, float* out, int reps, int ncu) {
@@ -155,7 +294,7 @@ int main(int argc, char** argv) {
       hipLaunchKernelGGL(narrow_idx, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, 0, idx,
                          idx16, e);
       CHK(hipDeviceSynchronize());
-      double ts[6] = {-1.0, -1.0, -1.0, -1.0, -1.0, -1.0};
+      double ts[10] = {-1.0, -1.0, -1.0, -1.0, -1.0, -1.0, -1.0, -1.0, -1.0, -1.0};
       const bool narrow = rows <= 65536;
       if (W == 8) {
         ts[0] = run<0, 8>(idx, idx16, e, X, rows, out, reps, ncu);
@@ -166,18 +305,26 @@ int main(int argc, char** argv) {
           ts[4] = run<4, 8>(idx, idx16, e, X, rows, out, reps, ncu);
           ts[5] = run<5, 8>(idx, idx16, e, X, rows, out, reps, ncu);
         }
+        ts[6] = run_pipe<1>(idx, e, X, out, reps, ncu);
+        ts[7] = run_pipe<2>(idx, e, X, out, reps, ncu);
+        ts[8] = run_wide<0>(idx, e, X, out, reps, ncu);
+        ts[9] = run_wide<1>(idx, e, X, out, reps, ncu);
       } else {
         ts[0] = run<0, 16>(idx, idx16, e, X, rows, out, reps, ncu);
         ts[1] = run<1, 16>(idx, idx16, e, X, rows, out, reps, ncu);
       }
-      const char* names[6] = {"stream+gather", "gather only", "stream only",
-                              "nt-stream+gather", "u16-stream+gather", "u16-stream only"};
-      for (int f = 0; f < 6; ++f) {
+      const char* names[10] = {"stream+gather", "gather only", "stream only",
+                              "nt-stream+gather", "u16-stream+gather", "u16-stream only",
+                              "nt-stream+gather, indices 1 batch ahead",
+                              "nt-stream+gather, indices 2 batches ahead",
+                              "nt-stream+gather, dword per lane + bpermute",
+                              "nt-stream+gather, dwordx2 per lane + bpermute"};
+      for (int f = 0; f < 10; ++f) {
         if (ts[f] < 0) continue;
         printf("{\"form\": \"%s\", \"row_bytes\": %d, \"panel_MB\": %g, \"entries\": %lld, "
                "\"ms\": %.4f, \"G_entries_per_s\": %.1f, \"index_GB_per_s\": %.0f}\n",
                names[f], 4 * W, m, (long long)e, ts[f], e / (ts[f] * 1e-3) / 1e9,
-               f == 1 ? 0.0 : (f >= 4 ? 2.0 : 4.0) * e / (ts[f] * 1e-3) / 1e9);
+               f == 1 ? 0.0 : (f == 4 || f == 5 ? 2.0 : 4.0) * e / (ts[f] * 1e-3) / 1e9);
         fflush(stdout);
       }
     }
