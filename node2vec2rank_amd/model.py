@@ -41,6 +41,21 @@ def _as_layer(g):
     return np.ascontiguousarray(np.asarray(g, dtype=np.float32))
 
 
+def _label_index(nodes):
+    """``pd.Index(nodes)``, the index of every output frame.  For a list of ``str`` labels (gene
+    names: the common case) the object array is filled by ``np.fromiter`` and checked to hold
+    strings only, which gives the identical Index about 2.5x faster than pandas' own list
+    conversion (cfg4: 36 ms of a 1.7 s API call for 1M labels); anything else -- numbers,
+    mixed or tuple labels, pandas' future string inference -- goes through ``pd.Index`` itself,
+    whose dtype inference it then keeps."""
+    if (isinstance(nodes, list) and len(nodes) > 4096 and isinstance(nodes[0], str)
+            and not pd.get_option("future.infer_string")):
+        arr = np.fromiter(nodes, dtype=object, count=len(nodes))
+        if pd.api.types.infer_dtype(arr, skipna=False) == "string":
+            return pd.Index(arr, dtype=object)
+    return pd.Index(nodes)
+
+
 class N2V2R:
     """``N2V2R(graphs, nodes, config)`` (reference ``model.py:18``)."""
 
@@ -103,7 +118,7 @@ class N2V2R:
         """``pd.Index`` of the node labels, built once per label list (building it from a
         Python list is the slowest host step of a 1M-node call; every output frame shares it)."""
         if getattr(self, "_index_src", None) is not self.node_names:
-            self._index = pd.Index(self.node_names)
+            self._index = _label_index(self.node_names)
             self._index_src = self.node_names
         return self._index
 
