@@ -184,15 +184,10 @@ __global__ __launch_bounds__(1024) void reduce_cols_kernel(const double* __restr
 // out[e] = sum_c partial[c][e] for the Gram forms below: the per-element wave form for small
 // Grams (<= 512 entries: the local pass's 192 spread over 48 workgroups instead of 3; 12.1 ->
 // 10.8 us per local Gram + reduce at cfg2), the coalesced form otherwise (the full pass's 3136:
-// 32.6 vs 33.1 us).  N2V2R_REDUCE=wave / cols forces one form (A/B).
+// 32.6 vs 33.1 us).
 static hipError_t launch_reduce(const double* partial, int64_t nchunks, int64_t elems, double* out,
                                 const int* cond, hipStream_t stream) {
-  static const int force = [] {
-    const char* s = getenv("N2V2R_REDUCE");
-    return !s ? 0 : (strcmp(s, "wave") == 0 ? 1 : (strcmp(s, "cols") == 0 ? 2 : 0));
-  }();
-  const bool wave_form = force == 1 || (force == 0 && elems <= 512);
-  if (wave_form)
+  if (elems <= 512)
     hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((elems + 3) / 4)), dim3(256), 0,
                        stream, partial, (int)nchunks, elems, out, cond);
   else
@@ -633,8 +628,8 @@ __global__ __launch_bounds__(256) void ts_tn_stream_lds_kernel(BlockList A, cons
   out[(int64_t)blk * 64 + 32 * h + e] = v[0];
 }
 
-// Gram-kernel selection for 8-wide blocks: streaming form unless N2V2R_TN_FORM=lines;
-// N2V2R_TN_WAVES overrides the streaming form's wave target (tuning runs)
+// Gram-kernel selection for 8-wide blocks: the streaming form (about 4096 waves, chunks of at
+// least 256 rows) unless N2V2R_TN_FORM=lines (the line form, A/B runs)
 static bool tn_stream_form() {
   static const int v = [] {
     const char* s = getenv("N2V2R_TN_FORM");
@@ -642,35 +637,8 @@ static bool tn_stream_form() {
   }();
   return v != 0;
 }
-static int tn_stream_u() {  // row-steps of 32 rows per iteration (N2V2R_TN_U: 4 or 8)
-  static const int v = [] {
-    const char* s = getenv("N2V2R_TN_U");
-    return s ? atoi(s) : 4;
-  }();
-  return v;
-}
-static int64_t tn_stream_min_rows() {  // rows per chunk at least this (N2V2R_TN_MINROWS)
-  static const int64_t v = [] {
-    const char* s = getenv("N2V2R_TN_MINROWS");
-    const int64_t r = s ? atoll(s) : 256;
-    return r < 32 ? (int64_t)32 : (r > TS_MAX_CHUNK ? (int64_t)TS_MAX_CHUNK : r);
-  }();
-  return v;
-}
-static bool tn_lds() {  // N2V2R_TN_LDS=0: the streaming Gram without the LDS-staged Z rows
-  static const bool v = [] {
-    const char* s = getenv("N2V2R_TN_LDS");
-    return !(s && s[0] == '0');
-  }();
-  return v;
-}
-static int64_t tn_stream_waves() {
-  static const int64_t v = [] {
-    const char* s = getenv("N2V2R_TN_WAVES");
-    return (int64_t)(s ? atoll(s) : 4096);
-  }();
-  return v;
-}
+#define TN_STREAM_WAVES 4096
+#define TN_STREAM_MIN_ROWS 256
 
 static hipError_t launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n,
                                double* partial, size_t partial_elems, double* out,
@@ -678,10 +646,10 @@ static hipError_t launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n
   const int ca = A.count * A.width, cb = B.count * B.width;
   int64_t s_chunks = 0, s_rows = 0;
   if (B.count == 1 && B.width == 8 && A.width == 8 && tn_stream_form()) {
-    // streaming form: ~tn_stream_waves() (4096) waves, chunks of <= TS_MAX_CHUNK rows, nchunks % 8 == 0
-    s_chunks = (tn_stream_waves() + A.count - 1) / A.count;
+    // streaming form: ~TN_STREAM_WAVES (4096) waves, chunks of <= TS_MAX_CHUNK rows, nchunks % 8 == 0
+    s_chunks = (TN_STREAM_WAVES + A.count - 1) / A.count;
     const int64_t lo = (n + TS_MAX_CHUNK - 1) / TS_MAX_CHUNK,
-                  hi = (n + tn_stream_min_rows() - 1) / tn_stream_min_rows();
+                  hi = (n + TN_STREAM_MIN_ROWS - 1) / TN_STREAM_MIN_ROWS;
     if (s_chunks > hi) s_chunks = hi;
     if (s_chunks < lo) s_chunks = lo;
     s_chunks = (s_chunks + 7) & ~(int64_t)7;
@@ -698,15 +666,9 @@ static hipError_t launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n
     if (zs && zs->count > 0)
       hipLaunchKernelGGL((ts_tn_stream_kernel<4, true>), grid, dim3(256), 0, stream, A, B.blk[0],
                          n, rows_per_chunk, partial, cond, *zs);
-    else if (tn_stream_u() == 8)
-      hipLaunchKernelGGL((ts_tn_stream_kernel<8, false>), grid, dim3(256), 0, stream, A, B.blk[0],
-                         n, rows_per_chunk, partial, cond, none);
-    else if (tn_lds())
+    else
       hipLaunchKernelGGL((ts_tn_stream_lds_kernel<4>), grid, dim3(256), 0, stream, A, B.blk[0],
                          n, rows_per_chunk, partial, cond);
-    else
-      hipLaunchKernelGGL((ts_tn_stream_kernel<4, false>), grid, dim3(256), 0, stream, A, B.blk[0],
-                         n, rows_per_chunk, partial, cond, none);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_reduce(partial, nchunks, elems, out, cond, stream);
@@ -923,9 +885,9 @@ extern "C" hipError_t n2v2r_launch_ts_tn2(const BlockList& A, const float* Za, c
                                           double* out, hipStream_t stream) {
   if (A.width != 8 || A.count < 1 || n < 1) return hipErrorInvalidValue;
   const int64_t elems = (int64_t)A.count * 128;
-  int64_t s_chunks = (tn_stream_waves() + A.count - 1) / A.count;
+  int64_t s_chunks = (TN_STREAM_WAVES + A.count - 1) / A.count;
   const int64_t lo = (n + TS_MAX_CHUNK - 1) / TS_MAX_CHUNK,
-                hi = (n + tn_stream_min_rows() - 1) / tn_stream_min_rows();
+                hi = (n + TN_STREAM_MIN_ROWS - 1) / TN_STREAM_MIN_ROWS;
   if (s_chunks > hi) s_chunks = hi;
   if (s_chunks < lo) s_chunks = lo;
   s_chunks = (s_chunks + 7) & ~(int64_t)7;
@@ -1869,8 +1831,7 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
                                                         int* any_flag, double* save, int save_row0,
                                                         int save_rows, int* sticky, uint64_t seed,
                                                         int64_t row0, double* rsave, float skip_tol,
-                                                        int* skipped, int stop) {
-  // stop = k > 0: timing probe (N2V2R_PIP_STOP, tools/pip_probe.cpp), return after phase k
+                                                        int* skipped) {
   const int tid = threadIdx.x;
   const bool lead = blockIdx.x == 0;
   if (cond && *cond == 0) {
@@ -1898,7 +1859,6 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
       reinterpret_cast<double2*>(gd)[min(e0 + 256 * u, ne2 - 1)] = t[u];
   }
   __syncthreads();
-  if (stop == 1) return;
   // the basis blocks this pass applies: all, or (skip_tol > 0: selective reorthogonalisation of
   // an in-place pass) those with max_ij |C_ij| / ||z_j|| > skip_tol; every workgroup decides
   // alike from the same G.  C^T C sums the applied blocks only, so R factors the applied pass.
@@ -1944,7 +1904,6 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
     }
   }
   __syncthreads();
-  if (stop == 2) return;
   const int napply = badw[1];
   if (skip_tol > 0.f) {
     if (napply == 0 && !badw[2]) {
@@ -1964,7 +1923,6 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
     const int g = blist[e >> 6] * 64 + (e & 63);
     cf[g] = (float)gd[g];
   }
-  if (stop == 4) return;
   {
     const int e = tid & 63, sl = tid >> 6, i = e >> 3, j = e & 7;
     // wave sl: list entries sl, sl + 4, ...; four independent chains (rows r mod 4)
@@ -1982,7 +1940,6 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
     part[sl * 64 + e] = (a0 + a1) + (a2 + a3);
   }
   __syncthreads();
-  if (stop == 5) return;
   if (tid < 64) {  // P = Z^T Z - C^T C (each lane reads only its own part[] entries)
     const int i = tid >> 3, j = tid & 7;
     const double v = 0.5 * (gd[(c + i) * 8 + j] + gd[(c + j) * 8 + i]);
@@ -2054,7 +2011,6 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
     }
   }
   __syncthreads();
-  if (stop == 6) return;
   // rows: wave w owns rows 32 NU w .. 32 NU (w + 1) - 1 of the workgroup's 128 NU, lane =
   // (row offset ro = lane >> 1, column half h = lane & 1) over NU 32-row parts u, so one load
   // instruction reads 32 consecutive 32-B rows of a block (1 KB contiguous)
@@ -2148,38 +2104,21 @@ extern "C" hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zi
   if (skip_tol != 0.f && (Zin != Zout || save)) return hipErrorInvalidValue;
   const size_t lds = sizeof(double) * ((size_t)(c + 8) * 8 + 256) + sizeof(float) * ((size_t)c * 8 + 64) + 16 + 256;
   if (lds > 64 * 1024 || c > 512) return hipErrorInvalidValue;
-  static const int qb = [] {
-    const char* s = getenv("N2V2R_PIP_QB");
-    return s ? atoi(s) : 4;
-  }();
   // rows per workgroup (64 or 128 per wave); 128 rows: cfg2 flat, cfg4 +20 % (every workgroup
   // stages the (c + 8) x 8 fp64 Gram, 33 KB at c = 512)
   // 512 rows per workgroup from N = 512k rows on (the per-workgroup prologue -- Gram staging,
   // selective test, Cholesky -- amortised over twice the rows: cfg4 fit 1,632 vs 1,645 ms; at
-  // cfg2's 100k rows the 196 workgroups leave CUs idle: 34.0 vs 33.1 ms).  N2V2R_PIP_ROWS = 128,
-  // 256 or 512 forces one (A/B)
-  static const int rows_env = [] {
-    const char* s = getenv("N2V2R_PIP_ROWS");
-    const int v = s ? atoi(s) : 0;
-    return v == 128 || v == 256 || v == 512 ? v : 0;
-  }();
-  const int rows = rows_env ? rows_env : (n >= (int64_t)1 << 19 ? 512 : 256);
-  static const int pip_stop = [] {  // timing probe only: phases after k skipped
-    const char* s = getenv("N2V2R_PIP_STOP");
-    return s ? atoi(s) : 0;
-  }();
+  // cfg2's 100k rows the 196 workgroups leave CUs idle: 34.0 vs 33.1 ms)
+  const int rows = n >= (int64_t)1 << 19 ? 512 : 256;
   const unsigned grid = (unsigned)((n + rows - 1) / rows);
 #define PIP_LAUNCH(QB_, NU_)                                                                   \
   hipLaunchKernelGGL((pip_fused_kernel<QB_, NU_>), dim3(grid ? grid : 1), dim3(256), lds, stream, Q, \
                      Zin, Zout, G, c, n, cond, flags, any_flag, save, save_row0, save_rows, sticky,  \
-                     seed, row0, rsave, skip_tol, skipped, pip_stop)
-  if (rows == 256) {
-    if (qb == 8) PIP_LAUNCH(8, 2); else PIP_LAUNCH(4, 2);
-  } else if (rows == 512) {
+                     seed, row0, rsave, skip_tol, skipped)
+  if (rows == 256)
+    PIP_LAUNCH(4, 2);
+  else
     PIP_LAUNCH(2, 4);
-  } else {
-    if (qb == 4) PIP_LAUNCH(4, 1); else PIP_LAUNCH(8, 1);
-  }
 #undef PIP_LAUNCH
   return hipGetLastError();
 }

@@ -60,19 +60,17 @@ __device__ __forceinline__ void dg_store_a(float (*as)[DG_AP], const f32x4 (&v)[
 
 // (Round 4, measured and not kept: X rows loaded a round ahead with the A tile and each 16-k
 // group's LDS operands read before the previous group's MFMAs: 0.447 vs 0.407 ms per cfg3
-// launch, profiles/r04_dense_forms.jsonl.)
-// XT = false (default): xs[k][column], one LDS read per MFMA.  XT = true (N2V2R_DG_XT=1, A/B):
-// X staged transposed, xs[column][k] (pitch DG_AP), so a lane reads its 8 consecutive k of a
-// 16-k group as two 16-B LDS reads like its A operands -- measured 0.40 vs 0.39 ms per cfg3
-// launch, not kept.
-template <int NT, bool XT>
+// launch, profiles/r04_dense_forms.jsonl; X staged transposed, xs[column][k], so a lane reads
+// its 8 consecutive k of a 16-k group as two 16-B LDS reads like its A operands: 0.40 vs 0.39
+// ms per cfg3 launch.)  xs[k][column], one LDS read per MFMA.
+template <int NT>
 __global__ __launch_bounds__(256) void dense_gemm_kernel(const float* __restrict__ A, int64_t lda,
                                                          int64_t rows, int64_t kdim,
                                                          int64_t kper, const float* __restrict__ X,
                                                          int ldx, int b, float* __restrict__ out,
                                                          int64_t ldo, int64_t slab) {
   constexpr int XP = NT * 32 + 4;  // padded LDS row pitch of xs
-  __shared__ __attribute__((aligned(16))) float xs[XT ? NT * 32 : DG_KC][XT ? DG_AP : XP];
+  __shared__ __attribute__((aligned(16))) float xs[DG_KC][XP];
   __shared__ __attribute__((aligned(16))) float as[128][DG_AP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i = lane & 31, h = lane >> 5;
@@ -105,11 +103,7 @@ __global__ __launch_bounds__(256) void dense_gemm_kernel(const float* __restrict
       for (int u = 0; u < XN; ++u) {
         const int e = threadIdx.x + 256 * u;
         const int kk = e / (NT * 32), j = e % (NT * 32);
-        const float x = (kk < kn && j < b) ? xv[u] : 0.f;
-        if constexpr (XT)
-          xs[j][kk] = x;
-        else
-          xs[kk][j] = x;
+        xs[kk][j] = (kk < kn && j < b) ? xv[u] : 0.f;
       }
     }
     __syncthreads();
@@ -118,30 +112,13 @@ __global__ __launch_bounds__(256) void dense_gemm_kernel(const float* __restrict
       for (int kk = 0; kk < kn; kk += 16) {
         const f32x4 a0 = *reinterpret_cast<const f32x4*>(&as[wave * 32 + i][kk + 8 * h]);
         const f32x4 a1 = *reinterpret_cast<const f32x4*>(&as[wave * 32 + i][kk + 8 * h + 4]);
-        if constexpr (XT) {
-          f32x4 x0[NT], x1[NT];
 #pragma unroll
-          for (int t = 0; t < NT; ++t) {
-            x0[t] = *reinterpret_cast<const f32x4*>(&xs[t * 32 + i][kk + 8 * h]);
-            x1[t] = *reinterpret_cast<const f32x4*>(&xs[t * 32 + i][kk + 8 * h + 4]);
-          }
+        for (int m = 0; m < 8; ++m) {
+          const float av = m < 4 ? a0[m] : a1[m - 4];
 #pragma unroll
-          for (int m = 0; m < 8; ++m) {
-            const float av = m < 4 ? a0[m] : a1[m - 4];
-#pragma unroll
-            for (int t = 0; t < NT; ++t)
-              acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, m < 4 ? x0[t][m] : x1[t][m - 4],
-                                                            acc[t], 0, 0, 0);
-          }
-        } else {
-#pragma unroll
-          for (int m = 0; m < 8; ++m) {
-            const float av = m < 4 ? a0[m] : a1[m - 4];
-#pragma unroll
-            for (int t = 0; t < NT; ++t)
-              acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xs[kk + 8 * h + m][t * 32 + i],
-                                                            acc[t], 0, 0, 0);
-          }
+          for (int t = 0; t < NT; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xs[kk + 8 * h + m][t * 32 + i],
+                                                          acc[t], 0, 0, 0);
         }
       }
     }
@@ -211,20 +188,13 @@ extern "C" hipError_t n2v2r_launch_dense_gemm(const float* A, int64_t lda, int64
   const int64_t ldo = work ? b : ldy;
   const int64_t slab = work ? rows * b : 0;
   const dim3 grid((unsigned)tiles, (unsigned)nsplit);
-  static const bool xt = [] {  // N2V2R_DG_XT=1: X staged transposed (A/B: 0.40 vs 0.39 ms)
-    const char* s = getenv("N2V2R_DG_XT");
-    return s && s[0] == '1';
-  }();
-#define DG_LAUNCH(NT, XT)                                                                      \
-  hipLaunchKernelGGL((dense_gemm_kernel<NT, XT>), grid, dim3(256), 0, stream, A, lda, rows, kdim, \
-                     kper, X, ldx, b, dst, ldo, slab)
-  if (b <= 32) {
-    if (xt) DG_LAUNCH(1, true);
-    else DG_LAUNCH(1, false);
-  } else {
-    if (xt) DG_LAUNCH(2, true);
-    else DG_LAUNCH(2, false);
-  }
+#define DG_LAUNCH(NT)                                                                          \
+  hipLaunchKernelGGL((dense_gemm_kernel<NT>), grid, dim3(256), 0, stream, A, lda, rows, kdim, kper, \
+                     X, ldx, b, dst, ldo, slab)
+  if (b <= 32)
+    DG_LAUNCH(1);
+  else
+    DG_LAUNCH(2);
 #undef DG_LAUNCH
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !work) return e;

@@ -756,7 +756,7 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
                                                               double* __restrict__ wout,
                                                               double* __restrict__ Y,
                                                               float* __restrict__ S, int ldS,
-                                                              int* __restrict__ err, int inv_stop,
+                                                              int* __restrict__ err,
                                                               bool inv_par, bool start_warm) {
   extern __shared__ __attribute__((aligned(16))) double il[];
   const int lane = threadIdx.x;
@@ -778,10 +778,8 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
   double* sch = dX + kp;    // [64] the X rows' Schur complement on the E block
   double* fe = sch + 64;    // [8]
   __syncthreads();
-  const int stop = inv_stop;
   for (int j = j0; j < p && (j == j0 || fabs(w[j - 1] - w[j]) <= clus); ++j) {
     const double lam = w[j];
-    if (stop == 1) { if (lane == 0) err[0] = 1; return; }
     for (int a = lane; a < kp; a += 64) dX[a] = rs_rcp(rs_guard(Xd[a] - lam, tiny));
     __syncthreads();
     {
@@ -801,10 +799,8 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
       f[i] = warm ? ((i == j ? 1.0 : 0.0) + 1e-4 * u) : u;
     }
     __syncthreads();
-    if (stop == 2) { if (lane == 0) err[0] = 1; return; }
     if (lane == 0) rs_factor_lane(c, kp, Lb, sch, lam, tiny, F);
     __syncthreads();
-    if (stop == 3) { if (lane == 0) err[0] = 1; return; }
     // r = (H - lam) y: X rows, then the band rows (+ the X couplings of the E rows); the
     // Rayleigh quotient lam + y.r refines the eigenvalue, ||(H - rq) y||^2 = r.r - (y.r)^2
     double r2 = 0.0, yr = 0.0;
@@ -844,7 +840,6 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
     bool ok = true, done = false;
     for (int it = 0; it < 2 && ok; ++it) {
       rs_solve(c, kp, Xg, dX, F, fe, f, y, inv_par);
-      if (stop == 4) { if (lane == 0) err[0] = 1; return; }
       // classical Gram-Schmidt against the cluster's earlier members (Y columns j0 .. j-1)
       for (int q = j0; q < j; ++q) {
         double dq = 0.0;
@@ -872,7 +867,6 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
         }
       }
     }
-    if (stop == 5) { if (lane == 0) err[0] = 1; return; }
     if (!done) {
       residual();
       if (lane == 0) atomicAdd(&err[1], 1);  // diagnostics: vectors that took the second solve
@@ -896,13 +890,7 @@ static size_t rs_asm_elems(int c, int kp) {  // header + Xd + Xg + padded band r
 
 // scratch doubles for any kp <= c - 8: the assembly (at most RS_HDR + RS_LD (c + RS_PADR)), the
 // bisection values (c), the multisection brackets (2 x p x 2) and counts (2 x p x M ints)
-static int rs_msect_threads() {  // N2V2R_MSECT_THREADS=512: the two-waves-per-SIMD form (A/B)
-  static const int v = [] {
-    const char* e = getenv("N2V2R_MSECT_THREADS");
-    return (e && atoi(e) == 512) ? 512 : 256;
-  }();
-  return v;
-}
+static int rs_msect_threads() { return 256; }  // (512, two waves per SIMD: measured, not kept)
 
 // points per eigenvalue per round: nt x workgroups (about one workgroup per CU)
 static int rs_msect_m(int p, int nt = RS_MS_THREADS) {
@@ -954,9 +942,6 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
     if (a2 == hipSuccess) a2 = a5;
     hipError_t a3 = hipFuncSetAttribute((const void*)rr_msect_kernel<256>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-    hipError_t a4 = hipFuncSetAttribute((const void*)rr_msect_kernel<512>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-    if (a3 == hipSuccess) a3 = a4;
     if (a2 == hipSuccess) a2 = a3;
     (void)hipGetLastError();  // a refused attribute must not surface as a later launch error
     if (a1 != hipSuccess) return a1;
@@ -988,12 +973,8 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
     int rounds = 1;
     for (double wdt = 2.0 / ((double)pm * M + 1.0); wdt > 1e-10; wdt /= (double)(M + 1)) ++rounds;
     for (int r = 0; r < rounds; ++r) {
-      if (nt_ms == 256)
-        hipLaunchKernelGGL(rr_msect_kernel<256>, dim3(grid), dim3(256), lms, stream, scr, c, kp, pm,
-                           M, r, ms);
-      else
-        hipLaunchKernelGGL(rr_msect_kernel<512>, dim3(grid), dim3(512), lms, stream, scr, c, kp, pm,
-                           M, r, ms);
+      hipLaunchKernelGGL(rr_msect_kernel<256>, dim3(grid), dim3(256), lms, stream, scr, c, kp, pm,
+                         M, r, ms);
       e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
@@ -1002,16 +983,12 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
   }
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  static const int inv_stop = [] {  // N2V2R_INVITER_STOP=k: timing probe, phases after k skipped
-    const char* v = getenv("N2V2R_INVITER_STOP");
-    return v ? atoi(v) : 0;
-  }();
   // N2V2R_INV_SOLVE=lane: lane 0 runs the band solves (A/B; read per launch)
   const char* inv_env = getenv("N2V2R_INV_SOLVE");
   const bool inv_par = !(inv_env && inv_env[0] == 'l');
   const char* start_env = getenv("N2V2R_INV_START");  // "rand": random start vectors (A/B)
   const bool start_warm = !(start_env && start_env[0] == 'r');
   hipLaunchKernelGGL(rr_sturm_inviter_kernel, dim3((unsigned)p), dim3(64), linv, stream, scr, c,
-                     kp, p, pm, wbis, 1e-9, theta, Y, S, ldS, err, inv_stop, inv_par, start_warm);
+                     kp, p, pm, wbis, 1e-9, theta, Y, S, ldS, err, inv_par, start_warm);
   return hipGetLastError();
 }

@@ -396,8 +396,9 @@ __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1)
   }
 }
 
-template <bool NT, bool BAR>
+// NT: index / value words loaded non-temporally (read once; the panel gathers keep L2)
 __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
+  constexpr bool NT = true;
   // [tile_rows][8] row accumulators, then a 1-KB staging slot per wave
   extern __shared__ float tacf[];
   const int lane = threadIdx.x & 63;
@@ -473,7 +474,7 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
       // 0.36 ms per cfg4 layer launch; a bounded skew -- a wave starts phase g once all have
       // finished g - 2, LDS counters -- 0.393 vs 0.354 ms, fit 1,714 vs 1,603 ms,
       // profiles/r04_flat_sync.jsonl: the L2 locality of lockstep phases is worth the idling)
-      if (BAR) __syncthreads();
+      __syncthreads();
     }
     if (!a.sum || k == a.K - 1) {
       float* Y = a.Y[a.sum ? 0 : k];
@@ -506,30 +507,16 @@ extern "C" hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, hipStream_t 
   const size_t flds = sizeof(float) * 8 * (size_t)a.tile_rows + 16 * 1024;
   if (flds > 80 * 1024) return hipErrorInvalidValue;
   static const bool fattr = [] {
-    (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel<false, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-    (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel<true, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-    (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel<true, false>,
+    (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
     (void)hipGetLastError();
     return true;
   }();
   (void)fattr;
-  // Non-temporal index / value loads (the stream is read once; the panel gathers keep L2):
-  // cfg4 layer launch 0.354 vs 0.363 ms, fit 1,599 vs 1,609 ms (profiles/r04_flat_nt.jsonl;
-  // N2V2R_FLAT_NT=0 for the plain loads).  N2V2R_FLAT_BAR=0 (A/B): no barrier between phases.
-  // Both read per launch.
-  const char* ntv = getenv("N2V2R_FLAT_NT");
-  const char* bav = getenv("N2V2R_FLAT_BAR");
-  const bool nt = !(ntv && ntv[0] == '0');
-  const bool bar = !(bav && bav[0] == '0');
-  if (!nt)
-    hipLaunchKernelGGL((spmm8_flat_kernel<false, true>), dim3(grid), dim3(1024), flds, stream, a);
-  else if (bar)
-    hipLaunchKernelGGL((spmm8_flat_kernel<true, true>), dim3(grid), dim3(1024), flds, stream, a);
-  else
-    hipLaunchKernelGGL((spmm8_flat_kernel<true, false>), dim3(grid), dim3(1024), flds, stream, a);
+  // (Non-temporal index / value loads: cfg4 layer launch 0.354 vs 0.363 ms, fit 1,599 vs
+  // 1,609 ms, profiles/r04_flat_nt.jsonl; no phase barrier: 0.57 vs 0.36 ms,
+  // profiles/r04_flat_bar.jsonl -- the A/B switches of those runs are gone.)
+  hipLaunchKernelGGL(spmm8_flat_kernel, dim3(grid), dim3(1024), flds, stream, a);
   return hipGetLastError();
 }
 
