@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4, final build: closing bench lines (cfg4 = the default, cfg3, cfg2, cfg1) and the cfg4
+# Round 4, final build (rerun in the second session): closing bench lines (cfg4 = the default, cfg3, cfg2, cfg1) and the cfg4
 # kernel trace of a one-step bench (csv stats)
 set -o pipefail
 mkdir -p gpurun_out
