@@ -1570,21 +1570,32 @@ struct Eig {
     const int64_t nglob = h->n;
     // small graphs: shrink the block until the Krylov space fits well inside R^n
     int keep = 0, maxc = 0;
+    // CSR layers: keep 21d/16 (rounded up to b) -- round 4, on two graphs each: cfg4 795-838
+    // block applications against 812-856 at the former 5d/4 (1.51-1.59 vs 1.53-1.63 s), cfg2
+    // (84 -> 88) 270 against 276-314, and 11d/8 mixed (profiles/r04_keep_sweep.jsonl)
     // dense layers (b = 32): keep d + b, basis <= 704 -- on three cfg3-family graphs 61 block
     // applications and 215-218 ms per fit against 66 and 236-240 ms with the general rule's
     // keep 5d/4 = 320 and basis 768 (profiles/r04_cfg3_sweep*.jsonl)
     const bool dense_rule = h->dense_layers() && !o.block;
     for (;; b /= 2) {
-      keep = o.keep ? o.keep : (dense_rule ? d + b : std::max(d + 16, (d * 5) / 4));
+      keep = o.keep ? o.keep : (dense_rule ? d + b : std::max(d + 16, (d * 21) / 16));
       keep = ((keep + b - 1) / b) * b;
+      // (not past the banded Rayleigh-Ritz's 184 kept vectors where the former rule fit them)
+      if (!o.keep && !dense_rule && b == 8 && keep > 184 && std::max(d + 16, (d * 5) / 4) <= 184)
+        keep = 184;
       // default basis: 3.2 keep for the dense Rayleigh-Ritz (its cost grows as c^3); 4.8 keep
       // (<= 512) for the banded one (b = 8), where fewer, longer cycles win (cfg2: 14 cycles
       // at c = 256, 7 at c = 384, 13 % fewer block applications)
       // (a keep that does not fit the banded form's 512-column basis takes the dense one's)
+      // (the banded form's basis follows the former keep rule, 5d/4: cfg2 keeps c = 384 -- 270
+      // block applications against 305 at 4.8 x 88 = 424)
+      const int keep_basis = (o.keep || dense_rule)
+                                 ? keep
+                                 : ((std::max(d + 16, (d * 5) / 4) + b - 1) / b) * b;
       const bool band_ok = b == 8 && !(o.solver_flags & N2V2R_EIG_DENSE_RR) && keep + b <= 512;
       maxc = o.max_basis ? o.max_basis
-                         : (band_ok ? std::min(512, std::max(keep + 3 * b, (24 * keep) / 5))
-                                    : std::max(keep + 3 * b, (16 * keep) / 5));
+                         : (band_ok ? std::min(512, std::max(keep + 3 * b, (24 * keep_basis) / 5))
+                                    : std::max(keep + 3 * b, (16 * keep_basis) / 5));
       maxc = ((maxc + b - 1) / b) * b;
       const int cap =
           (int)std::min<int64_t>((nglob / 2) / b * b, (int64_t)(N2V2R_MAX_BLOCKS - 1) * b);
@@ -1592,6 +1603,13 @@ struct Eig {
       if (maxc > 768) maxc = 768 / b * b;  // Rayleigh-Ritz kernels: c <= 768
       if (dense_rule && !o.max_basis && maxc > 704) maxc = 704 / b * b;
       if (maxc >= keep + b) break;
+      // the auto keep 21d/16 does not fit the basis (d near the 600 limit, small graphs): the
+      // former 5d/4
+      const int keep_old = ((std::max(d + 16, (d * 5) / 4) + b - 1) / b) * b;
+      if (!o.keep && !dense_rule && keep > keep_old && maxc >= keep_old + b) {
+        keep = keep_old;
+        break;
+      }
       if (b == 8)
         throw StatusFail{N2V2R_ERR_BAD_ARG,
                          "graph too small for the requested dimension: need n >= 2*(keep+8)"};
