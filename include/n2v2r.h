@@ -71,7 +71,8 @@ typedef struct n2v2r_simgroup n2v2r_simgroup;
 typedef struct {
   int block;          /* Krylov block width b: 8, 16, 32 or 64 (0 = auto: 8) */
   int max_basis;      /* max basis columns before a thick restart (0 = auto) */
-  int keep;           /* Ritz vectors kept at a restart (0 = auto) */
+  int keep;           /* Ritz vectors kept at a restart (0 = auto: max(d + 16, 21d/16) for CSR
+                         layers, at most 184 where the banded Rayleigh-Ritz fits; d + b for dense) */
   int max_restarts;   /* (0 = auto: 2000) */
   double tol;         /* stop when ||M x_j - theta_j x_j|| <= tol * theta_1 for j < d (<=0: 1e-6) */
   uint64_t seed;      /* start block seed */
