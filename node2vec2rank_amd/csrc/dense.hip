@@ -181,6 +181,20 @@ __global__ __launch_bounds__(1024) void reduce_cols_kernel(const double* __restr
   }
 }
 
+// Non-temporal loads of the Krylov basis (round 4): a basis beyond the 256 MB Infinity Cache is
+// streamed from HBM by every pass that reads it, so its lines are read once per pass -- nt
+// dwordx4 loads stream 2 GB at 6.8 TB/s against 6.0 for plain ones on MI355X
+// (profiles/r04_stream_ceiling.jsonl).  A basis that fits the cache keeps plain loads (it is
+// re-read from there by the next pass).  N2V2R_BASIS_NT=0 / 1 forces plain / nt (A/B).
+static bool basis_nt(int64_t n, int count) {
+  static const int force = [] {
+    const char* s = getenv("N2V2R_BASIS_NT");
+    return s ? (s[0] == '1' ? 1 : (s[0] == '0' ? 0 : -1)) : -1;
+  }();
+  if (force >= 0) return force == 1;
+  return (double)n * 32.0 * (double)count > 256.0 * 1024 * 1024;
+}
+
 // out[e] = sum_c partial[c][e] for the Gram forms below: the per-element wave form for small
 // Grams (<= 512 entries: the local pass's 192 spread over 48 workgroups instead of 3; 12.1 ->
 // 10.8 us per local Gram + reduce at cfg2), the coalesced form otherwise (the full pass's 3136:
@@ -779,7 +793,7 @@ extern "C" hipError_t n2v2r_launch_ts_tn_zsum(const BlockList& A, int64_t n, con
 // (row-major (blk * 8 + i, j)).  Same streaming form: one wave per (basis block, row chunk), a
 // lane owns 4 columns of its block over rows rl, rl + 32, ..., fp32 products of at most
 // TS_MAX_CHUNK / 32 rows per lane, then a fixed fp64 reduce-scatter over the 32 row lanes.
-template <int TS_U>
+template <int TS_U, bool NT>
 __global__ __launch_bounds__(256) void ts_tn_stream2_kernel(BlockList A, const float* __restrict__ Za,
                                                             const float* __restrict__ Zb, int64_t n,
                                                             int64_t rows_per_chunk,
@@ -825,8 +839,10 @@ __global__ __launch_bounds__(256) void ts_tn_stream2_kernel(BlockList A, const f
   auto load_step = [&](int64_t rs) {
     if (active) {
 #pragma unroll
-      for (int u = 0; u < TS_U; ++u)
-        an[u] = *reinterpret_cast<const f32x4*>(ab + (rs + 32 * u + rl) * 8);
+      for (int u = 0; u < TS_U; ++u) {
+        const f32x4* p = reinterpret_cast<const f32x4*>(ab + (rs + 32 * u + rl) * 8);
+        an[u] = NT ? __builtin_nontemporal_load(p) : *p;
+      }
     }
     zn = *reinterpret_cast<const f32x4*>(zsrc + (rs + zr) * 8);
   };
@@ -895,8 +911,12 @@ extern "C" hipError_t n2v2r_launch_ts_tn2(const BlockList& A, const float* Za, c
   s_chunks = (n + s_rows - 1) / s_rows;
   if ((size_t)(s_chunks * elems) > partial_elems || s_rows > TS_MAX_CHUNK) return hipErrorNotSupported;
   const dim3 grid((unsigned)s_chunks, (unsigned)((A.count + 3) / 4));
-  hipLaunchKernelGGL((ts_tn_stream2_kernel<2>), grid, dim3(256), 0, stream, A, Za, Zb, n, s_rows,
-                     partial);
+  if (basis_nt(n, A.count))
+    hipLaunchKernelGGL((ts_tn_stream2_kernel<2, true>), grid, dim3(256), 0, stream, A, Za, Zb, n,
+                       s_rows, partial);
+  else
+    hipLaunchKernelGGL((ts_tn_stream2_kernel<2, false>), grid, dim3(256), 0, stream, A, Za, Zb, n,
+                       s_rows, partial);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return launch_reduce(partial, s_chunks, elems, out, nullptr, stream);
@@ -1824,7 +1844,7 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   return __hiloint2double(hi, lo);
 }
 
-template <int QB, int NU>
+template <int QB, int NU, bool NT>
 __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float* Zin, float* Zout,
                                                         const double* __restrict__ G, int c,
                                                         int64_t n, const int* cond, int* flags,
@@ -2044,7 +2064,9 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
     for (int b4 = 0; b4 < QB; ++b4)
 #pragma unroll
       for (int u = 0; u < NU; ++u)
-        a4[b4][u] = *reinterpret_cast<const f32x4*>(Q.blk[bi[b4]] + rw[u] * 8 + 4 * h);
+        a4[b4][u] = NT ? __builtin_nontemporal_load(
+                             reinterpret_cast<const f32x4*>(Q.blk[bi[b4]] + rw[u] * 8 + 4 * h))
+                       : *reinterpret_cast<const f32x4*>(Q.blk[bi[b4]] + rw[u] * 8 + 4 * h);
 #pragma unroll
     for (int b4 = 0; b4 < QB; ++b4) {
       const float* g = cf + (bi[b4] * 8 + 4 * h) * 8;
@@ -2062,7 +2084,10 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
     f32x4 a4[NU];
     const int bq = __builtin_amdgcn_readfirstlane(blist[q]);
 #pragma unroll
-    for (int u = 0; u < NU; ++u) a4[u] = *reinterpret_cast<const f32x4*>(Q.blk[bq] + rw[u] * 8 + 4 * h);
+    for (int u = 0; u < NU; ++u)
+      a4[u] = NT ? __builtin_nontemporal_load(
+                       reinterpret_cast<const f32x4*>(Q.blk[bq] + rw[u] * 8 + 4 * h))
+                 : *reinterpret_cast<const f32x4*>(Q.blk[bq] + rw[u] * 8 + 4 * h);
     const float* g = cf + (bq * 8 + 4 * h) * 8;
 #pragma unroll
     for (int m = 0; m < 4; ++m)
@@ -2111,14 +2136,16 @@ extern "C" hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zi
   // cfg2's 100k rows the 196 workgroups leave CUs idle: 34.0 vs 33.1 ms)
   const int rows = n >= (int64_t)1 << 19 ? 512 : 256;
   const unsigned grid = (unsigned)((n + rows - 1) / rows);
-#define PIP_LAUNCH(QB_, NU_)                                                                   \
-  hipLaunchKernelGGL((pip_fused_kernel<QB_, NU_>), dim3(grid ? grid : 1), dim3(256), lds, stream, Q, \
+#define PIP_LAUNCH(QB_, NU_, NT_)                                                                \
+  hipLaunchKernelGGL((pip_fused_kernel<QB_, NU_, NT_>), dim3(grid ? grid : 1), dim3(256), lds, stream, Q, \
                      Zin, Zout, G, c, n, cond, flags, any_flag, save, save_row0, save_rows, sticky,  \
                      seed, row0, rsave, skip_tol, skipped)
-  if (rows == 256)
-    PIP_LAUNCH(4, 2);
-  else
-    PIP_LAUNCH(2, 4);
+  const bool nt = basis_nt(n, Q.count);
+  if (rows == 256) {
+    if (nt) PIP_LAUNCH(4, 2, true); else PIP_LAUNCH(4, 2, false);
+  } else {
+    if (nt) PIP_LAUNCH(2, 4, true); else PIP_LAUNCH(2, 4, false);
+  }
 #undef PIP_LAUNCH
   return hipGetLastError();
 }
