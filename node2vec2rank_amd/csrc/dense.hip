@@ -662,7 +662,7 @@ static hipError_t launch_ts_tn(const BlockList& A, const BlockList& B, int64_t n
   if (B.count == 1 && B.width == 8 && A.width == 8 && tn_stream_form()) {
     // streaming form: ~TN_STREAM_WAVES (4096) waves, chunks of <= TS_MAX_CHUNK rows, nchunks % 8 == 0
     // (<= 4 blocks -- the local pass -- aim at half the waves: longer chunks, half the partials
-    // to reduce; cfg4 Gram + reduce 29.2 -> 28.4 + 7.0 -> 5.0 us per pass, 1024 / 8192 worse;
+    // to reduce; cfg4 Gram 30.1 -> 28.4 us and reduce 7.0 -> 5.0 us per pass, 1024 / 8192 worse;
     // profiles/r04_tn_small_waves.txt)
     s_chunks = ((A.count <= 4 ? TN_STREAM_WAVES / 2 : TN_STREAM_WAVES) + A.count - 1) / A.count;
     const int64_t lo = (n + TS_MAX_CHUNK - 1) / TS_MAX_CHUNK,
