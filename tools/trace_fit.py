@@ -7,7 +7,7 @@ import json
 import sys
 import time
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from node2vec2rank_amd import _lib, synthetic  # noqa: E402
 
 n, deg, d = int(sys.argv[1]), float(sys.argv[2]), int(sys.argv[3])
