@@ -943,6 +943,11 @@ struct Eig {
   // the flat-window tiled column-block SpMM (b = 8, panels beyond 8 MB): row tiles with LDS
   // accumulators walking tile_nb column-block phases, one launch per stage
   bool col_blocks = false;
+  // the final lean check's stage-1 products Z_k = A_k^T X[q] of the d wanted Ritz vectors, kept
+  // in the embedding buffer (h->Y, unscaled): they ARE the embedding's A_k^T U before the sign
+  // and sigma^-1/2 column scaling -- the same tiled launch, the same summation order -- so the
+  // embedding step skips its d/8 SpMM launches (cfg4: 16 x 0.74 ms)
+  bool y_captured = false;
   int tile_rows = 0, tile_nb = CB_NB;
   // partitioned CSR handles: stage 2 as a reduce-scatter of this rank's column share (default
   // at W > 1) instead of all-gathers of every layer's stage-1 panel (N2V2R_DIST_STAGE2=gather)
@@ -1802,6 +1807,7 @@ struct Eig {
     double t_rr = 0;
     for (;; ++cycle) {
       dbg_cycle = cycle;
+      y_captured = false;
       const int q_start = (int)Q.size();
       // (cycle 0: armed here; later cycles: the previous cycle's read-back zeroed it)
       if (lazy && cycle == 0) HIPCHK(hipMemsetAsync(h->ews.anyflag.as<int>() + 3, 0, sizeof(int), st));
@@ -2098,11 +2104,24 @@ struct Eig {
         ++lean_checks;
         const int qd = (d + b - 1) / b;
         std::vector<float*> MV(qd);
+        // one GPU, tiled SpMM, every column of the embedding covered: keep the stage-1 products
+        // (N2V2R_YCAP=0, read per fit: the embedding step computes its SpMM launches; A/B, tests)
+        const char* ycv = std::getenv("N2V2R_YCAP");
+        const bool cap = col_blocks && !h->comm && b == 8 && qd * b == ldu &&
+                         !(ycv && ycv[0] == '0');
+        if (cap) h->Y.ensure(sizeof(float) * (size_t)K * npad * ldu, st);
         for (int q = 0; q < qd; ++q) {
           MV[q] = take();
           apply_M(X[q], MV[q]);
           materialize();
+          if (cap)
+            for (int k = 0; k < K; ++k)
+              HIPCHK(hipMemcpy2DAsync(h->Y.as<float>() + (size_t)k * npad * ldu + (size_t)q * b,
+                                      sizeof(float) * ldu, h->ews.zk[k]->as<float>(),
+                                      sizeof(float) * b, sizeof(float) * b, n,
+                                      hipMemcpyDeviceToDevice, st));
         }
+        y_captured = cap;
         HIPCHK(n2v2r_launch_resid(blocks(X, 0, qd), blocks(MV, 0, qd), h->theta.as<double>(), n,
                                   h->partial.as<double>(), h->partial_elems,
                                   h->resid.as<double>(), st));
@@ -2689,7 +2708,7 @@ int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_sta
     std::vector<double> theta;
     int st = 0, b = 0;
     // the fit's tiled column-block configuration, reused for the embedding images below
-    bool ytile = false;
+    bool ytile = false, ycap = false;
     int ytile_rows = 0, ytile_nb = 0;
     for (int attempt = 0;; ++attempt) {
       Eig eig{};
@@ -2711,6 +2730,7 @@ int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_sta
       }
       b = eig.b;
       ytile = eig.col_blocks && eig.b == 8;
+      ycap = ytile && eig.y_captured;
       ytile_rows = eig.tile_rows;
       ytile_nb = eig.tile_nb;
       break;
@@ -2738,6 +2758,15 @@ int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_sta
     for (int j = 0; j < d; ++j) {
       h->sigma[j] = std::sqrt(std::max(theta[j], 0.0));
       sc[j] = h->sigma[j] > 0 ? (float)(1.0 / std::sqrt(h->sigma[j])) : 0.f;
+    }
+    if (ycap) {
+      // the captured A_k^T X come from the Ritz vectors before the sign pass: fold each column's
+      // sign (+-1, exact) into its scale
+      std::vector<float> sgn(ldu, 1.f);
+      HIPCHK(hipMemcpyAsync(sgn.data(), h->colscale.p, sizeof(float) * ldu, hipMemcpyDeviceToHost,
+                            h->stream));
+      HIPCHK(hipStreamSynchronize(h->stream));
+      for (int j = 0; j < d; ++j) sc[j] *= sgn[j];
     }
     HIPCHK(hipMemcpyAsync(h->colscale.p, sc.data(), sizeof(float) * ldu, hipMemcpyHostToDevice,
                           h->stream));
@@ -2775,7 +2804,7 @@ int n2v2r_uase(n2v2r_handle* h, int d, const n2v2r_eig_opts* opts, n2v2r_eig_sta
       a.nb = ytile_nb;
       a.sum = 0;
       a.tile_rows = ytile_rows;
-      for (int q = 0; q * 8 < ldu; ++q) {
+      for (int q = 0; !ycap && q * 8 < ldu; ++q) {
         HIPCHK(hipMemcpy2DAsync(panel.p, sizeof(float) * 8, ug + q * 8, sizeof(float) * ldu,
                                 sizeof(float) * 8, ng, hipMemcpyDeviceToDevice, h->stream));
         for (int k = 0; k < h->K; ++k) {

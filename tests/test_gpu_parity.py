@@ -529,6 +529,32 @@ def test_spmm_tiled_flat_blocks(engine, nb):
         assert np.all(np.abs(Y[rows] - ref) <= bound), (nb, tr)
 
 
+@pytest.mark.parametrize("d", [64, 128])
+def test_embedding_from_lean_check_bit_identical(engine, monkeypatch, d):
+    """With the tiled SpMM on one GPU, the final lean check's stage-1 products A_k^T X of the d
+    wanted Ritz vectors are kept as the embedding (sign and sigma^-1/2 folded into one column
+    scale) instead of d/8 more SpMM launches: the same launch and summation order, so the
+    embedding is bit-identical to the computed one (N2V2R_YCAP=0), and it matches
+    A_k^T U diag(sigma)^-1/2 in fp64 on the host."""
+    from node2vec2rank_amd import synthetic
+    layers = synthetic.er_layers(60_000, 18, 2, seed_base=23)
+    engine.set_layers(layers)
+    monkeypatch.setenv("N2V2R_SPMM_CB", "1")
+    monkeypatch.setenv("N2V2R_YCAP", "0")
+    engine.uase(d, seed=42)
+    Y0 = engine.embedding().copy()
+    monkeypatch.setenv("N2V2R_YCAP", "1")
+    st = engine.uase(d, seed=42)
+    assert st["converged"] == d and st["lean_checks"] >= 1, st
+    Y1 = engine.embedding()
+    assert np.array_equal(Y0, Y1)
+    s = engine.singular_values()
+    U = engine.left_embedding().astype(np.float64) / np.sqrt(s)[None, :]
+    for k, A in enumerate(layers):
+        ref = (A.T.astype(np.float64) @ U) / np.sqrt(s)[None, :]
+        assert np.abs(Y1[k] - ref).max() <= 1e-5 * np.abs(ref).max(), k
+
+
 @pytest.mark.parametrize("defer", ["1", "0"])
 def test_uase_paired_full_passes(engine, monkeypatch, defer):
     """Paired full passes (the default with lean images) against one full pass per block
