@@ -529,13 +529,15 @@ def test_spmm_tiled_flat_blocks(engine, nb):
         assert np.all(np.abs(Y[rows] - ref) <= bound), (nb, tr)
 
 
-@pytest.mark.parametrize("d", [64, 128])
+@pytest.mark.parametrize("d", [60, 64, 100, 128])
 def test_embedding_from_lean_check_bit_identical(engine, monkeypatch, d):
     """With the tiled SpMM on one GPU, the final lean check's stage-1 products A_k^T X of the d
     wanted Ritz vectors are kept as the embedding (sign and sigma^-1/2 folded into one column
     scale) instead of d/8 more SpMM launches: the same launch and summation order, so the
     embedding is bit-identical to the computed one (N2V2R_YCAP=0), and it matches
-    A_k^T U diag(sigma)^-1/2 in fp64 on the host."""
+    A_k^T U diag(sigma)^-1/2 in fp64 on the host.  d = 60: the last kept block runs past d (its
+    extra columns scaled by 0); d = 100: the d/8 blocks do not cover the padded width, so the
+    embedding is computed (the same bar holds either way)."""
     from node2vec2rank_amd import synthetic
     layers = synthetic.er_layers(60_000, 18, 2, seed_base=23)
     engine.set_layers(layers)
