@@ -63,7 +63,9 @@ enum { N2V2R_EIG_FULL_FIRST_PASS = 1, N2V2R_EIG_DENSE_RR = 2,
                                          accepted) */,
        N2V2R_EIG_TIME_SPMM = 16 /* HIP events around every SpMM stage launch of the fit: fills
                                    n2v2r_eig_stats.gpu_ms_spmm / spmm_timed_launches (the in-fit
-                                   roofline of bench.py; adds an event pair per launch) */ };
+                                   roofline of bench.py; adds an event pair per launch) */,
+       N2V2R_EIG_TEST_NO_STAGNATION = 64 /* tests: no stop on flat residuals (the fit runs until
+                                            every residual meets tol or max_restarts) */ };
 
 typedef struct n2v2r_handle n2v2r_handle;
 typedef struct n2v2r_simgroup n2v2r_simgroup;
@@ -93,7 +95,9 @@ typedef struct {
                                                      asynchronous GPU stages) */
   int64_t spmm_launches;     /* SpMM kernel launches (for roofline accounting) */
   double spmm_algo_bytes;    /* sum over launches of the SURVEY 8(d) algorithmic bytes */
-  int stagnated;             /* 1: stopped at the fp32 residual floor (flat 8 cycles, <= 100x tol) */
+  int stagnated;             /* 1: stopped because the residuals went flat (the fp32 floor); the
+                                fit is N2V2R_OK only if max_residual <= stag_cap, else
+                                N2V2R_ERR_NO_CONVERGENCE */
   int rr_fallbacks;          /* Rayleigh-Ritz cycles whose Sturm/inverse-iteration vectors failed
                                 the residual check and were redone by the reducing path */
   /* N2V2R_EIG_TIME_SPMM only (else 0): device time of the fit's SpMM stage launches (HIP events
@@ -110,6 +114,13 @@ typedef struct {
                                 column blocks (one launch per stage over all layers, row
                                 groups), 4 dense, 5 tiled column blocks with packed flat windows
                                 (the default tiled form) */
+  double stag_cap;           /* the largest max_residual a stagnated fit may end with and still
+                                return N2V2R_OK: 2 max(tol, sqrt(c) 2^-24), c = the basis columns
+                                (the fp32 rounding floor of a Ritz vector assembled from c of them) */
+  int y_captured;            /* 1: the embedding A_k^T U came from the final residual check's SpMM
+                                products (no separate embedding launches) */
+  int tri_fallbacks;         /* dense Rayleigh-Ritz: multi-workgroup tridiagonalisations that timed
+                                out (a workgroup not resident) and were redone on one workgroup */
 } n2v2r_eig_stats;
 
 /* lifecycle */

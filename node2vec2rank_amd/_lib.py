@@ -27,6 +27,7 @@ ERR_INTERNAL = 8
 ERR_RCCL = 9
 AGG_BORDA, AGG_NONE = 0, -1
 EIG_TIME_SPMM = 16
+EIG_TEST_NO_STAGNATION = 64
 
 STRATEGY = {"sequential": 0, "one_vs_before": 1, "one_vs_rest": 2}
 METRIC = {"cosine": 0, "euclidean": 1, "correlation": 2}
@@ -70,7 +71,8 @@ class EigStats(ctypes.Structure):
                 ("spmm_timed_launches", ctypes.c_int64 * 2),
                 ("spmm_stage_bytes", ctypes.c_double * 2), ("est_scale", ctypes.c_double),
                 ("lean_checks", ctypes.c_int), ("pool_blocks", ctypes.c_int),
-                ("spmm_form", ctypes.c_int)]
+                ("spmm_form", ctypes.c_int), ("stag_cap", ctypes.c_double),
+                ("y_captured", ctypes.c_int), ("tri_fallbacks", ctypes.c_int)]
 
     def as_dict(self):
         out = {}

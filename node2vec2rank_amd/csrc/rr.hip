@@ -1053,12 +1053,28 @@ static hipError_t launch_rr_tridiag_coop(double* A, int c, double* d, double* e,
   int* err = reinterpret_cast<int*>(ctr + 1);  // 1 after a timed-out grid barrier
   hipError_t er = hipMemsetAsync(ctr, 0, 2 * sizeof(unsigned), stream);
   if (er != hipSuccess) return er;
-  // a plain launch: PR x nt <= 4 x 24 workgroups of one CU each are resident on the 256 CUs
-  // (the cooperative launch would only add its occupancy check, +15-19 us of host time; the
-  // bounded spin ends the launch even if a workgroup were held back)
-  hipLaunchKernelGGL(rr_tridiag_coop_kernel, dim3((unsigned)(PR * nt)), dim3(TRC_NT), shmem, stream,
-                     A, c, PR, d, e, tau, V, part, rowbuf, ctr, err);
-  return hipGetLastError();
+  // The grid barrier needs all PR x nt (<= 4 x 24) workgroups resident at once: a cooperative
+  // launch, which the runtime refuses (instead of starting) when the grid cannot be co-resident
+  // (+15-19 us of host time per call, a few calls per cfg3 fit).  Should a workgroup still be
+  // held back -- another kernel of this process or another one occupying CUs -- the bounded spin
+  // ends the launch with *err set and d[0] = NaN; the engine reads *err with the cycle's
+  // read-back (n2v2r_rr_tridiag_err) and redoes the step with the one-workgroup kernel.
+  void* args[] = {&A, &c, &PR, &d, &e, &tau, &V, &part, &rowbuf, &ctr, &err};
+  er = hipLaunchCooperativeKernel((const void*)rr_tridiag_coop_kernel, dim3((unsigned)(PR * nt)),
+                                  dim3(TRC_NT), args, (unsigned)shmem, stream);
+  if (er != hipSuccess) {
+    (void)hipGetLastError();  // (a refused launch must not surface at a later one)
+    return hipErrorInvalidValue;  // the caller falls back to the one-workgroup kernel
+  }
+  return hipSuccess;
+}
+
+// the multi-workgroup tridiagonalisation's error word in its scratch: 1 after a launch whose grid
+// barrier timed out (its output is then invalid), re-armed by every launch
+extern "C" int* n2v2r_rr_tridiag_err(void* scratch, int c) {
+  double* part = static_cast<double*>(scratch);
+  unsigned* ctr = reinterpret_cast<unsigned*>(part + (size_t)2 * 4 * c + (size_t)2 * c);
+  return reinterpret_cast<int*>(ctr + 1);
 }
 
 extern "C" hipError_t n2v2r_launch_rr_tridiag(double* A, int c, double* d, double* e, double* tau,

@@ -125,6 +125,22 @@ def sbm_layers(n: int, num_layers: int, k_comm: int = 5, p_in: float = 0.2,
     return layers, comm
 
 
+def lowrank_layers(us: np.ndarray, right: list) -> list:
+    """Dense float32 layers ``A_k = us @ right[k].T`` of a rank-r two-layer network given its
+    factors (``tests/golden/make_golden.py lowrank_exact``: ``us`` = left singular vectors x
+    singular values, ``right[k]`` = layer k's rows of the right singular vectors).  The product
+    is summed term by term in float64 with elementwise numpy operations (no BLAS, no fused
+    multiply-add), so the float32 result is the same bytes on every host; the fixture stores
+    their SHA-256."""
+    out = []
+    for v in right:
+        acc = np.zeros((us.shape[0], v.shape[0]), dtype=np.float64)
+        for j in range(us.shape[1]):
+            acc = acc + np.multiply.outer(us[:, j], v[:, j])
+        out.append(np.ascontiguousarray(acc.astype(np.float32)))
+    return out
+
+
 def corr_layer(n: int, samples: int = 200, seed: int = 0) -> np.ndarray:
     """Dense co-expression layer (BASELINE cfg3): |corrcoef| of an n x samples
     Gaussian matrix drawn from ``default_rng(seed)``, fp32, symmetric, unit diagonal."""

@@ -268,6 +268,118 @@ def _envelope(fname, seeds):
     print(f"wrote {path}")
 
 
+def _rotation_design(n, rho, lam, th, ms, seed=0, iters=12):
+    """Latent rows of a two-layer network whose UASE distances are known in closed form.
+
+    Node i carries B complex coordinates z_ib = rho_b exp(1j phi_ib) (the 2-D blocks of an
+    embedding of width 2B); in layer 2 block b is rotated by lam_b theta_i.  For every prefix of
+    whole blocks, cosine = 1 - sum rho_b^2 cos(lam_b theta_i) / sum rho_b^2 and euclidean^2 =
+    sum 4 rho_b^2 sin^2(lam_b theta_i / 2): strictly increasing in theta_i on [0, pi] when
+    0 <= lam_b <= 1, so equally spaced theta gives every distance column a designed minimum gap.
+    The phases phi are solved (Gauss-Newton from phi_ib = m_b 2 pi i / n) so that the stacked
+    rows Z = [Y1; Y2] have Z^T Z block diagonal: the SVD of Z then only rotates inside each 2-D
+    block, which leaves every whole-block prefix distance unchanged.  Returns Y1, Y2, theta."""
+    rng = np.random.default_rng(seed)
+    nb = len(rho)
+    rho = np.asarray(rho, dtype=np.float64)
+    lam = np.asarray(lam, dtype=np.float64)
+    i = np.arange(n)
+    alpha = 2 * np.pi * i / n
+    theta = th[0] + (th[1] - th[0]) * (i + 0.5) / n
+    ph = np.stack([m * alpha + rng.uniform(0, 2 * np.pi) for m in ms])
+    rot = np.exp(1j * lam[:, None] * theta[None, :])
+    pairs = [(b, c) for b in range(nb) for c in range(b + 1, nb)]
+
+    def resid_jac(ph):
+        z = rho[:, None] * np.exp(1j * ph)
+        r, jac = [], []
+        for b, c in pairs:
+            # off-block Gram entries over both layers: sum z_b conj(z_c) (1 + rot_b conj(rot_c))
+            # and sum z_b z_c (1 + rot_b rot_c), as complex numbers
+            t1 = z[b] * np.conj(z[c]) * (1 + rot[b] * np.conj(rot[c]))
+            t2 = z[b] * z[c] * (1 + rot[b] * rot[c])
+            r += [t1.sum(), t2.sum()]
+            j1 = np.zeros((nb, n), complex)
+            j1[b], j1[c] = 1j * t1, -1j * t1
+            j2 = np.zeros((nb, n), complex)
+            j2[b], j2[c] = 1j * t2, 1j * t2
+            jac += [j1.ravel(), j2.ravel()]
+        r, jac = np.asarray(r), np.asarray(jac)
+        return np.concatenate([r.real, r.imag]), np.vstack([jac.real, jac.imag])
+
+    for _ in range(iters):
+        r, jac = resid_jac(ph)
+        if np.abs(r).max() < 1e-13 * n:
+            break
+        ph = ph + np.linalg.lstsq(jac, -r, rcond=None)[0].reshape(nb, n)
+    z = rho[:, None] * np.exp(1j * ph)
+    w = z * rot
+    rows = lambda c: np.stack([c.real, c.imag], axis=2).transpose(1, 0, 2).reshape(n, 2 * nb)  # noqa: E731
+    return rows(z), rows(w), theta
+
+
+def make_lowrank_exact(N2V2R):
+    """SURVEY 8(c)(4)'s end-to-end clause: integer ranks bit-exact on a tie-free fixture whose
+    sorted distance columns have every adjacent gap >= 1e-4.
+
+    Why not a sampled SBM: the distances of a random graph are random, so with N values in a
+    range L about N^2 g / L adjacent gaps fall below g (birthday bound) -- 300 seeds of a
+    4-community, 120-node SBM gave a best smallest gap of 5e-6, and N = 1-2k is hopeless.  The
+    fixture is therefore a weighted directed two-layer network (dense float32, both signs, as a
+    co-expression network) of rank 8 built from a prescribed SVD: right singular vectors from
+    _rotation_design (every node rotates, by its own angle, in layer 2: no unchanged nodes),
+    singular values 1086 .. 268 (four 2-D blocks, ratio >= 1.5 between blocks), random
+    orthonormal left vectors, nodes relabelled by a random permutation.  The reference model.py
+    runs on it unchanged; the script asserts the oracle reproduces it bit-exactly and that every
+    sorted column of the REFERENCE's distance table has adjacent gaps >= 1e-4.  Stored: the
+    factors (the test regenerates the float32 layers with synthetic.lowrank_layers and checks
+    their SHA-256), the reference's sigma, Y, distance table, column names and Borda."""
+    import hashlib
+
+    from node2vec2rank_amd import synthetic
+    from oracle import n2v2r_oracle as orc
+    n, d, seed = 2000, 8, 42
+    dims, metrics = [2, 4, 6, 8], ["cosine", "euclidean"]
+    y1, y2, theta = _rotation_design(n, (1.0, 0.8, 0.64, 0.512), (1.0, 0.5, 0.25, 0.0),
+                                     (0.4, 2.7), (1, 3, 7, 12))
+    zst = np.vstack([y1, y2])
+    p, s, _ = np.linalg.svd(zst, full_matrices=False)
+    u, _ = np.linalg.qr(np.random.default_rng(7).standard_normal((n, d)))
+    perm = np.random.default_rng(3).permutation(n)
+    us = (u * (s ** 2)[None, :])[perm]
+    right = [p[:n][perm], p[n:][perm]]
+    layers = synthetic.lowrank_layers(us, right)
+    nodes = [f"v{int(x):04d}" for x in np.random.default_rng(5).permutation(n)]
+    model, ranks, agg, _ = _run_reference(N2V2R, layers, nodes, dims, metrics, "sequential", seed)
+    Y = np.asarray(model.node_embeddings, dtype=np.float64)
+    Yo, so, _ = orc.uase([sp.csc_matrix(g) for g in layers], d, seed=seed)
+    assert np.array_equal(Yo, Y), "lowrank_exact: oracle UASE differs from reference"
+    D = ranks["1"].to_numpy(dtype=np.float64)
+    cols = list(ranks["1"].columns)
+    oc, oD = orc.rank_distances(Yo, dims, metrics, "sequential", faithful=True)["1"]
+    assert cols == oc and np.array_equal(oD, D)
+    b = agg["1"]["borda_ranks"].to_numpy(dtype=np.int64)
+    assert np.array_equal(orc.borda(D, faithful=True), b)
+    gaps = np.array([np.diff(np.sort(D[:, c])).min() for c in range(D.shape[1])])
+    print("lowrank_exact: smallest adjacent gap per column", gaps)
+    assert gaps.min() >= 1e-4, gaps
+    # the design's closed form holds (monotone in the rotation angle theta[perm])
+    o = np.argsort(theta[perm])
+    assert np.all(np.diff(D[o], axis=0) > 0)
+    assert np.array_equal(orc.borda(D, faithful=False), b)  # tie-free: any correct sort agrees
+    out = {"n": np.int64(n), "num_layers": np.int64(2), "us": us, "right0": right[0],
+           "right1": right[1],
+           "sha256": np.asarray([hashlib.sha256(a.tobytes()).hexdigest() for a in layers]),
+           "nodes": np.asarray(nodes), "dims": np.asarray(dims, dtype=np.int64),
+           "metrics": np.asarray(metrics), "strategies": np.asarray(["sequential"]),
+           "seed": np.int64(seed), "sigma": so, "Y": Y, "min_gap": gaps,
+           "sequential/keys": np.asarray(["1"]), "sequential/1/D": D,
+           "sequential/1/cols": np.asarray(cols), "sequential/1/borda": b}
+    path = os.path.join(HERE, "lowrank_exact.npz")
+    np.savez_compressed(path, **out)
+    print(f"wrote {path} ({os.path.getsize(path) / 1024:.0f} KB)")
+
+
 def make_writer(N2V2R):
     """The reference's output files (model.py:40-48 config.json, :142-145 {key}.tsv,
     :193-196 {key}_agg.tsv, :306-309 {key}_degDif.tsv, :269-278 {key}_signed.tsv and
@@ -310,7 +422,7 @@ def main():
         for name in only:
             {"er_cfg2": make_cfg2, "er_cfg2_env": make_cfg2_env,
              "er_cfg4g": make_cfg4g, "er_cfg4g_env": make_cfg4g_env,
-             "writer": make_writer}[name](N2V2R)
+             "lowrank_exact": make_lowrank_exact, "writer": make_writer}[name](N2V2R)
         return
 
     # 1. the reference's demo graphs (data/networks/demo, configs/config_demo_adj.json)

@@ -121,14 +121,33 @@ def test_cfg4_grid_vs_reference():
     m = N2V2R(layers, list(range(n)), cfg)
     ranks = m.fit_transform_rank()
     agg = m.aggregate_transform()
-    # at N = 100k, degree 50, d = 128 the fp32 floor of the true residual sits at ~1.3e-6 theta_1
-    # for the last of the 128 vectors: the fit may end at that floor (stagnated), within 5x tol
+    # at N = 100k, degree 50, d = 128 the true residual of the last of the 128 vectors stops at
+    # ~1.3e-6 theta_1: the fp32 floor of a Ritz vector assembled from c = 512 basis columns
+    # (sqrt(512) 2^-24 = 1.35e-6).  The fit may end there (stagnated) only within the engine's
+    # stated cap 2 max(tol, sqrt(c) 2^-24) = 2.7e-6; past it the fit raises.
     st = m.eig_stats
     print(f"cfg4 grid at N=100k: {st['restarts']} cycles, {st['block_applications']} block "
           f"applications, converged {st['converged']}/128, max residual "
-          f"{st['max_residual']:.3e}, stagnated {st['stagnated']}")
-    assert st["converged"] == 128 or (st["stagnated"] and st["converged"] >= 120), st
-    assert st["max_residual"] <= 5e-6, st
+          f"{st['max_residual']:.3e}, stagnated {st['stagnated']}, cap {st['stag_cap']:.3e}")
+    assert st["converged"] == 128 or (st["stagnated"] and st["max_residual"] <= st["stag_cap"]), st
+    assert abs(st["stag_cap"] - 2 * max(1e-6, np.sqrt(st["basis"]) * 2.0 ** -24)) < 1e-12, st
+    if st["stagnated"]:
+        # the floor is real, not an early stop: (1) the host's fp64 residuals of the returned
+        # vectors agree with the engine's worst one, (2) the same fit without the stagnation stop,
+        # given 12 more cycles, ends no lower
+        eng = m._engine
+        s = eng.singular_values()
+        U = eng.left_embedding() / np.sqrt(s)[None, :].astype(np.float32)
+        res = _host_residuals(layers, U, s.astype(np.float64) ** 2, range(128), threads=16)
+        from node2vec2rank_amd import _lib
+        st2 = eng.uase(128, seed=int(fx["seed"]), max_restarts=st["restarts"] + 12,
+                       solver_flags=_lib.EIG_TEST_NO_STAGNATION, raise_on_no_convergence=False)
+        print(f"cfg4 grid at N=100k: host fp64 residual max {res.max():.3e} (column "
+              f"{int(res.argmax())}); without the stagnation stop, {st2['restarts']} cycles: "
+              f"max residual {st2['max_residual']:.3e}, converged {st2['converged']}/128")
+        assert abs(res.max() - st["max_residual"]) <= 0.2 * st["max_residual"], res.max()
+        assert st2["max_residual"] >= 0.7 * st["max_residual"], st2
+        # (the handle's embedding is now the second fit's: the checks below use the frames)
     np.testing.assert_allclose(m._engine.singular_values(), fx["sigma"], rtol=2e-5)
     assert list(ranks) == ["1"] and list(agg) == ["1"]
     cols = [str(c) for c in fx["sequential/1/cols"]]

@@ -543,11 +543,14 @@ def test_embedding_from_lean_check_bit_identical(engine, monkeypatch, d):
     engine.set_layers(layers)
     monkeypatch.setenv("N2V2R_SPMM_CB", "1")
     monkeypatch.setenv("N2V2R_YCAP", "0")
-    engine.uase(d, seed=42)
+    st0 = engine.uase(d, seed=42)
+    assert st0["y_captured"] == 0, st0
     Y0 = engine.embedding().copy()
     monkeypatch.setenv("N2V2R_YCAP", "1")
     st = engine.uase(d, seed=42)
     assert st["converged"] == d and st["lean_checks"] >= 1, st
+    # the capture ran where the d/8 blocks cover the padded width (d = 60, 64, 128), not at 100
+    assert st["y_captured"] == (0 if d == 100 else 1), st
     Y1 = engine.embedding()
     assert np.array_equal(Y0, Y1)
     s = engine.singular_values()
