@@ -148,6 +148,24 @@ void n2v2r_simgroup_destroy(n2v2r_simgroup* g);
 int n2v2r_create_sim(int device, n2v2r_simgroup* g, int rank, n2v2r_handle** out);
 int n2v2r_dist_info(const n2v2r_handle* h, int* rank, int* world, int64_t* row0, int64_t* n_local);
 
+/* One process, n_gpus GPUs, through the same API as a single-GPU handle (one host
+ * thread per GPU inside the library).  The handle row-partitions every layer, Krylov block and
+ * embedding over the devices and runs each call on all of them at once; results come back
+ * global (n2v2r_get_embedding: all N rows; distances, Borda, singular values as on one GPU), so
+ * a caller switches by creating the handle with n2v2r_create_multi instead of n2v2r_create.
+ * Collectives: RCCL over the listed devices (ncclCommInitAll) when they are distinct; when a
+ * device repeats, an in-process thread group (W ranks sharing one GPU: the same partitioned
+ * algorithm, for testing on fewer devices).  n2v2r_set_layer_csr with N2V2R_SYM_YES uploads to
+ * each device only its rows; other layers are ingested whole by every device (each runs the GPU
+ * transpose and symmetry test) before keeping its rows.  n2v2r_set_layer_csr_rows and
+ * n2v2r_set_embedding are refused; n2v2r_dist_info reports (0, n_gpus, 0, N).  Every call is
+ * collective inside the library; the handle is not thread-safe (as every handle).
+ * Reference: the reference is single-process (model.py:18, 51-55); this is the same drop-in
+ * N2V2R call (node2vec2rank_amd.model.N2V2R(..., n_gpus=N)) spread over N GPUs. */
+int n2v2r_create_multi(const int* devices, int n_gpus, n2v2r_handle** out);
+/* the devices of a handle (1 for a single-GPU handle); returns the count, fills up to cap */
+int n2v2r_multi_devices(const n2v2r_handle* h, int* devices, int cap);
+
 /* graph layers: K layers over the same N nodes.  CSR is copied to HBM (int64 row pointers;
  * int32 column indices; fp32 values).  The column-index range check, the transpose (stable LSD
  * radix sort of the entries by column on the GPU) and symmetric = N2V2R_SYM_DETECT (A compared

@@ -45,6 +45,7 @@ EXPORTED = [
     "n2v2r_comm_unique_id", "n2v2r_create_rccl", "n2v2r_simgroup_create",
     "n2v2r_simgroup_destroy", "n2v2r_create_sim", "n2v2r_dist_info", "n2v2r_set_layer_csr_rows",
     "n2v2r_rr_top", "n2v2r_rr_band_top", "n2v2r_set_layer_dense", "n2v2r_project",
+    "n2v2r_create_multi", "n2v2r_multi_devices",
 ]
 UNIQUE_ID_BYTES = 128
 
@@ -152,6 +153,8 @@ def load(path: str | None = None):
                                      ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
             "n2v2r_set_layer_csr_rows": (_i, [_vp, _i, _i64, _i64, _i64, _i64, _p(np.int64),
                                               _p(np.int32), _p(np.float32)]),
+            "n2v2r_create_multi": (_i, [_p(np.int32), _i, ctypes.POINTER(_vp)]),
+            "n2v2r_multi_devices": (_i, [_vp, _vp, _i]),
         }
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
@@ -220,6 +223,23 @@ class Engine:
         if st != OK:
             raise RuntimeError(f"n2v2r_create_rccl(rank={rank}, world={world}) failed: {st}")
         return cls(device, _handle=h)
+
+    @classmethod
+    def multi(cls, devices) -> "Engine":
+        """One process, len(devices) GPUs (n2v2r_create_multi): the row-partitioned fit with one
+        host thread per GPU inside the library, RCCL over distinct devices (a repeated device:
+        the in-process thread group, W ranks sharing it).  Used exactly like a one-GPU engine;
+        embeddings, distances and Borda come back global."""
+        lib = load()
+        devs = np.ascontiguousarray([int(d) for d in devices], dtype=np.int32)
+        h = _vp()
+        st = lib.n2v2r_create_multi(devs, int(devs.size), ctypes.byref(h))
+        if st != OK:
+            raise RuntimeError(f"n2v2r_create_multi(devices={devs.tolist()}) failed with status "
+                               f"{st}" + (" (RCCL)" if st == ERR_RCCL else ""))
+        eng = cls(int(devs[0]), _handle=h)
+        eng.devices = tuple(int(d) for d in devs)
+        return eng
 
     @classmethod
     def sim(cls, device: int, group: SimGroup, rank: int) -> "Engine":
@@ -551,6 +571,13 @@ def reference_descending_order(col) -> np.ndarray:
 _default = {}
 
 
+def new_engine(device) -> Engine:
+    """An engine on one device (int) or on several (a tuple of devices: Engine.multi)."""
+    if isinstance(device, tuple):
+        return Engine.multi(device)
+    return Engine(device)
+
+
 def default_engine(device: int = 0) -> Engine:
     """Process-wide engine per device (the handle is not thread-safe)."""
     e = _default.get(device)
@@ -613,7 +640,7 @@ def acquire_engine(device: int, owner) -> Engine:
         if free:
             eng = free[0]
         elif len(handles) < POOL_MAX:
-            eng = Engine(device)
+            eng = new_engine(device)
             handles.append(eng)
         else:
             eng = min(handles, key=lambda e: getattr(e, "_tick", 0))

@@ -16,9 +16,10 @@ LIB = os.path.join(OUT_DIR, "libn2v2r_hip.so")
 OBJ_DIR = os.path.join(OUT_DIR, "obj")
 
 HIP_SOURCES = ["spmm.hip", "dense.hip", "gemm.hip", "rank.hip", "rr.hip", "rr_band.hip",
-               "rr_sturm.hip", "ingest.hip", "engine.cpp"]
+               "rr_sturm.hip", "ingest.hip", "engine.cpp", "layers.cpp", "comm.cpp",
+               "solver.cpp", "ranking.cpp", "multi.cpp"]
 HOST_SOURCES: list = []
-HEADERS = ["common.h", "spmm_args.h", os.path.join("..", "..", "include", "n2v2r.h"),
+HEADERS = ["common.h", "spmm_args.h", "engine.h", os.path.join("..", "..", "include", "n2v2r.h"),
            os.path.join("..", "..", "include", "n2v2r_diag.h")]
 ARCH = os.environ.get("N2V2R_OFFLOAD_ARCH", "gfx950")
 
@@ -41,7 +42,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(OBJ_DIR, exist_ok=True)
     hipcc = _hipcc()
     headers = [os.path.join(CSRC, h) for h in HEADERS]
-    objs = []
+    objs, cmds = [], []
     for src in HIP_SOURCES + HOST_SOURCES:
         path = os.path.join(CSRC, src)
         obj = os.path.join(OBJ_DIR, src + ".o")
@@ -54,9 +55,18 @@ def build(force: bool = False, verbose: bool = False) -> str:
                    "-munsafe-fp-atomics", "-c", path, "-o", obj]
         else:
             cmd = ["g++", "-O3", "-march=x86-64-v3", "-std=c++17", "-fPIC", "-c", path, "-o", obj]
+        cmds.append(cmd)
+    # the sources compile independently: a few hipcc processes at once
+    from concurrent.futures import ThreadPoolExecutor
+    jobs = max(1, min(8, len(cmds), os.cpu_count() or 1))
+
+    def _run(cmd):
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
+
+    with ThreadPoolExecutor(jobs) as ex:
+        list(ex.map(_run, cmds))
     if force or _newer(LIB, objs):
         # linked beside the library and renamed over it, so a reader never sees a partial file
         tmp = LIB + ".tmp"

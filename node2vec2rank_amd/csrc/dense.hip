@@ -17,6 +17,13 @@
 //           random values by fill_flagged so the next CGS pass can orthogonalise them.
 #include "common.h"
 
+// Breakdown thresholds of the Cholesky-QR passes, relative to a column's squared norm before the
+// projection: below PIP_DEFICIENT (a norm ratio of 3.2e-5, ~500 fp32 ulps) the projected column
+// is rounding noise and is refilled; below PIP_CANCEL (ratio 1e-3) the fused pass asks for the
+// cycle to be expanded again with full passes before each SpMM (dense.hip, pip_fused_kernel).
+#define PIP_DEFICIENT 1e-9
+#define PIP_CANCEL 1e-6
+
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -1524,7 +1531,8 @@ __global__ __launch_bounds__(1024) void chol_inv_kernel(const double* __restrict
 // c-long sums split over 16 k-slices and folded in fixed order), then one wave does the
 // Cholesky P = R^T R and R^{-1} (xinv, fp64 b x b).  The apply pass builds
 // F = [-C R^{-1}; R^{-1}] in LDS and writes Z <- (Z - Q C) R^{-1} in ONE pass over [Q Z].
-// Rank-deficient columns (pivot below 1e-10 max diag) get a zero xinv column and a flag.
+// Rank-deficient columns (pivot below PIP_DEFICIENT of the column's own squared norm before the
+// projection, or below 1e-10 max diag) get a zero xinv column and a flag.
 // save (optional): rows [save_row0, save_row0 + save_rows) of G copied out (the banded
 // Rayleigh-Ritz keeps the local first-pass Gram Q_loc^T W_j as its band column j).
 // fout (optional): F = [-C R^{-1}; R^{-1}] as fp32 ((c + b) x b, flagged columns zero), the
@@ -1648,6 +1656,11 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
   }
   for (int e = tid; e < bb; e += nt) X[e / b][e % b] = (e / b == e % b) ? 1.0 : 0.0;
   if (tid < 64) bad[tid] = 0;
+  // the columns' squared norms before the projection (Z^T Z's diagonal): a column whose
+  // projected pivot falls below PIP_DEFICIENT of it is numerically in span(Q) -- its fp32 apply
+  // would be rounding noise -- and is refilled
+  __shared__ double zzd[64];
+  if (tid < b) zzd[tid] = PIP_DEFICIENT * G[(int64_t)(c + tid) * b + tid];
   __syncthreads();
   if (b > 8 && bb <= nt) {
     // 8 < b <= 32: one thread per entry of the b x b matrix, the upper triangle in registers,
@@ -1666,7 +1679,7 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
     for (int k = 0; k < b; ++k) {
       // row k of R in LDS holds its values after step k - 1 (written before the barrier)
       const double d = R[k][k];
-      const bool isbad = !(d > tiny);
+      const bool isbad = !(d > fmax(tiny, zzd[k]));
       const double pk = isbad ? 1.0 : sqrt(d);
       if (own && ei == k) {
         v = isbad ? (ej == k ? 1.0 : 0.0) : (ej == k ? pk : v / pk);
@@ -1706,7 +1719,7 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
     for (int j = 0; j < b; ++j) {
       if (tid == 0) {
         const double p = R[j][j];
-        if (!(p > tiny)) {
+        if (!(p > fmax(tiny, zzd[j]))) {
           bad[j] = 1;
           piv[j] = 0.0;
         } else {
@@ -1983,14 +1996,22 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
       dmax = fmax(dmax, R[r][r]);
     }
     const double tiny = 1e-10 * dmax;
-    int bad = 0;
+    int bad = 0, cancel = 0;
     double rinv[8];
-    // right-looking Cholesky: row jj of R = row jj of the Schur complement / sqrt(pivot)
+    // right-looking Cholesky: row jj of R = row jj of the Schur complement / sqrt(pivot).  A
+    // pivot below PIP_DEFICIENT of the column's squared norm before the projection (Z^T Z's
+    // diagonal) means the column is numerically in span(Q): what the fp32 apply would leave is
+    // rounding noise, so it is refilled (flagged).  Below PIP_CANCEL the apply loses more than
+    // ~1e-4 of orthogonality to cancellation: the pass sets the sticky flag, so a lazy cycle is
+    // expanded again with every full pass before its SpMM (an exhausted Krylov space: a layer of
+    // rank below the basis, tests/test_gpu_exact.py)
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
       const double p = R[jj][jj];
-      const bool bj = !(p > tiny);
+      const double zz = gd[(c + jj) * 8 + jj];
+      const bool bj = !(p > fmax(tiny, PIP_DEFICIENT * zz));
       bad |= (int)bj << jj;
+      cancel |= (int)!(p > PIP_CANCEL * zz) << jj;
       const double r = rsq_nr(bj ? 1.0 : p);
 #pragma unroll
       for (int q = jj + 1; q < 8; ++q) R[jj][q] = bj ? 0.0 : R[jj][q] * r;
@@ -2003,13 +2024,14 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
     }
     // R (row-major, upper): Z - Q C = Z_out R; its columns' norms give the Krylov-Schur
     // residual estimates of the lean-image solver mode
+    // (a refilled column's row is zero: the projected block has no component there)
     if (rsave && lead) {
       double rij = 0.0;
 #pragma unroll
       for (int r = 0; r < 8; ++r)
 #pragma unroll
         for (int q = r; q < 8; ++q) rij = (i == r && j == q) ? R[r][q] : rij;
-      rsave[tid] = rij;
+      rsave[tid] = ((bad >> i) & 1) ? 0.0 : rij;
     }
     // column j of R^{-1} by back substitution; this lane keeps entry i
     double xv[8];
@@ -2029,7 +2051,7 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
       if (tid < 8) flags[tid] = (bad >> tid) & 1;
       if (tid == 0) {
         *any_flag = bad != 0;
-        if (bad && sticky) *sticky = 1;
+        if ((bad | cancel) && sticky) *sticky = 1;
       }
     }
   }

@@ -330,22 +330,25 @@ extern "C" hipError_t n2v2r_launch_spmm(const SpmmArgs& args_in, int B, hipStrea
 // reduce launch, 2.2 s per cfg4 step; row groups per wave, 0.807 ms per stage launch at 8
 // blocks; two row groups per step at one workgroup per CU, 0.815 ms)
 
-// Packed flat windows: a wave owns windows of CB_WIN = 32 rows of the tile; a window's
-// entries in column block p are one contiguous run of the block's index array (rows are in
-// order), so the wave walks that run 32 entries per step -- lane pair i takes entry i, reads its
-// packed word (row in window, column in block), gathers the 32-B panel row as two 16-B halves
-// and stages weight x row in a 1-KB per-wave LDS slot; then lane pair r (owner of window row r)
-// adds the staged entries of its row in entry order to a register accumulator, and after the
-// window's last step adds that to the row's LDS accumulator.  Every lane gathers an entry
-// whatever the row lengths are (the row-group form idles the lanes of short rows: a block row
-// averages 6 entries at cfg4, the longest of a 16-row group ~12), and a window reads its row
-// pointers with one load.  No atomics: one wave owns each window, so every sum has a fixed
-// order (per row: layer, block, entry).  Index words and gathers of up to 4 steps are issued as
-// one batch.  (A first form added every entry with ds_add_f32 into the row accumulators: 4.4 vs
-// 0.8 ms per cfg4 stage launch -- LDS float atomics on shared addresses serialise.)  Measured
-// at cfg4: 0.896 ms per stage launch with 8 column blocks (4 MB panel blocks: 31 % of the
-// gathers miss L2), 0.748 ms with 16 (2 MB blocks; the default), against 0.807 / 0.923 ms for
-// the row-group form at 8 / 16 blocks, whose rows get shorter with every block.
+// Packed flat windows: a wave owns windows of W = 2^wbits rows of the tile (32 at cfg4, 64 at
+// cfg5's sparser blocks); a window's entries in column block p are one contiguous run of the
+// block's index array (rows in order), located by two window offsets (scalar loads: the block
+// keeps no per-row pointers).  The wave walks the run 32 entries per step -- lane pair i takes
+// entry i, reads its packed word (row in window, column in block), gathers the 32-B panel row as
+// two 16-B halves and stages weight x row in a 1-KB per-wave LDS slot.  Then, per step, the first
+// lane pair of each row's segment (rows are in entry order and every entry names its row, so a
+// segment starts where the row differs from the previous entry's: one bpermute and one ballot)
+// sums the segment's staged entries in entry order and adds the sum to the row's LDS accumulator.
+// Every lane gathers an entry whatever the row lengths are.  No atomics: one wave owns each
+// window, so every sum has a fixed order (per row: layer, block, step, entry).  Index words and
+// gathers of up to 4 steps are issued as one batch.  (A first form added every entry with
+// ds_add_f32 into the row accumulators: 4.4 vs 0.8 ms per cfg4 stage launch -- LDS float atomics
+// on shared addresses serialise.  Rounds 3-4 located each row's entries by per-row block
+// pointers, [nb][N + 1] int32 read by every launch: 64 MB per cfg4 layer launch, 1.28 GB at
+// cfg5, more than the index words there.)  Measured at cfg4 (round 3, row pointers): 0.896 ms per
+// stage launch with 8 column blocks (4 MB panel blocks: 31 % of the gathers miss L2), 0.748 ms
+// with 16 (2 MB blocks; the default), against 0.807 / 0.923 ms for a row-group form at 8 / 16
+// blocks, whose rows get shorter with every block.
 // a wave-uniform pointer loaded from memory, moved to SGPRs and tagged as global: loads through
 // it become global_load with a scalar base (a flat pointer's loads count on lgkmcnt too, so
 // every wait for them would also wait for the LDS traffic)
@@ -362,16 +365,17 @@ __device__ __forceinline__ int64_t uniform_i64(int64_t v) {
          (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
 }
 
-// NS steps of 32 entries of one window: index words and gathers of all NS steps issued as
-// straight-line batches, then per step: stage, and the row owners fold their entries (the fold is
-// ~5 % of the launch at cfg4: the gathers are the cost)
+// NS steps of 32 entries of one window run: index words and gathers of all NS steps issued as
+// straight-line batches, then per step: stage, and each row segment's first lane pair folds the
+// segment into the row's accumulator (tw: the window's first row)
 template <int NS, bool UNIT, bool NT>
 __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1))) int32_t* ind,
                                            const __attribute__((address_space(1))) float* dat,
                                            int64_t beg, int off, int left,
                                            const __attribute__((address_space(1))) float* Xb,
-                                           uint32_t ldx, int32_t cmask, int pr, int sub,
-                                           int rs, int re, f32x4* stage, f32x4& acc) {
+                                           uint32_t ldx, int32_t cmask, int cbits, int lane,
+                                           f32x4* stage, f32x4* tw) {
+  const int pr = lane >> 1, sub = lane & 1;
   int wd[NS];
   float v[NS];
   f32x4 x[NS];
@@ -389,10 +393,18 @@ __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1)
 #pragma unroll
   for (int u = 0; u < NS; ++u) {
     stage[pr * 2 + sub] = v[u] * x[u];  // entries past the end are never read
-    const int s0 = off + u * 32;
-    const int lo = (rs > s0 ? rs : s0) - s0;
-    const int hi = (re < s0 + 32 ? re : s0 + 32) - s0;
-    for (int j = lo; j < hi; ++j) acc += stage[j * 2 + sub];
+    const int nval = left - u * 32;     // valid entries of this step (>= 1; may exceed 32)
+    const int ri = wd[u] >> cbits;      // row in window
+    const int rprev = __shfl(ri, lane - 2, 64);
+    const bool start = pr < nval && (pr == 0 || rprev != ri);
+    const unsigned long long m = __ballot(start);
+    if (start) {
+      const unsigned long long rest = pr == 31 ? 0ull : (m >> (2 * pr + 2));
+      const int end = rest ? pr + 1 + (__builtin_ctzll(rest) >> 1) : (nval < 32 ? nval : 32);
+      f32x4 acc = stage[pr * 2 + sub];
+      for (int j = pr + 1; j < end; ++j) acc += stage[j * 2 + sub];
+      tw[ri * 2 + sub] += acc;
+    }
   }
 }
 
@@ -405,33 +417,34 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nwave = blockDim.x >> 6;
   const int pr = lane >> 1, sub = lane & 1;
+  const int wbits = __builtin_amdgcn_readfirstlane(a.wbits);
+  const int W = 1 << wbits;
   const int64_t r0 = (int64_t)blockIdx.x * a.tile_rows;
+  const int64_t gw0 = r0 >> wbits;  // the tile's first window (tile_rows is a multiple of W)
   const int64_t rem = a.n - r0;
   const int nrows = (int)(rem < a.tile_rows ? rem : a.tile_rows);
-  const int nwin = (nrows + CB_WIN - 1) / CB_WIN;
+  const int nwin = (nrows + W - 1) >> wbits;
   const uint32_t ldx = (uint32_t)a.ldx;
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
   f32x4* tacc = reinterpret_cast<f32x4*>(tacf);
   f32x4* stage = reinterpret_cast<f32x4*>(tacf + (size_t)a.tile_rows * 8) + wave * 64;
   // zero / write back by the same window -> wave map as the adds (no barrier needed).  Measured
-  // and not kept (cfg4 layer launch 0.367 ms): windows handed out per phase from an LDS
-  // counter (0.557 ms), the next window's row pointers loaded before the current window's
-  // entries (0.367 ms, flat); 512-thread workgroups with half the tile rows, 4 per CU
-  // (0.448 ms); round 4: a wave owning one contiguous span of 4 windows walked as one run (no
-  // partial step per window; the row sums folded by a per-lane row cursor): 0.393 vs 0.368 ms,
-  // fit 1,682 vs 1,613 ms, bit-identical sums (profiles/r04_span_ab.jsonl) -- the partial steps
-  // are not what the launch waits on
-  for (int w = wave; w < nwin; w += nwave) {
-    const int lr = w * CB_WIN + pr;
-    if (lr < nrows) tacc[lr * 2 + sub] = zero;
-  }
+  // and not kept (round 3-4, with per-row pointers; cfg4 layer launch 0.367 ms): windows handed
+  // out per phase from an LDS counter (0.557 ms), the next window's row pointers loaded before
+  // the current window's entries (flat); 512-thread workgroups with half the tile rows, 4 per CU
+  // (0.448 ms); a wave owning one contiguous span of 4 windows walked as one run: 0.393 ms
+  for (int w = wave; w < nwin; w += nwave)
+    for (int rr = pr; rr < W; rr += 32) {
+      const int lr = (w << wbits) + rr;
+      if (lr < nrows) tacc[lr * 2 + sub] = zero;
+    }
   for (int k = 0; k < a.K; ++k) {
     const float* X = a.X[k];
     for (int p = 0; p < a.nb; ++p) {
       const CsrBlk& A = a.blk[k * a.nb + p];
       const int cbits = __builtin_amdgcn_readfirstlane(A.cbits);
       const int unit = __builtin_amdgcn_readfirstlane(A.unit);
-      const auto rp = uniform_global(A.rp);
+      const auto wo = uniform_global(A.wo);
       const auto ind = uniform_global(A.indices);
       const auto dat = uniform_global(A.data);
       const int64_t base = uniform_i64(A.base);
@@ -439,28 +452,21 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
       const int32_t cmask = (1 << cbits) - 1;
       const auto Xb = uniform_global(X + col0 * a.ldx);
       for (int w = wave; w < nwin; w += nwave) {
-        const int wr = w * CB_WIN;
-        const int we = wr + CB_WIN < nrows ? wr + CB_WIN : nrows;
-        // the window's row boundaries: lane pair r holds rows wr + r's [rs, re)
-        const int rr = wr + pr < we ? wr + pr : we;
-        const int32_t ps = rp[r0 + rr];
-        const int32_t pe = rp[r0 + (wr + pr < we ? wr + pr + 1 : we)];
-        const int32_t e0 = __builtin_amdgcn_readfirstlane(ps);
-        const int len = __builtin_amdgcn_readlane(pe, 2 * (we - wr - 1)) - e0;
-        const int rs = ps - e0, re = pe - e0;
+        const int32_t e0 = wo[gw0 + w];
+        const int len = wo[gw0 + w + 1] - e0;
         const int64_t beg = base + e0;
-        f32x4 acc = zero;
+        f32x4* tw = tacc + ((size_t)w << wbits) * 2;
 #define FLAT_STEPS(U)                                                                          \
   for (int off = 0; off < len; off += 128) {                                                   \
     const int left = len - off;                                                                \
     if (left > 96)                                                                             \
-      flat_steps<4, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+      flat_steps<4, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, cbits, lane, stage, tw);  \
     else if (left > 64)                                                                        \
-      flat_steps<3, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+      flat_steps<3, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, cbits, lane, stage, tw);  \
     else if (left > 32)                                                                        \
-      flat_steps<2, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+      flat_steps<2, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, cbits, lane, stage, tw);  \
     else                                                                                       \
-      flat_steps<1, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, pr, sub, rs, re, stage, acc); \
+      flat_steps<1, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, cbits, lane, stage, tw);  \
   }
         if (unit) {
           FLAT_STEPS(true)
@@ -468,7 +474,6 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
           FLAT_STEPS(false)
         }
 #undef FLAT_STEPS
-        if (wr + pr < we) tacc[(wr + pr) * 2 + sub] += acc;
       }
       // the workgroup's waves move to the next panel block together.  (No barrier: 0.57 vs
       // 0.36 ms per cfg4 layer launch; a bounded skew -- a wave starts phase g once all have
@@ -478,29 +483,36 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
     }
     if (!a.sum || k == a.K - 1) {
       float* Y = a.Y[a.sum ? 0 : k];
-      for (int w = wave; w < nwin; w += nwave) {
-        const int lr = w * CB_WIN + pr;
-        if (lr < nrows) {
-          *reinterpret_cast<f32x4*>(Y + (r0 + lr) * a.ldy + sub * 4) = tacc[lr * 2 + sub];
-          tacc[lr * 2 + sub] = zero;
+      for (int w = wave; w < nwin; w += nwave)
+        for (int rr = pr; rr < W; rr += 32) {
+          const int lr = (w << wbits) + rr;
+          if (lr < nrows) {
+            *reinterpret_cast<f32x4*>(Y + (r0 + lr) * a.ldy + sub * 4) = tacc[lr * 2 + sub];
+            tacc[lr * 2 + sub] = zero;
+          }
         }
-      }
     }
   }
 }
 
 // rows per tile for the tiled form: `wpc` workgroups (1024 threads each) per CU sharing its
-// 160 KB of LDS (32 B of accumulators per row); a multiple of CB_WIN (the packed windows)
-extern "C" int n2v2r_spmm_tile_rows(int64_t n, int ncu, int wpc) {
-  int64_t t = (n + wpc * (int64_t)ncu - 1) / (wpc * (int64_t)ncu);
-  t = (t + CB_WIN - 1) / CB_WIN * CB_WIN;
+// 160 KB of LDS (32 B of accumulators per row), at most 2048 (4096 at one per CU); a multiple of
+// the window rows 2^wbits.  When the rows need more than one round of resident workgroups
+// (cfg5: 10M rows, ~10 rounds), the tiles are sized so that every round is full.
+extern "C" int n2v2r_spmm_tile_rows(int64_t n, int ncu, int wpc, int wbits) {
+  const int64_t slots = wpc * (int64_t)ncu;
   const int64_t cap = (wpc == 1 ? 4096 : 2048);
-  if (t > cap) t = cap;
+  const int64_t w = (int64_t)1 << wbits;
+  const int64_t rounds = (n + slots * cap - 1) / (slots * cap);
+  int64_t t = (n + slots * rounds - 1) / (slots * rounds);
+  t = (t + w - 1) / w * w;
+  if (t > cap) t = cap / w * w;
   return (int)t;
 }
 
 extern "C" hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, hipStream_t stream) {
-  if (a.K < 1 || a.K > 8 || a.tile_rows < 16 || a.n <= 0 || a.tile_rows % CB_WIN != 0)
+  if (a.K < 1 || a.K > 8 || a.n <= 0 || a.wbits < CB_WIN_BITS_MIN || a.wbits > CB_WIN_BITS_MAX ||
+      a.tile_rows < (1 << a.wbits) || a.tile_rows % (1 << a.wbits) != 0)
     return hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.n + a.tile_rows - 1) / a.tile_rows);
   // 32 B of accumulators per row + a 1-KB staging slot per wave
@@ -540,10 +552,11 @@ __global__ void cb_count_kernel(CsrDev A, int64_t cw, int32_t* __restrict__ cnt)
 
 // step 2 (after the host scan): scatter each row's entries to rp[j][r] + running count,
 // keeping their order inside the row.
-// cbits > 0: packed entries ((r % CB_WIN) << cbits | (col - block start)) for the flat form.
+// cbits > 0: packed entries ((r % 2^wbits) << cbits | (col - block start)) for the flat form.
 template <int NB>
 __global__ void cb_fill_kernel(CsrDev A, int64_t cw, const int64_t* __restrict__ rp,
-                               int32_t* __restrict__ idx, float* __restrict__ dat, int cbits) {
+                               int32_t* __restrict__ idx, float* __restrict__ dat, int cbits,
+                               int wbits) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= A.n_rows) return;
   int64_t pos[NB];
@@ -556,15 +569,17 @@ __global__ void cb_fill_kernel(CsrDev A, int64_t cw, const int64_t* __restrict__
 #pragma unroll
     for (int j = 0; j < NB; ++j)
       if (jb == j) q = pos[j]++;
-    idx[q] = cbits ? (int32_t)(((r % CB_WIN) << cbits) | (col - (int64_t)jb * cw)) : col;
+    idx[q] = cbits ? (int32_t)(((r & ((1 << wbits) - 1)) << cbits) | (col - (int64_t)jb * cw))
+                   : col;
     if (!A.unit) dat[q] = A.data[p];
   }
 }
 
 // Row pointers of the column blocks from the counts, on the GPU: an exclusive scan of the
 // counts flattened block-major (cnt[j][r]) gives every entry's absolute position in the
-// block-major entry array, rp[j][r] (int64, [nb][n + 1]); rp[j][n] = rp[j + 1][0] (nnz for the
-// last block); rp32[j][r] = rp[j][r] - rp[j][0] (int32, relative to the block's base).
+// block-major entry array, rp[j][r] (int64, [nb][n + 1], a build temporary); rp[j][n] =
+// rp[j + 1][0] (nnz for the last block).  What the blocks keep: the window offsets
+// wo[j][w] = rp[j][min(w 2^wbits, n)] - rp[j][0] (int32, [nb][ceil(n / 2^wbits) + 1]).
 #define SCAN_T 256
 #define SCAN_IT 8
 #define SCAN_TILE (SCAN_T * SCAN_IT)
@@ -650,21 +665,26 @@ __global__ __launch_bounds__(SCAN_T) void scan_tile_write_kernel(const int32_t* 
   }
 }
 
-__global__ void cb_rp_finish_kernel(int64_t* __restrict__ rp, int32_t* __restrict__ rp32,
-                                    int64_t n, int nb, int64_t nnz) {
+__global__ void cb_rp_finish_kernel(int64_t* __restrict__ rp, int64_t n, int nb, int64_t nnz) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nb) return;
+  rp[j * (n + 1) + n] = j + 1 < nb ? rp[(j + 1) * (n + 1)] : nnz;
+}
+
+__global__ void cb_wo_kernel(const int64_t* __restrict__ rp, int64_t n, int nb, int wbits,
+                             int64_t nnz, int32_t* __restrict__ wo) {
+  const int64_t nw1 = ((n + (1 << wbits) - 1) >> wbits) + 1;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (int64_t)nb * (n + 1)) return;
-  const int64_t j = e / (n + 1), r = e - j * (n + 1);
-  int64_t v;
-  if (r == n) v = j + 1 < nb ? rp[(j + 1) * (n + 1)] : nnz;
-  else v = rp[e];
-  if (r == n) rp[e] = v;
-  rp32[e] = (int32_t)(v - rp[j * (n + 1)]);
+  if (e >= (int64_t)nb * nw1) return;
+  const int64_t j = e / nw1, w = e - j * nw1;
+  const int64_t r = (w << wbits) < n ? (w << wbits) : n;
+  const int64_t v = r == n ? (j + 1 < nb ? rp[(j + 1) * (n + 1)] : nnz) : rp[j * (n + 1) + r];
+  wo[e] = (int32_t)(v - rp[j * (n + 1)]);
 }
 
 extern "C" hipError_t n2v2r_launch_cb_rowptrs(const int32_t* cnt, int64_t n, int nb, int64_t nnz,
                                               int64_t* tsum, size_t tsum_elems, int64_t* rp,
-                                              int32_t* rp32, hipStream_t stream) {
+                                              int32_t* wo, int wbits, hipStream_t stream) {
   const int64_t len = (int64_t)nb * n;
   const int64_t ntiles = (len + SCAN_TILE - 1) / SCAN_TILE;
   if (ntiles < 1 || (size_t)ntiles > tsum_elems) return hipErrorInvalidValue;
@@ -673,9 +693,11 @@ extern "C" hipError_t n2v2r_launch_cb_rowptrs(const int32_t* cnt, int64_t n, int
   hipLaunchKernelGGL(scan_tile_offsets_kernel, dim3(1), dim3(1024), 0, stream, tsum, ntiles);
   hipLaunchKernelGGL(scan_tile_write_kernel, dim3((unsigned)ntiles), dim3(SCAN_T), 0, stream, cnt,
                      n, nb, tsum, rp);
-  const int64_t tot = (int64_t)nb * (n + 1);
-  hipLaunchKernelGGL(cb_rp_finish_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
-                     stream, rp, rp32, n, nb, nnz);
+  hipLaunchKernelGGL(cb_rp_finish_kernel, dim3((unsigned)((nb + 63) / 64)), dim3(64), 0, stream,
+                     rp, n, nb, nnz);
+  const int64_t tot = (int64_t)nb * (((n + (1 << wbits) - 1) >> wbits) + 1);
+  hipLaunchKernelGGL(cb_wo_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, rp,
+                     n, nb, wbits, nnz, wo);
   return hipGetLastError();
 }
 
@@ -697,11 +719,11 @@ extern "C" hipError_t n2v2r_launch_cb_count(const CsrDev& A, int64_t cw, int nb,
 }
 
 extern "C" hipError_t n2v2r_launch_cb_fill(const CsrDev& A, int64_t cw, int nb, const int64_t* rp,
-                                           int32_t* idx, float* dat, int cbits,
+                                           int32_t* idx, float* dat, int cbits, int wbits,
                                            hipStream_t stream) {
   if (A.n_rows <= 0) return hipSuccess;
   const dim3 g((unsigned)((A.n_rows + 255) / 256));
-#define FILL(NB) hipLaunchKernelGGL(cb_fill_kernel<NB>, g, dim3(256), 0, stream, A, cw, rp, idx, dat, cbits)
+#define FILL(NB) hipLaunchKernelGGL(cb_fill_kernel<NB>, g, dim3(256), 0, stream, A, cw, rp, idx, dat, cbits, wbits)
   if (nb == 4) FILL(4);
   else if (nb == 8) FILL(8);
   else if (nb == 16) FILL(16);

@@ -25,23 +25,24 @@ struct SpmmArgs {
 // ---- column blocks (b = 8 panels beyond 8 MB: the flat-window tiled SpMM) --------------------
 #define CB_NB 8      // default column blocks when a caller names none (the fit picks 4-32)
 #define CB_MAX 64    // column blocks per layer at most (N2V2R_SPMM_TILE_NB)
-#define CB_WIN 32    // rows per window of the packed tiled form (row-in-window: 5 index bits)
-#define CB_WIN_BITS 5
+#define CB_WIN_BITS_MIN 5  // windows of 2^wbits rows: 32 ..
+#define CB_WIN_BITS_MAX 7  //                          .. 128 (row-in-window bits of a packed entry)
 
-// One column block: int32 row pointers relative to `base` (the block's first entry in the
-// shared index / value arrays; half the row-pointer bytes of int64).  cbits = 0: `indices`
-// hold global column indices.  cbits > 0 (packed): entry = (row % CB_WIN) << cbits | (column -
-// col0), so a wave walking a window of CB_WIN rows reads its entries as one flat run and each
-// entry names its own row.
+// One column block of a layer, packed for the flat tiled form: entry = (row % W) << cbits |
+// (column - col0), W = 2^wbits rows per window, in the layer's shared index array starting at
+// `base`.  The rows of a window have their entries in this block as ONE contiguous run (rows in
+// order), so the block keeps no per-row pointers: wo[w] .. wo[w + 1] (relative to base) is
+// window w's run, and each entry names its own row.  (Round 4 kept int32 row pointers
+// [n_rows + 1] per block: 4 MB per block at cfg4 and 40 MB at cfg5 read by every launch.)
 struct CsrBlk {
-  const int32_t* rp;       // n_rows + 1
+  const int32_t* wo;       // ceil(n_rows / W) + 1 window offsets, relative to base
   const int32_t* indices;  // shared by the blocks of a layer
   const float* data;       // shared (nullptr when unit)
   int64_t base;
   int64_t n_rows;
   int64_t nnz;
   int unit;
-  int cbits;               // packed column bits (0: plain global columns)
+  int cbits;               // column bits of a packed entry (the row-in-window bits sit above)
   int64_t col0;            // first column of the block
 };
 
@@ -54,5 +55,6 @@ struct SpmmTileArgs {  // row tiles x column-block phases (spmm8_flat_kernel)
   int K;
   int nb;              // column blocks (phases) per layer
   int sum;
-  int tile_rows;
+  int tile_rows;       // a multiple of the window rows 2^wbits
+  int wbits;           // window rows = 2^wbits (CB_WIN_BITS_MIN..MAX), as the blocks were packed
 };

@@ -60,7 +60,8 @@ class N2V2R:
     """``N2V2R(graphs, nodes, config)`` (reference ``model.py:18``)."""
 
     def __init__(self, graphs: list, nodes: list, config: dict, device: int = 0,
-                 eig_options: dict | None = None, tie_order: str = "reference"):
+                 eig_options: dict | None = None, tie_order: str = "reference",
+                 n_gpus: int | None = None, devices: list | None = None):
         self.config = config
         self.node_names = nodes
         self.graphs = graphs
@@ -96,8 +97,13 @@ class N2V2R:
                 json.dump(self.config, f)
 
         # one engine per device, shared by every model of the process (its allocations and
-        # solver workspace are reused across fits); the model that last loaded its layers owns it
-        self._device = device
+        # solver workspace are reused across fits); the model that last loaded its layers owns it.
+        # n_gpus / devices: one engine over several GPUs (the layers row-partitioned over them,
+        # one host thread per GPU inside the library, RCCL between them); the frames are the same
+        if devices is None and n_gpus is not None and int(n_gpus) > 1:
+            devices = list(range(int(n_gpus)))
+        self._device = tuple(int(d) for d in devices) if devices and len(devices) > 1 else (
+            int(devices[0]) if devices else device)
         if tie_order not in ("reference", "stable"):
             raise ValueError(f"unknown tie_order {tie_order!r}")
         self.tie_order = tie_order

@@ -1,0 +1,147 @@
+"""One process, N GPUs through the drop-in API (n2v2r_create_multi / N2V2R(..., devices=...)),
+SURVEY 8(b)/(e): the library row-partitions the layers over its devices and drives them with one
+host thread per GPU.  On a one-GPU box the devices repeat ([0, 0], [0, 0, 0, 0]): the same
+partitioned algorithm over the in-process thread communicator (RCCL refuses two ranks on one
+device); distinct devices take RCCL (ncclCommInitAll).  [0] alone is a one-rank RCCL
+communicator: every collective through RCCL.
+
+Checks: the frames of N2V2R(devices=...) against the reference's own outputs (er_cfg2: SURVEY
+8(c)'s bar; lowrank_exact: bit-exact integer ranks), the global embedding / distances / Borda of
+a multi engine against the partitioned ranks run by hand, host-sliced (symmetric) ingest equal
+to whole-layer ingest, and errors that leave the handle usable (reference model.py:18, 51-96,
+149-201)."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+from scipy.stats import kendalltau
+
+from conftest import load_fixture
+
+pytestmark = pytest.mark.gpu
+
+
+def _top(b, k):
+    return set(np.argsort(-np.asarray(b), kind="stable")[:k].tolist())
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0, 0]])
+def test_api_multi_cfg2_vs_reference(devices):
+    """BASELINE cfg2 (ER N = 100k, degree 20, d = 64) through N2V2R(devices=...): the frames meet
+    the bar the one-GPU API meets against the reference (test_gpu_configs.py)."""
+    from node2vec2rank_amd import synthetic
+    from node2vec2rank_amd.model import N2V2R
+    fx = load_fixture("er_cfg2")
+    n = int(fx["n"])
+    layers = synthetic.er_layers(n, float(fx["avg_deg"]), int(fx["num_layers"]),
+                                 seed_base=int(fx["seed_base"]))
+    np.testing.assert_array_equal(synthetic.fingerprint(layers), fx["checksum"])
+    cfg = dict(embed_dimensions=[int(x) for x in fx["dims"]],
+               distance_metrics=[str(x) for x in fx["metrics"]], seed=int(fx["seed"]),
+               comp_strategy="sequential", verbose=-1, save_dir=None)
+    m = N2V2R(layers, list(range(n)), cfg, devices=devices)
+    ranks = m.fit_transform_rank()
+    agg = m.aggregate_transform()
+    assert m._engine.devices == tuple(devices)
+    assert m.eig_stats["converged"] == 64, m.eig_stats
+    np.testing.assert_allclose(m._engine.singular_values(), fx["sigma"], rtol=2e-5)
+    assert list(ranks["1"].columns) == [str(c) for c in fx["sequential/1/cols"]]
+    assert list(ranks["1"].index) == list(range(n))
+    D = ranks["1"].to_numpy()
+    derr = np.abs(D - fx["sequential/1/D"]).max(axis=0)
+    env = fx["env_distance_per_col"]
+    b = agg["1"]["borda_ranks"].to_numpy()
+    ref = fx["sequential/1/borda"]
+    tau = kendalltau(b, ref).statistic
+    top = len(_top(b, 100) & _top(ref, 100))
+    print(f"cfg2 on devices {devices}: {m.eig_stats['block_applications']} block applications, "
+          f"distance err {derr} (envelope {env}), tau {tau:.6f}, top-100 {top}")
+    assert np.all(derr <= np.maximum(1e-4, env)), (derr, env)
+    assert tau >= 0.998, tau
+    assert top == 100, top
+    # the embedding comes back global (N rows per layer)
+    assert m.node_embeddings.shape == (2, n, 64)
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_api_multi_lowrank_exact_bit_exact(devices):
+    """SURVEY 8(c)(4) on the multi-GPU handle: integer ranks bit-exact with the reference's on
+    the tie-free fixture (tests/test_gpu_exact.py's bar), CSR layers."""
+    from test_oracle_golden import lowrank_exact_layers
+
+    from node2vec2rank_amd.model import N2V2R
+    fx = load_fixture("lowrank_exact")
+    layers = [sp.csr_matrix(a) for a in lowrank_exact_layers(fx)]
+    nodes = [str(x) for x in fx["nodes"]]
+    cfg = dict(embed_dimensions=[int(x) for x in fx["dims"]],
+               distance_metrics=[str(x) for x in fx["metrics"]], seed=int(fx["seed"]),
+               comp_strategy="sequential", verbose=-1, save_dir=None)
+    m = N2V2R(layers, nodes, cfg, devices=devices)
+    ranks = m.fit_transform_rank()
+    agg = m.aggregate_transform()
+    D = ranks["1"].to_numpy()
+    derr = np.abs(D - fx["sequential/1/D"]).max(axis=0)
+    exact = bool(np.array_equal(agg["1"]["borda_ranks"].to_numpy(), fx["sequential/1/borda"]))
+    print(f"lowrank_exact on devices {devices}: distance err {derr.max():.2e}, bit-exact {exact}")
+    assert np.all(derr < fx["min_gap"] / 2)
+    assert exact
+
+
+def test_multi_engine_matches_hand_run_ranks_and_ingest_forms():
+    """A multi engine over [0, 0, 0] against the same three thread ranks driven by hand
+    (test_gpu_dist.py's harness): identical singular values, distances and Borda (the same
+    partition and reduction order); the embedding and left vectors are the ranks' rows stacked;
+    whole-layer ingest (symmetry detected on every device) and host-sliced ingest
+    (symmetric = 1) give identical results; the column sums are global."""
+    from test_gpu_dist import _concat, _fit_rank, _run_ranks
+
+    from node2vec2rank_amd import _lib, synthetic
+    layers = synthetic.er_layers(20_000, 12, 2, seed_base=55)
+    dims, metrics = [4, 16], ["cosine", "euclidean"]
+    res = _run_ranks(3, _fit_rank(layers, 16, dims, metrics, "sequential", 9))
+    Y, X = _concat(res)
+    out = []
+    for sym in (_lib.SYM_DETECT, _lib.SYM_YES):
+        eng = _lib.Engine.multi([0, 0, 0])
+        try:
+            assert eng.dist_info()[:2] == (0, 3)
+            eng.set_layers(layers, symmetric=sym)
+            assert eng.dist_info() == (0, 3, 0, 20_000)
+            eng.uase(16, seed=9)
+            ncmp, _ = eng.rank("sequential", dims, metrics)
+            out.append(dict(s=eng.singular_values(), Y=eng.embedding(), X=eng.left_embedding(),
+                            D=eng.distances(0), B=eng.borda(0),
+                            cs=[eng.column_sums(k) for k in range(2)]))
+        finally:
+            eng.close()
+    for o in out:
+        np.testing.assert_array_equal(o["s"], res[0]["s"])
+        np.testing.assert_array_equal(o["Y"], Y)
+        np.testing.assert_array_equal(o["X"], X)
+        np.testing.assert_array_equal(o["D"], res[0]["D"][0])
+        np.testing.assert_array_equal(o["B"], res[0]["B"][0])
+        for k in range(2):
+            np.testing.assert_array_equal(o["cs"][k], res[0]["cs"][k])
+
+
+def test_multi_engine_errors_leave_it_usable():
+    """Arguments fail on every rank alike (no rank is left waiting in a collective): a bad
+    dimension raises ValueError, an unknown metric NotImplementedError, and the handle then fits
+    and ranks normally."""
+    from node2vec2rank_amd import _lib, synthetic
+    layers = synthetic.er_layers(5_000, 10, 2, seed_base=3)
+    eng = _lib.Engine.multi([0, 0])
+    try:
+        eng.set_layers(layers)
+        with pytest.raises(ValueError):
+            eng.uase(10_000, seed=1)
+        st = eng.uase(8, seed=1)
+        assert st["converged"] == 8
+        with pytest.raises(ValueError):
+            eng.rank("sequential", [64], ["cosine"])      # dim beyond the embedding
+        with pytest.raises(NotImplementedError):
+            eng.rank("sequential", [4], ["manhattan"])
+        ncmp, ncols = eng.rank("sequential", [4, 8], ["cosine", "euclidean"])
+        assert (ncmp, ncols) == (1, 4)
+        assert eng.distances(0).shape == (5_000, 4)
+    finally:
+        eng.close()

@@ -507,26 +507,46 @@ def test_uase_residuals_er_20k(engine):
     np.testing.assert_allclose(s, s_ref, rtol=1e-5)
 
 
-@pytest.mark.parametrize("nb", [0, 4, 32, 64])
-def test_spmm_tiled_flat_blocks(engine, nb):
-    """The flat-window tiled SpMM (b = 8) against scipy, on a directed weighted layer (A and A^T)
-    whose panel spans 4-64 column blocks (0: the fit's rule)."""
-    b = 8
+@pytest.fixture(scope="module")
+def tiled_layer():
+    """A directed weighted layer (N = 300,001) with hub rows of 5,000 entries (runs of many steps,
+    rows spanning steps) and 100 empty rows, for the tiled SpMM tests."""
     from node2vec2rank_amd import synthetic
-    n = 300_000
-    A = synthetic.er_layers(n, 12, 1, seed_base=91)[0].tocsr().astype(np.float32)
+    n = 300_001
     rng = np.random.default_rng(3)
-    A = sp.triu(A, k=1, format="csr")                      # directed
+    A = sp.triu(synthetic.er_layers(n, 12, 1, seed_base=91)[0], k=1, format="coo")
+    hubs = np.array([0, 77, 150_000, n - 1])
+    hr = np.repeat(hubs, 5000)
+    hc = np.concatenate([rng.choice(n, 5000, replace=False) for _ in hubs])
+    keep = (A.row < 1000) | (A.row >= 1100)                  # rows 1000..1099 empty
+    A = sp.coo_matrix((np.ones(keep.sum() + hr.size, np.float32),
+                       (np.concatenate([A.row[keep], hr]), np.concatenate([A.col[keep], hc]))),
+                      shape=(n, n)).tocsr()
+    A.sum_duplicates()
     A.data = rng.uniform(0.5, 2.0, A.nnz).astype(np.float32)  # weighted
+    X = rng.standard_normal((n, 8)).astype(np.float32)
+    refs = {}
+    for tr in (False, True):
+        M = (A.T if tr else A).tocsr().astype(np.float64)
+        refs[tr] = (M @ X.astype(np.float64),
+                    1e-5 * (abs(M) @ np.abs(X).astype(np.float64)) + 1e-6)
+    return A, X, refs
+
+
+@pytest.mark.parametrize("wbits", ["", "5", "6", "7"])
+@pytest.mark.parametrize("nb", [0, 4, 32, 64])
+def test_spmm_tiled_flat_blocks(engine, monkeypatch, tiled_layer, nb, wbits):
+    """The flat-window tiled SpMM (b = 8) against scipy on every row, on a directed weighted layer
+    (A and A^T) whose panel spans 4-64 column blocks (0: the fit's rule), windows of 32, 64 or
+    128 rows ("": the fit's rule), hub rows, empty rows and an odd row count."""
+    if wbits:
+        monkeypatch.setenv("N2V2R_SPMM_WBITS", wbits)
+    A, X, refs = tiled_layer
     engine.set_layers([A])
-    X = rng.standard_normal((n, b)).astype(np.float32)
-    rows = rng.choice(n, 3000, replace=False)
     for tr in (False, True):
         Y, ms = engine.bench_spmm_tiled(0, X, transpose=tr, nb=nb, reps=2)
-        M = (A.T if tr else A).tocsr()[rows].astype(np.float64)
-        ref = M @ X.astype(np.float64)
-        bound = 1e-5 * (abs(M) @ np.abs(X).astype(np.float64)) + 1e-6
-        assert np.all(np.abs(Y[rows] - ref) <= bound), (nb, tr)
+        ref, bound = refs[tr]
+        assert np.all(np.abs(Y - ref) <= bound), (nb, wbits, tr)
 
 
 @pytest.mark.parametrize("d", [60, 64, 100, 128])
