@@ -25,11 +25,16 @@ Extra keys:
     on all host cores available to the process (capped at 16, the box's CPU share), on a bounded
     sample of the same graph family; full-size CPU time extrapolated (labelled) from it.
 
-Multi-GPU (torchrun, one process per GPU): cfg1-4 run independent replicas (every rank its own
-graph through the API on its own GPU, "scaling": "weak"); cfg5 (or --mode partitioned) runs ONE
-row-partitioned graph over an RCCL communicator, every rank ingesting its own rows inside the
-timed step ("scaling": "strong").  A gloo group gives the barrier, the max-over-ranks and the
-broadcast of the RCCL unique id.
+Multi-GPU, --gpus N > 1 (cfg1-4; with or without torchrun): the headline is the SAME drop-in
+API call on ONE graph of the workload, row-partitioned over N GPUs by the library itself
+(``N2V2R(..., devices=[0..N-1])``: one host thread per GPU inside libn2v2r_hip.so, RCCL over
+the N devices), "scaling": "strong".  Under torchrun (the driver's launcher)
+rank 0 makes that call and the other ranks wait at the barriers; they then join the side legs:
+``replicas`` (every rank its own graph through the API on its own GPU, weak scaling) and
+``partitioned_per_process`` (one graph row-partitioned over one process per GPU, RCCL between
+processes).  cfg5 (or --mode partitioned) runs one row-partitioned graph with every rank
+ingesting only its own rows (one process per GPU under torchrun; the multi-GPU engine without
+it).  A gloo group gives the barrier, the max-over-ranks and the RCCL unique id broadcast.
 """
 from __future__ import annotations
 
@@ -134,10 +139,11 @@ def _config(cfg):
                 comp_strategy="sequential", verbose=-1, save_dir=None)
 
 
-def api_step(layers, nodes, cfg, device):
-    """The reference's call sequence on the drop-in API (model.py:18, 98, 149)."""
+def api_step(layers, nodes, cfg, device, devices=None):
+    """The reference's call sequence on the drop-in API (model.py:18, 98, 149); devices: the
+    same call row-partitioned over several GPUs by the library."""
     from node2vec2rank_amd.model import N2V2R
-    model = N2V2R(layers, nodes, _config(cfg), device=device)
+    model = N2V2R(layers, nodes, _config(cfg), device=device, devices=devices)
     ranks = model.fit_transform_rank()
     agg = model.aggregate_transform()
     return model, ranks, agg
@@ -246,8 +252,11 @@ def cpu_baseline(cfg, n_faithful, workers, blas_threads=1):
 
 
 # ----------------------------------------------------------------------------- roofline
-def roofline_from_stats(st, cfg, b):
-    """Dominant SpMM stage of the fit (HIP events around every launch, N2V2R_EIG_TIME_SPMM)."""
+def roofline_from_stats(st, cfg, b, nnz_launch=None, n_launch=None):
+    """Dominant SpMM stage of the fit (HIP events around every launch, N2V2R_EIG_TIME_SPMM).
+    CSR layers: achieved / frac on BASELINE.md 3's bytes (8 nnz + 4 (N + 1) + 8 N b per layer of
+    the launch: nnz_launch entries over n_launch rows); the kernel's own bytes (no value stream
+    for unweighted layers, the row pointers it reads) beside them as kernel_bytes."""
     ms = st["gpu_ms_spmm"]
     cnt = st["spmm_timed_launches"]
     by = st["spmm_stage_bytes"]
@@ -256,11 +265,24 @@ def roofline_from_stats(st, cfg, b):
         return None
     t = ms[j] / cnt[j]
     bpl = by[j] / cnt[j]
-    out = {"bound": "hbm", "achieved": round(bpl / (t * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
-           "unit": "GB/s", "frac": round(bpl / (t * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+    head = bpl
+    if nnz_launch is not None and not cfg.get("dense"):
+        head = sum(8.0 * z for z in nnz_launch) + len(nnz_launch) * (4.0 * (n_launch + 1) +
+                                                                    8.0 * n_launch * b)
+    out = {"bound": "hbm", "achieved": round(head / (t * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
+           "unit": "GB/s", "frac": round(head / (t * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
            "traffic": None, "stage": ["Z_k = A_k^T X", "W = sum_k A_k Z_k"][j],
            "avg_launch_ms": round(t, 5), "launches_in_fit": int(cnt[j]),
-           "algo_bytes_per_launch": bpl,
+           "algo_bytes_per_launch": head,
+           "algo_bytes_definition": ("BASELINE.md 3 / SURVEY 8(d): 8 nnz + 4 (N + 1) + 8 N b per "
+                                     "layer of the launch" if head is not bpl else
+                                     "4 N^2 per layer (the dense layer streamed once)"),
+           "kernel_bytes": {"bytes_per_launch": bpl,
+                            "achieved": round(bpl / (t * 1e-3) / 1e9, 1),
+                            "frac": round(bpl / (t * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                            "definition": "what the launch form streams: 4 nnz index words (+4 nnz "
+                                          "values for weighted layers) + the window offsets + "
+                                          "the panel read and the output written once"},
            "fit_spmm_gpu_ms": [round(x, 2) for x in ms], "fit_spmm_launches": [int(c) for c in cnt]}
     if cfg.get("dense"):
         flops = 2.0 * cfg["n"] * cfg["n"] * b  # one layer's GEMM per launch
@@ -273,6 +295,9 @@ def roofline_from_stats(st, cfg, b):
 
 WATCHDOG_EXIT = 3
 GATHER_CEILING_G = 182.1  # G entries/s, profiles/r04_gather_ceiling.jsonl (stream+gather, 2 MB)
+# the flat tiled SpMM's revision: a PMC traffic record (profiles/spmm_traffic.json) is attached
+# to the line only when it was collected on this revision (round 5: window offsets, segment fold)
+SPMM_KERNEL_REV = "r05-window-offsets"
 
 
 def run_guarded(fn, limit_s, on_timeout):
@@ -327,51 +352,96 @@ def strong_scaling(group, cfg, args, local, rank, world):
             "block_applications": st.get("block_applications")}
 
 
+def _local_nnz(layers, row0, nrows):
+    """Entries of rows [row0, row0 + nrows) of each CSR layer (one rank's share of a launch)."""
+    return [int(a.indptr[row0 + nrows] - a.indptr[row0]) for a in layers]
+
+
+def replicas_leg(group, cfg, args, local, rank, world):
+    """Weak scaling beside the headline (torchrun only): every rank its own graph of the family
+    through the one-GPU API on its own GPU, timed like the main loop."""
+    from node2vec2rank_amd import synthetic
+    layers = synthetic.er_layers(cfg["n"], cfg["avg_deg"], 2, seed_base=1000 + 17 * rank)
+    nodes = [f"n{i}" for i in range(cfg["n"])]
+    api_step(layers, nodes, cfg, local)  # warm-up
+    _torch_sync()
+    group.barrier()
+    t0 = time.perf_counter()
+    steps = max(1, args.steps)
+    for _ in range(steps):
+        api_step(layers, nodes, cfg, local)
+    group.barrier()
+    t = group.max(time.perf_counter() - t0) / steps
+    return {"value": round(world * cfg["n"] / t, 1), "unit": "nodes/s",
+            "ms_per_step": round(t * 1e3, 3), "scaling": "weak", "n_gpus": world, "steps": steps,
+            "graph": "every rank its own graph of the family through the one-GPU API on its own "
+                     "GPU (one process per GPU)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="cfg4", choices=sorted(CONFIGS))
-    ap.add_argument("--mode", default="auto", choices=["auto", "replicas", "partitioned"])
+    ap.add_argument("--mode", default="auto", choices=["auto", "api", "partitioned"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=0, help="faithful sample N override")
     ap.add_argument("--resident-steps", type=int, default=3)
     args = ap.parse_args()
 
     world, rank, local = _dist_env()
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world > 1 and world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world} GPUs",
+              file=sys.stderr)
+    n_gpus = world if world > 1 else max(1, args.gpus)
     group = _Group(world)
     cfg = CONFIGS[args.config]
-    mode = args.mode if args.mode != "auto" else cfg.get("mode", "replicas")
+    mode = args.mode if args.mode != "auto" else cfg.get("mode", "api")
+    if cfg.get("dense") and n_gpus > 1:
+        mode = "api"
+    devices = list(range(n_gpus)) if n_gpus > 1 else None
+    # the headline runs in this process: all of it without torchrun, rank 0's share (the whole
+    # multi-GPU API call) under torchrun; per-process partitioned runs on every rank
+    per_process = mode == "partitioned" and world > 1
+    active = per_process or rank == 0
 
     from node2vec2rank_amd import _lib, synthetic
     t_build = time.perf_counter()
     b = 32 if cfg.get("dense") else 8  # the solver's default panel width
+    eng = None
+    nnz = None
     if mode == "partitioned":
-        if world > 1:
+        if per_process:
             uid = group.bcast_bytes(_lib.comm_unique_id() if rank == 0 else None)
             eng = _lib.Engine.rccl(local, rank, world, uid)
         else:
-            eng = _lib.Engine(local)
-        eng.set_layer_rows(cfg["n"], 2, [])  # partition first
+            eng = _lib.Engine.multi(devices) if devices else _lib.Engine(local)
+        if not devices:
+            eng.set_layer_rows(cfg["n"], 2, [])  # the partition first
         _, _, row0, n_local = eng.dist_info()
-        rows = [synthetic.er_layer_rows(cfg["n"], cfg["avg_deg"], 2000 + k, row0, n_local)
-                for k in range(2)]
-        nnz = [int(group.sum(float(a.nnz))) for a in rows]
-        nodes_per_step = float(cfg["n"])  # one graph, ranked once, over all ranks
-        step = lambda: partitioned_step(eng, cfg, rows)  # noqa: E731
-    else:
+        if devices:  # one process: the global CSR, each GPU uploads its rows (symmetric)
+            rows = [synthetic.er_layer_rows(cfg["n"], cfg["avg_deg"], 2000 + k, 0, cfg["n"])
+                    for k in range(2)]
+            step = lambda: (eng.set_layers(rows, symmetric=_lib.SYM_YES),  # noqa: E731
+                            resident_step(eng, cfg))[1]
+        else:
+            rows = [synthetic.er_layer_rows(cfg["n"], cfg["avg_deg"], 2000 + k, row0, n_local)
+                    for k in range(2)]
+            step = lambda: partitioned_step(eng, cfg, rows)  # noqa: E731
+        nnz = [int(group.sum(float(a.nnz))) if per_process else int(a.nnz) for a in rows]
+    elif active:
         if cfg.get("dense"):
-            layers = synthetic.corr_layers(cfg["n"], cfg["layers"], seed_base=17 * rank)
+            layers = synthetic.corr_layers(cfg["n"], cfg["layers"], seed_base=0)
             nnz = [int(cfg["n"]) ** 2] * cfg["layers"]
         else:
-            layers = synthetic.er_layers(cfg["n"], cfg["avg_deg"], 2, seed_base=1000 + 17 * rank)
+            layers = synthetic.er_layers(cfg["n"], cfg["avg_deg"], 2, seed_base=1000)
             nnz = [int(a.nnz) for a in layers]
         nodes = [f"n{i}" for i in range(cfg["n"])]
-        nodes_per_step = group.sum(float(cfg["n"]))  # every rank ranks its own graph
-        step = lambda: api_step(layers, nodes, cfg, local)  # noqa: E731
+        step = lambda: api_step(layers, nodes, cfg, local, devices)  # noqa: E731
+    else:
+        step = lambda: None  # noqa: E731  (torchrun ranks > 0: the headline runs on rank 0)
+    nodes_per_step = float(cfg["n"])  # one graph, ranked once per step
     t_build = time.perf_counter() - t_build
 
     for _ in range(args.warmup):
@@ -386,45 +456,63 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed_max = group.max(elapsed)
     ncmp = 1  # comparisons per step (K - 1 for "sequential" with K = 2; cfg3: 3)
-    if mode == "partitioned":
-        stats = res[0]
-    else:
-        model = res[0]
-        ncmp = len(res[1])
-        stats = model.eig_stats
+    stats = None
+    if active:
+        if mode == "partitioned":
+            stats = res[0]
+        else:
+            ncmp = len(res[1])
+            stats = res[0].eig_stats
     value = nodes_per_step * ncmp * args.steps / elapsed_max
 
-    # device-resident form of the same work, and one instrumented fit for the roofline
-    if mode == "partitioned":
-        reng = eng
-    else:
-        reng = _lib.Engine(local)  # a handle of its own (the API's shared one keeps its state)
-        if cfg.get("dense"):
-            reng.set_layers(layers, storage="dense", symmetric=1)
+    # device-resident form of the same work (layers already in HBM), and one instrumented fit
+    # for the roofline (HIP events around every SpMM launch; rank 0's launches on N GPUs)
+    res_ms = None
+    roof = None
+    st_t = {}
+    if active:
+        if mode == "partitioned":
+            reng = eng
         else:
-            reng.set_layers(layers)
-    resident_step(reng, cfg)  # warm-up: the new handle's first fit allocates its workspace
-    reng.synchronize()
-    group.barrier()
-    t1 = time.perf_counter()
-    for _ in range(args.resident_steps):
-        resident_step(reng, cfg)
-    reng.synchronize()
-    group.barrier()
-    res_ms = group.max(time.perf_counter() - t1) / max(1, args.resident_steps) * 1e3
-    st_t, _ = resident_step(reng, cfg, flags=_lib.EIG_TIME_SPMM)
-    roof = roofline_from_stats(st_t, cfg, b)
+            reng = _lib.Engine.multi(devices) if devices else _lib.Engine(local)
+            if cfg.get("dense"):
+                reng.set_layers(layers, storage="dense", symmetric=1)
+            else:
+                reng.set_layers(layers)
+        if args.resident_steps > 0:
+            resident_step(reng, cfg)  # warm-up: a new handle's first fit allocates its workspace
+            reng.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(args.resident_steps):
+                resident_step(reng, cfg)
+            reng.synchronize()
+            res_ms = (time.perf_counter() - t1) / args.resident_steps * 1e3
+        st_t, _ = resident_step(reng, cfg, flags=_lib.EIG_TIME_SPMM)
+        _, _, row0, nl = reng.dist_info()
+        if devices:  # a multi engine reports rank 0's launches: rows [0, ceil(N / n_gpus))
+            nl = (cfg["n"] + n_gpus - 1) // n_gpus
+            row0 = 0
+        if cfg.get("dense"):
+            roof = roofline_from_stats(st_t, cfg, b)
+        else:
+            if mode == "partitioned" and not devices:
+                nnz_launch = [int(a.nnz) for a in rows]     # this rank's own rows
+            else:
+                nnz_launch = _local_nnz(rows if mode == "partitioned" else layers, row0, nl)
+            roof = roofline_from_stats(st_t, cfg, b, nnz_launch, nl)
+    if res_ms is not None:
+        res_ms = group.max(res_ms) if per_process else res_ms
     if roof is not None and not cfg.get("dense"):
         form = int(st_t.get("spmm_form", 0))
         roof["kernel"] = {0: "spmm8_pipe_kernel (b = 8)",
                           1: "spmm8_pipe_kernel (b = 8, layers split over the XCDs)",
                           5: "spmm8_flat_kernel (row tiles x column-block phases, packed flat "
-                             "windows, LDS accumulators, non-temporal index stream)"
+                             "windows located by window offsets, segment fold into LDS "
+                             "accumulators, non-temporal index stream)"
                           }.get(form, str(form))
         # one 32-B panel row gathered per stored entry (served by L2 / Infinity Cache): the
         # line-access rate, reported beside the HBM roofline
-        nnz_launch = float(sum(nnz)) / (world if mode == "partitioned" else 1)
-        ent = nnz_launch
+        ent = float(sum(nnz_launch))
         roof["gathered_entries_per_launch"] = ent
         roof["gather_G_entries_per_s"] = round(ent / (roof["avg_launch_ms"] * 1e-3) / 1e9, 1)
         # the same launch against the measured gather ceiling (tools/gather_ceiling.hip, 32-B
@@ -432,43 +520,44 @@ def main():
         # profiles/r04_gather_ceiling.jsonl)
         roof["gather_ceiling_G_entries_per_s"] = GATHER_CEILING_G
         roof["gather_ceiling_frac"] = round(roof["gather_G_entries_per_s"] / GATHER_CEILING_G, 3)
-        # SURVEY 8(d)'s bytes as written (a value stream even for unweighted layers, 4-B row
-        # pointers, panel + output): 8 nnz + 4 (N + 1) + 8 N b per layer
-        n_launch = cfg["n"] / (world if mode == "partitioned" else 1)
-        lit = sum(8.0 * z / (world if mode == "partitioned" else 1) for z in nnz) + \
-            len(nnz) * (4.0 * (n_launch + 1) + 8.0 * n_launch * b)
-        roof["literal_8d"] = {"bytes_per_launch": lit,
-                              "achieved": round(lit / (roof["avg_launch_ms"] * 1e-3) / 1e9, 1),
-                              "frac": round(lit / (roof["avg_launch_ms"] * 1e-3) / 1e9
-                                            / HBM_PEAK_GBPS, 4)}
+        if n_gpus > 1:
+            roof["per_gpu"] = (f"rank 0's launches ({nl} of {cfg['n']} rows, "
+                               f"{int(sum(nnz_launch))} entries per launch)")
     tpath = os.path.join(REPO, "profiles", "spmm_traffic.json")
-    if roof is not None and os.path.exists(tpath) and world == 1:
+    if roof is not None and os.path.exists(tpath) and n_gpus == 1:
         try:
             t = json.load(open(tpath))
-            # the record must come from the same config, stage and SpMM form as this run
+            # the record must come from the same config, stage, SpMM form and kernel revision
             if (t.get("config") == args.config and t.get("stage") == roof["stage"]
-                    and t.get("spmm_form") == int(st_t.get("spmm_form", -1))):
+                    and t.get("spmm_form") == int(st_t.get("spmm_form", -1))
+                    and t.get("kernel_rev") == SPMM_KERNEL_REV):
                 roof["traffic"] = t.get("bytes_per_launch")
                 roof["traffic_source"] = t.get("source")
+                if t.get("fabric_read_requests_per_launch") is not None:
+                    roof["traffic_requests"] = t.get("fabric_read_requests_per_launch")
         except Exception:
             pass
 
     if mode == "partitioned":
-        par = f"row-partitioned x{world} (RCCL)" if world > 1 else "row-partitioned x1"
+        par = (f"row-partitioned x{n_gpus}, one process per GPU (RCCL)" if per_process else
+               f"row-partitioned x{n_gpus}, one process (RCCL over {n_gpus} devices)"
+               if devices else "row-partitioned x1")
     else:
-        par = f"replicas x{world}" if world > 1 else "single"
+        par = (f"row-partitioned x{n_gpus} by the library: N2V2R(..., devices=range({n_gpus})), "
+               f"one process, one host thread per GPU, RCCL over the devices" if devices else
+               "single GPU")
     result = {
         "metric": BASELINE_METRIC,
         "metric_detail": "nodes ranked/sec (fit_transform_rank + aggregate_transform, host CSR "
                          "in, host DataFrames out); the SpMM GB/s half is roofline.achieved",
         "value": round(value, 1),
         "unit": "nodes/s",
-        "n_gpus": world,
+        "n_gpus": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "strong" if mode == "partitioned" else "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic",
@@ -480,8 +569,6 @@ def main():
                                   if mode == "partitioned" else
                                   "host CSR -> N2V2R -> fit_transform_rank -> "
                                   "aggregate_transform -> host DataFrames (H2D included)")},
-        "device_resident": {"ms_per_step": round(res_ms, 3),
-                            "value": round(nodes_per_step * ncmp / (res_ms * 1e-3), 1)},
         "roofline": roof,
         # solver counters of the timed fit (ms_spmm / ms_ortho are host-side launch times of
         # asynchronous work, so they are left out; the device time is in roofline)
@@ -489,38 +576,38 @@ def main():
                 for k, v in (stats or {}).items() if k not in ("ms_spmm", "ms_ortho")},
         "setup_s": round(t_build, 2),
     }
-    # N > 1 replicas: the same graph family ALSO as one graph row-partitioned over every rank
-    # (RCCL all-gathers of the panels, all-reduces of the Gram / Rayleigh-Ritz / residual
-    # reductions), strong scaling -- the multi-GPU path SURVEY 8(e) describes, measured beside
-    # the weak-scaling value (N2V2R_BENCH_PARTITIONED=0 skips it).  A watchdog guards the
-    # replicas line: if the partitioned leg has not finished in N2V2R_BENCH_PARTITIONED_S
-    # seconds (default 300), rank 0 prints the line with the leg marked as timed out and every
-    # rank exits with status WATCHDOG_EXIT.
-    if (world > 1 and mode == "replicas" and not cfg.get("dense")
-            and os.environ.get("N2V2R_BENCH_PARTITIONED", "1") != "0"):
-        limit = float(os.environ.get("N2V2R_BENCH_PARTITIONED_S", "300"))
+    if res_ms is not None:
+        result["device_resident"] = {"ms_per_step": round(res_ms, 3),
+                                     "value": round(nodes_per_step * ncmp / (res_ms * 1e-3), 1)}
+    # torchrun at N > 1: side legs beside the headline, each under a watchdog (rank 0 prints the
+    # line with a leg marked as timed out and every rank exits with WATCHDOG_EXIT) --
+    # N2V2R_BENCH_SIDE=0 skips them
+    if (world > 1 and mode == "api" and not cfg.get("dense")
+            and os.environ.get("N2V2R_BENCH_SIDE", "1") != "0"):
+        limit = float(os.environ.get("N2V2R_BENCH_SIDE_S", "300"))
+        for key, fn in (("replicas", replicas_leg),
+                        ("partitioned_per_process", strong_scaling)):
+            def _expire(key=key):
+                if rank == 0:
+                    result[key] = {"error": f"timed out after {limit:g} s"}
+                    print(json.dumps(result), flush=True)
 
-        def _expire():
-            if rank == 0:
-                result["partitioned_same_family"] = {"error": f"timed out after {limit:g} s"}
-                print(json.dumps(result), flush=True)
+            def _leg(fn=fn):
+                try:
+                    return fn(group, cfg, args, local, rank, world)
+                except Exception as e:  # reported in the line; the headline stands
+                    return {"error": repr(e)[:300]}
 
-        def _leg():
-            try:
-                return strong_scaling(group, cfg, args, local, rank, world)
-            except Exception as e:  # reported in the line; the weak-scaling value stands
-                return {"error": repr(e)[:300]}
-
-        result["partitioned_same_family"] = run_guarded(_leg, limit, _expire)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            result[key] = run_guarded(_leg, limit, _expire)
+    if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
         workers = max(1, min(16, os.cpu_count() or 1))
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample or CPU_SAMPLE[args.config],
                                               workers)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if mode == "partitioned":
+    if eng is not None:
         eng.close()
-    else:
+    elif active:
         reng.close()
     group.close()
 

@@ -12,8 +12,11 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "lib")
-LIB = os.path.join(OUT_DIR, "libn2v2r_hip.so")
-OBJ_DIR = os.path.join(OUT_DIR, "obj")
+# N2V2R_BUILD_TAG=x: an experimental build beside the product library (lib/libn2v2r_hip_x.so,
+# objects in lib/obj_x), loaded only by a process that sets N2V2R_LIB to it (A/B probes)
+_TAG = os.environ.get("N2V2R_BUILD_TAG", "")
+LIB = os.path.join(OUT_DIR, f"libn2v2r_hip_{_TAG}.so" if _TAG else "libn2v2r_hip.so")
+OBJ_DIR = os.path.join(OUT_DIR, f"obj_{_TAG}" if _TAG else "obj")
 
 HIP_SOURCES = ["spmm.hip", "dense.hip", "gemm.hip", "rank.hip", "rr.hip", "rr_band.hip",
                "rr_sturm.hip", "ingest.hip", "engine.cpp", "layers.cpp", "comm.cpp",

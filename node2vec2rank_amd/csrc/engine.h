@@ -235,6 +235,12 @@ inline bool debug_finite() {
   static const bool v = env_flag("N2V2R_DEBUG_FINITE");
   return v;
 }
+// N2V2R_DEBUG_ORTHO=1: every orthogonalisation pass reports on stderr a block that leaves
+// orthonormality (its Gram against the basis and itself), with the pass's refill flags
+inline bool debug_ortho() {
+  static const bool v = env_flag("N2V2R_DEBUG_ORTHO");
+  return v;
+}
 
 // Device allocation owned by the handle (zero-filled on allocation: padded rows stay zero).
 struct DevBuf {
@@ -444,6 +450,7 @@ struct EigWorkspace {
   DevBuf rres;                                // lean images: R of the restart projection
   DevBuf skipc;                               // full passes skipped (selective reorthogonalisation)
   DevBuf tblk;                                // tiled SpMM: CsrBlk [2][K][nb] (stage 1, stage 2)
+  DevBuf xsync;                               // tiled SpMM: XCD phase counters (probe)
 };
 }  // namespace n2v2r_int
 

@@ -182,6 +182,45 @@ struct Eig {
       throw StatusFail{N2V2R_ERR_INTERNAL, msg};
     }
   }
+  // N2V2R_DEBUG_ORTHO=1 (diagnostics): the Gram of a new block against the basis and itself,
+  // reported on stderr when it is off the identity by more than 1e-3 (the block may still be
+  // waiting for its deferred full pass: then its coupling to the old blocks is expected)
+  void dbg_ortho(float* z, const std::vector<float*>& basis, const char* what,
+                 const int* flags = nullptr) {
+    if (!debug_ortho()) return;
+    std::vector<float*> all(basis);
+    all.push_back(z);
+    const int nq = (int)all.size();
+    DevBuf g;
+    g.ensure(sizeof(double) * (size_t)nq * b * b);
+    tn(blocks(all, 0, nq), one(z), g.as<double>(), nullptr);
+    std::vector<double> hg((size_t)nq * b * b);
+    HIPCHK(hipMemcpyAsync(hg.data(), g.p, sizeof(double) * hg.size(), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    double off = 0.0, self = 0.0, nrm = 0.0;
+    for (int r = 0; r < nq * b; ++r)
+      for (int j = 0; j < b; ++j) {
+        const double v = hg[(size_t)r * b + j];
+        if (r >= (nq - 1) * b) {
+          const int i = r - (nq - 1) * b;
+          self = std::max(self, std::fabs(v - (i == j ? 1.0 : 0.0)));
+          if (i == j) nrm = std::max(nrm, v);
+        } else {
+          off = std::max(off, std::fabs(v));
+        }
+      }
+    int fl[8] = {};
+    if (flags) {
+      HIPCHK(hipMemcpyAsync(fl, flags, sizeof(fl), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+    }
+    if (off > 1e-3 || self > 1e-3)
+      fprintf(stderr, "[n2v2r] %s: cycle %d, application %d, basis %d blocks: |Q^T z| %.3e, "
+              "|z^T z - I| %.3e, max z_j^T z_j %.3e%s flags %d%d%d%d%d%d%d%d\n", what,
+              dbg_cycle, dbg_apps, nq - 1, off, self, nrm, deferred == z ? " (deferred)" : "",
+              fl[0], fl[1], fl[2], fl[3], fl[4], fl[5], fl[6], fl[7]);
+  }
+
   // N2V2R_POISON: NaN-fill the scratch a fit must write before it reads it
   void poison_scratch() {
     if (!debug_poison()) return;
@@ -440,6 +479,16 @@ struct Eig {
   }
 
   // apply_M with the tiled column-block SpMM: one launch per stage over all layers
+  // N2V2R_SPMM_XSYNC=s (probe, off by default): the tiled launches align the phases of the
+  // workgroups of an XCD to a lag of s phases (spmm_args.h)
+  int xsync_skew = -1;
+  void xsync_arm(SpmmTileArgs& a, int stage) {
+    if (xsync_skew < 0) return;
+    unsigned* c = h->ews.xsync.as<unsigned>() + (size_t)stage * 8 * SPMM_MAX_LAYERS * CB_MAX;
+    HIPCHK(hipMemsetAsync(c, 0, sizeof(unsigned) * 8 * (size_t)a.K * a.nb, st));
+    a.xsync = c;
+    a.xskew = xsync_skew;
+  }
   void apply_M_tiled(const float* xg, float* Wout, int64_t ng) {
     const CsrBlk* tb = h->ews.tblk.as<CsrBlk>();
     SpmmTileArgs a{};
@@ -476,6 +525,7 @@ struct Eig {
       }
       for (int k = 0; k < K; ++k) h->gather_wait(k);
     } else {
+      xsync_arm(a, 0);
       te = tbeg();
       HIPCHK(n2v2r_launch_spmm_tile(a, st));
       tend(te, 0, b0);
@@ -483,6 +533,8 @@ struct Eig {
     SpmmTileArgs s2 = a;
     s2.blk = tb + (size_t)K * tile_nb;
     s2.sum = 1;
+    s2.xsync = nullptr;
+    if (!ovl) xsync_arm(s2, 1);
     for (int k = 0; k < K; ++k) {
       s2.X[k] = h->ews.zk[k]->as<float>();
       if (h->comm) {
@@ -574,9 +626,27 @@ struct Eig {
     // (lazy: a refill or heavy cancellation in the first pass also sets the cycle's sticky flag)
     pip_pass(Z, first, nullptr, flg, any, Zin, nsave ? save : nullptr,
              ((int)first.size() - nsave) * b, nsave * b, lazy ? any + 3 : nullptr, rsave_first);
+    if (debug_ortho()) {  // pass 1's Gram [Q Z]^T Z (still in gsm_p)
+      const int c1 = (int)first.size() * b;
+      std::vector<double> g((size_t)(c1 + b) * b);
+      HIPCHK(hipMemcpyAsync(g.data(), gsm_p, sizeof(double) * g.size(), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      fprintf(stderr, "[n2v2r] pass 1 Gram (c %d): Z^T Z diag", c1);
+      for (int j = 0; j < b; ++j) fprintf(stderr, " %.4e", g[(size_t)(c1 + j) * b + j]);
+      fprintf(stderr, "; C^T C diag");
+      for (int j = 0; j < b; ++j) {
+        double a = 0.0;
+        for (int r = 0; r < c1; ++r) a += g[(size_t)r * b + j] * g[(size_t)r * b + j];
+        fprintf(stderr, " %.4e", a);
+      }
+      fprintf(stderr, "\n");
+    }
+    dbg_ortho(Z, first, "after pass 1 (local)", flg);
     pip_pass(Z, basis, nullptr, flg + 64, any + 1, nullptr, nullptr, 0, 0,
              lazy ? any + 3 : nullptr, nullptr, reorth_tol);
+    dbg_ortho(Z, basis, "after pass 2 (full, selective)", flg + 64);
     if (!lazy) pip_pass(Z, basis, any + 1, flg + 128, any + 2);
+    if (!lazy) dbg_ortho(Z, basis, "after pass 3", flg + 128);
     t_ortho += now_ms() - t0;
   }
 
@@ -686,6 +756,7 @@ struct Eig {
       orthonormalize(z, basis, w_from, &loc, save, lazy);  // reads W_from, writes z: no copy
     }
     dbg(z, n * b, false, "orthonormalised Krylov block");
+    dbg_ortho(z, basis, "Krylov block before its SpMM");
     float* w = take();
     apply_M(z, w);
     if (debug_finite()) materialize();
@@ -813,6 +884,13 @@ struct Eig {
         int ncu = 0;
         HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
         tile_rows = n2v2r_spmm_tile_rows(n, ncu, 2, tile_wb);
+        xsync_skew = -1;
+        if (const char* xe = std::getenv("N2V2R_SPMM_XSYNC")) {
+          // only when every workgroup is resident at once (one round of 2 per CU)
+          if ((n + tile_rows - 1) / tile_rows <= 2 * (int64_t)ncu) xsync_skew = std::atoi(xe);
+          if (xsync_skew >= 0)
+            h->ews.xsync.ensure(sizeof(unsigned) * 2 * 8 * SPMM_MAX_LAYERS * CB_MAX, st);
+        }
         const int nb = tile_nb;
         std::vector<CsrBlk> hb((size_t)2 * K * nb);
         for (int k = 0; k < K; ++k) {

@@ -63,6 +63,7 @@ def main():
     ap.add_argument("--algo-bytes", type=float, default=None)
     ap.add_argument("--stats")
     ap.add_argument("--form", type=int, default=None, help="n2v2r_eig_stats.spmm_form profiled")
+    ap.add_argument("--rev", default=None, help="kernel revision tag (bench.SPMM_KERNEL_REV)")
     a = ap.parse_args()
     rx = re.compile(a.regex)
 
@@ -116,6 +117,10 @@ def main():
             rd = fs * 2 * 1024 if fs is not None else None
             wr = ws * 1024 if ws is not None else None
             hh, hm = mean("TCC_HIT_sum"), mean("TCC_MISS_sum")
+            # one fabric read request per L2 miss, a whole 128-B line each, for wide streams
+            # and for 32-B gathers alike (profiles/r04_fabric_req_calibration.md)
+            rq = mean("TCC_EA0_RDREQ_sum")
+            rq_bytes = rq * 128 if rq is not None else None
             hit = hh / max(1.0, hh + hm) if hh is not None else None
             busy, act = mean("SQ_VALU_MFMA_BUSY_CYCLES"), mean("GRBM_GUI_ACTIVE")
             # GRBM_GUI_ACTIVE comes summed over the 8 XCDs (7.0M per 394-us cfg3 dispatch = 8 x
@@ -126,7 +131,11 @@ def main():
             print(f"| `{k}` | {ph} | {len(ts)} | {avg_ns / 1e3:.1f} | "
                   f"{fmt(rd and rd / 1e6, '{:.1f}')} | {fmt(wr and wr / 1e6, '{:.1f}')} | "
                   f"{fmt(rate, '{:.2f}')} | {fmt(hit, '{:.2f}')} | {fmt(mf, '{:.3f}')} |")
+            if rq is not None:
+                print(f"|   (fabric read requests) | {ph} | | | {rq / 1e6:.3f} M = "
+                      f"{rq_bytes / 1e6:.1f} MB | | | | |")
             out[(k, ph)] = dict(launches=len(ts), avg_ns=avg_ns, read=rd, write=wr, l2_hit=hit,
+                                rdreq=rq, rdreq_bytes=rq_bytes,
                                 mfma_busy=mf, mops_f32=mean("SQ_INSTS_VALU_MFMA_MOPS_F32"),
                                 busy_cycles=busy, gui_active=act)
     if a.json and out:
@@ -138,6 +147,19 @@ def main():
                    source=f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes ({a.dir}), "
                           "2*FETCH_SIZE+WRITE_SIZE (gfx950 correction; Infinity-Cache hits "
                           f"counted), phase 0 of {a.alternate} (stage 1 of each application)")
+        if v.get("rdreq") is not None:
+            # the calibrated fabric read traffic: TCC_EA0_RDREQ x 128 B (+ WRITE_SIZE) from a
+            # pass of its own over the same command; 2 x FETCH_SIZE kept beside it
+            rec["fabric_read_requests_per_launch"] = v["rdreq"]
+            rec["fetch_size_x2_bytes_per_launch"] = v["read"]
+            rec["read_bytes_per_launch"] = v["rdreq_bytes"]
+            rec["bytes_per_launch"] = v["rdreq_bytes"] + (v["write"] or 0)
+            rec["source"] = (f"rocprofv3 --pmc passes over the same command ({a.dir}): "
+                             "TCC_EA0_RDREQ_sum x 128 B (one 128-B fabric request per L2 miss, "
+                             "profiles/r04_fabric_req_calibration.md) + WRITE_SIZE; phase 0 of "
+                             f"{a.alternate} (stage 1 of each application)")
+        if a.rev:
+            rec["kernel_rev"] = a.rev
         if a.algo_bytes:
             rec["algo_bytes_per_launch"] = a.algo_bytes
         if a.form is not None:
