@@ -25,6 +25,8 @@ HOST_SOURCES: list = []
 HEADERS = ["common.h", "spmm_args.h", "engine.h", os.path.join("..", "..", "include", "n2v2r.h"),
            os.path.join("..", "..", "include", "n2v2r_diag.h")]
 ARCH = os.environ.get("N2V2R_OFFLOAD_ARCH", "gfx950")
+# probe builds only (with N2V2R_BUILD_TAG): extra -D flags for the HIP sources
+_EXTRA = os.environ.get("N2V2R_EXTRA_HIP_FLAGS", "").split() if _TAG else []
 
 
 def _hipcc():
@@ -55,7 +57,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if src in HIP_SOURCES:
             lang = ["-x", "hip"]
             cmd = [hipcc, *lang, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-                   "-munsafe-fp-atomics", "-c", path, "-o", obj]
+                   "-munsafe-fp-atomics", *_EXTRA, "-c", path, "-o", obj]
         else:
             cmd = ["g++", "-O3", "-march=x86-64-v3", "-std=c++17", "-fPIC", "-c", path, "-o", obj]
         cmds.append(cmd)

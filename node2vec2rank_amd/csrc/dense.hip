@@ -17,17 +17,23 @@
 //           random values by fill_flagged so the next CGS pass can orthogonalise them.
 #include "common.h"
 
-// Breakdown thresholds of the Cholesky-QR passes, relative to a column's squared norm before the
-// projection.  Below PIP_DEFICIENT (a norm ratio of 1e-3) the projected column is refilled: the
-// fp32 SpMM that made the column carries ~N eps32 of rounding relative to it when its rows sum
-// thousands of mixed-sign terms (the rank-8 lowrank_exact layers, 2000 entries per row: 1.2e-4),
-// so a column whose true residual has vanished (an exhausted Krylov space) still shows one of
-// that size, and normalising it makes a basis vector that is not orthogonal to the basis.  A
-// refilled column is a random restart direction, safe at any ratio.  Below PIP_CANCEL (ratio
-// 3.2e-3) the fused pass asks for the cycle to be expanded again with every full pass before its
-// SpMM (pip_fused_kernel, the sticky flag).
-#define PIP_DEFICIENT 1e-6
-#define PIP_CANCEL 1e-5
+// Breakdown handling of the Cholesky-QR passes.  The pivot p of column j is the squared norm of
+// Z_j - Q C_j by Pythagoras (Z_j^T Z_j - C_j^T C_j), which carries an error of ~1e-8 .. 1e-7 of
+// zz = Z_j^T Z_j (the fp32 data under the fp64 Gram, the basis's own loss of orthogonality).
+// Below PIP_CANCEL * zz (a norm ratio of 1e-3) p is not trusted: the column is scaled by the
+// clamped pivot PIP_CANCEL * zz instead (its remainder, legitimate or rounding noise, is KEPT,
+// at a norm of at most ~1), the column is marked cancelled, and the next pass -- whose Gram is
+// explicit for it -- normalises it.  A lazy cycle whose block went to its SpMM with a cancelled
+// column is expanded again with every full pass first (the sticky flag); a pass that cancels
+// asks for the pass after it (any_flag).  Refilled with random values (flagged) are only columns
+// that are zero (or not finite) before the projection.  Discarding a small but legitimate
+// remainder breaks the Krylov-Schur relation the lean images rely on (a converging Ritz vector
+// lost its residual direction for good: BASELINE cfg3 stalled at 4e-4), and normalising an
+// untrusted pivot made non-orthonormal basis vectors (an exhausted Krylov space: the rank-8
+// lowrank_exact layers, whose images of the second block are rounding noise).
+#ifndef PIP_CANCEL
+#define PIP_CANCEL 1e-6
+#endif
 
 #include <algorithm>
 #include <cstdlib>
@@ -1000,6 +1006,29 @@ extern "C" hipError_t n2v2r_launch_pair_fixup(double* g2, int nblk_all, int nq_o
   return hipGetLastError();
 }
 
+// r1 <- r2 r1 (8 x 8 fp64, row-major upper triangular): the R of two passes over one block,
+// (Z - Q C1) = Z1 R1 and (Z1 - Q C2) = Z2 R2 give Z - Q (C1 + C2 R1) = Z2 (R2 R1).  The lean
+// residual estimates read R of the restart block; a pass that clamped a pivot (PIP_CANCEL) left
+// R1 scaled, not normalised, and the second pass's R2 corrects it.  One wave.
+__global__ __launch_bounds__(64) void rmul8_kernel(const double* __restrict__ r2,
+                                                   double* __restrict__ r1) {
+  __shared__ double a[64], b[64];
+  const int tid = threadIdx.x, i = tid >> 3, j = tid & 7;
+  a[tid] = r2[tid];
+  b[tid] = r1[tid];
+  __syncthreads();
+  double v = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v += a[i * 8 + k] * b[k * 8 + j];
+  r1[tid] = v;
+}
+
+extern "C" hipError_t n2v2r_launch_rmul8(const double* r2, double* r1, hipStream_t stream) {
+  if (!r2 || !r1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rmul8_kernel, dim3(1), dim3(64), 0, stream, r2, r1);
+  return hipGetLastError();
+}
+
 // out = sum of `count` partial panels (fixed order), n x 8 fp32
 __global__ void zsum_kernel(ZSum zs, int64_t n) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one half row (16 B)
@@ -1536,8 +1565,9 @@ __global__ __launch_bounds__(1024) void chol_inv_kernel(const double* __restrict
 // c-long sums split over 16 k-slices and folded in fixed order), then one wave does the
 // Cholesky P = R^T R and R^{-1} (xinv, fp64 b x b).  The apply pass builds
 // F = [-C R^{-1}; R^{-1}] in LDS and writes Z <- (Z - Q C) R^{-1} in ONE pass over [Q Z].
-// Rank-deficient columns (pivot below PIP_DEFICIENT of the column's own squared norm before the
-// projection, or below 1e-10 max diag) get a zero xinv column and a flag.
+// Pivots below PIP_CANCEL of the column's own squared norm before the projection are clamped to
+// it (the column is scaled, not normalised: any_flag asks for the next pass); zero columns get a
+// zero xinv column and a flag (refilled).
 // save (optional): rows [save_row0, save_row0 + save_rows) of G copied out (the banded
 // Rayleigh-Ritz keeps the local first-pass Gram Q_loc^T W_j as its band column j).
 // fout (optional): F = [-C R^{-1}; R^{-1}] as fp32 ((c + b) x b, flagged columns zero), the
@@ -1547,7 +1577,8 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
                                                         int* any_flag, const int* cond,
                                                         double* __restrict__ save, int save_row0,
                                                         int save_rows, float* __restrict__ fout,
-                                                        int stage, int* sticky) {
+                                                        int stage, int* sticky,
+                                                        double* __restrict__ rsave, int first) {
   // grid.x > 1 (wide blocks, long bases): every workgroup forms P and factors it (redundant,
   // bit-identical), workgroup g writes rows [g, g + 1) * ceil((c + b) / grid.x) of F, and
   // workgroup 0 alone the other outputs
@@ -1555,6 +1586,8 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
   if (cond && *cond == 0) {
     if (lead && threadIdx.x < b) flags[threadIdx.x] = 0;
     if (lead && threadIdx.x == 0) *any_flag = 0;
+    if (rsave && lead && threadIdx.x < b * b)
+      rsave[threadIdx.x] = (int)threadIdx.x / b == (int)threadIdx.x % b ? 1.0 : 0.0;
     return;
   }
   const int fper = (c + b + gridDim.x - 1) / gridDim.x;
@@ -1661,11 +1694,18 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
   }
   for (int e = tid; e < bb; e += nt) X[e / b][e % b] = (e / b == e % b) ? 1.0 : 0.0;
   if (tid < 64) bad[tid] = 0;
-  // the columns' squared norms before the projection (Z^T Z's diagonal): a column whose
-  // projected pivot falls below PIP_DEFICIENT of it is numerically in span(Q) -- its fp32 apply
-  // would be rounding noise -- and is refilled
+  // the columns' squared norms before the projection (Z^T Z's diagonal): the pivots are clamped
+  // to PIP_CANCEL of them, and zero columns (relative to the block's largest) are refilled
   __shared__ double zzd[64];
-  if (tid < b) zzd[tid] = PIP_DEFICIENT * G[(int64_t)(c + tid) * b + tid];
+  __shared__ int canc[64];
+  if (tid < b) zzd[tid] = G[(int64_t)(c + tid) * b + tid];
+  if (tid < 64) canc[tid] = 0;
+  __syncthreads();
+  if (tid < 64) {
+    double m = (tid < b) ? zzd[tid] : 0.0;
+    for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    if (tid == 0) dmax = 1e-30 * m;  // the zero-column floor
+  }
   __syncthreads();
   if (b > 8 && bb <= nt) {
     // 8 < b <= 32: one thread per entry of the b x b matrix, the upper triangle in registers,
@@ -1673,25 +1713,25 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
     // below serialises ~b^3 / 64 dependent LDS updates: ~110 us per call at b = 32)
     const int ei = tid / b, ej = tid % b;
     const bool own = tid < bb;
-    if (tid < 64) {
-      double m = (tid < b) ? R[tid][tid] : 0.0;
-      for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
-      if (tid == 0) dmax = m;
-    }
     double v = own ? R[ei][ej] : 0.0;
-    __syncthreads();
-    const double tiny = 1e-10 * dmax;
+    const double zfloor = dmax;
     for (int k = 0; k < b; ++k) {
       // row k of R in LDS holds its values after step k - 1 (written before the barrier)
       const double d = R[k][k];
-      const bool isbad = !(d > fmax(tiny, zzd[k]));
-      const double pk = isbad ? 1.0 : sqrt(d);
-      if (own && ei == k) {
-        v = isbad ? (ej == k ? 1.0 : 0.0) : (ej == k ? pk : v / pk);
-      } else if (own && ei > k && ej >= ei && !isbad) {
+      const double zz = zzd[k];
+      const bool cn = !(d > PIP_CANCEL * zz);  // (a later pass refills: see pip_fused_kernel)
+      const bool isbad = !(zz > zfloor) || !(d == d) || (cn && !first);
+      const bool cj = !isbad && cn;
+      const double pk = isbad ? 1.0 : sqrt(cj ? PIP_CANCEL * zz : d);
+      if (own && ei == k) {  // (a clamped column is decoupled: see pip_fused_kernel)
+        v = (isbad || cj) ? (ej == k ? pk : 0.0) : (ej == k ? pk : v / pk);
+      } else if (own && ei > k && ej >= ei && !isbad && !cj) {
         v -= (R[k][ei] / pk) * (R[k][ej] / pk);
       }
-      if (tid == 0) bad[k] = isbad ? 1 : 0;
+      if (tid == 0) {
+        bad[k] = isbad ? 1 : 0;
+        canc[k] = cj ? 1 : 0;
+      }
       if (own && ei == k + 1) R[k + 1][ej] = v;  // the next pivot row (no reader this step)
       __syncthreads();
     }
@@ -1714,28 +1754,27 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
     // barrier below -- no block-wide barrier per elimination step
     const int nw = 64;
 #define PIP_WSYNC() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
-    {
-      double m = (tid < b) ? R[tid][tid] : 0.0;
-      for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
-      if (tid == 0) dmax = m;
-    }
-    PIP_WSYNC();
-    const double tiny = 1e-10 * dmax;
+    const double zfloor = dmax;
     for (int j = 0; j < b; ++j) {
       if (tid == 0) {
         const double p = R[j][j];
-        if (!(p > fmax(tiny, zzd[j]))) {
+        const double zz = zzd[j];
+        const bool cn = !(p > PIP_CANCEL * zz);
+        if (!(zz > zfloor) || !(p == p) || (cn && !first)) {
           bad[j] = 1;
           piv[j] = 0.0;
         } else {
-          piv[j] = sqrt(p);
+          const bool cj = cn;
+          canc[j] = cj ? 1 : 0;
+          piv[j] = sqrt(cj ? PIP_CANCEL * zz : p);
         }
       }
       PIP_WSYNC();
       const double pj = piv[j];
-      const int isbad = bad[j];
+      const int isbad = bad[j], iscanc = canc[j];
       for (int cc = j + tid; cc < b; cc += nw)
-        R[j][cc] = isbad ? (cc == j ? 1.0 : 0.0) : (cc == j ? pj : R[j][cc] / pj);
+        R[j][cc] = isbad ? (cc == j ? 1.0 : 0.0)
+                         : (cc == j ? pj : (iscanc ? 0.0 : R[j][cc] / pj));
       PIP_WSYNC();
       const int m = b - j - 1;
       for (int e = tid; e < m * m; e += nw) {
@@ -1761,11 +1800,13 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
     for (int e = tid; e < bb; e += nt) {
       const int r = e / b, cc = e % b;
       xinv[e] = bad[cc] ? 0.0 : X[r][cc];
+      // R (upper, row-major; a refilled column's row zero): Z - Q C = Z_out R
+      if (rsave) rsave[e] = (cc >= r && !bad[r]) ? R[r][cc] : 0.0;
     }
   if (lead && tid < b) flags[tid] = bad[tid];
   if (lead && tid == 0) {
     int any = 0;
-    for (int j = 0; j < b; ++j) any |= bad[j];
+    for (int j = 0; j < b; ++j) any |= bad[j] | canc[j];
     *any_flag = any;
     if (any && sticky) *sticky = 1;
   }
@@ -1825,14 +1866,16 @@ __global__ __launch_bounds__(1024) void pip_chol_kernel(const double* __restrict
 extern "C" hipError_t n2v2r_launch_pip_chol(const double* G, int c, int b, double* xinv,
                                             int* flags, int* any_flag, const int* cond,
                                             double* save, int save_row0, int save_rows,
-                                            float* fout, int* sticky, hipStream_t stream) {
+                                            float* fout, int* sticky, double* rsave,
+                                            int first, hipStream_t stream) {
   if (b > 64) return hipErrorInvalidValue;
   const size_t gbytes = sizeof(double) * (size_t)(c + b) * b;
   const int stage = gbytes <= 56 * 1024 ? 1 : 0;
   // wide blocks with F wanted: F's rows over up to 8 workgroups (each factors P itself)
   const int nwg = (fout && b > 8) ? std::min(8, (c + b + 127) / 128) : 1;
   hipLaunchKernelGGL(pip_chol_kernel, dim3(nwg), dim3(1024), stage ? gbytes : 0, stream, G, c, b,
-                     xinv, flags, any_flag, cond, save, save_row0, save_rows, fout, stage, sticky);
+                     xinv, flags, any_flag, cond, save, save_row0, save_rows, fout, stage, sticky,
+                     rsave, first);
   return hipGetLastError();
 }
 
@@ -1851,7 +1894,7 @@ extern "C" hipError_t n2v2r_launch_chol_inv(const double* G, int b, float* Rinv,
 // block barrier per step), then streams its 256 rows: Z <- (Z - Q C) R^{-1}, flagged columns
 // refilled by counter deviates.  Every workgroup forms the same R from the same G (the
 // factorisation is deterministic); workgroup 0 alone writes flags / any_flag / sticky / save.
-// Same pivot rule as pip_chol_kernel (pivot <= 1e-10 max diag: unit row, zero R^{-1} column).
+// Same pivot rule as pip_chol_kernel (PIP_CANCEL clamp; zero columns: unit row, zero R^{-1} column).
 // 1 / sqrt(p), p > 0: hardware estimate + two Newton steps (full fp64 precision)
 __device__ __forceinline__ double rsq_nr(double p) {
   double r = __builtin_amdgcn_rsq(p);
@@ -1872,7 +1915,7 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
                                                         int* any_flag, double* save, int save_row0,
                                                         int save_rows, int* sticky, uint64_t seed,
                                                         int64_t row0, double* rsave, float skip_tol,
-                                                        int* skipped) {
+                                                        int* skipped, int first) {
   const int tid = threadIdx.x;
   const bool lead = blockIdx.x == 0;
   if (cond && *cond == 0) {
@@ -1949,6 +1992,7 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
   if (skip_tol > 0.f) {
     if (napply == 0 && !badw[2]) {
       if (lead && tid < 8) flags[tid] = 0;
+      if (rsave && lead && tid < 64) rsave[tid] = (tid >> 3) == (tid & 7) ? 1.0 : 0.0;  // R = I
       if (lead && tid == 0) {
         *any_flag = 0;
         if (skipped) atomicAdd(skipped, 1);
@@ -1993,34 +2037,38 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
     // pivots by rsq + Newton, so no division or square root on the chain (the lane-per-entry
     // form, two fp64 shuffles and a division per step, was 2.5 us of every launch)
     double R[8][8];
-    double dmax = 0.0;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
+    for (int r = 0; r < 8; ++r)
 #pragma unroll
       for (int q = r; q < 8; ++q) R[r][q] = part[r * 8 + q];
-      dmax = fmax(dmax, R[r][r]);
-    }
-    const double tiny = 1e-10 * dmax;
+    // zero columns (relative to the block's largest) are refilled; see PIP_CANCEL
+    double zmax = 0.0;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) zmax = fmax(zmax, gd[(c + r) * 8 + r]);
+    const double zfloor = 1e-30 * zmax;
     int bad = 0, cancel = 0;
     double rinv[8];
-    // right-looking Cholesky: row jj of R = row jj of the Schur complement / sqrt(pivot).  A
-    // pivot below PIP_DEFICIENT of the column's squared norm before the projection (Z^T Z's
-    // diagonal) means the column is numerically in span(Q): what the fp32 apply would leave is
-    // rounding noise, so it is refilled (flagged).  Below PIP_CANCEL the apply loses more than
-    // ~1e-4 of orthogonality to cancellation: the pass sets the sticky flag, so a lazy cycle is
-    // expanded again with every full pass before its SpMM (an exhausted Krylov space: a layer of
-    // rank below the basis, tests/test_gpu_exact.py)
+    // right-looking Cholesky: row jj of R = row jj of the Schur complement / sqrt(pivot), the
+    // pivot clamped to PIP_CANCEL of the column's squared norm before the projection
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
       const double p = R[jj][jj];
       const double zz = gd[(c + jj) * 8 + jj];
-      const bool bj = !(p > fmax(tiny, PIP_DEFICIENT * zz));
+      // (a later pass: a cancelled column is what the first pass left of a remainder at the
+      // rounding level, or a near-copy of another column of the block -- refilled)
+      const bool cn = !(p > PIP_CANCEL * zz);
+      const bool bj = !(zz > zfloor) || !(p == p) || (cn && !first);
+      const bool cj = !bj && cn;
       bad |= (int)bj << jj;
-      cancel |= (int)!(p > PIP_CANCEL * zz) << jj;
-      const double r = rsq_nr(bj ? 1.0 : p);
+      cancel |= (int)cj << jj;
+      const double pe = bj ? 1.0 : (cj ? PIP_CANCEL * zz : p);
+      const double r = rsq_nr(pe);
+      // a clamped column is decoupled (its row's coupling entries are as untrusted as its pivot:
+      // keeping them grew R^{-1} without bound over a block of cancelled columns); the next
+      // pass orthogonalises the block's columns against each other
 #pragma unroll
-      for (int q = jj + 1; q < 8; ++q) R[jj][q] = bj ? 0.0 : R[jj][q] * r;
-      R[jj][jj] = bj ? 1.0 : p * r;
+      for (int q = jj + 1; q < 8; ++q) R[jj][q] = (bj || cj) ? 0.0 : R[jj][q] * r;
+      R[jj][jj] = bj ? 1.0 : pe * r;
       rinv[jj] = bj ? 1.0 : r;
 #pragma unroll
       for (int a = jj + 1; a < 8; ++a)
@@ -2055,7 +2103,7 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
     if (lead) {
       if (tid < 8) flags[tid] = (bad >> tid) & 1;
       if (tid == 0) {
-        *any_flag = bad != 0;
+        *any_flag = (bad | cancel) != 0;
         if ((bad | cancel) && sticky) *sticky = 1;
       }
     }
@@ -2153,7 +2201,8 @@ extern "C" hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zi
                                              int* flags, int* any_flag, double* save,
                                              int save_row0, int save_rows, int* sticky,
                                              uint64_t seed, int64_t row0, double* rsave,
-                                             float skip_tol, int* skipped, hipStream_t stream) {
+                                             float skip_tol, int* skipped, int first,
+                                             hipStream_t stream) {
   if (Q.width != 8 || c != Q.count * 8) return hipErrorInvalidValue;
   // a skipped block leaves Z in place; the band save reads G before the skipped rows are zeroed
   if (skip_tol != 0.f && (Zin != Zout || save)) return hipErrorInvalidValue;
@@ -2169,7 +2218,7 @@ extern "C" hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zi
 #define PIP_LAUNCH(QB_, NU_, NT_)                                                                \
   hipLaunchKernelGGL((pip_fused_kernel<QB_, NU_, NT_>), dim3(grid ? grid : 1), dim3(256), lds, stream, Q, \
                      Zin, Zout, G, c, n, cond, flags, any_flag, save, save_row0, save_rows, sticky,  \
-                     seed, row0, rsave, skip_tol, skipped)
+                     seed, row0, rsave, skip_tol, skipped, first)
   const bool nt = basis_nt(n, Q.count);
   if (rows == 256) {
     if (nt) PIP_LAUNCH(4, 2, true); else PIP_LAUNCH(4, 2, false);

@@ -63,7 +63,8 @@ hipError_t n2v2r_launch_ts_nn(const BlockList& A, const float* G, int ldg, int c
                               hipStream_t stream);
 hipError_t n2v2r_launch_pip_chol(const double* G, int c, int b, double* xinv, int* flags,
                                  int* any_flag, const int* cond, double* save, int save_row0,
-                                 int save_rows, float* fout, int* sticky, hipStream_t stream);
+                                 int save_rows, float* fout, int* sticky, double* rsave,
+                                 int first, hipStream_t stream);
 hipError_t n2v2r_launch_rr_band(const double* hband, int c, int kp, double* theta, double* AB,
                                 double* Varr, double* taua, double* d, double* e, double* refl,
                                 double* Y, float* S, int ldS, int p, int* err,
@@ -80,13 +81,14 @@ inline bool pip_fused() {
 hipError_t n2v2r_launch_ts_tn2(const BlockList& A, const float* Za, const float* Zb, int64_t n,
                                double* partial, size_t partial_elems, double* out,
                                hipStream_t stream);
+hipError_t n2v2r_launch_rmul8(const double* r2, double* r1, hipStream_t stream);
 hipError_t n2v2r_launch_pair_fixup(double* g2, int nblk_all, int nq_old, double* ra,
                                    hipStream_t stream);
 hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zin, float* Zout,
                                   const double* G, int c, int64_t n, const int* cond, int* flags,
                                   int* any_flag, double* save, int save_row0, int save_rows,
                                   int* sticky, uint64_t seed, int64_t row0, double* rsave,
-                                  float skip_tol, int* skipped, hipStream_t stream);
+                                  float skip_tol, int* skipped, int first, hipStream_t stream);
 hipError_t n2v2r_launch_pip_apply(const BlockList& QZ, const float* F, int c, int b,
                                   const OutBlockList& Z, int64_t n, const int* cond,
                                   const int* flags, uint64_t seed, int64_t row0,

@@ -285,6 +285,41 @@ __device__ __forceinline__ void st_sc1(double* p, double x) {
                      __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Sharded form (the default): workgroup b adds to the counter of its XCD group b % 8 (each on a
+// 128-B line of its own), and the poll reads all 8 shards at once (lane i of wave 0 shard i) until
+// each has reached its group's arrivals for this barrier: an sc1-load poll of every shard of a
+// sharded counter, the valid hand-off of MI355X_MICROARCH.md's table (first row), with 1/8 of the
+// atomic traffic on each line.  gen: this barrier's 1-based index.  true when the wait timed out.
+__device__ __forceinline__ bool trc_grid_barrier_sharded(unsigned* ctr, unsigned gen, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int G = gridDim.x;
+    const int lane = threadIdx.x;
+    if (lane == 0)
+      __hip_atomic_fetch_add(ctr + 32 * (1 + (blockIdx.x & 7)), 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    const int gl = lane & 7;
+    const unsigned want = gl < G ? gen * (unsigned)((G - gl + 7) >> 3) : 0u;
+    const unsigned* c = ctr + 32 * (1 + gl);
+    int f = 0;
+    long it = 0;
+    while (true) {
+      const unsigned v = lane < 8 ? __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                  : want;
+      if (__ballot(v < want) == 0ull) break;
+      if (++it > (1l << 24)) {
+        f = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) *flag = f;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
 // returns true when the wait timed out
 __device__ __forceinline__ bool trc_grid_barrier(unsigned* ctr, unsigned target, int* flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -309,7 +344,7 @@ __device__ __forceinline__ bool trc_grid_barrier(unsigned* ctr, unsigned target,
 __global__ __launch_bounds__(TRC_NT) void rr_tridiag_coop_kernel(
     const double* __restrict__ A, int c, int PR, double* __restrict__ dd, double* __restrict__ ee,
     double* __restrict__ tau, double* __restrict__ V, double* part /* [2][PR][c] */,
-    double* rowbuf /* [2][c] */, unsigned* ctr, int* err) {
+    double* rowbuf /* [2][c] */, unsigned* ctr, int* err, int sharded) {
   constexpr int NW = TRC_NT / 64;
   extern __shared__ double lds[];
   const int nt = (c + TRC_TS - 1) / TRC_TS;
@@ -417,7 +452,11 @@ __global__ __launch_bounds__(TRC_NT) void rr_tridiag_coop_kernel(
   double t = make_reflector(v, 1, 0);
   pass(1, false, v, 0);
   unsigned nbar = 1;
-  bool failed = trc_grid_barrier(ctr, (unsigned)G * nbar, &flag);
+  auto grid_barrier = [&](unsigned nb) {
+    return sharded ? trc_grid_barrier_sharded(ctr, nb, &flag)
+                   : trc_grid_barrier(ctr, (unsigned)G * nb, &flag);
+  };
+  bool failed = grid_barrier(nbar);
   for (int k = 0; !failed; ++k) {
     const int o = k + 1, par = k & 1;
     for (int i = o + tid; i < c; i += TRC_NT) {
@@ -453,7 +492,7 @@ __global__ __launch_bounds__(TRC_NT) void rr_tridiag_coop_kernel(
     // every read of v in the pass precedes the partials' barrier inside it
     for (int i = o + 1 + tid; i < c; i += TRC_NT) v[i] = vn[i];
     t = tn;
-    failed = trc_grid_barrier(ctr, (unsigned)G * ++nbar, &flag);
+    failed = grid_barrier(++nbar);
   }
   if (failed && tid == 0) {
     __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -461,8 +500,11 @@ __global__ __launch_bounds__(TRC_NT) void rr_tridiag_coop_kernel(
   }
 }
 
+// [2][4][c] partials | [2][c] pivot rows | counters: [0] the single counter, [1] the error
+// word, the 8 shard counters at [32 (1 + g)] (a 128-B line each)
+#define TRC_CTR_WORDS (32 * 9)
 extern "C" size_t n2v2r_rr_tridiag_scratch_bytes(int c) {
-  return sizeof(double) * ((size_t)2 * 4 * c + (size_t)2 * c) + 64;
+  return sizeof(double) * ((size_t)2 * 4 * c + (size_t)2 * c) + sizeof(unsigned) * TRC_CTR_WORDS;
 }
 
 // Y: p eigenvectors of T, column-major (vector j at Y[j * c]).  S[i * lds + j] = (P Y)[i][j],
@@ -1051,15 +1093,18 @@ static hipError_t launch_rr_tridiag_coop(double* A, int c, double* d, double* e,
   double* rowbuf = part + (size_t)2 * 4 * c;
   unsigned* ctr = reinterpret_cast<unsigned*>(rowbuf + (size_t)2 * c);
   int* err = reinterpret_cast<int*>(ctr + 1);  // 1 after a timed-out grid barrier
-  hipError_t er = hipMemsetAsync(ctr, 0, 2 * sizeof(unsigned), stream);
+  hipError_t er = hipMemsetAsync(ctr, 0, sizeof(unsigned) * TRC_CTR_WORDS, stream);
   if (er != hipSuccess) return er;
+  // the grid barrier: sharded per XCD group (default) or one counter (N2V2R_RR_TRI_BAR=single)
+  const char* bev = std::getenv("N2V2R_RR_TRI_BAR");
+  int sharded = !(bev && bev[0] == 's' && bev[1] == 'i');
   // The grid barrier needs all PR x nt (<= 4 x 24) workgroups resident at once: a cooperative
   // launch, which the runtime refuses (instead of starting) when the grid cannot be co-resident
   // (+15-19 us of host time per call, a few calls per cfg3 fit).  Should a workgroup still be
   // held back -- another kernel of this process or another one occupying CUs -- the bounded spin
   // ends the launch with *err set and d[0] = NaN; the engine reads *err with the cycle's
   // read-back (n2v2r_rr_tridiag_err) and redoes the step with the one-workgroup kernel.
-  void* args[] = {&A, &c, &PR, &d, &e, &tau, &V, &part, &rowbuf, &ctr, &err};
+  void* args[] = {&A, &c, &PR, &d, &e, &tau, &V, &part, &rowbuf, &ctr, &err, &sharded};
   er = hipLaunchCooperativeKernel((const void*)rr_tridiag_coop_kernel, dim3((unsigned)(PR * nt)),
                                   dim3(TRC_NT), args, (unsigned)shmem, stream);
   if (er != hipSuccess) {

@@ -557,7 +557,9 @@ struct Eig {
   void pip_pass(float* Z, const std::vector<float*>& basis, const int* cond, int* flags_out,
                 int* any_out, const float* Zin = nullptr, double* save = nullptr,
                 int save_row0 = 0, int save_rows = 0, int* sticky = nullptr,
-                double* rsave = nullptr, float skip_tol = 0.f) {
+                double* rsave = nullptr, float skip_tol = 0.f, bool first = false) {
+    // first: the block's first pass (a pivot the Pythagorean Gram cannot resolve is clamped and
+    // the column kept); later passes refill such columns (dense.hip, PIP_CANCEL)
     // Zin (default Z): the block to orthogonalise; the result is written to Z
     const float* zin = Zin ? Zin : Z;
     const int nq = (int)basis.size();
@@ -588,14 +590,14 @@ struct Eig {
                                     n, cond, flags_out, any_out, save, save_row0, save_rows,
                                     sticky, seed ^ (0xABCDull + ++fill_counter), row0, rsave,
                                     skip_tol, skip_tol != 0.f ? h->ews.skipc.as<int>() : nullptr,
-                                    st));
+                                    first ? 1 : 0, st));
       return;
     }
-    if (rsave) throw StatusFail{N2V2R_ERR_INTERNAL, "R output needs the fused PIP pass"};
+    if (rsave && b != 8) throw StatusFail{N2V2R_ERR_INTERNAL, "R output needs b = 8"};
     // (skip_tol: the unfused pass always applies)
     HIPCHK(n2v2r_launch_pip_chol(gsm_p, nq * b, b, h->ews.rinv.as<double>(),
                                  flags_out, any_out, cond, save, save_row0, save_rows,
-                                 h->ews.fcoef.as<float>(), sticky, st));
+                                 h->ews.fcoef.as<float>(), sticky, rsave, first ? 1 : 0, st));
     // rank-deficient columns (flags_out) are refilled with random values by the same launch
     HIPCHK(n2v2r_launch_pip_apply(L, h->ews.fcoef.as<float>(), nq * b, b, out_one(Z), n, cond,
                                   flags_out, seed ^ (0xABCDull + ++fill_counter), row0, st));
@@ -625,7 +627,8 @@ struct Eig {
     const int nsave = (save && local) ? (int)local->size() : 0;
     // (lazy: a refill or heavy cancellation in the first pass also sets the cycle's sticky flag)
     pip_pass(Z, first, nullptr, flg, any, Zin, nsave ? save : nullptr,
-             ((int)first.size() - nsave) * b, nsave * b, lazy ? any + 3 : nullptr, rsave_first);
+             ((int)first.size() - nsave) * b, nsave * b, lazy ? any + 3 : nullptr, rsave_first,
+             0.f, true);
     if (debug_ortho()) {  // pass 1's Gram [Q Z]^T Z (still in gsm_p)
       const int c1 = (int)first.size() * b;
       std::vector<double> g((size_t)(c1 + b) * b);
@@ -642,8 +645,10 @@ struct Eig {
       fprintf(stderr, "\n");
     }
     dbg_ortho(Z, first, "after pass 1 (local)", flg);
+    // (rsave_first: the second pass's R too, folded into the first's: R2 R1)
     pip_pass(Z, basis, nullptr, flg + 64, any + 1, nullptr, nullptr, 0, 0,
-             lazy ? any + 3 : nullptr, nullptr, reorth_tol);
+             lazy ? any + 3 : nullptr, rsave_first ? rsave_first + 64 : nullptr, reorth_tol);
+    if (rsave_first) HIPCHK(n2v2r_launch_rmul8(rsave_first + 64, rsave_first, st));
     dbg_ortho(Z, basis, "after pass 2 (full, selective)", flg + 64);
     if (!lazy) pip_pass(Z, basis, any + 1, flg + 128, any + 2);
     if (!lazy) dbg_ortho(Z, basis, "after pass 3", flg + 128);
@@ -691,13 +696,13 @@ struct Eig {
     HIPCHK(n2v2r_launch_pip_fused(blocks(basis, 0, nq_old), deferred, deferred, g2, nq_old * b, n,
                                   nullptr, flg_p + 64, any_p + 1, nullptr, 0, 0, any_p + 3,
                                   seed ^ (0xABCDull + ++fill_counter), row0, ra, reorth_tol, skc,
-                                  st));
+                                  0, st));
     HIPCHK(n2v2r_launch_pair_fixup(g2, nq_old + 2, nq_old, ra, st));
     HIPCHK(n2v2r_launch_pip_fused(blocks(basis, 0, nq_old + 1), zb, zb,
                                   g2 + (size_t)(nq_old + 2) * 64, (nq_old + 1) * b, n, nullptr,
                                   flg_p + 64, any_p + 1, nullptr, 0, 0, any_p + 3,
                                   seed ^ (0xABCDull + ++fill_counter), row0, nullptr, reorth_tol,
-                                  skc, st));
+                                  skc, 0, st));
     t_ortho += now_ms() - t0;
     deferred = nullptr;
     return true;
@@ -739,7 +744,7 @@ struct Eig {
       // a refill or heavy cancellation here sets the sticky flag: the block may not go to its
       // SpMM before its full pass, so the cycle is expanded again without deferral
       pip_pass(z, first, nullptr, flg_p, any_p, w_from, nsave ? save : nullptr,
-               ((int)first.size() - nsave) * b, nsave * b, any_p + 3);
+               ((int)first.size() - nsave) * b, nsave * b, any_p + 3, nullptr, 0.f, true);
       t_ortho += now_ms() - t0;
       if (deferred && pair_gram && pair_pass(z, basis)) {
         // (both full passes done)
@@ -998,7 +1003,7 @@ struct Eig {
     }
     h->ews.skipc.ensure(sizeof(int) * 68);
     HIPCHK(hipMemsetAsync(h->ews.skipc.p, 0, sizeof(int) * 68, st));
-    if (lean) h->ews.rres.ensure(sizeof(double) * 64);
+    if (lean) h->ews.rres.ensure(sizeof(double) * 128);  // R of the restart block's two passes
     double est_scale = 1.0;  // lean: true / estimated residual seen at a failed final check
     double last_true = 1e300;  // lean: the worst true residual of the previous check
     bool rr_armed = false;   // the Rayleigh-Ritz error words zeroed (then by every read-back)
