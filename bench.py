@@ -390,6 +390,19 @@ def main():
     ap.add_argument("--resident-steps", type=int, default=3)
     args = ap.parse_args()
 
+    # a progress line on stderr every 45 s (long configurations: cfg5's synthesis and ingest
+    # print nothing for minutes)
+    import threading
+    t_hb = time.perf_counter()
+
+    def _heartbeat():
+        while True:
+            time.sleep(45)
+            print(f"[bench] {args.config}: {time.perf_counter() - t_hb:.0f} s", file=sys.stderr,
+                  flush=True)
+
+    threading.Thread(target=_heartbeat, daemon=True).start()
+
     world, rank, local = _dist_env()
     if world > 1 and world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world} GPUs",

@@ -179,13 +179,13 @@ int n2v2r_spmm_col_blocks(const n2v2r_handle* h, int b) {
 }
 
 // The flat-window tiled SpMM of layer k (A_k X, or A_k^T X) with `nb` column blocks (0: the fit's
-// rule, panel blocks of <= 2 MB, at most 32) from device panels, timed with HIP events over `reps`
+// rule, panel blocks of <= 2 MB, at most 64) from device panels, timed with HIP events over `reps`
 // launches after a warm-up.  N2V2R_ERR_BAD_ARG when the layer cannot take packed blocks.
 static int time_tiled(n2v2r_handle* h, int k, int transpose, int nb, const float* xd, float* yd,
                       int reps, double* avg_ms) {
   if (nb <= 0) {
     nb = 4;
-    while (nb < 32 && (double)h->n * 32.0 / nb > 2.0 * 1024 * 1024) nb *= 2;
+    while (nb < 64 && (double)h->n * 32.0 / nb > 2.0 * 1024 * 1024) nb *= 2;
   }
   if (nb != 4 && nb != 8 && nb != 16 && nb != 32 && nb != 64) return N2V2R_ERR_BAD_ARG;
   LayerDev& L = *h->layers[k];

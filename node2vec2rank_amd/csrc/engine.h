@@ -452,7 +452,6 @@ struct EigWorkspace {
   DevBuf rres;                                // lean images: R of the restart projection
   DevBuf skipc;                               // full passes skipped (selective reorthogonalisation)
   DevBuf tblk;                                // tiled SpMM: CsrBlk [2][K][nb] (stage 1, stage 2)
-  DevBuf xsync;                               // tiled SpMM: XCD phase counters (probe)
 };
 }  // namespace n2v2r_int
 

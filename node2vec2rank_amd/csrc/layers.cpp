@@ -73,9 +73,11 @@ bool ensure_col_blocks(LayerDev& L, int64_t ncols, hipStream_t st, int nb, int w
 }
 
 // Window rows of the flat tiled SpMM for nb column blocks: windows of 2^wbits rows, so that a
-// window's run in one block holds ~40 or more entries (32 rows at cfg4's ~3 entries per row and
-// block; 64 at cfg5's ~1): a short run leaves most lanes of its step idle.  N2V2R_SPMM_WBITS
-// (5..7) overrides (read per call).
+// window's run in one block holds ~20 or more entries (32 rows at cfg4's ~3 entries per row and
+// block; 64 at cfg5's ~0.5 with 64 blocks): a short run leaves most lanes of its step idle, a
+// long window fewer windows per wave.  cfg5 layer launch at 64 blocks: 5.13 / 4.36 / 4.79 ms at
+// 32 / 64 / 128 rows (profiles/r05_tile_cfg5.jsonl).  N2V2R_SPMM_WBITS (5..7) overrides (read
+// per call).
 int tile_wbits(const std::vector<std::unique_ptr<LayerDev>>& layers, int nb) {
   if (const char* e = std::getenv("N2V2R_SPMM_WBITS")) {
     const int v = std::atoi(e);
@@ -85,7 +87,7 @@ int tile_wbits(const std::vector<std::unique_ptr<LayerDev>>& layers, int nb) {
   for (const auto& L : layers)
     if (L->n_rows > 0) avg = std::max(avg, (double)L->nnz / (double)L->n_rows);
   int wb = CB_WIN_BITS_MIN;
-  while (wb < CB_WIN_BITS_MAX && (double)(1 << wb) * avg / nb < 40.0) ++wb;
+  while (wb < CB_WIN_BITS_MAX && (double)(1 << wb) * avg / nb < 20.0) ++wb;
   return wb;
 }
 

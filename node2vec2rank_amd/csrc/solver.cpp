@@ -479,16 +479,6 @@ struct Eig {
   }
 
   // apply_M with the tiled column-block SpMM: one launch per stage over all layers
-  // N2V2R_SPMM_XSYNC=s (probe, off by default): the tiled launches align the phases of the
-  // workgroups of an XCD to a lag of s phases (spmm_args.h)
-  int xsync_skew = -1;
-  void xsync_arm(SpmmTileArgs& a, int stage) {
-    if (xsync_skew < 0) return;
-    unsigned* c = h->ews.xsync.as<unsigned>() + (size_t)stage * 8 * SPMM_MAX_LAYERS * CB_MAX;
-    HIPCHK(hipMemsetAsync(c, 0, sizeof(unsigned) * 8 * (size_t)a.K * a.nb, st));
-    a.xsync = c;
-    a.xskew = xsync_skew;
-  }
   void apply_M_tiled(const float* xg, float* Wout, int64_t ng) {
     const CsrBlk* tb = h->ews.tblk.as<CsrBlk>();
     SpmmTileArgs a{};
@@ -525,7 +515,6 @@ struct Eig {
       }
       for (int k = 0; k < K; ++k) h->gather_wait(k);
     } else {
-      xsync_arm(a, 0);
       te = tbeg();
       HIPCHK(n2v2r_launch_spmm_tile(a, st));
       tend(te, 0, b0);
@@ -533,8 +522,6 @@ struct Eig {
     SpmmTileArgs s2 = a;
     s2.blk = tb + (size_t)K * tile_nb;
     s2.sum = 1;
-    s2.xsync = nullptr;
-    if (!ovl) xsync_arm(s2, 1);
     for (int k = 0; k < K; ++k) {
       s2.X[k] = h->ews.zk[k]->as<float>();
       if (h->comm) {
@@ -871,11 +858,12 @@ struct Eig {
       // the flat-window tiled SpMM: column blocks (phases) per layer of <= 2 MB of panel, so a
       // phase's block stays in the XCD's 4 MB L2 beside the index stream (cfg4: 16 blocks,
       // 0.748 ms per stage launch; 8 blocks 0.896, 32 blocks 0.817: 4 MB blocks left 31 % of
-      // the gathers missing L2), at most 32 (cfg5's 320 MB panel: 9.47 ms per stage launch at 32
-      // blocks of 10 MB, 11.53 at 64 of 5 MB -- a window's run per block gets too short).
+      // the gathers missing L2), at most 64 (cfg5's 320 MB panel, one layer launch: 4.36 ms at
+      // 64 blocks of 5 MB, 4.62 at 32 of 10 MB, 5.14 at 16 -- round 5, window offsets,
+      // profiles/r05_tile_cfg5.jsonl; with round 4's per-row block pointers 64 blocks lost).
       // N2V2R_SPMM_TILE_NB = 4..64 overrides (read per fit).
       int nb_auto = 4;
-      while (nb_auto < 32 && (double)nglob * 32.0 / nb_auto > 2.0 * 1024 * 1024) nb_auto *= 2;
+      while (nb_auto < 64 && (double)nglob * 32.0 / nb_auto > 2.0 * 1024 * 1024) nb_auto *= 2;
       const char* tn_ = std::getenv("N2V2R_SPMM_TILE_NB");
       tile_nb = tn_ ? std::atoi(tn_) : nb_auto;
       if (tile_nb != 4 && tile_nb != 8 && tile_nb != 16 && tile_nb != 32 && tile_nb != 64)
@@ -889,13 +877,6 @@ struct Eig {
         int ncu = 0;
         HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
         tile_rows = n2v2r_spmm_tile_rows(n, ncu, 2, tile_wb);
-        xsync_skew = -1;
-        if (const char* xe = std::getenv("N2V2R_SPMM_XSYNC")) {
-          // only when every workgroup is resident at once (one round of 2 per CU)
-          if ((n + tile_rows - 1) / tile_rows <= 2 * (int64_t)ncu) xsync_skew = std::atoi(xe);
-          if (xsync_skew >= 0)
-            h->ews.xsync.ensure(sizeof(unsigned) * 2 * 8 * SPMM_MAX_LAYERS * CB_MAX, st);
-        }
         const int nb = tile_nb;
         std::vector<CsrBlk> hb((size_t)2 * K * nb);
         for (int k = 0; k < K; ++k) {

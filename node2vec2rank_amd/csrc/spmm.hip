@@ -438,25 +438,9 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
       const int lr = (w << wbits) + rr;
       if (lr < nrows) tacc[lr * 2 + sub] = zero;
     }
-  // XCD phase alignment (a.xsync): counters of this workgroup's XCD group (blockIdx % 8)
-  const int xg = blockIdx.x & 7;
-  const unsigned npeer = (gridDim.x - xg + 7) >> 3;
   for (int k = 0; k < a.K; ++k) {
     const float* X = a.X[k];
     for (int p = 0; p < a.nb; ++p) {
-      if (a.xsync) {
-        const int gw = k * a.nb + p - 1 - a.xskew;  // the phase every peer must have finished
-        if (gw >= 0) {
-          if (threadIdx.x == 0) {
-            const unsigned* c = a.xsync + (size_t)gw * 8 + xg;
-            for (int it = 0; it < 8192 && __hip_atomic_load(c, __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT) < npeer;
-                 ++it)
-              __builtin_amdgcn_s_sleep(2);
-          }
-          __syncthreads();
-        }
-      }
       const CsrBlk& A = a.blk[k * a.nb + p];
       const int cbits = __builtin_amdgcn_readfirstlane(A.cbits);
       const int unit = __builtin_amdgcn_readfirstlane(A.unit);
@@ -495,10 +479,10 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
       // 0.36 ms per cfg4 layer launch; a bounded skew -- a wave starts phase g once all have
       // finished g - 2, LDS counters -- 0.393 vs 0.354 ms, fit 1,714 vs 1,603 ms,
       // profiles/r04_flat_sync.jsonl: the L2 locality of lockstep phases is worth the idling)
+      // (XCD phase alignment -- a workgroup starts phase g once the workgroups of its XCD have
+      // finished g - 1 - s, counters in HBM: 1.11 / 1.24 / 1.34 vs 0.72 ms per cfg4 stage launch
+      // at s = 2 / 1 / 0, profiles/r05_xsync_ab.jsonl; removed)
       __syncthreads();
-      if (a.xsync && threadIdx.x == 0)
-        __hip_atomic_fetch_add(a.xsync + (size_t)(k * a.nb + p) * 8 + xg, 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
     }
     if (!a.sum || k == a.K - 1) {
       float* Y = a.Y[a.sum ? 0 : k];

@@ -58,8 +58,4 @@ struct SpmmTileArgs {  // row tiles x column-block phases (spmm8_flat_kernel)
   int tile_rows;       // a multiple of the window rows 2^wbits
   int wbits;           // window rows = 2^wbits (CB_WIN_BITS_MIN..MAX), as the blocks were packed
   // optional phase alignment of the workgroups that share an XCD (blockIdx % 8), a speed hint:
-  // a workgroup starts phase g once its XCD peers have finished phase g - 1 - xskew (bounded
-  // wait: it never changes results).  xsync: zeroed counters [K * nb][8]; nullptr = off
-  unsigned* xsync;
-  int xskew;
 };
