@@ -182,7 +182,7 @@ int n2v2r_spmm_col_blocks(const n2v2r_handle* h, int b) {
 // rule, panel blocks of <= 2 MB, at most 64) from device panels, timed with HIP events over `reps`
 // launches after a warm-up.  N2V2R_ERR_BAD_ARG when the layer cannot take packed blocks.
 static int time_tiled(n2v2r_handle* h, int k, int transpose, int nb, const float* xd, float* yd,
-                      int reps, double* avg_ms) {
+                      int reps, double* avg_ms, int b = 8) {
   if (nb <= 0) {
     nb = 4;
     while (nb < 64 && (double)h->n * 32.0 / nb > 2.0 * 1024 * 1024) nb *= 2;
@@ -201,14 +201,15 @@ static int time_tiled(n2v2r_handle* h, int k, int transpose, int nb, const float
   a.blk = tb.as<CsrBlk>();
   a.X[0] = xd;
   a.Y[0] = yd;
-  a.ldx = 8;
-  a.ldy = 8;
+  a.ldx = b;
+  a.ldy = b;
   a.n = h->nloc;
   a.K = 1;
   a.nb = nb;
   a.sum = 0;
-  a.tile_rows = n2v2r_spmm_tile_rows(h->nloc, ncu, 2, wb);
+  a.tile_rows = n2v2r_spmm_tile_rows_b(h->nloc, ncu, 2, wb, b);
   a.wbits = wb;
+  a.width = b;
   HIPCHK(n2v2r_launch_spmm_tile(a, h->stream));  // warm-up
   hipEvent_t e0, e1;
   HIPCHK(hipEventCreate(&e0));
@@ -316,14 +317,15 @@ int n2v2r_bench_spmm_tiled(n2v2r_handle* h, int k, int transpose, int b, int nb,
                            const float* X, float* Y, double* avg_ms) {
   if (h && h->multi()) h = h->ranks[0];  // (diagnostics: rank 0)
   return guarded(h, [&]() -> int {
-    if (k < 0 || k >= h->K || !h->layers[k]->loaded || h->layers[k]->dense || b != 8 ||
-        reps < 1 || !X || h->comm)
+    if (k < 0 || k >= h->K || !h->layers[k]->loaded || h->layers[k]->dense ||
+        (b != 8 && b != 16) || reps < 1 || !X || h->comm)
       return N2V2R_ERR_BAD_ARG;
     DevBuf xd, yd;
     xd.ensure(sizeof(float) * h->n * b);
     yd.ensure(sizeof(float) * std::max<int64_t>(h->nloc, 1) * b);
     HIPCHK(hipMemcpyAsync(xd.p, X, sizeof(float) * h->n * b, hipMemcpyHostToDevice, h->stream));
-    const int st_ = time_tiled(h, k, transpose, nb, xd.as<float>(), yd.as<float>(), reps, avg_ms);
+    const int st_ =
+        time_tiled(h, k, transpose, nb, xd.as<float>(), yd.as<float>(), reps, avg_ms, b);
     if (st_ != N2V2R_OK) return st_;
     if (Y)
       HIPCHK(hipMemcpyAsync(Y, yd.p, sizeof(float) * h->nloc * b, hipMemcpyDeviceToHost,

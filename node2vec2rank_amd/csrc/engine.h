@@ -42,6 +42,7 @@ hipError_t n2v2r_launch_spmm(const SpmmArgs& args, int B, hipStream_t stream);
 hipError_t n2v2r_launch_row_sums(const CsrDev& A, float* out, hipStream_t stream);
 hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, hipStream_t stream);
 int n2v2r_spmm_tile_rows(int64_t n, int ncu, int wpc, int wbits);
+int n2v2r_spmm_tile_rows_b(int64_t n, int ncu, int wpc, int wbits, int b);
 hipError_t n2v2r_launch_cb_count(const CsrDev& A, int64_t cw, int nb, int32_t* cnt,
                                  hipStream_t stream);
 hipError_t n2v2r_launch_cb_rowptrs(const int32_t* cnt, int64_t n, int nb, int64_t nnz,

@@ -390,6 +390,14 @@ __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1)
   for (int u = 0; u < NS; ++u)
     x[u] = *reinterpret_cast<const __attribute__((address_space(1))) f32x4*>(
         Xb + ((uint32_t)(wd[u] & cmask) * ldx + sub * 4));
+#ifdef FLAT_NOFOLD  // probe builds only: the fold's cost (wrong sums: a lane's entries into one row)
+  f32x4 racc = stage[pr * 2 + sub];
+#pragma unroll
+  for (int u = 0; u < NS; ++u)
+    if (u * 32 + pr < left) racc += v[u] * x[u];
+  stage[pr * 2 + sub] = racc;
+  return;
+#endif
 #pragma unroll
   for (int u = 0; u < NS; ++u) {
     stage[pr * 2 + sub] = v[u] * x[u];  // entries past the end are never read
@@ -498,13 +506,144 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
   }
 }
 
+// b = 16 panels (64-B rows): a lane quad per entry (lane = (entry q = lane >> 2, quarter
+// sub = lane & 3), each lane one 16-B load), 16 entries per wave step, up to 4 steps per batch
+// (8 spilled 24 VGPRs at the 8-waves-per-SIMD register budget).
+// The same packed blocks, windows, segment fold and fixed summation order as flat_steps; one
+// gathered row is still one L2 request, so a vector column costs about half of b = 8's
+// (the gather microbenchmark: 162 vs 182 G entries/s at 64- vs 32-B rows, tools/gather_ceiling.hip).
+template <int NS, bool UNIT, bool NT>
+__device__ __forceinline__ void flat16_steps(const __attribute__((address_space(1))) int32_t* ind,
+                                             const __attribute__((address_space(1))) float* dat,
+                                             int64_t beg, int off, int left,
+                                             const __attribute__((address_space(1))) float* Xb,
+                                             uint32_t ldx, int32_t cmask, int cbits, int lane,
+                                             f32x4* stage, f32x4* tw) {
+  const int q = lane >> 2, sub = lane & 3;
+  int wd[NS];
+  float v[NS];
+  f32x4 x[NS];
+#pragma unroll
+  for (int u = 0; u < NS; ++u) {
+    const int qq = u * 16 + q;
+    const int64_t e = beg + off + (qq < left ? qq : 0);
+    wd[u] = NT ? __builtin_nontemporal_load(ind + e) : ind[e];
+    v[u] = UNIT ? 1.f : (NT ? __builtin_nontemporal_load(dat + e) : dat[e]);
+  }
+#pragma unroll
+  for (int u = 0; u < NS; ++u)
+    x[u] = *reinterpret_cast<const __attribute__((address_space(1))) f32x4*>(
+        Xb + ((uint32_t)(wd[u] & cmask) * ldx + sub * 4));
+#pragma unroll
+  for (int u = 0; u < NS; ++u) {
+    stage[q * 4 + sub] = v[u] * x[u];  // entries past the end are never read
+    const int nval = left - u * 16;     // valid entries of this step (>= 1; may exceed 16)
+    const int ri = wd[u] >> cbits;      // row in window
+    const int rprev = __shfl(ri, lane - 4, 64);
+    const bool start = q < nval && (q == 0 || rprev != ri);
+    const unsigned long long m = __ballot(start);
+    if (start) {
+      const unsigned long long rest = q == 15 ? 0ull : (m >> (4 * q + 4));
+      const int end = rest ? q + 1 + (__builtin_ctzll(rest) >> 2) : (nval < 16 ? nval : 16);
+      f32x4 acc = stage[q * 4 + sub];
+      for (int j = q + 1; j < end; ++j) acc += stage[j * 4 + sub];
+      tw[ri * 4 + sub] += acc;
+    }
+  }
+}
+
+__global__ __launch_bounds__(1024, 8) void spmm16_flat_kernel(SpmmTileArgs a) {
+  constexpr bool NT = true;
+  // [tile_rows][16] row accumulators, then a 1-KB staging slot per wave
+  extern __shared__ float tacf[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nwave = blockDim.x >> 6;
+  const int q = lane >> 2, sub = lane & 3;
+  const int wbits = __builtin_amdgcn_readfirstlane(a.wbits);
+  const int W = 1 << wbits;
+  const int64_t r0 = (int64_t)blockIdx.x * a.tile_rows;
+  const int64_t gw0 = r0 >> wbits;
+  const int64_t rem = a.n - r0;
+  const int nrows = (int)(rem < a.tile_rows ? rem : a.tile_rows);
+  const int nwin = (nrows + W - 1) >> wbits;
+  const uint32_t ldx = (uint32_t)a.ldx;
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  f32x4* tacc = reinterpret_cast<f32x4*>(tacf);
+  f32x4* stage = reinterpret_cast<f32x4*>(tacf + (size_t)a.tile_rows * 16) + wave * 64;
+  for (int w = wave; w < nwin; w += nwave)
+    for (int rr = q; rr < W; rr += 16) {
+      const int lr = (w << wbits) + rr;
+      if (lr < nrows) tacc[lr * 4 + sub] = zero;
+    }
+  for (int k = 0; k < a.K; ++k) {
+    const float* X = a.X[k];
+    for (int p = 0; p < a.nb; ++p) {
+      const CsrBlk& A = a.blk[k * a.nb + p];
+      const int cbits = __builtin_amdgcn_readfirstlane(A.cbits);
+      const int unit = __builtin_amdgcn_readfirstlane(A.unit);
+      const auto wo = uniform_global(A.wo);
+      const auto ind = uniform_global(A.indices);
+      const auto dat = uniform_global(A.data);
+      const int64_t base = uniform_i64(A.base);
+      const int64_t col0 = uniform_i64(A.col0);
+      const int32_t cmask = (1 << cbits) - 1;
+      const auto Xb = uniform_global(X + col0 * a.ldx);
+      for (int w = wave; w < nwin; w += nwave) {
+        const int32_t e0 = wo[gw0 + w];
+        const int len = wo[gw0 + w + 1] - e0;
+        const int64_t beg = base + e0;
+        f32x4* tw = tacc + ((size_t)w << wbits) * 4;
+#define FLAT16_STEPS(U)                                                                          \
+  for (int off = 0; off < len; off += 64) {                                                      \
+    const int left = len - off;                                                                  \
+    if (left > 48)                                                                               \
+      flat16_steps<4, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, cbits, lane, stage, tw);  \
+    else if (left > 32)                                                                          \
+      flat16_steps<3, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, cbits, lane, stage, tw);  \
+    else if (left > 16)                                                                          \
+      flat16_steps<2, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, cbits, lane, stage, tw);  \
+    else                                                                                         \
+      flat16_steps<1, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, cbits, lane, stage, tw);  \
+  }
+        if (unit) {
+          FLAT16_STEPS(true)
+        } else {
+          FLAT16_STEPS(false)
+        }
+#undef FLAT16_STEPS
+      }
+      __syncthreads();
+    }
+    if (!a.sum || k == a.K - 1) {
+      float* Y = a.Y[a.sum ? 0 : k];
+      for (int w = wave; w < nwin; w += nwave)
+        for (int rr = q; rr < W; rr += 16) {
+          const int lr = (w << wbits) + rr;
+          if (lr < nrows) {
+            *reinterpret_cast<f32x4*>(Y + (r0 + lr) * a.ldy + sub * 4) = tacc[lr * 4 + sub];
+            tacc[lr * 4 + sub] = zero;
+          }
+        }
+    }
+  }
+}
+
 // rows per tile for the tiled form: `wpc` workgroups (1024 threads each) per CU sharing its
 // 160 KB of LDS (32 B of accumulators per row), at most 2048 (4096 at one per CU); a multiple of
 // the window rows 2^wbits.  When the rows need more than one round of resident workgroups
 // (cfg5: 10M rows, ~10 rounds), the tiles are sized so that every round is full.
+extern "C" int n2v2r_spmm_tile_rows_b(int64_t n, int ncu, int wpc, int wbits, int b);
 extern "C" int n2v2r_spmm_tile_rows(int64_t n, int ncu, int wpc, int wbits) {
+  return n2v2r_spmm_tile_rows_b(n, ncu, wpc, wbits, 8);
+}
+
+// (b = 16: 64 B of accumulators per row, half the rows)
+extern "C" int n2v2r_spmm_tile_rows_b(int64_t n, int ncu, int wpc, int wbits, int b) {
   const int64_t slots = wpc * (int64_t)ncu;
-  const int64_t cap = (wpc == 1 ? 4096 : 2048);
+  // (b = 16: 1024 rows, 80 KB with the staging slots, two per CU: 0.549 ms per cfg4 layer
+  // launch against 0.60-0.63 at 960 / 768 / 512 rows)
+  const int64_t cap = (wpc == 1 ? 4096 : 2048) * 8 / (b == 16 ? 16 : 8);
   const int64_t w = (int64_t)1 << wbits;
   const int64_t rounds = (n + slots * cap - 1) / (slots * cap);
   int64_t t = (n + slots * rounds - 1) / (slots * rounds);
@@ -518,16 +657,24 @@ extern "C" hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, hipStream_t 
       a.tile_rows < (1 << a.wbits) || a.tile_rows % (1 << a.wbits) != 0)
     return hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.n + a.tile_rows - 1) / a.tile_rows);
-  // 32 B of accumulators per row + a 1-KB staging slot per wave
-  const size_t flds = sizeof(float) * 8 * (size_t)a.tile_rows + 16 * 1024;
+  const int width = a.width ? a.width : 8;
+  if (width != 8 && width != 16) return hipErrorInvalidValue;
+  // 4 b B of accumulators per row + a 1-KB staging slot per wave
+  const size_t flds = sizeof(float) * width * (size_t)a.tile_rows + 16 * 1024;
   if (flds > 80 * 1024) return hipErrorInvalidValue;
   static const bool fattr = [] {
     (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    (void)hipFuncSetAttribute((const void*)spmm16_flat_kernel,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
     (void)hipGetLastError();
     return true;
   }();
   (void)fattr;
+  if (width == 16) {
+    hipLaunchKernelGGL(spmm16_flat_kernel, dim3(grid), dim3(1024), flds, stream, a);
+    return hipGetLastError();
+  }
   // (Non-temporal index / value loads: cfg4 layer launch 0.354 vs 0.363 ms, fit 1,599 vs
   // 1,609 ms, profiles/r04_flat_nt.jsonl; no phase barrier: 0.57 vs 0.36 ms,
   // profiles/r04_flat_bar.jsonl -- the A/B switches of those runs are gone.)

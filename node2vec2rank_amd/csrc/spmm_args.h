@@ -46,7 +46,7 @@ struct CsrBlk {
   int64_t col0;            // first column of the block
 };
 
-struct SpmmTileArgs {  // row tiles x column-block phases (spmm8_flat_kernel)
+struct SpmmTileArgs {  // row tiles x column-block phases (spmm8/16_flat_kernel)
   const CsrBlk* blk;   // device array [K][nb]
   const float* X[SPMM_MAX_LAYERS];  // panel per layer (gathered, global rows)
   float* Y[SPMM_MAX_LAYERS];        // output per layer (sum: Y[0])
@@ -57,5 +57,5 @@ struct SpmmTileArgs {  // row tiles x column-block phases (spmm8_flat_kernel)
   int sum;
   int tile_rows;       // a multiple of the window rows 2^wbits
   int wbits;           // window rows = 2^wbits (CB_WIN_BITS_MIN..MAX), as the blocks were packed
-  // optional phase alignment of the workgroups that share an XCD (blockIdx % 8), a speed hint:
+  int width;           // panel width b: 8 (spmm8_flat_kernel) or 16 (spmm16_flat_kernel); 0 = 8
 };

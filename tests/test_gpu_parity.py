@@ -549,6 +549,24 @@ def test_spmm_tiled_flat_blocks(engine, monkeypatch, tiled_layer, nb, wbits):
         assert np.all(np.abs(Y - ref) <= bound), (nb, wbits, tr)
 
 
+@pytest.mark.parametrize("wbits", ["5", "7"])
+@pytest.mark.parametrize("nb", [4, 32])
+def test_spmm16_tiled_flat_blocks(engine, monkeypatch, tiled_layer, nb, wbits):
+    """The b = 16 flat-window kernel (a lane quad per entry, 64-B panel rows) on the same layer:
+    every row against scipy, both orientations (its steps hold 16 entries, not 32: a row's
+    partial sums split at other places than the b = 8 kernel's, so the two agree to rounding)."""
+    monkeypatch.setenv("N2V2R_SPMM_WBITS", wbits)
+    A, X, _ = tiled_layer
+    X16 = np.ascontiguousarray(np.concatenate([X, X[::-1] * 0.5], axis=1))
+    engine.set_layers([A])
+    for tr in (False, True):
+        M = (A.T if tr else A).tocsr().astype(np.float64)
+        ref = M @ X16.astype(np.float64)
+        bound = 1e-5 * (abs(M) @ np.abs(X16).astype(np.float64)) + 1e-6
+        Y16, _ = engine.bench_spmm_tiled(0, X16, transpose=tr, nb=nb, reps=2)
+        assert np.all(np.abs(Y16 - ref) <= bound), (nb, wbits, tr)
+
+
 @pytest.mark.parametrize("d", [60, 64, 100, 128])
 def test_embedding_from_lean_check_bit_identical(engine, monkeypatch, d):
     """With the tiled SpMM on one GPU, the final lean check's stage-1 products A_k^T X of the d
