@@ -612,10 +612,11 @@ struct Eig {
     const bool loc = local && !full_first && local->size() < basis.size();
     const std::vector<float*>& first = loc ? *local : basis;
     const int nsave = (save && local) ? (int)local->size() : 0;
-    // (lazy: a refill or heavy cancellation in the first pass also sets the cycle's sticky flag)
+    // (no sticky flag here: a column the first pass cancelled -- scaled, not normalised -- is
+    // normalised by the full pass that always follows; a refill there (a later pass) sets it.
+    // BASELINE cfg3's first images cancel: with the flag each fit expanded cycle 0 twice)
     pip_pass(Z, first, nullptr, flg, any, Zin, nsave ? save : nullptr,
-             ((int)first.size() - nsave) * b, nsave * b, lazy ? any + 3 : nullptr, rsave_first,
-             0.f, true);
+             ((int)first.size() - nsave) * b, nsave * b, nullptr, rsave_first, 0.f, true);
     if (debug_ortho()) {  // pass 1's Gram [Q Z]^T Z (still in gsm_p)
       const int c1 = (int)first.size() * b;
       std::vector<double> g((size_t)(c1 + b) * b);
