@@ -414,6 +414,14 @@ def main():
     if cfg.get("dense") and n_gpus > 1:
         mode = "api"
     devices = list(range(n_gpus)) if n_gpus > 1 else None
+    # (rehearsal on a one-GPU box: N2V2R_BENCH_DEVICES=0,0 runs the N > 1 path over a repeated
+    # device -- the library's in-process thread communicator instead of RCCL)
+    dev_env = os.environ.get("N2V2R_BENCH_DEVICES")
+    if dev_env and world == 1:
+        devices = [int(v) for v in dev_env.split(",")]
+        n_gpus = len(devices)
+        if n_gpus == 1:
+            devices = None
     # the headline runs in this process: all of it without torchrun, rank 0's share (the whole
     # multi-GPU API call) under torchrun; per-process partitioned runs on every rank
     per_process = mode == "partitioned" and world > 1
