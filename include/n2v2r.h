@@ -172,6 +172,9 @@ int n2v2r_multi_devices(const n2v2r_handle* h, int* devices, int cap);
  * with A^T entry by entry on the GPU) run on the device.  Non-symmetric layers also keep A^T.
  * The transpose sorts int32 entry indices: a layer with more than 2^31 - 1 entries needs
  * symmetric = N2V2R_SYM_YES (N2V2R_ERR_BAD_ARG otherwise).
+ * The first fit on one GPU adds a column-blocked copy of the entries for the tiled SpMM
+ * (~4 nnz bytes, + 4 nnz of values for a weighted layer, + 4 nb (N / 2^wbits + 1) of window
+ * offsets; A^T's as well when not symmetric), kept with the layer.
  * Memory: on a partitioned handle this call still uploads the WHOLE layer to every rank (and,
  * unless N2V2R_SYM_YES, sorts its transpose there, ~40 B per global entry at the peak) before
  * keeping the rank's rows; n2v2r_set_layer_csr_rows is the ingest whose memory scales with the
