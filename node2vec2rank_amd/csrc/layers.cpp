@@ -72,23 +72,19 @@ bool ensure_col_blocks(LayerDev& L, int64_t ncols, hipStream_t st, int nb, int w
   return L.cb.usable && L.cb.cbits && (L.symmetric || (L.cb_t.usable && L.cb_t.cbits));
 }
 
-// Window rows of the flat tiled SpMM for nb column blocks: windows of 2^wbits rows, so that a
-// window's run in one block holds ~20 or more entries (32 rows at cfg4's ~3 entries per row and
-// block; 64 at cfg5's ~0.5 with 64 blocks): a short run leaves most lanes of its step idle, a
-// long window fewer windows per wave.  cfg5 layer launch at 64 blocks: 5.13 / 4.36 / 4.79 ms at
-// 32 / 64 / 128 rows (profiles/r05_tile_cfg5.jsonl).  N2V2R_SPMM_WBITS (5..7) overrides (read
-// per call).
+// Window rows of the flat tiled SpMM: 64 (wbits 6).  Layer launches, round 5 sweeps
+// (profiles/r05_tile_cfg4.jsonl, r05_tile_cfg5.jsonl): cfg4 (16 blocks, ~3 entries per row and
+// block) 0.356 / 0.348 / 0.357 ms at windows of 32 / 64 / 128 rows; cfg5 (64 blocks, ~0.5)
+// 5.13 / 4.36 / 4.79 ms -- longer runs per window and block until a wave's windows get too
+// few to balance.  N2V2R_SPMM_WBITS (5..7) overrides (read per call).
 int tile_wbits(const std::vector<std::unique_ptr<LayerDev>>& layers, int nb) {
+  (void)layers;
+  (void)nb;
   if (const char* e = std::getenv("N2V2R_SPMM_WBITS")) {
     const int v = std::atoi(e);
     if (v >= CB_WIN_BITS_MIN && v <= CB_WIN_BITS_MAX) return v;
   }
-  double avg = 0.0;
-  for (const auto& L : layers)
-    if (L->n_rows > 0) avg = std::max(avg, (double)L->nnz / (double)L->n_rows);
-  int wb = CB_WIN_BITS_MIN;
-  while (wb < CB_WIN_BITS_MAX && (double)(1 << wb) * avg / nb < 20.0) ++wb;
-  return wb;
+  return 6;
 }
 
 // A[:, own rows] of a partitioned layer as a CSR over rows_out (>= N) global rows, columns local:
