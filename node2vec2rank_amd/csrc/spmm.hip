@@ -390,14 +390,6 @@ __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1)
   for (int u = 0; u < NS; ++u)
     x[u] = *reinterpret_cast<const __attribute__((address_space(1))) f32x4*>(
         Xb + ((uint32_t)(wd[u] & cmask) * ldx + sub * 4));
-#ifdef FLAT_NOFOLD  // probe builds only: the fold's cost (wrong sums: a lane's entries into one row)
-  f32x4 racc = stage[pr * 2 + sub];
-#pragma unroll
-  for (int u = 0; u < NS; ++u)
-    if (u * 32 + pr < left) racc += v[u] * x[u];
-  stage[pr * 2 + sub] = racc;
-  return;
-#endif
 #pragma unroll
   for (int u = 0; u < NS; ++u) {
     stage[pr * 2 + sub] = v[u] * x[u];  // entries past the end are never read
@@ -508,7 +500,9 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
 
 // b = 16 panels (64-B rows): a lane quad per entry (lane = (entry q = lane >> 2, quarter
 // sub = lane & 3), each lane one 16-B load), 16 entries per wave step, up to 4 steps per batch
-// (8 spilled 24 VGPRs at the 8-waves-per-SIMD register budget).
+// (8 spilled 24 VGPRs at the 8-waves-per-SIMD register budget).  A lane-pair form (32 entries
+// per step, two 16-B loads of one row per lane, the halves staged and folded in turn) ran
+// 0.57-0.59 ms against this form's 0.52-0.56 per cfg4 layer launch: not kept.
 // The same packed blocks, windows, segment fold and fixed summation order as flat_steps; one
 // gathered row is still one L2 request, so a vector column costs about half of b = 8's
 // (the gather microbenchmark: 162 vs 182 G entries/s at 64- vs 32-B rows, tools/gather_ceiling.hip).
