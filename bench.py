@@ -297,7 +297,7 @@ WATCHDOG_EXIT = 3
 GATHER_CEILING_G = 182.1  # G entries/s, profiles/r04_gather_ceiling.jsonl (stream+gather, 2 MB)
 # the flat tiled SpMM's revision: a PMC traffic record (profiles/spmm_traffic.json) is attached
 # to the line only when it was collected on this revision (round 5: window offsets, segment fold)
-SPMM_KERNEL_REV = "r05-window-offsets"
+SPMM_KERNEL_REV = "r05-window-offsets-w64"
 
 
 def run_guarded(fn, limit_s, on_timeout):
