@@ -217,7 +217,7 @@ extern "C" hipError_t n2v2r_launch_dense_gemm(const float* A, int64_t lda, int64
 // its workgroup's k range; the 4 quarters are summed in LDS in fixed order, split-K slabs over
 // grid.y are folded by dense_fold_kernel (deterministic).  dense_gemm_kernel above stages A
 // through LDS as the A operand: 0.39 ms per cfg3 launch (0.50 of HBM, MFMA busy 0.45).
-template <int DT_D, int OCC>
+template <int DT_D, int OCC, bool NTB>
 __global__ __launch_bounds__(256, OCC) void dense_tn_kernel(const float* __restrict__ B, int64_t ldb,
                                                           int64_t ncols, int64_t kdim, int64_t kper,
                                                           const float* __restrict__ X, int ldx,
@@ -259,7 +259,8 @@ __global__ __launch_bounds__(256, OCC) void dense_tn_kernel(const float* __restr
     for (int u = 0; u < DT_D; ++u) {
       const int kr = (int)(2 * (p0 + u)) + h;
       const uint32_t krc = (uint32_t)(kr < krel_max ? kr : krel_max);  // clamped: one batch
-      bb[u] = *reinterpret_cast<const f32x4*>(Bw + (krc * lb + ncl));
+      const f32x4* src = reinterpret_cast<const f32x4*>(Bw + (krc * lb + ncl));
+      bb[u] = NTB ? __builtin_nontemporal_load(src) : *src;
       xb[u] = Xw[krc * lx + (uint32_t)jc];  // raw: masked at the use (a select here becomes a
                                             // branch with a wait; a multiply, a wait per load)
     }
@@ -342,14 +343,16 @@ extern "C" hipError_t n2v2r_launch_dense_tn(const float* B, int64_t ldb, int64_t
   kper = (kper + 7) & ~(int64_t)7;
   nsplit = (kdim + kper - 1) / kper;
   static const bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)dense_tn_kernel<8, 2>,
+    (void)hipFuncSetAttribute((const void*)dense_tn_kernel<8, 2, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 33 * 4);
     (void)hipGetLastError();
     return true;
   }();
   (void)attr;
   const dim3 grid((unsigned)tiles, (unsigned)nsplit);
-  hipLaunchKernelGGL((dense_tn_kernel<8, 2>), grid, dim3(256), 128 * 33 * sizeof(float),
+  // the stored matrix (read once per launch, 1.6 GB per cfg3 layer) loaded non-temporally:
+  // cfg3 fit 216.3 vs 219.5 ms (profiles/r05_dense_nt.jsonl)
+  hipLaunchKernelGGL((dense_tn_kernel<8, 2, true>), grid, dim3(256), 128 * 33 * sizeof(float),
                      stream, B, ldb, ncols, kdim, kper, X, ldx, b, work, (int64_t)b, ncols * b);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
