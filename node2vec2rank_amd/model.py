@@ -42,17 +42,16 @@ def _as_layer(g):
 
 
 def _label_index(nodes):
-    """``pd.Index(nodes)``, the index of every output frame.  For a list of ``str`` labels (gene
-    names: the common case) the object array is filled by ``np.fromiter`` and checked to hold
-    strings only, which gives the identical Index about 2.5x faster than pandas' own list
-    conversion (cfg4: 36 ms of a 1.7 s API call for 1M labels); anything else -- numbers,
-    mixed or tuple labels, pandas' future string inference -- goes through ``pd.Index`` itself,
-    whose dtype inference it then keeps."""
+    """``pd.Index(nodes)``, the index of every output frame.  For a list whose first label is a
+    ``str`` (gene names: the common case) pandas' inference can only give an object-dtype Index
+    (all strings, or strings mixed with anything else), so the object array is filled by
+    ``np.fromiter`` and wrapped as is: the identical Index about 6x faster than pandas' own list
+    conversion (1M labels: 25 vs 157 ms here; the type scan of round 4 cost 14 ms more).
+    Anything else -- numbers, tuples, pandas' future string inference -- goes through
+    ``pd.Index`` itself, whose dtype inference it then keeps."""
     if (isinstance(nodes, list) and len(nodes) > 4096 and isinstance(nodes[0], str)
             and not pd.get_option("future.infer_string")):
-        arr = np.fromiter(nodes, dtype=object, count=len(nodes))
-        if pd.api.types.infer_dtype(arr, skipna=False) == "string":
-            return pd.Index(arr, dtype=object)
+        return pd.Index(np.fromiter(nodes, dtype=object, count=len(nodes)), dtype=object)
     return pd.Index(nodes)
 
 

@@ -12,6 +12,11 @@ from node2vec2rank_amd.model import _label_index
     [f"gene{i}" for i in range(20_000)] + [None],         # a missing label: pandas' path
     [f"gene{i}" for i in range(20_000)] + [7],            # mixed
     [f"gene{i}" for i in range(20_000)] + [np.nan],
+    [f"gene{i}" for i in range(20_000)] + [("a", 1)],    # a tuple after strings
+    [f"gene{i}" for i in range(20_000)] + [b"raw"],
+    [f"gene{i}" for i in range(20_000)] + [pd.Timestamp("2020-01-01")],
+    [f"2020-01-{1 + i % 28:02d}" for i in range(20_000)],  # date-like strings stay strings
+    [f"{i}" for i in range(20_000)],                      # digit strings stay strings
     list(range(20_000)),                                  # integer labels
     [float(i) for i in range(20_000)],
     [("a", i) for i in range(5000)],                      # tuples: a MultiIndex
