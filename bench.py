@@ -606,8 +606,10 @@ def main():
     if (world > 1 and mode == "api" and not cfg.get("dense")
             and os.environ.get("N2V2R_BENCH_SIDE", "1") != "0"):
         limit = float(os.environ.get("N2V2R_BENCH_SIDE_S", "300"))
-        for key, fn in (("replicas", replicas_leg),
-                        ("partitioned_per_process", strong_scaling)):
+        legs = [("replicas", replicas_leg)]
+        if os.environ.get("N2V2R_BENCH_SIDE") == "all":  # (opt-in: an RCCL world per process)
+            legs.append(("partitioned_per_process", strong_scaling))
+        for key, fn in legs:
             def _expire(key=key):
                 if rank == 0:
                     result[key] = {"error": f"timed out after {limit:g} s"}
