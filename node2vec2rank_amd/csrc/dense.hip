@@ -203,13 +203,8 @@ __global__ __launch_bounds__(1024) void reduce_cols_kernel(const double* __restr
 // streamed from HBM by every pass that reads it, so its lines are read once per pass -- nt
 // dwordx4 loads stream 2 GB at 6.8 TB/s against 6.0 for plain ones on MI355X
 // (profiles/r04_stream_ceiling.jsonl).  A basis that fits the cache keeps plain loads (it is
-// re-read from there by the next pass).  N2V2R_BASIS_NT=0 / 1 forces plain / nt (A/B).
+// re-read from there by the next pass).  (Its A/B switch retired in round 5.)
 static bool basis_nt(int64_t n, int count) {
-  static const int force = [] {
-    const char* s = getenv("N2V2R_BASIS_NT");
-    return s ? (s[0] == '1' ? 1 : (s[0] == '0' ? 0 : -1)) : -1;
-  }();
-  if (force >= 0) return force == 1;
   return (double)n * 32.0 * (double)count > 256.0 * 1024 * 1024;
 }
 
@@ -661,14 +656,9 @@ __global__ __launch_bounds__(256) void ts_tn_stream_lds_kernel(BlockList A, cons
 }
 
 // Gram-kernel selection for 8-wide blocks: the streaming form (about 4096 waves, chunks of at
-// least 256 rows) unless N2V2R_TN_FORM=lines (the line form, A/B runs)
-static bool tn_stream_form() {
-  static const int v = [] {
-    const char* s = getenv("N2V2R_TN_FORM");
-    return (s && strcmp(s, "lines") == 0) ? 0 : 1;
-  }();
-  return v != 0;
-}
+// least 256 rows); the line form where its partials would not fit (the A/B switch retired in
+// round 5)
+static bool tn_stream_form() { return true; }
 #define TN_STREAM_WAVES 4096
 #define TN_STREAM_MIN_ROWS 256
 

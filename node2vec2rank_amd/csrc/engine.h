@@ -71,14 +71,9 @@ hipError_t n2v2r_launch_rr_band(const double* hband, int c, int kp, double* thet
                                 double* Y, float* S, int ldS, int p, int* err,
                                 hipStream_t stream);
 int n2v2r_rr_band_jm(int c);
-// b = 8 PIP passes use the fused Cholesky + apply launch unless N2V2R_PIP_FUSED=0 (A/B runs)
-inline bool pip_fused() {
-  static const bool v = [] {
-    const char* s = std::getenv("N2V2R_PIP_FUSED");
-    return !(s && s[0] == '0');
-  }();
-  return v;
-}
+// b = 8 PIP passes use the fused Cholesky + apply launch (its A/B switch retired in round 5;
+// the two-launch form serves b > 8 and bases beyond 512 columns)
+inline bool pip_fused() { return true; }
 hipError_t n2v2r_launch_ts_tn2(const BlockList& A, const float* Za, const float* Zb, int64_t n,
                                double* partial, size_t partial_elems, double* out,
                                hipStream_t stream);
@@ -185,11 +180,8 @@ inline bool rr_sturm_enabled() {
 }
 
 // Ritz vectors and images by one launch with the coefficients staged once per CU
-// (ritz_nn_kernel) unless N2V2R_RITZ_NN=0.  Read per fit.
-inline bool ritz_nn_enabled() {
-  const char* e = std::getenv("N2V2R_RITZ_NN");
-  return !(e && e[0] == '0');
-}
+// (ritz_nn_kernel) where it applies (its A/B switch retired in round 5)
+inline bool ritz_nn_enabled() { return true; }
 
 // Lean images (banded Sturm Rayleigh-Ritz, one GPU) unless N2V2R_LEAN_W=0.  Read per fit.
 inline bool lean_enabled() {

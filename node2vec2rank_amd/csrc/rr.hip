@@ -320,31 +320,10 @@ __device__ __forceinline__ bool trc_grid_barrier_sharded(unsigned* ctr, unsigned
   return *flag != 0;
 }
 
-// returns true when the wait timed out
-__device__ __forceinline__ bool trc_grid_barrier(unsigned* ctr, unsigned target, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int f = 0;
-    long it = 0;
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if (++it > (1l << 24)) {
-        f = 1;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    *flag = f;
-  }
-  __syncthreads();
-  return *flag != 0;
-}
-
 __global__ __launch_bounds__(TRC_NT) void rr_tridiag_coop_kernel(
     const double* __restrict__ A, int c, int PR, double* __restrict__ dd, double* __restrict__ ee,
     double* __restrict__ tau, double* __restrict__ V, double* part /* [2][PR][c] */,
-    double* rowbuf /* [2][c] */, unsigned* ctr, int* err, int sharded) {
+    double* rowbuf /* [2][c] */, unsigned* ctr, int* err) {
   constexpr int NW = TRC_NT / 64;
   extern __shared__ double lds[];
   const int nt = (c + TRC_TS - 1) / TRC_TS;
@@ -452,10 +431,9 @@ __global__ __launch_bounds__(TRC_NT) void rr_tridiag_coop_kernel(
   double t = make_reflector(v, 1, 0);
   pass(1, false, v, 0);
   unsigned nbar = 1;
-  auto grid_barrier = [&](unsigned nb) {
-    return sharded ? trc_grid_barrier_sharded(ctr, nb, &flag)
-                   : trc_grid_barrier(ctr, (unsigned)G * nb, &flag);
-  };
+  // (one counter for the whole grid instead of one per XCD group: 5.70 vs 5.15 ms per cfg3
+  // call, profiles/r05_cfg3_single_bar_kernel_stats.csv; removed)
+  auto grid_barrier = [&](unsigned nb) { return trc_grid_barrier_sharded(ctr, nb, &flag); };
   bool failed = grid_barrier(nbar);
   for (int k = 0; !failed; ++k) {
     const int o = k + 1, par = k & 1;
@@ -1095,16 +1073,13 @@ static hipError_t launch_rr_tridiag_coop(double* A, int c, double* d, double* e,
   int* err = reinterpret_cast<int*>(ctr + 1);  // 1 after a timed-out grid barrier
   hipError_t er = hipMemsetAsync(ctr, 0, sizeof(unsigned) * TRC_CTR_WORDS, stream);
   if (er != hipSuccess) return er;
-  // the grid barrier: sharded per XCD group (default) or one counter (N2V2R_RR_TRI_BAR=single)
-  const char* bev = std::getenv("N2V2R_RR_TRI_BAR");
-  int sharded = !(bev && bev[0] == 's' && bev[1] == 'i');
   // The grid barrier needs all PR x nt (<= 4 x 24) workgroups resident at once: a cooperative
   // launch, which the runtime refuses (instead of starting) when the grid cannot be co-resident
   // (+15-19 us of host time per call, a few calls per cfg3 fit).  Should a workgroup still be
   // held back -- another kernel of this process or another one occupying CUs -- the bounded spin
   // ends the launch with *err set and d[0] = NaN; the engine reads *err with the cycle's
   // read-back (n2v2r_rr_tridiag_err) and redoes the step with the one-workgroup kernel.
-  void* args[] = {&A, &c, &PR, &d, &e, &tau, &V, &part, &rowbuf, &ctr, &err, &sharded};
+  void* args[] = {&A, &c, &PR, &d, &e, &tau, &V, &part, &rowbuf, &ctr, &err};
   er = hipLaunchCooperativeKernel((const void*)rr_tridiag_coop_kernel, dim3((unsigned)(PR * nt)),
                                   dim3(TRC_NT), args, (unsigned)shmem, stream);
   if (er != hipSuccess) {

@@ -111,7 +111,7 @@ struct Eig {
   // next block's (a pair shares one read of the old basis once a two-block Gram exists); its
   // image keeps the uncorrected block, whose components along older blocks are removed from
   // the next block by that block's full pass.  `deferred`: the block awaiting its full pass.
-  bool defer = false, pair_gram = true;  // N2V2R_REORTH_PAIR=0: the two passes one by one
+  bool defer = false, pair_gram = true;
   float* deferred = nullptr;
   struct LeanRetry {};
   // Gram scratch of the orthogonalisation passes (the workspace's)
@@ -969,8 +969,7 @@ struct Eig {
       // images themselves, and a deferred block's image is the uncorrected block's
       defer = !(e && e[0] == '0') && b == 8 && pip_fused() && lean;
       deferred = nullptr;
-      const char* pg = std::getenv("N2V2R_REORTH_PAIR");
-      pair_gram = !(pg && pg[0] == '0');
+      pair_gram = true;  // (the A/B switch of the pairing retired in round 5)
       if (defer) {
         h->ews.g2.ensure(sizeof(double) * 2 * (size_t)(nb_max + 2) * 64, st);
         // R of the pair's first pass: the identity until a pass writes it
