@@ -1937,7 +1937,7 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
   // an in-place pass) those with max_ij |C_ij| / ||z_j|| > skip_tol; every workgroup decides
   // alike from the same G.  C^T C sums the applied blocks only, so R factors the applied pass.
   // (skip_tol < 0: the whole pass, all blocks or none, by |skip_tol|)
-  int* blist = badw + 4;  // compact list of applied blocks (<= 64)
+  int* blist = badw + 4;  // compact list of applied blocks (<= N2V2R_BAND_MAXC / 8)
   const int nblk = c >> 3;
   const bool skip_whole = skip_tol < 0.f;
   skip_tol = fabsf(skip_tol);
@@ -1962,17 +1962,27 @@ __global__ __launch_bounds__(256) void pip_fused_kernel(BlockList Q, const float
     zz_off = __ballot(fabs(gd[(c + i) * 8 + j] - (i == j ? 1.0 : 0.0)) > (double)skip_tol) != 0ull;
   }
   if (tid < 64) {
-    bool on = tid < nblk;
-    if (on && skip_tol > 0.f) on = bflag[tid] != 0;
-    unsigned long long m = __ballot(on);
-    if (skip_whole && m) {
-      m = nblk == 64 ? ~0ull : ((1ull << nblk) - 1ull);
-      on = tid < nblk;
+    // wave 0 compacts the verdicts 64 blocks at a time (bases up to N2V2R_BAND_MAXC columns:
+    // 80 blocks; round 4's single ballot covered 64, so blocks past 512 columns were never
+    // applied)
+    bool any_on = false;
+    for (int c0 = 0; c0 < nblk; c0 += 64) {
+      const int bk = c0 + tid;
+      const bool on = bk < nblk && (skip_tol <= 0.f || bflag[bk] != 0);
+      any_on |= __ballot(on) != 0ull;
     }
-    if (on) blist[__popcll(m & ((1ull << tid) - 1ull))] = tid;
-    if (skipped && lead && on && skip_tol > 0.f) atomicAdd(skipped + 1 + tid, 1);  // histogram
+    const bool all = skip_whole && any_on;
+    int count = 0;
+    for (int c0 = 0; c0 < nblk; c0 += 64) {
+      const int bk = c0 + tid;
+      const bool on = bk < nblk && (all || skip_tol <= 0.f || bflag[bk] != 0);
+      const unsigned long long m = __ballot(on);
+      if (on) blist[count + __popcll(m & ((1ull << tid) - 1ull))] = bk;
+      if (skipped && lead && on && skip_tol > 0.f) atomicAdd(skipped + 1 + bk, 1);  // histogram
+      count += __popcll(m);
+    }
     if (tid == 0) {
-      badw[1] = (int)__popcll(m);
+      badw[1] = count;
       badw[2] = zz_off;
       badw[3] = 0;
     }
@@ -2196,8 +2206,9 @@ extern "C" hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zi
   if (Q.width != 8 || c != Q.count * 8) return hipErrorInvalidValue;
   // a skipped block leaves Z in place; the band save reads G before the skipped rows are zeroed
   if (skip_tol != 0.f && (Zin != Zout || save)) return hipErrorInvalidValue;
-  const size_t lds = sizeof(double) * ((size_t)(c + 8) * 8 + 256) + sizeof(float) * ((size_t)c * 8 + 64) + 16 + 256;
-  if (lds > 64 * 1024 || c > 512) return hipErrorInvalidValue;
+  const size_t lds = sizeof(double) * ((size_t)(c + 8) * 8 + 256) + sizeof(float) * ((size_t)c * 8 + 64) + 16 +
+                     4 * (size_t)(c / 8 > 64 ? c / 8 : 64);
+  if (lds > 64 * 1024 || c > N2V2R_BAND_MAXC) return hipErrorInvalidValue;
   // rows per workgroup (64 or 128 per wave); 128 rows: cfg2 flat, cfg4 +20 % (every workgroup
   // stages the (c + 8) x 8 fp64 Gram, 33 KB at c = 512)
   // 512 rows per workgroup from N = 512k rows on (the per-workgroup prologue -- Gram staging,

@@ -27,7 +27,7 @@
 #include "common.h"
 
 #define RB_W 8
-#define RB_MAXC 512
+#define RB_MAXC N2V2R_BAND_MAXC
 #define RB_MAXNA 192
 #define RB_DONE_ALL 0x3fffffff
 

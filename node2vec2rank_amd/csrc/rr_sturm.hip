@@ -30,7 +30,7 @@
 #include "common.h"
 
 #define RS_W 8
-#define RS_MAXC 512
+#define RS_MAXC N2V2R_BAND_MAXC
 #define RS_BIS_THREADS 512  // points per multisection round (2 waves per SIMD)
 #define RS_HDR 4  // scratch header: glo, ghi, tn, (unused)
 #define RS_LD 10  // band row stride in the scratch (9 entries + 1 pad: 16-B aligned rows)

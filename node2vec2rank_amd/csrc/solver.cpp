@@ -571,7 +571,7 @@ struct Eig {
       if (zin == pending) materialize();
       tn(L, one(zin), gsm_p, cond);
     }
-    if (b == 8 && nq * b <= 512 && pip_fused()) {
+    if (b == 8 && nq * b <= N2V2R_BAND_MAXC && pip_fused()) {
       // b = 8: the Cholesky step runs inside the apply launch (every workgroup factors G)
       HIPCHK(n2v2r_launch_pip_fused(blocks(qz, 0, nq), zin, Z, gsm_p, nq * b,
                                     n, cond, flags_out, any_out, save, save_row0, save_rows,
@@ -665,7 +665,7 @@ struct Eig {
   bool pair_pass(float* zb, const std::vector<float*>& basis) {
     if (!deferred || basis.empty() || basis.back() != deferred) return false;
     const int nq_old = (int)basis.size() - 1;
-    if (nq_old + 2 > N2V2R_MAX_BLOCKS || (nq_old + 1) * 8 > 512) return false;
+    if (nq_old + 2 > N2V2R_MAX_BLOCKS || (nq_old + 1) * 8 > N2V2R_BAND_MAXC) return false;
     std::vector<float*> all(basis);
     all.push_back(zb);
     // sized for the largest basis when the fit starts (a growing buffer reallocated here cost a
@@ -807,8 +807,12 @@ struct Eig {
                                  ? keep
                                  : ((std::max(d + 16, (d * 5) / 4) + b - 1) / b) * b;
       const bool band_ok = b == 8 && !(o.solver_flags & N2V2R_EIG_DENSE_RR) && keep + b <= 512;
+      // (round 5: up to N2V2R_BAND_MAXC = 640 columns -- cfg4 786-791 block applications and
+      // 1.41-1.42 s per fit at c = 576-640 against 838 and 1.51 s at 512,
+      // profiles/r05_basis_b8.jsonl)
       maxc = o.max_basis ? o.max_basis
-                         : (band_ok ? std::min(512, std::max(keep + 3 * b, (24 * keep_basis) / 5))
+                         : (band_ok ? std::min(N2V2R_BAND_MAXC,
+                                               std::max(keep + 3 * b, (24 * keep_basis) / 5))
                                     : std::max(keep + 3 * b, (16 * keep_basis) / 5));
       maxc = ((maxc + b - 1) / b) * b;
       const int cap =
@@ -929,7 +933,7 @@ struct Eig {
     h->ews.anyflag.ensure(sizeof(int) * 4);
     h->theta.ensure(sizeof(double) * c_max);
     h->resid.ensure(sizeof(double) * c_max);
-    band_rr = b == 8 && !(o.solver_flags & N2V2R_EIG_DENSE_RR) && c_max <= 512 &&
+    band_rr = b == 8 && !(o.solver_flags & N2V2R_EIG_DENSE_RR) && c_max <= N2V2R_BAND_MAXC &&
               keep + 8 <= 192;
     if (band_rr) {
       h->ews.hband.ensure(sizeof(double) * ((size_t)(keep + b) * b + (size_t)nb_max * 2 * b * b));
@@ -982,8 +986,8 @@ struct Eig {
         HIPCHK(hipStreamSynchronize(st));
       }
     }
-    h->ews.skipc.ensure(sizeof(int) * 68);
-    HIPCHK(hipMemsetAsync(h->ews.skipc.p, 0, sizeof(int) * 68, st));
+    h->ews.skipc.ensure(sizeof(int) * (4 + N2V2R_BAND_MAXC / 8));  // [0]: skipped, [1 + blk]
+    HIPCHK(hipMemsetAsync(h->ews.skipc.p, 0, sizeof(int) * (4 + N2V2R_BAND_MAXC / 8), st));
     if (lean) h->ews.rres.ensure(sizeof(double) * 128);  // R of the restart block's two passes
     double est_scale = 1.0;  // lean: true / estimated residual seen at a failed final check
     double last_true = 1e300;  // lean: the worst true residual of the previous check
