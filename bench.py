@@ -414,6 +414,23 @@ def main():
     if cfg.get("dense") and n_gpus > 1:
         mode = "api"
     devices = list(range(n_gpus)) if n_gpus > 1 else None
+    if world > 1 and mode == "api" and devices:
+        # rank 0 drives every GPU of the node through the library; should a launcher have hidden
+        # the other GPUs from it, the same graph is row-partitioned one process per GPU instead
+        visible = n_gpus
+        if rank == 0:
+            try:
+                import torch
+                visible = torch.cuda.device_count()  # (does not initialise the GPU here)
+            except Exception:
+                pass
+        visible = int(group.bcast_bytes(str(visible).encode() if rank == 0 else None))
+        if visible < n_gpus:
+            if rank == 0:
+                print(f"warning: rank 0 sees {visible} of {n_gpus} GPUs; the graph is "
+                      f"row-partitioned one process per GPU instead", file=sys.stderr)
+            mode = "partitioned"
+            devices = None
     # (rehearsal on a one-GPU box: N2V2R_BENCH_DEVICES=0,0 runs the N > 1 path over a repeated
     # device -- the library's in-process thread communicator instead of RCCL)
     dev_env = os.environ.get("N2V2R_BENCH_DEVICES")
