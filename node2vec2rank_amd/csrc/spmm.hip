@@ -432,7 +432,9 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
   // and not kept (round 3-4, with per-row pointers; cfg4 layer launch 0.367 ms): windows handed
   // out per phase from an LDS counter (0.557 ms), the next window's row pointers loaded before
   // the current window's entries (flat); 512-thread workgroups with half the tile rows, 4 per CU
-  // (0.448 ms); a wave owning one contiguous span of 4 windows walked as one run: 0.393 ms
+  // (0.448 ms); a wave owning one contiguous span of 4 windows walked as one run: 0.393 ms.
+  // Round 5 (window offsets): two consecutive 64-row windows walked as one run, 0.351-0.356 vs
+  // 0.351-0.353 ms, fit 1,441 vs 1,424 ms (profiles/r05_span2_ab.jsonl)
   for (int w = wave; w < nwin; w += nwave)
     for (int rr = pr; rr < W; rr += 32) {
       const int lr = (w << wbits) + rr;
