@@ -106,14 +106,25 @@ struct ThreadComm : Comm {
     g->barrier();  // no rank rewrites its send buffer while another still reads it
   }
   const char* kind() const override { return "thread"; }
+  bool shares_device() const override {
+    std::lock_guard<std::mutex> lk(g->m);
+    for (int r = 0; r < world; ++r)
+      if (r != rank && g->dev[r] == g->dev[rank]) return true;
+    return false;
+  }
   void abort() override { g->abort(); }
 };
 
-std::unique_ptr<Comm> make_thread_comm(n2v2r_simgroup* g, int rank) {
+std::unique_ptr<Comm> make_thread_comm(n2v2r_simgroup* g, int rank, int device) {
   auto t = std::make_unique<ThreadComm>();
   t->g = g;
   t->rank = rank;
   t->world = g->world;
+  {
+    std::lock_guard<std::mutex> lk(g->m);
+    if (g->dev.size() != (size_t)g->world) g->dev.assign(g->world, -1);
+    g->dev[rank] = device;
+  }
   return t;
 }
 }  // namespace n2v2r_int
@@ -157,6 +168,7 @@ int n2v2r_simgroup_create(int world, n2v2r_simgroup** out) {
   g->world = world;
   g->ptrs.assign(world, nullptr);
   g->host.resize(world);
+  g->dev.assign(world, -1);
   *out = g;
   return N2V2R_OK;
 }
@@ -168,13 +180,9 @@ int n2v2r_create_sim(int device, n2v2r_simgroup* g, int rank, n2v2r_handle** out
   *out = nullptr;
   n2v2r_handle* h = new_handle(device);
   if (!h) return N2V2R_ERR_HIP;
-  auto c = std::make_unique<ThreadComm>();
-  c->g = g;
-  c->rank = rank;
-  c->world = g->world;
   h->rank = rank;
   h->world = g->world;
-  h->comm = std::move(c);
+  h->comm = make_thread_comm(g, rank, device);
   *out = h;
   return N2V2R_OK;
 }

@@ -370,6 +370,9 @@ struct Comm {
   virtual void reduce_scatter_sum_f32(const float* send, float* recv, size_t count,
                                       hipStream_t st) = 0;
   virtual const char* kind() const = 0;
+  // another rank of this communicator launches on this rank's device (the thread group's ranks
+  // may share one GPU; RCCL ranks never do)
+  virtual bool shares_device() const { return false; }
   // unblock this rank's pending collectives after a peer failed (the communicator is dead after)
   virtual void abort() {}
 };
@@ -399,6 +402,7 @@ struct n2v2r_simgroup {
   bool aborted = false;  // a rank failed: every barrier from here on throws (no rank hangs)
   std::vector<const void*> ptrs;
   std::vector<std::vector<unsigned char>> host;
+  std::vector<int> dev;  // each rank's device (-1 = not created yet), under m
   void barrier() {
     std::unique_lock<std::mutex> lk(m);
     const uint64_t gen = generation;
@@ -422,7 +426,7 @@ struct n2v2r_simgroup {
 
 namespace n2v2r_int {
 // in-process communicator of rank `rank` of the thread group g (comm.cpp)
-std::unique_ptr<Comm> make_thread_comm(n2v2r_simgroup* g, int rank);
+std::unique_ptr<Comm> make_thread_comm(n2v2r_simgroup* g, int rank, int device);
 
 // Solver buffers kept by the handle across n2v2r_uase calls (repeated fits of the same graph
 // reuse every allocation; the zero-filled padding rows of pool blocks stay zero).

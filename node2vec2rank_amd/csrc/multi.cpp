@@ -257,7 +257,7 @@ int n2v2r_create_multi(const int* devices, int n_gpus, n2v2r_handle** out) {
     r->rank = i;
     r->world = n_gpus;
     r->comm = distinct ? make_rccl_comm(comms[i], i, n_gpus)
-                       : make_thread_comm(h->own_group.get(), i);
+                       : make_thread_comm(h->own_group.get(), i, devices[i]);
     h->ranks.push_back(r);
   }
   *out = h;

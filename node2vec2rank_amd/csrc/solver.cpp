@@ -1089,10 +1089,10 @@ struct Eig {
         tn(blocks(Q, 0, nq), blocks(W, 0, nq), h->ews.gsmall.as<double>(), nullptr);
         dbg(h->ews.gsmall.p, (int64_t)c * c, true, "projected matrix H = Q^T W");
         lds_poison();
-        // thread-communicator ranks share one device: their concurrent launches of the
+        // ranks that share this device (thread group): their concurrent launches of the
         // multi-workgroup form could not all be resident, so they keep the one-workgroup kernel;
         // so does a fit whose multi-workgroup launch once timed out (tri_err below)
-        const bool shared_device = h->comm && std::strcmp(h->comm->kind(), "thread") == 0;
+        const bool shared_device = h->comm && h->comm->shares_device();
         const bool coop = !shared_device && !tri_single;
         tri_err = coop ? n2v2r_rr_tridiag_err(h->ews.trcoop.p, c) : nullptr;
         HIPCHK(n2v2r_launch_rr_tridiag(h->ews.gsmall.as<double>(), c, trid, trid + c_max,
