@@ -121,11 +121,13 @@ class _Group:
             self.dist.destroy_process_group()
 
 
-def _torch_sync():
+def _torch_sync(device=0):
+    """torch.cuda.synchronize on this process's own GPU (LOCAL_RANK): under torchrun every
+    process touches only its own device, never device 0 of every rank"""
     try:
         import torch
         if torch.cuda.is_available():
-            torch.cuda.synchronize()
+            torch.cuda.synchronize(device)
     except Exception:
         pass
 
@@ -364,12 +366,13 @@ def replicas_leg(group, cfg, args, local, rank, world):
     layers = synthetic.er_layers(cfg["n"], cfg["avg_deg"], 2, seed_base=1000 + 17 * rank)
     nodes = [f"n{i}" for i in range(cfg["n"])]
     api_step(layers, nodes, cfg, local)  # warm-up
-    _torch_sync()
+    _torch_sync(local)
     group.barrier()
     t0 = time.perf_counter()
     steps = max(1, args.steps)
     for _ in range(steps):
         api_step(layers, nodes, cfg, local)
+    _torch_sync(local)
     group.barrier()
     t = group.max(time.perf_counter() - t0) / steps
     return {"value": round(world * cfg["n"] / t, 1), "unit": "nodes/s",
@@ -484,12 +487,12 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    _torch_sync()
+    _torch_sync(local)
     group.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = step()
-    _torch_sync()
+    _torch_sync(local)
     group.barrier()
     elapsed = time.perf_counter() - t0
     elapsed_max = group.max(elapsed)
