@@ -1103,9 +1103,15 @@ __device__ __forceinline__ float coef_at(const Coef& F, int k, int j, int cb) {
 // rows and all output columns (NT 32-wide tiles), so O may alias A or C.  A rows are read as
 // 16-B loads; the k order inside each 8-column group is permuted consistently for A and F
 // (lane half h carries columns 4h..4h+3).  F is staged through LDS 64 rows at a time.
+#ifndef NN_KCH
 #define NN_KCH 64
+#endif
+#ifndef NN_WAVES
+#define NN_WAVES 4  // waves per workgroup (32 rows each), sharing one staged F chunk
+#endif
+#define NN_T (64 * NN_WAVES)
 template <int NT>
-__global__ __launch_bounds__(256) void ts_nn_kernel(BlockList A, Coef F, int cb, OutBlockList O,
+__global__ __launch_bounds__(NN_T) void ts_nn_kernel(BlockList A, Coef F, int cb, OutBlockList O,
                                                     BlockList C, float alpha, float beta,
                                                     int64_t n, const int* cond, const int* flags,
                                                     uint64_t seed, int64_t row0) {
@@ -1113,7 +1119,7 @@ __global__ __launch_bounds__(256) void ts_nn_kernel(BlockList A, Coef F, int cb,
   __shared__ __attribute__((aligned(16))) float fs[NN_KCH][NT * 32];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 32;
+  const int64_t r0 = ((int64_t)blockIdx.x * NN_WAVES + wave) * 32;
   const int i = lane & 31;
   const int h = lane >> 5;
   const int64_t row = r0 + i;
@@ -1139,11 +1145,12 @@ __global__ __launch_bounds__(256) void ts_nn_kernel(BlockList A, Coef F, int cb,
     }
     if (F.G && vec4) {  // plain coefficients, 16-B aligned: 6 float4 loads per thread in flight
       constexpr int R4 = NT * 8;  // float4 per staged row
-      constexpr int PER = NN_KCH * R4 / 256;
+      constexpr int PER = NN_KCH * R4 / NN_T;
+      static_assert(PER >= 1 && PER * NN_T == NN_KCH * R4, "F chunk split over the threads");
       f32x4 tv[PER];
 #pragma unroll
       for (int u = 0; u < PER; ++u) {
-        const int e = threadIdx.x + u * 256;
+        const int e = threadIdx.x + u * NN_T;
         const int k = e / R4, j = (e % R4) * 4;
         const bool ok = k < kn && j < cb;
         const f32x4 v = *reinterpret_cast<const f32x4*>(F.G + (ok ? (int64_t)(k0 + k) * F.ldg + j : 0));
@@ -1152,7 +1159,7 @@ __global__ __launch_bounds__(256) void ts_nn_kernel(BlockList A, Coef F, int cb,
       __syncthreads();
 #pragma unroll
       for (int u = 0; u < PER; ++u) {
-        const int e = threadIdx.x + u * 256;
+        const int e = threadIdx.x + u * NN_T;
         *reinterpret_cast<f32x4*>(&fs[e / R4][(e % R4) * 4]) = tv[u];
       }
     } else {
@@ -1426,12 +1433,12 @@ static hipError_t launch_nn(const BlockList& A, const Coef& F, int cb, const Out
                        stream, A, F, cb, O, C, alpha, beta, n, cond, flags, seed, row0);
     return hipGetLastError();
   }
-  dim3 grid((unsigned)((n + 127) / 128));
+  dim3 grid((unsigned)((n + 32 * NN_WAVES - 1) / (32 * NN_WAVES)));
   switch ((cb + 31) / 32) {
-    case 1: hipLaunchKernelGGL(ts_nn_kernel<1>, grid, dim3(256), 0, stream, A, F, cb, O, C, alpha, beta, n, cond, flags, seed, row0); break;
-    case 2: hipLaunchKernelGGL(ts_nn_kernel<2>, grid, dim3(256), 0, stream, A, F, cb, O, C, alpha, beta, n, cond, flags, seed, row0); break;
-    case 3: hipLaunchKernelGGL(ts_nn_kernel<3>, grid, dim3(256), 0, stream, A, F, cb, O, C, alpha, beta, n, cond, flags, seed, row0); break;
-    case 4: hipLaunchKernelGGL(ts_nn_kernel<4>, grid, dim3(256), 0, stream, A, F, cb, O, C, alpha, beta, n, cond, flags, seed, row0); break;
+    case 1: hipLaunchKernelGGL(ts_nn_kernel<1>, grid, dim3(NN_T), 0, stream, A, F, cb, O, C, alpha, beta, n, cond, flags, seed, row0); break;
+    case 2: hipLaunchKernelGGL(ts_nn_kernel<2>, grid, dim3(NN_T), 0, stream, A, F, cb, O, C, alpha, beta, n, cond, flags, seed, row0); break;
+    case 3: hipLaunchKernelGGL(ts_nn_kernel<3>, grid, dim3(NN_T), 0, stream, A, F, cb, O, C, alpha, beta, n, cond, flags, seed, row0); break;
+    case 4: hipLaunchKernelGGL(ts_nn_kernel<4>, grid, dim3(NN_T), 0, stream, A, F, cb, O, C, alpha, beta, n, cond, flags, seed, row0); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
