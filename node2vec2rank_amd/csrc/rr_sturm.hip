@@ -10,7 +10,8 @@
 // Schur update lands in the 8 x 8 E block), then the band, one row per step with a 9 x 9 window
 // kept in registers (unrolled by 9 so the window shift is register renaming).  Pivots smaller
 // than eps ||H|| are replaced by -eps ||H|| (dstebz's rule, at the matrix's own noise level).
-// One workgroup per wanted eigenvalue runs a 256-point multisection, like rr_bisect_kernel.
+// The wanted eigenvalues are bracketed by a multisection over all CUs (rr_msect_kernel; round 4
+// replaced one 512-point multisection workgroup per eigenvalue, its A/B switch retired round 5).
 // Eigenvectors: inverse iteration on the same structure, one 64-thread workgroup per cluster
 // start (its members in order): the X rows eliminated exactly (their Schur complement is an
 // 8 x 8 update of the E block), then the same symmetric elimination of the band as the Sturm
@@ -31,7 +32,6 @@
 
 #define RS_W 8
 #define RS_MAXC N2V2R_BAND_MAXC
-#define RS_BIS_THREADS 512  // points per multisection round (2 waves per SIMD)
 #define RS_HDR 4  // scratch header: glo, ghi, tn, (unused)
 #define RS_LD 10  // band row stride in the scratch (9 entries + 1 pad: 16-B aligned rows)
 #define RS_PADR 10  // zero rows past c (the elimination reads up to row c + 9)
@@ -246,97 +246,6 @@ __device__ __forceinline__ int rs_count(double x, int c, int kp, const double* _
   }
 #undef RS_CSTEP
   return neg;
-}
-
-// One workgroup per wanted eigenvalue j (j-th largest), 256-point multisection.  Round 0 for
-// a kept index (j < kp) is anchored on the previous Ritz value theta_j, a lower bound by
-// interlacing (diag(Theta) is a principal submatrix of H): half the points at theta_j + tn
-// 10^(-16 + 16 t / 128) (log-spaced: a converged pair brackets to a width of a third of its
-// shift), half uniform on the Gershgorin interval; the two brackets are intersected.  Later
-// rounds are uniform, until the bracket is below 1e-11 ||H|| (the Rayleigh quotient of the
-// inverse-iteration vector refines the value).
-__global__ __launch_bounds__(RS_BIS_THREADS, RS_BIS_THREADS / 256) void rr_sturm_bisect_kernel(const double* __restrict__ scr,
-                                                                        int c, int kp, int p,
-                                                                        double* __restrict__ w) {
-  extern __shared__ __attribute__((aligned(16))) double sl[];
-  __shared__ int cnt[RS_BIS_THREADS];
-  __shared__ double xs[RS_BIS_THREADS];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nb = c - kp;
-  const int total = kp + kp * RS_W + (nb + RS_PADR) * RS_LD;
-  stage_to_lds<RS_BIS_THREADS, 8>(sl, scr + RS_HDR, total, tid);
-  __syncthreads();
-  const double* Xd = sl;
-  const double* Xg = sl + kp;
-  const double* Lb = Xg + kp * RS_W;
-  const double tn = fmax(scr[2], 1e-300);
-  const double tiny = 2.220446049250313e-16 * tn;
-  double lo = scr[0] - 1e-14 * tn - 1e-300, hi = scr[1] + 1e-14 * tn + 1e-300;
-  const int jw = (int)blockIdx.x;
-  const int a = c - 1 - jw;  // ascending index of the wanted eigenvalue
-  constexpr int HALF = RS_BIS_THREADS / 2;
-  for (int round = 0; round < 8; ++round) {
-    const bool anchored = round == 0 && jw < kp;
-    double x;
-    if (anchored) {
-      x = (tid < HALF) ? Xd[jw] + tn * exp10(-16.0 + 16.0 * (double)tid / HALF)
-                       : lo + (hi - lo) * (double)(tid - HALF + 1) / (double)(HALF + 1);
-    } else {
-      x = lo + (hi - lo) * (double)(tid + 1) / (double)(RS_BIS_THREADS + 1);
-    }
-    const int neg = rs_count(x, c, kp, Xd, Xg, Lb, tiny);
-    __syncthreads();
-    cnt[tid] = neg;
-    xs[tid] = x;
-    __syncthreads();
-    // lambda_a in (x_{t-1}, x_t] for the first t with nu(x_t) > a, per increasing point set
-    // (a count perturbed by rounding cannot send the bracket backwards: the first such t)
-    const int s0 = (anchored && tid >= HALF) ? HALF : 0;
-    int first = RS_BIS_THREADS;
-    if (cnt[tid] > a && (tid == s0 || cnt[tid - 1] <= a)) first = tid;
-    if (anchored) {
-      // first hit in each half: lanes of waves 0-1 (half A) and 2-3 (half B) reduced apart
-      for (int o = 32; o >= 1; o >>= 1) first = min(first, __shfl_xor(first, o, 64));
-      __syncthreads();
-      if (lane == 0) cnt[wave] = first;
-      __syncthreads();
-      int fa = RS_BIS_THREADS, fb = RS_BIS_THREADS;
-#pragma unroll
-      for (int v = 0; v < RS_BIS_THREADS / 64; ++v) {
-        if (v < RS_BIS_THREADS / 128) fa = min(fa, cnt[v]);
-        else fb = min(fb, cnt[v]);
-      }
-      // half A: points are theta_j + offsets (a miss: lambda above the last one)
-      double alo = (fa == 0) ? lo : ((fa >= HALF) ? xs[HALF - 1] : xs[fa - 1]);
-      double ahi = (fa >= HALF) ? hi : xs[fa];
-      if (fa == 0) alo = fmax(lo, Xd[jw] - 1e-14 * tn);  // lambda_j >= theta_j (interlacing)
-      const double blo = (fb == HALF) ? lo : xs[fb - 1];
-      const double bhi = (fb >= RS_BIS_THREADS) ? hi : xs[fb];
-      const double nlo = fmax(alo, (fb >= RS_BIS_THREADS) ? xs[RS_BIS_THREADS - 1] : blo);
-      const double nhi = fmin(ahi, bhi);
-      if (nlo < nhi) {
-        lo = nlo;
-        hi = nhi;
-      }
-    } else {
-      for (int o = 32; o >= 1; o >>= 1) first = min(first, __shfl_xor(first, o, 64));
-      __syncthreads();
-      if (lane == 0) cnt[wave] = first;
-      __syncthreads();
-#pragma unroll
-      for (int v = 0; v < RS_BIS_THREADS / 64; ++v) first = min(first, cnt[v]);
-      const double step = (hi - lo) / (double)(RS_BIS_THREADS + 1);
-      const double nlo = lo + step * first;
-      const double nhi = (first < RS_BIS_THREADS) ? lo + step * (first + 1) : hi;
-      lo = nlo;
-      hi = nhi;
-    }
-    // 1e-11 ||H||: two orders below the cluster threshold; the inverse iteration's Rayleigh
-    // quotient then gives the eigenvalue to fp64 accuracy
-    if (hi - lo <= fmax(1e-11 * tn, 8.0 * 2.220446049250313e-16 * fmax(fabs(lo), fabs(hi)))) break;
-    __syncthreads();
-  }
-  if (tid == 0) w[blockIdx.x] = 0.5 * (lo + hi);
 }
 
 // ---- global multisection (all CUs) ---------------------------------------------------------
@@ -933,8 +842,6 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
   ms.cnt[1] = ms.cnt[0] + (size_t)pm * M;
   static bool attr = false;
   if (!attr) {  // room for the dynamic LDS checked below (the static arrays stay under 10 KB)
-    hipError_t a1 = hipFuncSetAttribute((const void*)rr_sturm_bisect_kernel,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     hipError_t a2 = hipFuncSetAttribute((const void*)rr_sturm_inviter_kernel,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     hipError_t a5 = hipFuncSetAttribute((const void*)rr_sturm_prep_kernel,
@@ -944,14 +851,13 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     if (a2 == hipSuccess) a2 = a3;
     (void)hipGetLastError();  // a refused attribute must not surface as a later launch error
-    if (a1 != hipSuccess) return a1;
     if (a2 != hipSuccess) return a2;
     attr = true;
   }
   const size_t asm_d = rs_asm_elems(c, kp);
-  const size_t lbis = sizeof(double) * (asm_d - RS_HDR);
+  const size_t lms = sizeof(double) * (asm_d - RS_HDR);  // the multisection's assembled H
   const size_t linv = rs_inviter_lds(c, kp);
-  if (lbis > 150 * 1024 || linv > 150 * 1024) return hipErrorInvalidValue;
+  if (lms > 150 * 1024 || linv > 150 * 1024) return hipErrorInvalidValue;
   const size_t lprep = sizeof(double) * ((size_t)(kp + RS_W) * RS_W + (size_t)((c - kp) / RS_W - 1) * 2 * RS_W * RS_W);
   if (lprep > 150 * 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(rr_sturm_prep_kernel, dim3(1), dim3(256), lprep, stream, hband, c, kp, theta, scr);
@@ -959,15 +865,7 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
   if (e != hipSuccess) return e;
   // theta holds the kept Ritz values (kp) until the prep kernel has copied them; the
   // bisection writes wbis, the inverse iteration the refined values into theta
-  static const bool per_wg = [] {  // N2V2R_RR_MSECT=wg: one multisection per workgroup (A/B)
-    const char* v = getenv("N2V2R_RR_MSECT");
-    return v && v[0] == 'w';
-  }();
-  if (per_wg) {
-    hipLaunchKernelGGL(rr_sturm_bisect_kernel, dim3((unsigned)pm), dim3(RS_BIS_THREADS), lbis, stream,
-                       scr, c, kp, pm, wbis);
-  } else {
-    const size_t lms = sizeof(double) * (asm_d - RS_HDR);
+  {
     const unsigned grid = (unsigned)(pm * (M / nt_ms));
     // rounds until the bracket is below 1e-10 ||H|| (3 at p = 80, M = 768; 4 at p = 160, M = 256)
     int rounds = 1;
