@@ -786,7 +786,9 @@ struct Eig {
     int keep = 0, maxc = 0;
     // CSR layers: keep 21d/16 (rounded up to b) -- round 4, on two graphs each: cfg4 795-838
     // block applications against 812-856 at the former 5d/4 (1.51-1.59 vs 1.53-1.63 s), cfg2
-    // (84 -> 88) 270 against 276-314, and 11d/8 mixed (profiles/r04_keep_sweep.jsonl)
+    // (84 -> 88) 270 against 276-314, and 11d/8 mixed (profiles/r04_keep_sweep.jsonl); round 5
+    // at basis 640, cfg4: keep 152 / 168 / 184 / 200 / 224 / 256 -> 812 / 788 / 821 / 795 / 808
+    // / 800 block applications (profiles/r05_keep_b8.jsonl)
     // dense layers (b = 32): keep d + b, basis <= 704 -- on three cfg3-family graphs 61 block
     // applications and 215-218 ms per fit against 66 and 236-240 ms with the general rule's
     // keep 5d/4 = 320 and basis 768 (profiles/r04_cfg3_sweep*.jsonl)
