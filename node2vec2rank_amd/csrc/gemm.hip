@@ -217,6 +217,15 @@ extern "C" hipError_t n2v2r_launch_dense_gemm(const float* A, int64_t lda, int64
 // its workgroup's k range; the 4 quarters are summed in LDS in fixed order, split-K slabs over
 // grid.y are folded by dense_fold_kernel (deterministic).  dense_gemm_kernel above stages A
 // through LDS as the A operand: 0.39 ms per cfg3 launch (0.50 of HBM, MFMA busy 0.45).
+// k pairs per load stage: 6 (cfg3 fit 212.1 ms) against 8 (215.9), 4 (217.4 at 3 workgroups per
+// CU), 12 (222.8), 16 at one workgroup per CU (238.1); 3 workgroups per CU at 6 / 8: 212.9 /
+// 219.8 (profiles/r05_dense_tn_stages.txt)
+#ifndef DTN_D
+#define DTN_D 6
+#endif
+#ifndef DTN_OCC
+#define DTN_OCC 2  // workgroups per CU the register budget is sized for
+#endif
 template <int DT_D, int OCC, bool NTB>
 __global__ __launch_bounds__(256, OCC) void dense_tn_kernel(const float* __restrict__ B, int64_t ldb,
                                                           int64_t ncols, int64_t kdim, int64_t kper,
@@ -343,7 +352,7 @@ extern "C" hipError_t n2v2r_launch_dense_tn(const float* B, int64_t ldb, int64_t
   kper = (kper + 7) & ~(int64_t)7;
   nsplit = (kdim + kper - 1) / kper;
   static const bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)dense_tn_kernel<8, 2, true>,
+    (void)hipFuncSetAttribute((const void*)dense_tn_kernel<DTN_D, DTN_OCC, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 33 * 4);
     (void)hipGetLastError();
     return true;
@@ -352,7 +361,7 @@ extern "C" hipError_t n2v2r_launch_dense_tn(const float* B, int64_t ldb, int64_t
   const dim3 grid((unsigned)tiles, (unsigned)nsplit);
   // the stored matrix (read once per launch, 1.6 GB per cfg3 layer) loaded non-temporally:
   // cfg3 fit 216.3 vs 219.5 ms (profiles/r05_dense_nt.jsonl)
-  hipLaunchKernelGGL((dense_tn_kernel<8, 2, true>), grid, dim3(256), 128 * 33 * sizeof(float),
+  hipLaunchKernelGGL((dense_tn_kernel<DTN_D, DTN_OCC, true>), grid, dim3(256), 128 * 33 * sizeof(float),
                      stream, B, ldb, ncols, kdim, kper, X, ldx, b, work, (int64_t)b, ncols * b);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
