@@ -21,8 +21,9 @@ Extra keys:
     launch (for the launch form that runs) / mean launch time; rocprofv3 summaries of the same
     command are committed under profiles/;
   * ``cpu_baseline`` (rank 0, N=1): BASELINE.md 3's faithful CPU restatement (ARPACK svds,
-    per-row scipy distances, O(C N^2) list.index Borda over a joblib pool) and its fast variant,
-    on all host cores available to the process (capped at 16, the box's CPU share), on a bounded
+    per-row scipy distances, O(C N^2) list.index Borda over a joblib pool of n_jobs=-2 = the
+    CPUs available to the process (its cgroup quota, else its affinity mask) minus one, as the
+    reference's model_utils.py:31-32) and its fast variant, on a bounded
     sample of the same graph family; full-size CPU time extrapolated (labelled) from it.
 
 Multi-GPU, --gpus N > 1 (cfg1-4; with or without torchrun): the headline is the SAME drop-in
@@ -182,6 +183,23 @@ def _cpu_info():
     return model, blas
 
 
+def host_cpus():
+    """CPUs this process may use: the cgroup CPU quota when one is set (the GPU box gives a
+    one-GPU job a share of a large host whose os.cpu_count() / affinity list every CPU), else the
+    affinity mask."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            return max(1, int(int(quota) // int(period))), "cgroup cpu.max"
+    except (OSError, ValueError):
+        pass
+    try:
+        return len(os.sched_getaffinity(0)), "affinity"
+    except AttributeError:
+        return os.cpu_count() or 1, "os.cpu_count"
+
+
 def _sample_layers(cfg, n, seed_base=7000):
     from node2vec2rank_amd import synthetic
     if cfg.get("dense"):
@@ -234,7 +252,7 @@ def cpu_baseline(cfg, n_faithful, workers, blas_threads=1):
            f"2-layer ER avg-deg {cfg['avg_deg']:g}")
     return {
         "value": round(n_faithful * ncmp / tot_fa, 1), "unit": "nodes/s", "cores": workers,
-        "kind": "port",
+        "kind": "port", "blas_threads": blas_threads,
         "sample": (f"{fam} N={n_faithful}, d={cfg['d']}, dims {list(cfg['dims'])} x "
                    f"cosine+euclidean, sequential: oracle faithful mode (ARPACK svds, per-row "
                    f"scipy distances, O(C N^2) list.index Borda over a {workers}-process joblib "
@@ -643,9 +661,13 @@ def main():
 
             result[key] = run_guarded(_leg, limit, _expire)
     if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
-        workers = max(1, min(16, os.cpu_count() or 1))
+        avail, how = host_cpus()
+        # the reference's pool: joblib n_jobs=-2 = all CPUs but one (model_utils.py:31-32)
+        workers = max(1, avail - 1)
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample or CPU_SAMPLE[args.config],
                                               workers)
+        result["cpu_baseline"]["host"]["cpus_available"] = avail
+        result["cpu_baseline"]["host"]["cpus_available_from"] = how
     if rank == 0:
         print(json.dumps(result), flush=True)
     if eng is not None:

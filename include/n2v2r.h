@@ -65,7 +65,10 @@ enum { N2V2R_EIG_FULL_FIRST_PASS = 1, N2V2R_EIG_DENSE_RR = 2,
                                    n2v2r_eig_stats.gpu_ms_spmm / spmm_timed_launches (the in-fit
                                    roofline of bench.py; adds an event pair per launch) */,
        N2V2R_EIG_TEST_NO_STAGNATION = 64 /* tests: no stop on flat residuals (the fit runs until
-                                            every residual meets tol or max_restarts) */ };
+                                            every residual meets tol or max_restarts) */,
+       N2V2R_EIG_TEST_FAIL_ALONE = 128 /* tests, multi-GPU handles: rank 1 fails alone after its
+                                          first block application while its peers go on into
+                                          their next collective (the abort path) */ };
 
 typedef struct n2v2r_handle n2v2r_handle;
 typedef struct n2v2r_simgroup n2v2r_simgroup;

@@ -28,6 +28,7 @@ ERR_RCCL = 9
 AGG_BORDA, AGG_NONE = 0, -1
 EIG_TIME_SPMM = 16
 EIG_TEST_NO_STAGNATION = 64
+EIG_TEST_FAIL_ALONE = 128
 
 STRATEGY = {"sequential": 0, "one_vs_before": 1, "one_vs_rest": 2}
 METRIC = {"cosine": 0, "euclidean": 1, "correlation": 2}

@@ -2,36 +2,57 @@
 // thread group (W ranks on one device), and their C-ABI constructors.
 #include "engine.h"
 
+#include <atomic>
+#include <shared_mutex>
+
 using namespace n2v2r_int;
 
 namespace n2v2r_int {
+// abort() may come from the multi handle's coordinator thread while rank threads enqueue
+// collectives on the same communicator.  `aborted` is atomic and every operation checks it
+// under a shared lock held only while it enqueues (the host call returns once the collective is
+// queued; a rank stuck later waits in its stream synchronisation, which the abort unblocks), so
+// no operation is enqueued on a communicator ncclCommAbort has freed: it throws NcclFail
+// (ncclInvalidUsage) instead.  The abort takes the lock exclusively, waiting at most 2 s for
+// enqueues in progress (an enqueue that never returns must not keep the peers hanging).
 struct RcclComm : Comm {
   ncclComm_t c = nullptr;
-  bool aborted = false;
+  std::atomic<bool> aborted{false};
+  std::shared_timed_mutex mu;
   ~RcclComm() override {
-    if (c && !aborted) (void)ncclCommDestroy(c);
+    if (c && !aborted.load()) (void)ncclCommDestroy(c);
   }
   void abort() override {
-    if (c && !aborted) {
-      aborted = true;
-      (void)ncclCommAbort(c);
-    }
+    const bool locked = mu.try_lock_for(std::chrono::seconds(2));
+    if (c && !aborted.exchange(true)) (void)ncclCommAbort(c);
+    if (locked) mu.unlock();
+  }
+  template <class F>
+  void op(const char* what, F&& f) {
+    std::shared_lock<std::shared_timed_mutex> lk(mu);
+    if (aborted.load()) throw NcclFail{ncclInvalidUsage, std::string(what) + " (communicator aborted)"};
+    const ncclResult_t r = f();
+    if (r != ncclSuccess) throw NcclFail{r, what};
   }
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t st) override {
-    NCCLCHK(ncclAllGather(send, recv, bytes, ncclChar, c, st));
+    op("ncclAllGather", [&] { return ncclAllGather(send, recv, bytes, ncclChar, c, st); });
   }
   void allreduce_sum_f64(double* buf, size_t count, hipStream_t st) override {
-    NCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c, st));
+    op("ncclAllReduce(f64 sum)",
+       [&] { return ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c, st); });
   }
   void allreduce_max_u64(unsigned long long* buf, size_t count, hipStream_t st) override {
-    NCCLCHK(ncclAllReduce(buf, buf, count, ncclUint64, ncclMax, c, st));
+    op("ncclAllReduce(u64 max)",
+       [&] { return ncclAllReduce(buf, buf, count, ncclUint64, ncclMax, c, st); });
   }
   void allreduce_sum_f32(float* buf, size_t count, hipStream_t st) override {
-    NCCLCHK(ncclAllReduce(buf, buf, count, ncclFloat, ncclSum, c, st));
+    op("ncclAllReduce(f32 sum)",
+       [&] { return ncclAllReduce(buf, buf, count, ncclFloat, ncclSum, c, st); });
   }
   void reduce_scatter_sum_f32(const float* send, float* recv, size_t count,
                               hipStream_t st) override {
-    NCCLCHK(ncclReduceScatter(send, recv, count, ncclFloat, ncclSum, c, st));
+    op("ncclReduceScatter",
+       [&] { return ncclReduceScatter(send, recv, count, ncclFloat, ncclSum, c, st); });
   }
   const char* kind() const override { return "rccl"; }
 };

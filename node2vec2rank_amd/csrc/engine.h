@@ -443,7 +443,8 @@ struct EigWorkspace {
   DevBuf hband, band, varr, taua, rrerr;      // banded RR: band columns, band matrix, arrow
   DevBuf fcoef;                               // fp32 [-C R^-1; R^-1] of the apply pass
   DevBuf dbgflag;                             // N2V2R_DEBUG_FINITE result flag
-  DevBuf s2part;                              // [K][npad][8] XCD-split second-stage outputs
+  DevBuf tflag;                               // partitioned: a per-cycle flag agreed over ranks
+  DevBuf s2part;                             // [K][npad][8] XCD-split second-stage outputs
   DevBuf g2, pair_ra;                         // paired full passes: the two Grams, R of the first
   DevBuf sturm;                               // Sturm Rayleigh-Ritz: assembled arrow + band
   DevBuf rres;                                // lean images: R of the restart projection

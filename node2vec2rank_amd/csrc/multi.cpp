@@ -159,6 +159,16 @@ int multi_set_layer_dense(n2v2r_handle* h, int k, int64_t n, const float* A, int
 }
 
 int multi_column_sums(n2v2r_handle* h, int k, float* out) {
+  // validated here, alike for every rank (rank 0 alone would see a null `out`, and the others
+  // would wait for it in the all-gather)
+  if (!out) {
+    h->err = "column sums: null output buffer";
+    return N2V2R_ERR_BAD_ARG;
+  }
+  if (k < 0 || k >= h->K) {
+    h->set_err("column sums: layer %d out of range [0, %d)", k, h->K);
+    return N2V2R_ERR_BAD_ARG;
+  }
   // every rank returns the global sums (an all-gather inside); rank 0 writes the caller's buffer
   std::vector<std::vector<float>> tmp(h->ranks.size());
   return fanout(h, [&](n2v2r_handle* r, int i) {

@@ -1000,6 +1000,7 @@ struct Eig {
                              sizeof(double) * 64 + sizeof(float) * 8 * (size_t)keep;
 
     h->ews.dbgflag.ensure(sizeof(int) * 4);
+    h->ews.tflag.ensure(sizeof(double) * 2);
     poison_scratch();
     std::vector<double> wh(keep);
     std::vector<double> res2(keep);
@@ -1014,6 +1015,8 @@ struct Eig {
     apply_M(Q[0], W[0]);
     if (debug_finite()) materialize();
     dbg(W[0], n * b, false, "SpMM image of the start block");
+    if ((o.solver_flags & N2V2R_EIG_TEST_FAIL_ALONE) && h->comm && h->rank == 1)
+      throw StatusFail{N2V2R_ERR_INTERNAL, "test: rank 1 fails alone"};
     int apps = 1;
     int cycle = 0;
     double maxres = 0;
@@ -1237,6 +1240,19 @@ struct Eig {
                 pflag[3], keep);
       int refilled = lazy ? pflag[1] : 0;
       t_ortho += now_ms() - to0;
+      if (dense_rr && h->comm) {
+        // each rank read its own device's error word: agree on it (max over ranks) before
+        // branching, so every rank redoes the step together (a rank that alone went back to
+        // rayleigh_ritz would run one more all-reduce of H than its peers)
+        double* fl = h->ews.tflag.as<double>();
+        const double mine = pflag[4] ? 1.0 : 0.0;
+        HIPCHK(hipMemcpyAsync(fl, &mine, sizeof(double), hipMemcpyHostToDevice, st));
+        h->allreduce_f64(fl, 1);
+        double any_to = 0.0;
+        HIPCHK(hipMemcpyAsync(&any_to, fl, sizeof(double), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        pflag[4] = any_to > 0.0 ? 1 : 0;
+      }
       if (dense_rr && pflag[4]) {
         // the multi-workgroup tridiagonalisation's grid barrier timed out (a workgroup was not
         // resident): its output is invalid; this cycle's Rayleigh-Ritz again, and every later

@@ -101,8 +101,9 @@ class N2V2R:
         # one host thread per GPU inside the library, RCCL between them); the frames are the same
         if devices is None and n_gpus is not None and int(n_gpus) > 1:
             devices = list(range(int(n_gpus)))
-        self._device = tuple(int(d) for d in devices) if devices and len(devices) > 1 else (
-            int(devices[0]) if devices else device)
+        # (an explicit `devices` list is a multi-GPU engine even with one entry: [0] is a one-rank
+        # RCCL communicator, every collective of the partitioned path through RCCL)
+        self._device = tuple(int(d) for d in devices) if devices else device
         if tie_order not in ("reference", "stable"):
             raise ValueError(f"unknown tie_order {tie_order!r}")
         self.tie_order = tie_order

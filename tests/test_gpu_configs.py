@@ -224,7 +224,7 @@ def test_cfg3_dense_full_size(engine):
     layers = synthetic.corr_layers(20_000, 4)
     engine.set_layers(layers, storage="dense", symmetric=1)
     st = engine.uase(256, seed=42)
-    assert st["converged"] == 256 or st["stagnated"], st
+    assert st["converged"] == 256 or (st["stagnated"] and st["max_residual"] <= st["stag_cap"]), st
     s = engine.singular_values()
     theta = s ** 2
     U = engine.left_embedding() / np.sqrt(s)[None, :].astype(np.float32)
@@ -335,7 +335,7 @@ def test_cfg5_path_w8_one_million(engine):
 
     res = _run_ranks(world, fn, timeout=600)
     for r in res:
-        assert r["st"]["converged"] == d or r["st"]["stagnated"] == 1, r["st"]
+        assert r["st"]["converged"] == d or (r["st"]["stagnated"] == 1 and r["st"]["max_residual"] <= r["st"]["stag_cap"]), r["st"]
     for r in res[1:]:
         np.testing.assert_array_equal(r["s"], res[0]["s"])
         np.testing.assert_array_equal(r["D"], res[0]["D"])
@@ -355,7 +355,7 @@ def test_cfg5_path_w8_one_million(engine):
         s_r = reng.singular_values()
     finally:
         reng.close()
-    assert st_r["converged"] == d or st_r["stagnated"] == 1, st_r
+    assert st_r["converged"] == d or (st_r["stagnated"] == 1 and st_r["max_residual"] <= st_r["stag_cap"]), st_r
     np.testing.assert_allclose(s_r, s1, rtol=1e-5)
     X = np.concatenate([r["X"] for r in res], axis=0)
     U = X / np.sqrt(res[0]["s"])[None, :].astype(np.float32)

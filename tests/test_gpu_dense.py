@@ -67,7 +67,7 @@ def test_uase_dense_corr_residuals(engine):
     engine.set_layers(layers)
     assert engine.storage == "dense"
     st = engine.uase(d, seed=42)
-    assert st["converged"] == d or st["stagnated"] == 1, st
+    assert st["converged"] == d or (st["stagnated"] == 1 and st["max_residual"] <= st["stag_cap"]), st
     s = engine.singular_values()
     X = engine.left_embedding().astype(np.float64) / np.sqrt(s)[None, :]
     A = np.hstack([a.astype(np.float64) for a in layers])

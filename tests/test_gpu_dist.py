@@ -154,7 +154,7 @@ def test_partitioned_er_large_rows_ingest(engine):
     np.testing.assert_allclose(res[0]["s"], one["s"], rtol=1e-5)
     for r in res:
         st = r["stats"]
-        assert st["converged"] == d or st["stagnated"] == 1, st
+        assert st["converged"] == d or (st["stagnated"] == 1 and st["max_residual"] <= st["stag_cap"]), st
     # Ritz residual of the gathered result in fp64
     M = sum((A @ A.T) for A in layers)
     U = X / np.sqrt(res[0]["s"])[None, :]

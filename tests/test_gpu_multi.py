@@ -78,6 +78,8 @@ def test_api_multi_lowrank_exact_bit_exact(devices):
     m = N2V2R(layers, nodes, cfg, devices=devices)
     ranks = m.fit_transform_rank()
     agg = m.aggregate_transform()
+    # an explicit device list is a multi engine, [0] included (one-rank RCCL communicator)
+    assert m._engine.devices == tuple(devices)
     D = ranks["1"].to_numpy()
     derr = np.abs(D - fx["sequential/1/D"]).max(axis=0)
     exact = bool(np.array_equal(agg["1"]["borda_ranks"].to_numpy(), fx["sequential/1/borda"]))
@@ -143,5 +145,36 @@ def test_multi_engine_errors_leave_it_usable():
         ncmp, ncols = eng.rank("sequential", [4, 8], ["cosine", "euclidean"])
         assert (ncmp, ncols) == (1, 4)
         assert eng.distances(0).shape == (5_000, 4)
+    finally:
+        eng.close()
+
+
+def test_multi_rank_failing_alone_breaks_handle():
+    """A rank that fails alone (multi.cpp's abort path): rank 1 raises after its first
+    block application while ranks 0 and 2 go on into their next collective.  The coordinator
+    waits its 10-s window, aborts the thread group (their barriers throw), every rank's call
+    returns, the call raises, and the handle reports itself broken until it is destroyed."""
+    import time
+
+    from node2vec2rank_amd import _lib, synthetic
+    layers = synthetic.er_layers(5_000, 10, 2, seed_base=4)
+    eng = _lib.Engine.multi([0, 0, 0])
+    try:
+        eng.set_layers(layers)
+        t0 = time.time()
+        with pytest.raises(RuntimeError, match="aborted|fails alone"):
+            eng.uase(8, seed=1, solver_flags=_lib.EIG_TEST_FAIL_ALONE)
+        dt = time.time() - t0
+        print(f"rank 1 failed alone: call returned after {dt:.1f} s")
+        assert 9.0 <= dt < 40.0, dt
+        with pytest.raises(RuntimeError, match="destroy the handle"):
+            eng.uase(8, seed=1)
+    finally:
+        eng.close()
+    # a fresh handle works as before
+    eng = _lib.Engine.multi([0, 0])
+    try:
+        eng.set_layers(layers)
+        assert eng.uase(8, seed=1)["converged"] == 8
     finally:
         eng.close()

@@ -948,7 +948,7 @@ def test_uase_large_dimension(engine, d):
     layers = synthetic.er_layers(3000, 40, 2, seed_base=77)
     engine.set_layers(layers)
     st = engine.uase(d, seed=5)
-    assert st["converged"] == d or st["stagnated"], st
+    assert st["converged"] == d or (st["stagnated"] and st["max_residual"] <= st["stag_cap"]), st
     s = engine.singular_values()
     M = sum((A @ A.T).astype(np.float64) for A in layers)
     ev = np.sort(sla.eigsh(M, k=d + 10, which="LA")[0])[::-1][:d]
