@@ -6,9 +6,11 @@ conditions (model_utils.py:64-65, model.py:182-183, model.py:199).
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 import threading
+import weakref
 
 import numpy as np
 
@@ -108,6 +110,9 @@ def load(path: str | None = None):
                 f"n2v2r HIP library not found at {p}; build it with "
                 "`python -m node2vec2rank_amd.build` (there is no CPU fallback)")
         lib = ctypes.CDLL(p)
+        # (registered after the library's own load-time registrations -- HIP's fat-binary
+        # module constructor -- and after torch's, so it runs before their teardown)
+        atexit.register(_teardown)
         sig = {
             "n2v2r_create": (_i, [_i, ctypes.POINTER(_vp)]),
             "n2v2r_destroy": (None, [_vp]),
@@ -194,6 +199,29 @@ class SimGroup:
             self.g = None
 
 
+_live = weakref.WeakSet()  # every open Engine (closed by _teardown at interpreter exit)
+
+
+def _teardown():
+    """At interpreter exit, while the HIP runtime (and a profiler tool, under rocprofv3) is
+    still up: destroy every open handle -- its device allocations, streams, events and RCCL
+    communicators -- before the C exit handlers unregister the library's kernels and tear the
+    runtime down, so no library object outlives the runtime.  N2V2R_EXIT_MAPS=path also writes
+    /proc/self/maps there (to map the PCs of a crash trace printed later in exit to libraries)."""
+    for eng in list(_live):
+        try:
+            eng.close()
+        except Exception:
+            pass
+    path = os.environ.get("N2V2R_EXIT_MAPS")
+    if path:
+        try:
+            with open("/proc/self/maps") as src, open(path, "w") as dst:
+                dst.write(src.read())
+        except OSError:
+            pass
+
+
 class Engine:
     """One GPU, one handle.  Thin, typed wrapper over the C-ABI.
 
@@ -214,6 +242,7 @@ class Engine:
             h = _handle
         self.h = h
         self.device = device
+        _live.add(self)
 
     @classmethod
     def rccl(cls, device: int, rank: int, world: int, unique_id: bytes) -> "Engine":

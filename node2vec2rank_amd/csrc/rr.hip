@@ -1073,20 +1073,31 @@ static hipError_t launch_rr_tridiag_coop(double* A, int c, double* d, double* e,
   int* err = reinterpret_cast<int*>(ctr + 1);  // 1 after a timed-out grid barrier
   hipError_t er = hipMemsetAsync(ctr, 0, sizeof(unsigned) * TRC_CTR_WORDS, stream);
   if (er != hipSuccess) return er;
-  // The grid barrier needs all PR x nt (<= 4 x 24) workgroups resident at once: a cooperative
-  // launch, which the runtime refuses (instead of starting) when the grid cannot be co-resident
-  // (+15-19 us of host time per call, a few calls per cfg3 fit).  Should a workgroup still be
-  // held back -- another kernel of this process or another one occupying CUs -- the bounded spin
-  // ends the launch with *err set and d[0] = NaN; the engine reads *err with the cycle's
-  // read-back (n2v2r_rr_tridiag_err) and redoes the step with the one-workgroup kernel.
-  void* args[] = {&A, &c, &PR, &d, &e, &tau, &V, &part, &rowbuf, &ctr, &err};
-  er = hipLaunchCooperativeKernel((const void*)rr_tridiag_coop_kernel, dim3((unsigned)(PR * nt)),
-                                  dim3(TRC_NT), args, (unsigned)shmem, stream);
-  if (er != hipSuccess) {
-    (void)hipGetLastError();  // (a refused launch must not surface at a later one)
+  // The grid barrier needs all PR x nt (<= 4 x 24) workgroups resident at once.  The grid is
+  // launched only when the occupancy the runtime reports for this kernel at this LDS size times
+  // the device's CUs covers it (otherwise the caller takes the one-workgroup kernel).  Should a
+  // workgroup still be held back -- another kernel of this process or another one occupying CUs
+  // -- the bounded spin ends the launch with *err set and d[0] = NaN; the engine reads *err with
+  // the cycle's read-back (n2v2r_rr_tridiag_err) and redoes the step with the one-workgroup
+  // kernel.  (Round 5 launched it with hipLaunchCooperativeKernel.  Every process that made a
+  // cooperative launch then died with SIGSEGV at exit under rocprofv3's kernel trace; round 6's
+  // tools/coop_exit_repro.hip does the same with one trivial cooperative kernel and no n2v2r
+  // code -- a plain launch of the same kernel exits cleanly -- so the fault is the runtime's /
+  // profiler's teardown of the cooperative launch, which this plain launch avoids,
+  // profiles/r06_coop_exit.md.)
+  const unsigned grid = (unsigned)(PR * nt);
+  int dev = 0, ncu = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)rr_tridiag_coop_kernel,
+                                                   TRC_NT, shmem) != hipSuccess ||
+      (int64_t)per_cu * ncu < (int64_t)grid) {
+    (void)hipGetLastError();
     return hipErrorInvalidValue;  // the caller falls back to the one-workgroup kernel
   }
-  return hipSuccess;
+  hipLaunchKernelGGL(rr_tridiag_coop_kernel, dim3(grid), dim3(TRC_NT), shmem, stream, A, c, PR, d,
+                     e, tau, V, part, rowbuf, ctr, err);
+  return hipGetLastError();
 }
 
 // the multi-workgroup tridiagonalisation's error word in its scratch: 1 after a launch whose grid
