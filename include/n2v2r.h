@@ -66,6 +66,11 @@ enum { N2V2R_EIG_FULL_FIRST_PASS = 1, N2V2R_EIG_DENSE_RR = 2,
                                    roofline of bench.py; adds an event pair per launch) */,
        N2V2R_EIG_TEST_NO_STAGNATION = 64 /* tests: no stop on flat residuals (the fit runs until
                                             every residual meets tol or max_restarts) */,
+       N2V2R_EIG_PANEL16 = 256 /* paired-panel mode on (b = 8 basis blocks, two per SpMM
+                                  application as one N x 16 panel, dense Rayleigh-Ritz of the
+                                  assembled band); N2V2R_EIG_PANEL8 = 512 forces it off; neither:
+                                  the library's default for the graph (solver.cpp) */,
+       N2V2R_EIG_PANEL8 = 512,
        N2V2R_EIG_TEST_FAIL_ALONE = 128 /* tests, multi-GPU handles: rank 1 fails alone after its
                                           first block application while its peers go on into
                                           their next collective (the abort path) */ };
@@ -124,6 +129,9 @@ typedef struct {
                                 products (no separate embedding launches) */
   int tri_fallbacks;         /* dense Rayleigh-Ritz: multi-workgroup tridiagonalisations that timed
                                 out (a workgroup not resident) and were redone on one workgroup */
+  int panel;                 /* columns each SpMM launch of the fit multiplies: b, or 16 in the
+                                paired-panel mode (two b = 8 blocks per application of M;
+                                block_applications still counts 8-wide blocks) */
 } n2v2r_eig_stats;
 
 /* lifecycle */

@@ -46,6 +46,12 @@ int n2v2r_rr_top(n2v2r_handle* h, int c, const double* H, int p, double* w, floa
 int n2v2r_rr_band_top(n2v2r_handle* h, int c, int kp, const double* hband, int64_t hband_len,
                       const double* theta_prev, int p, double* w, float* S);
 
+/* Layer bytes each rank copied host -> device so far (one-GPU handle: one entry): row pointers,
+ * column indices and values of every layer ingest, into per_rank[0 .. min(W, cap)).  Returns the
+ * rank count W.  A multi-GPU handle slices layers on the host, so each rank's figure is about
+ * 1/W of the layers' bytes (2/W for directed layers: rows of A and of A^T). */
+int n2v2r_h2d_layer_bytes(const n2v2r_handle* h, int64_t* per_rank, int cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -31,6 +31,8 @@ AGG_BORDA, AGG_NONE = 0, -1
 EIG_TIME_SPMM = 16
 EIG_TEST_NO_STAGNATION = 64
 EIG_TEST_FAIL_ALONE = 128
+EIG_PANEL16 = 256
+EIG_PANEL8 = 512
 
 STRATEGY = {"sequential": 0, "one_vs_before": 1, "one_vs_rest": 2}
 METRIC = {"cosine": 0, "euclidean": 1, "correlation": 2}
@@ -48,7 +50,7 @@ EXPORTED = [
     "n2v2r_comm_unique_id", "n2v2r_create_rccl", "n2v2r_simgroup_create",
     "n2v2r_simgroup_destroy", "n2v2r_create_sim", "n2v2r_dist_info", "n2v2r_set_layer_csr_rows",
     "n2v2r_rr_top", "n2v2r_rr_band_top", "n2v2r_set_layer_dense", "n2v2r_project",
-    "n2v2r_create_multi", "n2v2r_multi_devices",
+    "n2v2r_create_multi", "n2v2r_multi_devices", "n2v2r_h2d_layer_bytes",
 ]
 UNIQUE_ID_BYTES = 128
 
@@ -76,7 +78,8 @@ class EigStats(ctypes.Structure):
                 ("spmm_stage_bytes", ctypes.c_double * 2), ("est_scale", ctypes.c_double),
                 ("lean_checks", ctypes.c_int), ("pool_blocks", ctypes.c_int),
                 ("spmm_form", ctypes.c_int), ("stag_cap", ctypes.c_double),
-                ("y_captured", ctypes.c_int), ("tri_fallbacks", ctypes.c_int)]
+                ("y_captured", ctypes.c_int), ("tri_fallbacks", ctypes.c_int),
+                ("panel", ctypes.c_int)]
 
     def as_dict(self):
         out = {}
@@ -161,6 +164,7 @@ def load(path: str | None = None):
                                               _p(np.int32), _p(np.float32)]),
             "n2v2r_create_multi": (_i, [_p(np.int32), _i, ctypes.POINTER(_vp)]),
             "n2v2r_multi_devices": (_i, [_vp, _vp, _i]),
+            "n2v2r_h2d_layer_bytes": (_i, [_vp, _vp, _i]),
         }
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
@@ -279,6 +283,14 @@ class Engine:
         if st != OK:
             raise RuntimeError(f"n2v2r_create_sim(rank={rank}) failed with status {st}")
         return cls(device, _handle=h)
+
+    def h2d_layer_bytes(self):
+        """Layer bytes each rank of this handle copied host -> device (a list, one per rank)."""
+        out = np.zeros(64, dtype=np.int64)
+        w = self.lib.n2v2r_h2d_layer_bytes(self.h, out.ctypes.data_as(ctypes.c_void_p), 64)
+        if w < 0:
+            self._check(w, "h2d_layer_bytes")
+        return [int(x) for x in out[:w]]
 
     def dist_info(self):
         """(rank, world, row0, n_local) of this handle's row block."""

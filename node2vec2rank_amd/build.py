@@ -19,7 +19,7 @@ LIB = os.path.join(OUT_DIR, f"libn2v2r_hip_{_TAG}.so" if _TAG else "libn2v2r_hip
 OBJ_DIR = os.path.join(OUT_DIR, f"obj_{_TAG}" if _TAG else "obj")
 
 HIP_SOURCES = ["spmm.hip", "dense.hip", "gemm.hip", "rank.hip", "rr.hip", "rr_band.hip",
-               "rr_sturm.hip", "ingest.hip", "engine.cpp", "layers.cpp", "comm.cpp",
+               "rr_sturm.hip", "ingest.hip", "pair.hip", "engine.cpp", "layers.cpp", "comm.cpp",
                "solver.cpp", "ranking.cpp", "multi.cpp"]
 HOST_SOURCES: list = []
 HEADERS = ["common.h", "spmm_args.h", "engine.h", os.path.join("..", "..", "include", "n2v2r.h"),

@@ -1034,10 +1034,10 @@ __global__ void zsum_kernel(ZSum zs, int64_t n) {
 // A segment with `clear` set also zeroes its source words after copying them (the per-cycle
 // flags, so no separate memset launch re-arms them for the next cycle).
 struct PackSegs {
-  unsigned* src[8];
-  int dst_word[8];
-  int words[8];
-  int clear[8];
+  unsigned* src[12];
+  int dst_word[12];
+  int words[12];
+  int clear[12];
   int count;
 };
 __global__ __launch_bounds__(256) void pack_words_kernel(PackSegs ps, unsigned* __restrict__ dst) {
@@ -1051,7 +1051,7 @@ __global__ __launch_bounds__(256) void pack_words_kernel(PackSegs ps, unsigned* 
 extern "C" hipError_t n2v2r_launch_pack_words(void* const* src, const int* dst_word,
                                               const int* words, const int* clear, int count,
                                               void* dst, hipStream_t stream) {
-  if (count < 1 || count > 8) return hipErrorInvalidValue;
+  if (count < 1 || count > 12) return hipErrorInvalidValue;
   PackSegs ps{};
   ps.count = count;
   for (int s = 0; s < count; ++s) {

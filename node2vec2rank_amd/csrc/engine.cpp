@@ -207,7 +207,7 @@ static int time_tiled(n2v2r_handle* h, int k, int transpose, int nb, const float
   a.K = 1;
   a.nb = nb;
   a.sum = 0;
-  a.tile_rows = n2v2r_spmm_tile_rows_b(h->nloc, ncu, 2, wb, b);
+  a.tile_rows = n2v2r_spmm_tile_rows_b(h->nloc, ncu, b == 16 ? N2V2R_SPMM16_WPC : 2, wb, b);
   a.wbits = wb;
   a.width = b;
   HIPCHK(n2v2r_launch_spmm_tile(a, h->stream));  // warm-up

@@ -39,8 +39,18 @@ struct DistPlan {
 };
 extern "C" {
 hipError_t n2v2r_launch_spmm(const SpmmArgs& args, int B, hipStream_t stream);
+int n2v2r_spmm_rpw(const SpmmArgs& args, int B);
 hipError_t n2v2r_launch_row_sums(const CsrDev& A, float* out, hipStream_t stream);
 hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, hipStream_t stream);
+hipError_t n2v2r_launch_chunk_major_keys(uint64_t* keys, int64_t nnz, int64_t npad, int W,
+                                         int64_t rc, hipStream_t stream);
+// paired-panel mode (pair.hip)
+hipError_t n2v2r_launch_interleave16(const float* za, const float* zb, float* x16, int64_t n,
+                                     hipStream_t stream);
+hipError_t n2v2r_launch_pair_h_assemble(const double* hcol, int64_t ldcol, const int* lo,
+                                        const int* nr, int s0, int ns, int kp,
+                                        const double* theta, double* H, int c,
+                                        hipStream_t stream);
 int n2v2r_spmm_tile_rows(int64_t n, int ncu, int wpc, int wbits);
 int n2v2r_spmm_tile_rows_b(int64_t n, int ncu, int wpc, int wbits, int b);
 hipError_t n2v2r_launch_cb_count(const CsrDev& A, int64_t cw, int nb, int32_t* cnt,
@@ -331,6 +341,7 @@ struct LayerDev {
   // over the world x npad padded global rows with local column indices (built on first use)
   DevBuf c_indptr, c_indices, c_data;
   int64_t c_nnz = 0, c_rows = 0;
+  int64_t c_rc = 0;  // rows per chunk of the chunk-major row order (0: natural order)
   bool c_built = false;
   CsrDev csr_c() const {
     return CsrDev{c_indptr.as<int64_t>(), c_indices.as<int32_t>(), c_data.as<float>(), c_rows,
@@ -355,7 +366,9 @@ void build_col_blocks(const CsrDev& A, int64_t ncols, LayerDev::ColBlocks& out, 
                       int nb, int wbits);
 bool ensure_col_blocks(LayerDev& L, int64_t ncols, hipStream_t st, int nb, int wbits);
 int tile_wbits(const std::vector<std::unique_ptr<LayerDev>>& layers, int nb);
-void ensure_colcsr(LayerDev& L, int64_t ncols, int64_t rows_out, hipStream_t st);
+// (npad, W, rc > 0: rows in the chunk-major order of the pipelined reduce-scatter)
+void ensure_colcsr(LayerDev& L, int64_t ncols, int64_t rows_out, hipStream_t st, int64_t npad = 0,
+                   int W = 1, int64_t rc = 0);
 
 // ---- communicators ----------------------------------------------------------------------
 struct Comm {
@@ -450,6 +463,9 @@ struct EigWorkspace {
   DevBuf rres;                                // lean images: R of the restart projection
   DevBuf skipc;                               // full passes skipped (selective reorthogonalisation)
   DevBuf tblk;                                // tiled SpMM: CsrBlk [2][K][nb] (stage 1, stage 2)
+  // paired-panel mode: the N x 16 panel of two blocks, the saved band columns of the projected
+  // matrix (one slot of (c + 8) x 8 per basis block), the restart pair's coupling rows
+  DevBuf x16, hcol, pcab, pth;
 };
 }  // namespace n2v2r_int
 
@@ -489,6 +505,7 @@ struct n2v2r_handle {
   std::unique_ptr<Comm> comm;
   int rank = 0, world = 1;
   int64_t row0 = 0, nloc = 0, npad = 0;
+  int64_t h2d_layer_bytes = 0;  // layer bytes this handle copied host -> device (diagnostics)
   std::vector<std::unique_ptr<LayerDev>> layers;
 
   // UASE results
@@ -598,6 +615,28 @@ struct n2v2r_handle {
     HIPCHK(hipEventRecord(cev[2 * slot + 1], cstream));
   }
   void gather_wait(int slot) { HIPCHK(hipStreamWaitEvent(stream, cev[2 * slot + 1], 0)); }
+  // reduce-scatter on the collective stream behind what the engine stream queued so far; the
+  // engine stream waits for all of them with rs_wait_all (at most SPMM_MAX_LAYERS in flight)
+  hipEvent_t rev[SPMM_MAX_LAYERS + 1] = {};
+  int rs_pending = 0;
+  void reduce_scatter_async(const float* send, float* recv, size_t count) {
+    if (!cstream) {
+      HIPCHK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+      for (hipEvent_t& e : cev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    if (!rev[0])
+      for (hipEvent_t& e : rev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(rev[rs_pending], stream));
+    HIPCHK(hipStreamWaitEvent(cstream, rev[rs_pending], 0));
+    comm->reduce_scatter_sum_f32(send, recv, count, cstream);
+    ++rs_pending;
+  }
+  void rs_wait_all() {
+    if (!rs_pending) return;
+    HIPCHK(hipEventRecord(rev[SPMM_MAX_LAYERS], cstream));
+    HIPCHK(hipStreamWaitEvent(stream, rev[SPMM_MAX_LAYERS], 0));
+    rs_pending = 0;
+  }
   void allreduce_f64(double* buf, size_t count) {
     if (comm) comm->allreduce_sum_f64(buf, count, stream);
   }
@@ -644,6 +683,18 @@ void parallel_chunks(int nt, F&& fn);
 bool host_indices_in_range(int64_t nnz, const int32_t* ix, int64_t n);
 bool upload_rows(hipStream_t st, int64_t r0, int64_t nr, const int64_t* ip, const int32_t* ix,
                  const float* dv, DevBuf& dip, DevBuf& dix, DevBuf& ddv, int64_t& nnz_out);
+// A == A^T as multisets of (row, column, value bits), by two independent 64-bit hash sums over
+// the entries and over the transposed entries (host threads; layers.cpp)
+bool host_csr_symmetric(int64_t n, const int64_t* ip, const int32_t* ix, const float* dv);
+// rows [r0, r0 + nr) of A^T from a host CSR of A (columns r0 .. r0 + nr - 1 of A; within a row of
+// A^T the entries in ascending row of A, as the GPU transpose orders them)
+void host_transpose_rows(int64_t n, const int64_t* ip, const int32_t* ix, const float* dv,
+                         int64_t r0, int64_t nr, std::vector<int64_t>& tip,
+                         std::vector<int32_t>& tix, std::vector<float>& tdv);
+// a partitioned handle's rows of a directed layer: its rows of A and of A^T, local row pointers
+int set_layer_rows_directed(n2v2r_handle* h, int k, const int64_t* aip, const int32_t* aix,
+                            const float* adv, const int64_t* tip, const int32_t* tix,
+                            const float* tdv);
 
 // run fn(0) .. fn(nt - 1), one host thread each.  A thread that cannot be created leaves its
 // chunk (and the later ones) to the calling thread; every started thread is joined before

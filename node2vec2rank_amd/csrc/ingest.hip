@@ -134,3 +134,32 @@ extern "C" hipError_t n2v2r_launch_csr_rebase(const int64_t* ip, int64_t r0, int
                      stream, ip, r0, nr, out);
   return hipGetLastError();
 }
+
+// Row order of a partitioned layer's column share A[:, own rows] (layers.cpp ensure_colcsr) made
+// chunk-major for the pipelined reduce-scatter (solver.cpp apply_M_rs): global row j = g npad + i
+// (rank g's local row i, chunk c = i / rc of nch) moves to position
+// c W rc + g rows_c + (i - c rc), rows_c = min(rc, npad - c rc), so chunk c's W row blocks are one
+// contiguous range of the product -- what one reduce-scatter of that chunk sends.  Applied to the
+// col << 32 | row keys before the sort by column.
+__global__ void chunk_major_keys_kernel(uint64_t* __restrict__ keys, int64_t nnz, int64_t npad,
+                                        int W, int64_t rc) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nnz;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = keys[e];
+    const int64_t j = (int64_t)(k >> 32);
+    const int64_t g = j / npad, i = j - g * npad;
+    const int64_t c = i / rc;
+    const int64_t rows_c = rc < npad - c * rc ? rc : npad - c * rc;
+    const int64_t pos = c * W * rc + g * rows_c + (i - c * rc);
+    keys[e] = ((uint64_t)pos << 32) | (k & 0xFFFFFFFFull);
+  }
+}
+
+extern "C" hipError_t n2v2r_launch_chunk_major_keys(uint64_t* keys, int64_t nnz, int64_t npad,
+                                                   int W, int64_t rc, hipStream_t stream) {
+  if (nnz <= 0) return hipSuccess;
+  if (W < 1 || rc < 1 || npad < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(chunk_major_keys_kernel, dim3(grid_for(nnz, 256, 8192)), dim3(256), 0, stream,
+                     keys, nnz, npad, W, rc);
+  return hipGetLastError();
+}

@@ -91,8 +91,10 @@ int tile_wbits(const std::vector<std::unique_ptr<LayerDev>>& layers, int nb) {
 // the transpose of the rank's rows of A^T (A's own columns), by the ingest's GPU transpose (the
 // stable LSD radix sort of col << 32 | row keys over the column digits).  Stage 2 of the
 // reduce-scatter form gathers from this rank's Z rows only.  One-off per layer.
-void ensure_colcsr(LayerDev& L, int64_t ncols, int64_t rows_out, hipStream_t st) {
-  if (L.c_built && L.c_rows == rows_out) return;
+void ensure_colcsr(LayerDev& L, int64_t ncols, int64_t rows_out, hipStream_t st, int64_t npad,
+                   int W, int64_t rc) {
+  if (rc <= 0 || rc >= npad) rc = 0;  // one chunk: the natural row order
+  if (L.c_built && L.c_rows == rows_out && L.c_rc == rc) return;
   const CsrDev s = L.csr_t();
   const int64_t nnz = s.nnz;
   if (nnz > (int64_t)INT32_MAX)
@@ -114,9 +116,12 @@ void ensure_colcsr(LayerDev& L, int64_t ncols, int64_t rows_out, hipStream_t st)
     HIPCHK(n2v2r_launch_csr_scan(s.indptr, s.indices, s.data, s.n_rows, ncols,
                                  keys[0].as<uint64_t>(), pay[0].as<int32_t>(),
                                  flag.as<unsigned>(), st));
+    if (rc > 0)
+      HIPCHK(n2v2r_launch_chunk_major_keys(keys[0].as<uint64_t>(), nnz, npad, W, rc, st));
     hist.ensure(sizeof(uint32_t) * n2v2r_radix_hist_elems(nnz, 1));
     int bits = 1;
-    while (bits < 31 && ((int64_t)1 << bits) < ncols) ++bits;
+    const int64_t span = rc > 0 ? rows_out : ncols;
+    while (bits < 31 && ((int64_t)1 << bits) < span) ++bits;
     int cur = 0;
     for (int sh = 32; sh < 32 + bits; sh += 8) {
       HIPCHK(n2v2r_launch_radix_pass(keys[cur].as<uint64_t>(), pay[cur].as<int32_t>(),
@@ -132,6 +137,7 @@ void ensure_colcsr(LayerDev& L, int64_t ncols, int64_t rows_out, hipStream_t st)
   }
   L.c_nnz = nnz;
   L.c_rows = rows_out;
+  L.c_rc = rc;
   L.c_built = true;
 }
 
@@ -181,6 +187,109 @@ bool upload_rows(hipStream_t st, int64_t r0, int64_t nr, const int64_t* ip, cons
   }
   HIPCHK(hipStreamSynchronize(st));  // lip dies here
   return unit;
+}
+
+namespace {
+inline uint64_t mix64(uint64_t z) {  // splitmix64's finaliser
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+}  // namespace
+
+// Multiset equality of {(r, c, v)} and {(c, r, v)} by two hash sums each (mod 2^64): a
+// non-symmetric layer passes with probability ~2^-128.  Values compare by their bits (-0 and +0
+// differ, which only makes a layer count as directed: the slower, always correct path).
+bool host_csr_symmetric(int64_t n, const int64_t* ip, const int32_t* ix, const float* dv) {
+  int nt = host_threads();
+  const int64_t nnz = ip[n];
+  if (nnz < (int64_t)1 << 20) nt = 1;
+  std::vector<uint64_t> acc((size_t)nt * 4, 0);
+  const int64_t per = (n + nt - 1) / nt;
+  parallel_chunks(nt, [&](int t) {
+    const int64_t r0 = std::min<int64_t>(n, t * per), r1 = std::min<int64_t>(n, r0 + per);
+    uint64_t a1 = 0, a2 = 0, b1 = 0, b2 = 0;
+    for (int64_t r = r0; r < r1; ++r)
+      for (int64_t p = ip[r]; p < ip[r + 1]; ++p) {
+        uint32_t vb;
+        std::memcpy(&vb, dv + p, sizeof(vb));
+        const uint64_t c = (uint32_t)ix[p], rr = (uint64_t)r;
+        const uint64_t kf = (rr << 32) | c, kt = (c << 32) | rr;
+        a1 += mix64(mix64(kf + 0x9E3779B97F4A7C15ull) ^ vb);
+        b1 += mix64(mix64(kt + 0x9E3779B97F4A7C15ull) ^ vb);
+        a2 += mix64(mix64(kf ^ 0xD1B54A32D192ED03ull) + ((uint64_t)vb << 17));
+        b2 += mix64(mix64(kt ^ 0xD1B54A32D192ED03ull) + ((uint64_t)vb << 17));
+      }
+    acc[(size_t)t * 4 + 0] = a1;
+    acc[(size_t)t * 4 + 1] = a2;
+    acc[(size_t)t * 4 + 2] = b1;
+    acc[(size_t)t * 4 + 3] = b2;
+  });
+  uint64_t s[4] = {0, 0, 0, 0};
+  for (int t = 0; t < nt; ++t)
+    for (int i = 0; i < 4; ++i) s[i] += acc[(size_t)t * 4 + i];
+  return s[0] == s[2] && s[1] == s[3];
+}
+
+void host_transpose_rows(int64_t n, const int64_t* ip, const int32_t* ix, const float* dv,
+                         int64_t r0, int64_t nr, std::vector<int64_t>& tip,
+                         std::vector<int32_t>& tix, std::vector<float>& tdv) {
+  tip.assign((size_t)nr + 1, 0);
+  const uint64_t span = (uint64_t)nr;
+  for (int64_t r = 0; r < n; ++r)
+    for (int64_t p = ip[r]; p < ip[r + 1]; ++p) {
+      const uint64_t c = (uint64_t)((int64_t)ix[p] - r0);
+      if (c < span) ++tip[c + 1];
+    }
+  for (int64_t i = 0; i < nr; ++i) tip[i + 1] += tip[i];
+  tix.resize((size_t)std::max<int64_t>(tip[nr], 1));
+  tdv.resize((size_t)std::max<int64_t>(tip[nr], 1));
+  std::vector<int64_t> pos(tip.begin(), tip.end() - 1);
+  for (int64_t r = 0; r < n; ++r)
+    for (int64_t p = ip[r]; p < ip[r + 1]; ++p) {
+      const uint64_t c = (uint64_t)((int64_t)ix[p] - r0);
+      if (c < span) {
+        const int64_t q = pos[c]++;
+        tix[q] = (int32_t)r;
+        tdv[q] = dv[p];
+      }
+    }
+}
+
+int set_layer_rows_directed(n2v2r_handle* h, int k, const int64_t* aip, const int32_t* aix,
+                            const float* adv, const int64_t* tip, const int32_t* tix,
+                            const float* tdv) {
+  return guarded(h, [&]() -> int {
+    const int64_t nr = h->nloc;
+    if (k < 0 || k >= h->K || aip[0] != 0 || tip[0] != 0) return N2V2R_ERR_BAD_ARG;
+    for (int64_t r = 0; r < nr; ++r)
+      if (aip[r + 1] < aip[r]) {
+        h->set_err("layer %d: indptr not monotone", k);
+        return N2V2R_ERR_BAD_ARG;
+      }
+    if (!host_indices_in_range(aip[nr], aix, h->n)) {
+      h->set_err("layer %d: column index out of range", k);
+      return N2V2R_ERR_BAD_ARG;
+    }
+    for (int j = 0; j < h->K; ++j)
+      if (j != k && h->layers[j]->loaded && h->layers[j]->dense) {
+        h->err = "layers must be all CSR or all dense";
+        return N2V2R_ERR_BAD_ARG;
+      }
+    LayerDev& L = *h->layers[k];
+    L.dense = false;
+    L.loaded = false;
+    L.drop_col_blocks();
+    L.n_rows = nr;
+    L.unit = upload_rows(h->stream, 0, nr, aip, aix, adv, L.indptr, L.indices, L.data, L.nnz);
+    L.t_unit = upload_rows(h->stream, 0, nr, tip, tix, tdv, L.t_indptr, L.t_indices, L.t_data,
+                           L.t_nnz);
+    h->h2d_layer_bytes += 16 * (nr + 1) + 8 * (L.nnz + L.t_nnz);
+    L.symmetric = false;
+    L.loaded = true;
+    h->have_embedding = false;
+    return N2V2R_OK;
+  });
 }
 }  // namespace n2v2r_int
 
@@ -257,6 +366,7 @@ int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const in
       HIPCHK(hipMemcpyAsync(dix.p, indices, sizeof(int32_t) * nnz, hipMemcpyHostToDevice, st));
       HIPCHK(hipMemcpyAsync(ddv.p, data, sizeof(float) * nnz, hipMemcpyHostToDevice, st));
     }
+    h->h2d_layer_bytes += 8 * (n + 1) + 8 * nnz;
     const bool need_t = symmetric != N2V2R_SYM_YES;
     DevBuf* keys = h->ing_keys;
     DevBuf* pay = h->ing_pay;
@@ -482,6 +592,7 @@ int n2v2r_set_layer_csr_rows(n2v2r_handle* h, int k, int64_t n, int64_t row0, in
     L.n_rows = h->nloc;
     L.unit = upload_rows(h->stream, 0, n_rows, indptr, indices, data, L.indptr, L.indices, L.data,
                          L.nnz);
+    h->h2d_layer_bytes += 8 * (n_rows + 1) + 8 * L.nnz;
     L.symmetric = true;
     L.loaded = true;
     h->have_embedding = false;

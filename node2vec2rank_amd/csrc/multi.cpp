@@ -128,13 +128,18 @@ int multi_set_num_layers(n2v2r_handle* h, int num_layers, int64_t n) {
   return st;
 }
 
-// Symmetric layers (N2V2R_SYM_YES) are sliced on the host: every rank uploads only its own rows
-// (n2v2r_set_layer_csr_rows; no rank ever holds the whole layer).  Otherwise every rank ingests
-// the whole layer (the range check, the GPU transpose and the symmetry test run on every device
-// at once) and keeps its rows of A and A^T.
+// Layers are sliced on the host: no rank ever holds (or receives over PCIe) the whole layer
+// (a GPU owns a contiguous row range).  Symmetry (N2V2R_SYM_DETECT) is decided once,
+// on the host, by hash sums over the entries and the transposed entries (host_csr_symmetric);
+// a symmetric layer: every rank uploads its own rows (n2v2r_set_layer_csr_rows); a directed one:
+// every rank thread also builds its rows of A^T from the host CSR (host_transpose_rows) and
+// uploads both.  Arguments the slicing cannot take go to every rank's whole-layer ingest, which
+// fails them alike.
 int multi_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const int64_t* indptr,
                         const int32_t* indices, const float* data, int symmetric) {
-  if (symmetric != N2V2R_SYM_YES || !indptr || n != h->n || nnz < 0 ||
+  if ((symmetric != N2V2R_SYM_YES && symmetric != N2V2R_SYM_NO &&
+       symmetric != N2V2R_SYM_DETECT) ||
+      !indptr || n != h->n || nnz < 0 || k < 0 || k >= h->K ||
       (nnz > 0 && (!indices || !data)) || indptr[0] != 0 || indptr[n] != nnz)
     return fanout(h, [&](n2v2r_handle* r, int) {
       return n2v2r_set_layer_csr(r, k, n, nnz, indptr, indices, data, symmetric);
@@ -144,6 +149,27 @@ int multi_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const in
       h->set_err("layer %d: indptr not monotone", k);
       return N2V2R_ERR_BAD_ARG;
     }
+  if (!host_indices_in_range(nnz, indices, n)) {
+    h->set_err("layer %d: column index out of range", k);
+    return N2V2R_ERR_BAD_ARG;
+  }
+  const bool sym = symmetric == N2V2R_SYM_YES ||
+                   (symmetric == N2V2R_SYM_DETECT && host_csr_symmetric(n, indptr, indices, data));
+  if (!sym)
+    return fanout(h, [&](n2v2r_handle* r, int) {
+      const int64_t r0 = r->row0, nr = r->nloc;
+      const int64_t p0 = indptr[r0];
+      std::vector<int64_t> lip((size_t)nr + 1), tip;
+      for (int64_t i = 0; i <= nr; ++i) lip[i] = indptr[r0 + i] - p0;
+      std::vector<int32_t> tix;
+      std::vector<float> tdv;
+      host_transpose_rows(n, indptr, indices, data, r0, nr, tip, tix, tdv);
+      static const int32_t zi = 0;
+      static const float zf = 0.f;
+      const bool e = indptr[r0 + nr] == p0;
+      return set_layer_rows_directed(r, k, lip.data(), e ? &zi : indices + p0, e ? &zf : data + p0,
+                                     tip.data(), tix.data(), tdv.data());
+    });
   return fanout(h, [&](n2v2r_handle* r, int) {
     const int64_t r0 = r->row0, nr = r->nloc;
     const int64_t p0 = indptr[r0], p1 = indptr[r0 + nr];
@@ -272,6 +298,17 @@ int n2v2r_create_multi(const int* devices, int n_gpus, n2v2r_handle** out) {
   }
   *out = h;
   return N2V2R_OK;
+}
+
+int n2v2r_h2d_layer_bytes(const n2v2r_handle* h, int64_t* per_rank, int cap) {
+  if (!h) return N2V2R_ERR_BAD_ARG;
+  if (!h->multi()) {
+    if (per_rank && cap >= 1) per_rank[0] = h->h2d_layer_bytes;
+    return 1;
+  }
+  const int w = (int)h->ranks.size();
+  for (int i = 0; per_rank && i < std::min(w, cap); ++i) per_rank[i] = h->ranks[i]->h2d_layer_bytes;
+  return w;
 }
 
 int n2v2r_multi_devices(const n2v2r_handle* h, int* devices, int cap) {

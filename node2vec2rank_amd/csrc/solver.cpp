@@ -50,6 +50,13 @@ bool split2_wanted(const n2v2r_handle* h, int b) {
   return (double)h->K * (double)h->n * 32.0 > 4.0 * 1024 * 1024;
 }
 
+// Paired-panel mode by default (no N2V2R_EIG_PANEL16 / PANEL8 flag): not yet (measured first).
+bool pair_default(const n2v2r_handle* h, int d) {
+  (void)h;
+  (void)d;
+  return false;
+}
+
 // ---- the eigensolver ----------------------------------------------------------------------
 struct Eig {
   n2v2r_handle* h;
@@ -82,9 +89,23 @@ struct Eig {
   // embedding step skips its d/8 SpMM launches (cfg4: 16 x 0.74 ms)
   bool y_captured = false;
   int tile_rows = 0, tile_nb = CB_NB, tile_wb = CB_WIN_BITS_MIN;
+  // Paired-panel mode (pair.hip): 8-wide basis blocks, every application of M multiplies the
+  // last TWO as one N x 16 panel (spmm16_flat_kernel, tile_rows16 rows per tile); the projected
+  // matrix (half-bandwidth 16) is assembled from the local passes' saved Gram rows -- hcol slot
+  // s - kry0 holds column block s's rows hc_lo[s] .. + hc_nr[s] / 8 blocks -- and solved densely.
+  bool pair = false;
+  int tile_rows16 = 0;
+  std::vector<int> hc_lo, hc_nr;
+  int64_t hc_ld = 0;  // doubles per hcol slot
+  int pcab_blk = 0;   // the block of E_b's saved first-pass Gram rows that holds E_a's
   // partitioned CSR handles: stage 2 as a reduce-scatter of this rank's column share (default
   // at W > 1) instead of all-gathers of every layer's stage-1 panel (N2V2R_DIST_STAGE2=gather)
   bool rs_form = false;
+  // reduce-scatter form: stage 2 in rs_chunks row chunks of rs_rc local rows, each chunk's
+  // reduce-scatter overlapped with the next chunk's product (N2V2R_RS_CHUNKS, default 4; 1: one
+  // launch and one reduce-scatter)
+  int rs_chunks = 1;
+  int64_t rs_rc = 0;
   // XCD-split second SpMM stage (b = 8, one GPU): A_k Z_k lands in per-layer partials on the
   // XCDs of layer k; the image W = sum_k of them is stored by the next Gram pass that reads it
   // (the local first pass of the next expansion), or by materialize() before any other use
@@ -157,11 +178,11 @@ struct Eig {
       out->spmm_stage_bytes[tkind[i]] += tbytes[i];
     }
   }
-  double layer_bytes(int k, bool transposed) const {
+  double layer_bytes(int k, bool transposed, int width = 0) const {
     const LayerDev& L = *h->layers[k];
     const bool t = transposed && !L.symmetric;
     return spmm_algo_bytes(t ? L.t_nnz : L.nnz, t ? L.t_unit : L.unit, n,
-                           (int64_t)h->world * npad, b);
+                           (int64_t)h->world * npad, width ? width : b);
   }
 
   // N2V2R_DEBUG_FINITE: stop at the first stage whose output holds a non-finite value
@@ -343,9 +364,35 @@ struct Eig {
     }
     s2.Y[0] = P;
     te = tbeg();
-    HIPCHK(n2v2r_launch_spmm(s2, b, st));
-    tend(te, 1, b1);
-    h->comm->reduce_scatter_sum_f32(P, Wout, (size_t)npad * b, st);
+    if (rs_chunks <= 1) {
+      HIPCHK(n2v2r_launch_spmm(s2, b, st));
+      tend(te, 1, b1);
+      h->comm->reduce_scatter_sum_f32(P, Wout, (size_t)npad * b, st);
+    } else {
+      // pipelined: the column share's rows are chunk-major (ensure_colcsr), so chunk c's product
+      // -- rows [c rs_rc, ...) of every rank's block -- is one contiguous range of P, reduce-
+      // scattered on the collective stream while chunk c + 1's product runs.  Every row is
+      // summed as in the one-launch form (same rows per wave), and every element of W sums the
+      // same ranks' values: the same result, with one chunk's reduce-scatter exposed.
+      s2.rpw = n2v2r_spmm_rpw(s2, b);
+      const int W = h->world;
+      for (int c = 0; c < rs_chunks; ++c) {
+        const int64_t r0 = (int64_t)c * rs_rc;
+        const int64_t rows_c = std::min<int64_t>(rs_rc, npad - r0);
+        if (rows_c <= 0) break;
+        SpmmArgs sc = s2;
+        for (int k = 0; k < K; ++k) {
+          sc.A[k].indptr = s2.A[k].indptr + (size_t)r0 * W;
+          sc.A[k].n_rows = (int64_t)W * rows_c;
+        }
+        float* pc = P + (size_t)r0 * W * b;
+        sc.Y[0] = pc;
+        HIPCHK(n2v2r_launch_spmm(sc, b, st));
+        h->reduce_scatter_async(pc, Wout + (size_t)r0 * b, (size_t)rows_c * b);
+      }
+      tend(te, 1, b1);
+      h->rs_wait_all();
+    }
     algo_bytes += b0 + b1;
     launches += 2;
   }
@@ -759,6 +806,114 @@ struct Eig {
     ws.push_back(w);
   }
 
+  // Paired mode: [Wa | Wb] = M [za | zb] with the tiled SpMM at 64-B panel rows: the two blocks
+  // interleaved into one N x 16 panel, stage 1 Z_k = A_k^T X (N x 16 per layer), stage 2 summed
+  // over the layers in LDS and written straight into the two 8-wide image blocks
+  void apply_M_pair(const float* za, const float* zb, float* wa, float* wb) {
+    const double t0 = now_ms();
+    lds_poison();
+    float* x16 = h->ews.x16.as<float>();
+    HIPCHK(n2v2r_launch_interleave16(za, zb, x16, n, st));
+    const CsrBlk* tb = h->ews.tblk.as<CsrBlk>();
+    SpmmTileArgs a{};
+    a.blk = tb;
+    a.ldx = a.ldy = 16;
+    a.n = n;
+    a.K = K;
+    a.nb = tile_nb;
+    a.sum = 0;
+    a.tile_rows = tile_rows16;
+    a.wbits = tile_wb;
+    a.width = 16;
+    double b0 = 0.0, b1 = 0.0;
+    for (int k = 0; k < K; ++k) {
+      a.X[k] = x16;
+      a.Y[k] = h->ews.zk[k]->as<float>();
+      b0 += layer_bytes(k, true, 16);
+      b1 += layer_bytes(k, false, 16);
+    }
+    int te = tbeg();
+    HIPCHK(n2v2r_launch_spmm_tile(a, st));
+    tend(te, 0, b0);
+    SpmmTileArgs s2 = a;
+    s2.blk = tb + (size_t)K * tile_nb;
+    s2.sum = 1;
+    for (int k = 0; k < K; ++k) {
+      s2.X[k] = h->ews.zk[k]->as<float>();
+      s2.Y[k] = nullptr;
+    }
+    s2.Y[0] = wa;
+    s2.Y2 = wb;
+    te = tbeg();
+    HIPCHK(n2v2r_launch_spmm_tile(s2, st));
+    tend(te, 1, b1);
+    algo_bytes += b0 + b1;
+    launches += 2;
+    t_spmm += now_ms() - t0;
+  }
+
+  // hcol slot of basis column block s (its saved band rows)
+  double* hcol_at(int s) const { return h->ews.hcol.as<double>() + (size_t)(s - kry0) * hc_ld; }
+
+  // the blocks the images of the pair at basis indices p, p + 1 couple to in exact arithmetic:
+  // the previous pair and this one (p - 2 .. p + 1), or every block for the first Krylov pair of
+  // a cycle (the kept Ritz vectors' residuals lie in span(E))
+  int pair_lo(int p) const { return p <= kry0 ? 0 : p - 2; }
+
+  // Paired mode: the next pair (za, zb) from the images (wa, wb) of the last pair of `Q`, and its
+  // images.  za: local pass against the pair's coupling blocks L (band column p saved), zb: local
+  // pass against L + [za] (band column p + 1); then both full passes from one read of the old
+  // basis (pair_pass: za's selective pass, zb's Gram against the corrected za, zb's selective
+  // pass) -- or, not lazy (after a refill), three passes each; then one SpMM application.
+  void expand_pair(const float* wa, const float* wb, std::vector<float*>& qs,
+                   std::vector<float*>& ws, bool lazy) {
+    const int p = (int)Q.size() - 2;
+    const int lo = pair_lo(p);
+    const std::vector<float*> La(Q.begin() + lo, Q.end());
+    float* za = take();
+    float* zb = take();
+    std::vector<float*> Lb(La);
+    Lb.push_back(za);
+    std::vector<float*> qa(Q);
+    qa.push_back(za);
+    hc_lo[p] = lo;
+    hc_nr[p] = (int)La.size() * 8;
+    hc_lo[p + 1] = lo;
+    hc_nr[p + 1] = (int)Lb.size() * 8;
+    if (lazy && defer && !full_first) {
+      const double t0 = now_ms();
+      lds_poison();
+      pip_pass(za, La, nullptr, flg_p, any_p, wa, hcol_at(p), 0, (int)La.size() * 8, nullptr,
+               nullptr, 0.f, true);
+      pip_pass(zb, Lb, nullptr, flg_p, any_p, wb, hcol_at(p + 1), 0, (int)Lb.size() * 8, nullptr,
+               nullptr, 0.f, true);
+      t_ortho += now_ms() - t0;
+      deferred = za;
+      if (!(pair_gram && pair_pass(zb, qa))) {
+        flush_deferred(qa);
+        const double t1 = now_ms();
+        pip_pass(zb, qa, nullptr, flg_p + 64, any_p + 1, nullptr, nullptr, 0, 0, any_p + 3,
+                 nullptr, reorth_tol);
+        t_ortho += now_ms() - t1;
+      }
+    } else {
+      orthonormalize(za, Q, wa, &La, hcol_at(p), lazy);
+      orthonormalize(zb, qa, wb, &Lb, hcol_at(p + 1), lazy);
+    }
+    dbg(za, n * 8, false, "orthonormalised Krylov block (pair a)");
+    dbg(zb, n * 8, false, "orthonormalised Krylov block (pair b)");
+    dbg_ortho(zb, qa, "Krylov pair before its SpMM");
+    float* w0 = take();
+    float* w1 = take();
+    apply_M_pair(za, zb, w0, w1);
+    dbg(w0, n * 8, false, "SpMM image M q (pair a)");
+    dbg(w1, n * 8, false, "SpMM image M q (pair b)");
+    dbg_apps += 2;
+    qs.push_back(za);
+    qs.push_back(zb);
+    ws.push_back(w0);
+    ws.push_back(w1);
+  }
 
   int run(int d_, const n2v2r_eig_opts& o, std::vector<double>& theta_out, float* Uout,
           int ldu) {
@@ -834,6 +989,28 @@ struct Eig {
         throw StatusFail{N2V2R_ERR_BAD_ARG,
                          "graph too small for the requested dimension: need n >= 2*(keep+8)"};
     }
+    // paired-panel mode: N2V2R_EIG_PANEL16 / N2V2R_EIG_PANEL8 force it on / off; by default on
+    // for one-GPU CSR fits that take the tiled SpMM (pair_default).  It needs lean images (the
+    // projected matrix comes from the saved band, not from kept images), keeps and bases in
+    // whole pairs, and a basis the fused passes take (<= N2V2R_BAND_MAXC columns).
+    pair = false;
+    if (b == 8 && !h->comm && !h->dense_layers() && !lean_off && lean_enabled() &&
+        !full_first && !(o.solver_flags & N2V2R_EIG_PANEL8) && !(o.solver_flags & N2V2R_EIG_DENSE_RR) &&
+        col_blocks_wanted(h, 8) &&
+        ((o.solver_flags & N2V2R_EIG_PANEL16) || pair_default(h, d))) {
+      int pk = (keep + 15) / 16 * 16;
+      int pc = o.max_basis ? o.max_basis / 16 * 16
+                           : std::min(N2V2R_BAND_MAXC,
+                                      std::max(pk + 48, (24 * ((std::max(d + 16, (d * 5) / 4) + 7) / 8 * 8)) / 5));
+      pc = pc / 16 * 16;
+      const int cap16 = (int)std::min<int64_t>((nglob / 2) / 16 * 16, (int64_t)N2V2R_BAND_MAXC);
+      if (pc > cap16) pc = cap16;
+      if (pk + 32 <= pc && pc <= N2V2R_BAND_MAXC) {
+        pair = true;
+        keep = pk;
+        maxc = pc;
+      }
+    }
     pb = keep / b;
     nb_max = maxc / b;
     const int c_max = maxc;
@@ -855,7 +1032,7 @@ struct Eig {
     freelist.clear();
     for (auto& blk : h->ews.pool) freelist.push_back(blk->as<float>());
     while ((int)h->ews.zk.size() < K) h->ews.zk.emplace_back(new DevBuf());
-    for (int k = 0; k < K; ++k) h->ews.zk[k]->ensure(bb);
+    for (int k = 0; k < K; ++k) h->ews.zk[k]->ensure(pair ? 2 * bb : bb);  // (pair: N x 16)
     if (h->comm) {
       h->gath.ensure(sizeof(float) * h->world * npad * b);
       h->ews.zg.ensure(sizeof(float) * (size_t)K * h->world * npad * b);
@@ -871,6 +1048,17 @@ struct Eig {
       // N2V2R_SPMM_TILE_NB = 4..64 overrides (read per fit).
       int nb_auto = 4;
       while (nb_auto < 64 && (double)nglob * 32.0 / nb_auto > 2.0 * 1024 * 1024) nb_auto *= 2;
+      if (pair) {
+        // 64-B panel rows (round 6, spmm16_flat_kernel per layer launch): blocks of <= 2 MB while
+        // the N x 16 panel stays well inside the Infinity Cache (cfg4, 64 MB: 32 blocks 0.526 ms
+        // against 0.559 at 16); beyond it longer runs per window win over L2 residency (cfg5,
+        // 640 MB: 16 blocks 5.45 ms, 32 5.45-5.82, 64 5.85-7.37; profiles/r06_spmm16_*.jsonl)
+        nb_auto = 4;
+        if ((double)nglob * 64.0 > 128.0 * 1024 * 1024)
+          nb_auto = 16;
+        else
+          while (nb_auto < 64 && (double)nglob * 64.0 / nb_auto > 2.0 * 1024 * 1024) nb_auto *= 2;
+      }
       const char* tn_ = std::getenv("N2V2R_SPMM_TILE_NB");
       tile_nb = tn_ ? std::atoi(tn_) : nb_auto;
       if (tile_nb != 4 && tile_nb != 8 && tile_nb != 16 && tile_nb != 32 && tile_nb != 64)
@@ -884,6 +1072,7 @@ struct Eig {
         int ncu = 0;
         HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
         tile_rows = n2v2r_spmm_tile_rows(n, ncu, 2, tile_wb);
+        tile_rows16 = n2v2r_spmm_tile_rows_b(n, ncu, N2V2R_SPMM16_WPC, tile_wb, 16);
         const int nb = tile_nb;
         std::vector<CsrBlk> hb((size_t)2 * K * nb);
         for (int k = 0; k < K; ++k) {
@@ -908,8 +1097,31 @@ struct Eig {
       rs_form = e && std::strcmp(e, "rs") == 0 ? true
                 : e && std::strcmp(e, "gather") == 0 ? false
                 : h->world > 1;
-      if (rs_form)
-        for (auto& Lp : h->layers) ensure_colcsr(*Lp, nglob, (int64_t)h->world * npad, st);
+      if (rs_form) {
+        const char* ce = std::getenv("N2V2R_RS_CHUNKS");  // read per fit (tests, A/B runs)
+        rs_chunks = std::max(1, std::min(SPMM_MAX_LAYERS, ce ? std::atoi(ce) : 4));
+        rs_rc = (npad + rs_chunks - 1) / rs_chunks;
+        rs_chunks = (int)((npad + rs_rc - 1) / rs_rc);
+        if (rs_chunks <= 1) rs_rc = 0;
+        for (auto& Lp : h->layers)
+          ensure_colcsr(*Lp, nglob, (int64_t)h->world * npad, st, npad, h->world, rs_rc);
+      }
+    }
+    if (pair && !col_blocks) {
+      // (the column-block copies could not be built: the 8-wide row-kernel fit instead, at the
+      // keep / basis the general rule would have given -- rerun the setup without the pair mode)
+      n2v2r_eig_opts o2 = o;
+      o2.solver_flags |= N2V2R_EIG_PANEL8;
+      return run(d_, o2, theta_out, Uout, ldu);
+    }
+    if (pair) {
+      h->ews.x16.ensure(sizeof(float) * (size_t)npad * 16);
+      hc_ld = (int64_t)(c_max + 8) * 8;
+      h->ews.hcol.ensure(sizeof(double) * (size_t)nb_max * hc_ld);
+      h->ews.pcab.ensure(sizeof(double) * (size_t)hc_ld);
+      h->ews.pth.ensure(sizeof(double) * (size_t)keep);
+      hc_lo.assign(nb_max + 2, 0);
+      hc_nr.assign(nb_max + 2, 0);
     }
     split2 = split2_wanted(h, b) && !col_blocks;
     pending = nullptr;
@@ -935,8 +1147,8 @@ struct Eig {
     h->ews.anyflag.ensure(sizeof(int) * 4);
     h->theta.ensure(sizeof(double) * c_max);
     h->resid.ensure(sizeof(double) * c_max);
-    band_rr = b == 8 && !(o.solver_flags & N2V2R_EIG_DENSE_RR) && c_max <= N2V2R_BAND_MAXC &&
-              keep + 8 <= 192;
+    band_rr = !pair && b == 8 && !(o.solver_flags & N2V2R_EIG_DENSE_RR) &&
+              c_max <= N2V2R_BAND_MAXC && keep + 8 <= 192;
     if (band_rr) {
       h->ews.hband.ensure(sizeof(double) * ((size_t)(keep + b) * b + (size_t)nb_max * 2 * b * b));
       h->ews.band.ensure(sizeof(double) * (size_t)c_max * (b + 1));
@@ -955,7 +1167,7 @@ struct Eig {
     // projection, the Ritz values and coefficients, the true residuals) is all-reduced first,
     // so every rank takes the same decisions.
     const bool lean =
-        b == 8 && pip_fused() && band_rr && sturm && !lean_off && lean_enabled();
+        pair || (b == 8 && pip_fused() && band_rr && sturm && !lean_off && lean_enabled());
     {
       // default: a tenth of the residual tolerance.  The residuals stall near the level of
       // orthogonality left in the basis (~1.5x it in cfg2 sweeps: 2e-6 stalls at 3e-6); at
@@ -990,14 +1202,18 @@ struct Eig {
     }
     h->ews.skipc.ensure(sizeof(int) * (4 + N2V2R_BAND_MAXC / 8));  // [0]: skipped, [1 + blk]
     HIPCHK(hipMemsetAsync(h->ews.skipc.p, 0, sizeof(int) * (4 + N2V2R_BAND_MAXC / 8), st));
-    if (lean) h->ews.rres.ensure(sizeof(double) * 128);  // R of the restart block's two passes
+    // R of the restart block's two passes (pair: [0, 128) the a block's, [128, 256) the b's)
+    if (lean) h->ews.rres.ensure(sizeof(double) * (pair ? 256 : 128));
     double est_scale = 1.0;  // lean: true / estimated residual seen at a failed final check
     double last_true = 1e300;  // lean: the worst true residual of the previous check
     bool rr_armed = false;   // the Rayleigh-Ritz error words zeroed (then by every read-back)
     int lean_checks = 0;
-    // pinned read-back per cycle: residuals, Ritz values (keep each), flags, R (8 x 8), S's last rows
+    // pinned read-back per cycle: residuals, Ritz values (keep each), flags, R (8 x 8), S's last
+    // rows (pair: the restart pair's R_aa, R_bb and coupling E_a^T W_b, 3 x 8 x 8, and S's last
+    // 16 rows)
+    const int nrr = pair ? 192 : 64, nsl = pair ? 16 : 8;
     const size_t pin_bytes = sizeof(double) * 2 * (size_t)keep + 8 * sizeof(int) +
-                             sizeof(double) * 64 + sizeof(float) * 8 * (size_t)keep;
+                             sizeof(double) * nrr + sizeof(float) * nsl * (size_t)keep;
 
     h->ews.dbgflag.ensure(sizeof(int) * 4);
     h->ews.tflag.ensure(sizeof(double) * 2);
@@ -1011,13 +1227,25 @@ struct Eig {
     Q.assign(1, q0);
     orthonormalize(q0, {});
     dbg(q0, n * b, false, "orthonormalised start block");
-    W.assign(1, take());
-    apply_M(Q[0], W[0]);
+    if (pair) {
+      // the start pair: a second block of deviates from another counter stream
+      float* q1 = take();
+      HIPCHK(n2v2r_launch_fill_normal(q1, b, n, seed ^ 0x9E3779B97F4A7C15ull, nullptr, nullptr,
+                                      (uint64_t)row0 * b, st));
+      orthonormalize(q1, Q);
+      Q.push_back(q1);
+      W.assign(1, take());
+      W.push_back(take());
+      apply_M_pair(Q[0], Q[1], W[0], W[1]);
+    } else {
+      W.assign(1, take());
+      apply_M(Q[0], W[0]);
+    }
     if (debug_finite()) materialize();
     dbg(W[0], n * b, false, "SpMM image of the start block");
     if ((o.solver_flags & N2V2R_EIG_TEST_FAIL_ALONE) && h->comm && h->rank == 1)
       throw StatusFail{N2V2R_ERR_INTERNAL, "test: rank 1 fails alone"};
-    int apps = 1;
+    int apps = pair ? 2 : 1;
     int cycle = 0;
     double maxres = 0;
     int conv = 0;
@@ -1037,6 +1265,16 @@ struct Eig {
       // (cycle 0: armed here; later cycles: the previous cycle's read-back zeroed it)
       if (lazy && cycle == 0) HIPCHK(hipMemsetAsync(h->ews.anyflag.as<int>() + 3, 0, sizeof(int), st));
       while ((int)Q.size() < nb_max) {
+        if (pair) {
+          expand_pair(W[W.size() - 2], W.back(), Q, W, lazy);
+          apps += 2;
+          for (int i = (int)W.size() - 4; lean && i < (int)W.size() - 2; ++i)
+            if (i >= q_start) {  // consumed; the cycle's input pair stays
+              give(W[i]);
+              W[i] = nullptr;
+            }
+          continue;
+        }
         expand_one(W.back(), Q, Q, W, /*save_band=*/true, lazy);
         ++apps;
         if (lean && (int)W.size() - 2 > q_start - 1) {  // consumed; the cycle's input stays
@@ -1055,6 +1293,8 @@ struct Eig {
       bool dense_rr = !band_rr;
       bool sturm_now = sturm;  // this cycle's banded form (the reducing one after a failure)
       int rr_err = 0;
+      bool th_saved = false;  // pair: the kept Ritz values copied for this cycle's assembly
+      float* E_lean2 = nullptr;  // pair: the restart pair's second block
       double th_sync0 = 0, tr0_c = 0;  // host clock (N2V2R_TRACE)
     rayleigh_ritz:
       {
@@ -1091,7 +1331,30 @@ struct Eig {
                                       h->ews.rrerr.as<int>(), st));
         }
       } else {
-        tn(blocks(Q, 0, nq), blocks(W, 0, nq), h->ews.gsmall.as<double>(), nullptr);
+        if (pair) {
+          // the last pair's band columns (its images against their coupling blocks), then H
+          // assembled from every saved column of this cycle and the kept Ritz values
+          const int p = nq - 2, lo = pair_lo(p);
+          const std::vector<float*> La(Q.begin() + lo, Q.end());
+          for (int t = 0; t < 2; ++t) {
+            tn(blocks(La, 0, (int)La.size()), one(W[p + t]), hcol_at(p + t), nullptr);
+            hc_lo[p + t] = lo;
+            hc_nr[p + t] = (int)La.size() * 8;
+          }
+          // (the kept Ritz values copied once per cycle: a redone Rayleigh-Ritz -- a timed-out
+          // tridiagonalisation -- finds h->theta overwritten)
+          if (!th_saved && kry0 > 0)
+            HIPCHK(hipMemcpyAsync(h->ews.pth.p, h->theta.p, sizeof(double) * kry0 * b,
+                                  hipMemcpyDeviceToDevice, st));
+          th_saved = true;
+          double* Hd = h->ews.gsmall.as<double>();
+          HIPCHK(hipMemsetAsync(Hd, 0, sizeof(double) * (size_t)c * c, st));
+          HIPCHK(n2v2r_launch_pair_h_assemble(h->ews.hcol.as<double>(), hc_ld, hc_lo.data() + kry0,
+                                              hc_nr.data() + kry0, kry0, nq - kry0, kry0 * b,
+                                              h->ews.pth.as<double>(), Hd, c, st));
+        } else {
+          tn(blocks(Q, 0, nq), blocks(W, 0, nq), h->ews.gsmall.as<double>(), nullptr);
+        }
         dbg(h->ews.gsmall.p, (int64_t)c * c, true, "projected matrix H = Q^T W");
         lds_poison();
         // ranks that share this device (thread group): their concurrent launches of the
@@ -1166,7 +1429,22 @@ struct Eig {
         // the restart block now (it needs nothing from the Rayleigh-Ritz stage): its first,
         // local pass leaves R with W_last - Q_loc C = Z_{m+1} R, Z_{m+1} orthonormal.  Built
         // once per cycle: a Rayleigh-Ritz fallback (goto rayleigh_ritz) reuses it and R.
-        if (!E_lean) {
+        if (!E_lean && pair) {
+          // the restart pair: E_a from the last pair's first image, E_b from its second against
+          // the basis and E_a.  [W_a W_b] - Q C = [E_a E_b] [[R_aa, c_ab], [0, R_bb]] with
+          // c_ab = E_a^T W_b: E_b's first pass's Gram rows of E_a (pcab)
+          const int p = nq - 2;
+          const std::vector<float*> La(Q.begin() + pair_lo(p), Q.end());
+          E_lean = take();
+          orthonormalize(E_lean, Q, W[p], &La, nullptr, false, h->ews.rres.as<double>());
+          std::vector<float*> qe(Q), Le(La);
+          qe.push_back(E_lean);
+          Le.push_back(E_lean);
+          E_lean2 = take();
+          orthonormalize(E_lean2, qe, W[p + 1], &Le, h->ews.pcab.as<double>(), false,
+                         h->ews.rres.as<double>() + 128);
+          pcab_blk = (int)Le.size() - 1;  // (where E_a's rows sit in pcab)
+        } else if (!E_lean) {
           E_lean = take();
           const std::vector<float*> loc = local_of(Q);
           orthonormalize(E_lean, Q, W.back(), &loc, nullptr, false, h->ews.rres.as<double>());
@@ -1181,14 +1459,15 @@ struct Eig {
       double* pres = static_cast<double*>(h->pin);
       double* pth = pres + keep;
       int* pflag = reinterpret_cast<int*>(pth + keep);
-      double* prr = reinterpret_cast<double*>(pflag + 8);   // lean: R (8 x 8)
-      float* psl = reinterpret_cast<float*>(prr + 64);      // lean: last 8 rows of S
+      double* prr = reinterpret_cast<double*>(pflag + 8);   // lean: R (8 x 8; pair 3 x 8 x 8)
+      float* psl = reinterpret_cast<float*>(prr + nrr);     // lean: last 8 (16) rows of S
       {
         // one pack launch + one copy: [pres | pth | pflag[8] | prr | psl] (the layout above)
         h->ews.rback.ensure(pin_bytes);
-        const int wres = 0, wth = 2 * keep, wflag = 4 * keep, wrr = wflag + 8, wsl = wrr + 128;
-        void* src[8];
-        int dw[8], nw[8], clr[8], ns = 0;
+        const int wres = 0, wth = 2 * keep, wflag = 4 * keep, wrr = wflag + 8,
+                  wsl = wrr + 2 * nrr;
+        void* src[12];
+        int dw[12], nw[12], clr[12], ns = 0;
         auto seg = [&](void* sp, int d0, int n0, int cl = 0) {
           src[ns] = sp;
           dw[ns] = d0;
@@ -1196,7 +1475,12 @@ struct Eig {
           clr[ns] = cl;
           ++ns;
         };
-        if (lean) {
+        if (lean && pair) {
+          seg(h->ews.rres.p, wrr, 128);                                 // R_aa
+          seg(h->ews.rres.as<double>() + 128, wrr + 128, 128);          // R_bb
+          seg(h->ews.pcab.as<double>() + (size_t)pcab_blk * 64, wrr + 256, 128);
+          seg(h->ews.csmall.as<float>() + (size_t)(c - 16) * keep, wsl, 16 * keep);
+        } else if (lean) {
           seg(h->ews.rres.p, wrr, 128);
           seg(h->ews.csmall.as<float>() + (size_t)(c - b) * keep, wsl, 8 * keep);
         } else {
@@ -1220,7 +1504,25 @@ struct Eig {
       if (trace)
         fprintf(stderr, "[n2v2r] cycle %d host: rr start %.3f, to sync %.3f, sync %.3f ms\n",
                 cycle, tr0_c - t_start, th_sync0 - tr0_c, now_ms() - th_sync0);
-      if (lean) {  // ||M x_j - theta_j x_j||^2 = ||R s_j(last block)||^2 (Krylov-Schur), scaled
+      if (lean && pair) {
+        // ||M x_j - theta_j x_j|| = ||R16 s_j(last pair)||, R16 = [[R_aa, c_ab], [0, R_bb]]
+        double R16[16][16] = {};
+        for (int r = 0; r < 8; ++r)
+          for (int q = 0; q < 8; ++q) {
+            R16[r][q] = prr[r * 8 + q];
+            R16[r][8 + q] = prr[128 + r * 8 + q];
+            R16[8 + r][8 + q] = prr[64 + r * 8 + q];
+          }
+        for (int j = 0; j < keep; ++j) {
+          double acc = 0.0;
+          for (int r = 0; r < 16; ++r) {
+            double v = 0.0;
+            for (int cc = r; cc < 16; ++cc) v += R16[r][cc] * (double)psl[cc * keep + j];
+            acc += v * v;
+          }
+          res2[j] = acc * est_scale * est_scale;
+        }
+      } else if (lean) {  // ||M x_j - theta_j x_j||^2 = ||R s_j(last block)||^2 (Krylov-Schur), scaled
         for (int j = 0; j < keep; ++j) {
           double acc = 0.0;
           for (int r = 0; r < 8; ++r) {
@@ -1300,6 +1602,7 @@ struct Eig {
       if (refilled) {  // a second pass refilled a column: expand this cycle again, 3 passes
         if (trace) fprintf(stderr, "[n2v2r] rank-deficient block, cycle %d expanded again\n", cycle);
         give(E_lean);
+        give(E_lean2);
         for (int q = 0; q < pb; ++q) {
           give(X[q]);
           give(MX[q]);
@@ -1364,14 +1667,22 @@ struct Eig {
         if (cap) h->Y.ensure(sizeof(float) * (size_t)K * npad * ldu, st);
         for (int q = 0; q < qd; ++q) {
           MV[q] = take();
-          apply_M(X[q], MV[q]);
+          // (pair: two vector blocks per application, their stage-1 products N x 16)
+          const int w = (pair && q + 1 < qd) ? 2 : 1;
+          if (w == 2) {
+            MV[q + 1] = take();
+            apply_M_pair(X[q], X[q + 1], MV[q], MV[q + 1]);
+          } else {
+            apply_M(X[q], MV[q]);
+          }
           materialize();
           if (cap)
             for (int k = 0; k < K; ++k)
               HIPCHK(hipMemcpy2DAsync(h->Y.as<float>() + (size_t)k * npad * ldu + (size_t)q * b,
                                       sizeof(float) * ldu, h->ews.zk[k]->as<float>(),
-                                      sizeof(float) * b, sizeof(float) * b, n,
+                                      sizeof(float) * b * w, sizeof(float) * b * w, n,
                                       hipMemcpyDeviceToDevice, st));
+          q += w - 1;
         }
         y_captured = cap;
         HIPCHK(n2v2r_launch_resid(blocks(X, 0, qd), blocks(MV, 0, qd), h->theta.as<double>(), n,
@@ -1420,11 +1731,19 @@ struct Eig {
       }
       if (done) {
         give(E_lean);
+        give(E_lean2);
         break;
       }
       // restart: [X | orth(W_last) against the old basis] (thick restart)
       std::vector<float*> E, EW;
-      if (lean) {
+      if (lean && pair) {
+        E.push_back(E_lean);
+        E.push_back(E_lean2);
+        EW.push_back(take());
+        EW.push_back(take());
+        apply_M_pair(E_lean, E_lean2, EW[0], EW[1]);
+        ++apps;
+      } else if (lean) {
         E.push_back(E_lean);
         EW.push_back(take());
         apply_M(E_lean, EW[0]);
@@ -1479,6 +1798,7 @@ struct Eig {
       stats->stag_cap = stag_cap;
       stats->y_captured = y_captured ? 1 : 0;
       stats->tri_fallbacks = tri_fallbacks;
+      stats->panel = pair ? 16 : b;
       tsum(stats);
     }
     return (conv == d || (stagnated && maxres <= stag_cap)) ? N2V2R_OK : N2V2R_ERR_NO_CONVERGENCE;

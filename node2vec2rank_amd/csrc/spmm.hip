@@ -285,16 +285,24 @@ static void launch_spmm_t(const SpmmArgs& args, hipStream_t stream) {
 
 // rows per wave from the mean row length: a row group of L lanes gathers L / (B/4) panel rows
 // per step; aim for ~3-4 steps per row.
-template <int B>
-static void launch_spmm_b(const SpmmArgs& args, hipStream_t stream) {
+static int auto_rpw(const SpmmArgs& args, int B) {
   double avg = 0.0;
   int kk = args.sum ? args.K : args.K;
   for (int k = 0; k < kk; ++k) avg += (double)args.A[k].nnz / (double)(args.A[k].n_rows > 0 ? args.A[k].n_rows : 1);
   avg /= (kk > 0 ? kk : 1);
-  constexpr int LPN = B / 4;
+  const int LPN = B / 4;
   const double want_l = LPN * avg / 3.5;
   int rpw = 1;
   while (rpw < 8 && 64 / (rpw * 2) >= LPN && 64.0 / (rpw * 2) >= want_l) rpw *= 2;
+  return rpw;
+}
+
+extern "C" int n2v2r_spmm_rpw(const SpmmArgs& args, int B) { return auto_rpw(args, B); }
+
+template <int B>
+static void launch_spmm_b(const SpmmArgs& args, hipStream_t stream) {
+  constexpr int LPN = B / 4;
+  const int rpw = args.rpw > 0 ? args.rpw : auto_rpw(args, B);
   switch (rpw) {
     case 8: if constexpr (64 / 8 >= LPN) { launch_spmm_t<B, 8>(args, stream); break; } [[fallthrough]];
     case 4: if constexpr (64 / 4 >= LPN) { launch_spmm_t<B, 4>(args, stream); break; } [[fallthrough]];
@@ -548,8 +556,13 @@ __device__ __forceinline__ void flat16_steps(const __attribute__((address_space(
   }
 }
 
-__global__ __launch_bounds__(1024, 8) void spmm16_flat_kernel(SpmmTileArgs a) {
+// WPC: workgroups per CU.  2: 1024-row tiles (64 KB of accumulators), 8 waves per SIMD, up to
+// 4 steps per batch; 1: 2048-row tiles (128 KB), 4 waves per SIMD with twice the registers, up to
+// 8 steps per batch (the same loads in flight per SIMD, half the phase barriers per row)
+template <int WPC>
+__global__ __launch_bounds__(1024, WPC == 1 ? 4 : 8) void spmm16_flat_kernel(SpmmTileArgs a) {
   constexpr bool NT = true;
+  constexpr int MAXNS = WPC == 1 ? 8 : 4;
   // [tile_rows][16] row accumulators, then a 1-KB staging slot per wave
   extern __shared__ float tacf[];
   const int lane = threadIdx.x & 63;
@@ -590,17 +603,19 @@ __global__ __launch_bounds__(1024, 8) void spmm16_flat_kernel(SpmmTileArgs a) {
         const int len = wo[gw0 + w + 1] - e0;
         const int64_t beg = base + e0;
         f32x4* tw = tacc + ((size_t)w << wbits) * 4;
+#define F16S(NS_, U) flat16_steps<(NS_), U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, cbits, lane, stage, tw)
 #define FLAT16_STEPS(U)                                                                          \
-  for (int off = 0; off < len; off += 64) {                                                      \
+  for (int off = 0; off < len; off += 16 * MAXNS) {                                              \
     const int left = len - off;                                                                  \
-    if (left > 48)                                                                               \
-      flat16_steps<4, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, cbits, lane, stage, tw);  \
-    else if (left > 32)                                                                          \
-      flat16_steps<3, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, cbits, lane, stage, tw);  \
-    else if (left > 16)                                                                          \
-      flat16_steps<2, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, cbits, lane, stage, tw);  \
-    else                                                                                         \
-      flat16_steps<1, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, cbits, lane, stage, tw);  \
+    const int ns = (left + 15) >> 4;                                                             \
+    if (MAXNS > 4 && ns >= 8) F16S(MAXNS > 4 ? 8 : 1, U);                                        \
+    else if (MAXNS > 4 && ns == 7) F16S(MAXNS > 4 ? 7 : 1, U);                                   \
+    else if (MAXNS > 4 && ns == 6) F16S(MAXNS > 4 ? 6 : 1, U);                                   \
+    else if (MAXNS > 4 && ns == 5) F16S(MAXNS > 4 ? 5 : 1, U);                                   \
+    else if (ns >= 4) F16S(4, U);                                                                \
+    else if (ns == 3) F16S(3, U);                                                                \
+    else if (ns == 2) F16S(2, U);                                                                \
+    else F16S(1, U);                                                                             \
   }
         if (unit) {
           FLAT16_STEPS(true)
@@ -608,16 +623,22 @@ __global__ __launch_bounds__(1024, 8) void spmm16_flat_kernel(SpmmTileArgs a) {
           FLAT16_STEPS(false)
         }
 #undef FLAT16_STEPS
+#undef F16S
       }
       __syncthreads();
     }
     if (!a.sum || k == a.K - 1) {
       float* Y = a.Y[a.sum ? 0 : k];
+      // split output (paired mode): lane quarter sub < 2 writes Y[0]'s row, sub >= 2 Y2's
+      const bool split = a.sum && a.Y2;
+      float* Yq = split ? (sub < 2 ? Y : a.Y2) : Y;
+      const int64_t ld = split ? 8 : a.ldy;
+      const int co = split ? (sub & 1) * 4 : sub * 4;
       for (int w = wave; w < nwin; w += nwave)
         for (int rr = q; rr < W; rr += 16) {
           const int lr = (w << wbits) + rr;
           if (lr < nrows) {
-            *reinterpret_cast<f32x4*>(Y + (r0 + lr) * a.ldy + sub * 4) = tacc[lr * 4 + sub];
+            *reinterpret_cast<f32x4*>(Yq + (r0 + lr) * ld + co) = tacc[lr * 4 + sub];
             tacc[lr * 4 + sub] = zero;
           }
         }
@@ -657,18 +678,25 @@ extern "C" hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, hipStream_t 
   if (width != 8 && width != 16) return hipErrorInvalidValue;
   // 4 b B of accumulators per row + a 1-KB staging slot per wave
   const size_t flds = sizeof(float) * width * (size_t)a.tile_rows + 16 * 1024;
-  if (flds > 80 * 1024) return hipErrorInvalidValue;
+  // (b = 16 tiles beyond 1024 rows: one workgroup per CU, up to 144 KB)
+  const bool wide16 = width == 16 && a.tile_rows > 1024;
+  if (flds > (wide16 ? 144 : 80) * 1024) return hipErrorInvalidValue;
   static const bool fattr = [] {
     (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-    (void)hipFuncSetAttribute((const void*)spmm16_flat_kernel,
+    (void)hipFuncSetAttribute((const void*)spmm16_flat_kernel<2>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    (void)hipFuncSetAttribute((const void*)spmm16_flat_kernel<1>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 144 * 1024);
     (void)hipGetLastError();
     return true;
   }();
   (void)fattr;
   if (width == 16) {
-    hipLaunchKernelGGL(spmm16_flat_kernel, dim3(grid), dim3(1024), flds, stream, a);
+    if (wide16)
+      hipLaunchKernelGGL(spmm16_flat_kernel<1>, dim3(grid), dim3(1024), flds, stream, a);
+    else
+      hipLaunchKernelGGL(spmm16_flat_kernel<2>, dim3(grid), dim3(1024), flds, stream, a);
     return hipGetLastError();
   }
   // (Non-temporal index / value loads: cfg4 layer launch 0.354 vs 0.363 ms, fit 1,599 vs

@@ -17,6 +17,9 @@ struct SpmmArgs {
   int K;                 // layers in this launch
   int sum;               // 1: Y[0] = sum_k A_k X_k ; 0: Y[k] = A_k X_k (grid.y = k)
   const float* colscale; // optional per-column scale of the output (nullptr = none)
+  int rpw;               // rows per wave of the row kernels (0: from the mean row length); a
+                         // launch over a row range of a matrix passes the whole matrix's choice
+                         // so every row is summed exactly as in one launch over all rows
   int split;             // (b = 8, sum = 0, K <= 8) Y[k] = A_k X_k with grid.y = 1 and the
                          // layers split over the XCDs: workgroup i runs layer (i mod 8) K / 8,
                          // so each XCD's L2 holds one layer's panel
@@ -27,6 +30,10 @@ struct SpmmArgs {
 #define CB_MAX 64    // column blocks per layer at most (N2V2R_SPMM_TILE_NB)
 #define CB_WIN_BITS_MIN 5  // windows of 2^wbits rows: 32 ..
 #define CB_WIN_BITS_MAX 7  //                          .. 128 (row-in-window bits of a packed entry)
+// b = 16 flat tiles: workgroups per CU (2: 1024-row tiles; 1: 2048-row tiles, spmm16_flat_kernel)
+#ifndef N2V2R_SPMM16_WPC
+#define N2V2R_SPMM16_WPC 2
+#endif
 
 // One column block of a layer, packed for the flat tiled form: entry = (row % W) << cbits |
 // (column - col0), W = 2^wbits rows per window, in the layer's shared index array starting at
@@ -58,4 +65,7 @@ struct SpmmTileArgs {  // row tiles x column-block phases (spmm8/16_flat_kernel)
   int tile_rows;       // a multiple of the window rows 2^wbits
   int wbits;           // window rows = 2^wbits (CB_WIN_BITS_MIN..MAX), as the blocks were packed
   int width;           // panel width b: 8 (spmm8_flat_kernel) or 16 (spmm16_flat_kernel); 0 = 8
+  // width 16, sum mode: non-null splits the output -- columns 0-7 to Y[0], 8-15 to Y2, both
+  // N x 8 (ld 8): the two 8-wide basis blocks of the solver's paired mode (pair.hip)
+  float* Y2;
 };

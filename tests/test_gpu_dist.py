@@ -189,3 +189,37 @@ def test_rccl_world1(engine, stage2):
     assert np.abs(res["Y"] - one["Y"]).max() <= 1e-4 * np.abs(one["Y"]).max()
     for c in range(len(one["D"])):
         np.testing.assert_allclose(res["D"][c], one["D"][c], rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("name", ["er20k", "directed_weighted"])
+def test_rs_chunks_bit_identical(monkeypatch, world, name):
+    """The reduce-scatter form's pipelined stage 2 (VERDICT r05 Missing 3): the column share's
+    rows chunk-major, each chunk's product reduce-scattered on the collective stream while the
+    next chunk's runs (N2V2R_RS_CHUNKS, default 4).  Every row is summed as in the one-launch form
+    and every element sums the same ranks' values, so the fit is bit-identical to the
+    unpipelined one (N2V2R_RS_CHUNKS=1) at W = 2, 3, 4."""
+    from node2vec2rank_amd import synthetic
+    if name == "er20k":
+        layers = synthetic.er_layers(20_000, 12, 2, seed_base=71)
+        d, dims, metrics, strategy, seed = 16, [4, 16], ["cosine", "euclidean"], "sequential", 5
+    else:
+        fx = load_fixture(name)
+        layers = fixture_layers(fx)
+        d = int(fx["dims"].max())
+        dims = [int(x) for x in fx["dims"]]
+        metrics = [str(x) for x in fx["metrics"]]
+        strategy, seed = str(fx["strategies"][0]), int(fx["seed"])
+    monkeypatch.setenv("N2V2R_DIST_STAGE2", "rs")
+    out = {}
+    for chunks in ("1", "4"):
+        monkeypatch.setenv("N2V2R_RS_CHUNKS", chunks)
+        out[chunks] = _run_ranks(world, _fit_rank(layers, d, dims, metrics, strategy, seed))
+    a, b = out["1"], out["4"]
+    for ra, rb in zip(a, b):
+        np.testing.assert_array_equal(ra["s"], rb["s"])
+        np.testing.assert_array_equal(ra["Y"], rb["Y"])
+        for c in range(len(ra["D"])):
+            np.testing.assert_array_equal(ra["D"][c], rb["D"][c])
+            np.testing.assert_array_equal(ra["B"][c], rb["B"][c])
+    assert a[0]["stats"]["block_applications"] == b[0]["stats"]["block_applications"]
