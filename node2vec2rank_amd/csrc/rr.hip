@@ -1050,13 +1050,13 @@ extern "C" hipError_t n2v2r_launch_rr_tri_inviter(const double* d, const double*
 // scratch (device, >= n2v2r_rr_tridiag_scratch_bytes(c)): the multi-workgroup form
 // (rr_tridiag_coop_kernel); NULL: the one-workgroup kernel (handles whose ranks share one device
 // pass NULL: their concurrent launches could not all be resident).  N2V2R_RR_TRI=1
-// forces the one-workgroup kernel, N2V2R_RR_TRI_PR the row-residue count (1..4) of the
-// multi-workgroup one.
+// forces the one-workgroup kernel.
 static hipError_t launch_rr_tridiag_coop(double* A, int c, double* d, double* e, double* tau,
                                          double* V, void* scratch, hipStream_t stream) {
   const int nt = (c + TRC_TS - 1) / TRC_TS;
-  int PR = nt > 12 ? 2 : 1;  // <= 12 row tiles per workgroup: <= 99 KB of tiles in LDS
-  if (const char* ev = std::getenv("N2V2R_RR_TRI_PR")) PR = std::max(1, std::min(4, std::atoi(ev)));
+  // <= 12 row tiles per workgroup: <= 99 KB of tiles in LDS (4 row residues were measured no
+  // faster; the N2V2R_RR_TRI_PR switch was retired in round 6)
+  const int PR = nt > 12 ? 2 : 1;
   const int ntr = (nt + PR - 1) / PR;
   const size_t shmem = sizeof(double) * ((size_t)ntr * TRC_TS * TRC_LD + 5 * (size_t)c + 8 * TRC_TS);
   if (shmem > 150 * 1024) return hipErrorInvalidValue;

@@ -415,103 +415,16 @@ __device__ __forceinline__ void rs_factor_lane(int c, int kp, const double* Lb, 
 #undef RS_FSTEP
 }
 
-// lane 0: z = L^{-1} (f_B - fe) in place of f_B, then y_B = L^{-T} D^{-1} z.  The serial chain
-// is one FMA per row; the coefficients of the next 4 rows are loaded from LDS while the
-// current 4 are processed (a row's loads otherwise stall the chain for an LDS round trip).
-#define RS_SG 4
-__device__ __forceinline__ void rs_band_solve_lane(int c, int kp, const double* F, const double* fe, double* f,
-                                   double* y) {
-  const int nb = c - kp;
-  double r[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) r[q] = (q < nb) ? f[kp + q] - fe[q] : 0.0;
-  // forward: row k needs F[k][1..8] and f[kp + k + 8] (rows past nb: zero padding in F is
-  // not there, so the indices are clamped and the values masked)
-  double ca[RS_SG][8], na[RS_SG];
-#pragma unroll
-  for (int u = 0; u < RS_SG; ++u) {
-    const int kk = min(u, nb - 1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) ca[u][i] = F[kk * 9 + 1 + i];
-    na[u] = (u + 8 < nb) ? f[kp + u + 8] : 0.0;
-  }
-  for (int k0 = 0; k0 < nb; k0 += RS_SG) {
-    double cb[RS_SG][8], nbv[RS_SG];
-#pragma unroll
-    for (int u = 0; u < RS_SG; ++u) {
-      const int kk = min(k0 + RS_SG + u, nb - 1);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) cb[u][i] = F[kk * 9 + 1 + i];
-      nbv[u] = (k0 + RS_SG + u + 8 < nb) ? f[kp + k0 + RS_SG + u + 8] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < RS_SG; ++u) {
-      if (k0 + u >= nb) break;
-      const double zk = r[0];
-      f[kp + k0 + u] = zk;
-#pragma unroll
-      for (int q = 0; q < 7; ++q) r[q] = r[q + 1] - ca[u][q] * zk;
-      r[7] = na[u] - ca[u][7] * zk;
-    }
-#pragma unroll
-    for (int u = 0; u < RS_SG; ++u) {
-      na[u] = nbv[u];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) ca[u][i] = cb[u][i];
-    }
-  }
-  // backward: y_k = z_k / d_k - sum_i t_k,i y_{k+i}; the terms with y_{k+2..k+8} are summed
-  // before y_{k+1} arrives, so the chain is one FMA per row
-  double yw[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // y_{k+1} .. y_{k+8}
-  double ba[RS_SG][9], za[RS_SG];
-  const int top = nb - 1;
-#pragma unroll
-  for (int u = 0; u < RS_SG; ++u) {
-    const int kk = max(top - u, 0);
-#pragma unroll
-    for (int i = 0; i < 9; ++i) ba[u][i] = F[kk * 9 + i];
-    za[u] = f[kp + kk];
-  }
-  for (int k0 = top; k0 >= 0; k0 -= RS_SG) {
-    double bb[RS_SG][9], zb[RS_SG];
-#pragma unroll
-    for (int u = 0; u < RS_SG; ++u) {
-      const int kk = max(k0 - RS_SG - u, 0);
-#pragma unroll
-      for (int i = 0; i < 9; ++i) bb[u][i] = F[kk * 9 + i];
-      zb[u] = f[kp + kk];
-    }
-#pragma unroll
-    for (int u = 0; u < RS_SG; ++u) {
-      const int k = k0 - u;
-      if (k < 0) break;
-      double sacc = za[u] * ba[u][0];
-#pragma unroll
-      for (int i = 8; i >= 2; --i) sacc -= ba[u][i] * yw[i - 1];
-      const double v = sacc - ba[u][1] * yw[0];
-#pragma unroll
-      for (int q = 7; q > 0; --q) yw[q] = yw[q - 1];
-      yw[0] = v;
-      y[kp + k] = v;
-    }
-#pragma unroll
-    for (int u = 0; u < RS_SG; ++u) {
-      za[u] = zb[u];
-#pragma unroll
-      for (int i = 0; i < 9; ++i) ba[u][i] = bb[u][i];
-    }
-  }
-}
-#undef RS_SG
 
-// The same two solves with the chains spread over lanes q = lane & 7 (every lane runs them; lanes
-// 0..7 carry the values).  Forward (right-looking): lane q holds r_q, the pending right-hand
+// z = L^{-1} (f_B - fe) in place of f_B, then y_B = L^{-T} D^{-1} z, the chains spread over
+// lanes q = lane & 7 (every lane runs them; lanes 0..7 carry the values).  (Round 2's form ran
+// both chains on lane 0, eight FMAs per row: 79 vs 52 us per solve; its A/B switch
+// N2V2R_INV_SOLVE was retired in round 6.)  Forward (right-looking): lane q holds r_q, the pending right-hand
 // side of row k + q; per row z_k = r_0 is broadcast (readlane), the window shifts one lane
 // (DPP row_shl:1) and each lane applies its own multiplier t_{k,q+1}: one FMA per row on the
 // chain instead of lane 0's eight.  Backward (column form): lane j holds the partial sum of
 // row k - j, y_k = z_k / d_k - acc_0 is broadcast, and every pending row adds t y_k in one FMA.
-// Coefficients are read RS_PF rows ahead.  Same products as rs_band_solve_lane, summed in a
-// different order (rounding differs at the 1e-16 level).
+// Coefficients are read RS_PF rows ahead.
 __device__ __forceinline__ double rs_dpp_shl1(double v) {  // lane l <- lane l + 1 (16-lane rows)
   // (lanes at a row's end keep their own value: callers mask lane 7 and ignore lanes >= 8)
   const int l = __double2loint(v), h = __double2hiint(v);
@@ -638,7 +551,7 @@ __device__ __forceinline__ double rs_wave_sum(double v) {
 
 // y = (H - lam)^{-1} f: the X rows lane-parallel (dX = 1 / (theta - lam)), the band by lane 0
 __device__ __forceinline__ void rs_solve(int c, int kp, const double* Xg, const double* dX, const double* F,
-                         double* fe, double* f, double* y, bool par) {
+                         double* fe, double* f, double* y) {
   const int lane = threadIdx.x;
   if (lane < 8) {  // f_E -= G^T D f_X
     double acc = 0.0;
@@ -646,8 +559,7 @@ __device__ __forceinline__ void rs_solve(int c, int kp, const double* Xg, const 
     fe[lane] = acc;
   }
   __syncthreads();
-  if (par) rs_band_solve_par(c, kp, F, fe, f, y);
-  else if (lane == 0) rs_band_solve_lane(c, kp, F, fe, f, y);
+  rs_band_solve_par(c, kp, F, fe, f, y);
   __syncthreads();
   for (int a = lane; a < kp; a += 64) {  // y_X = D (f_X - G y_E)
     double acc = f[a];
@@ -665,8 +577,7 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
                                                               double* __restrict__ wout,
                                                               double* __restrict__ Y,
                                                               float* __restrict__ S, int ldS,
-                                                              int* __restrict__ err,
-                                                              bool inv_par, bool start_warm) {
+                                                              int* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) double il[];
   const int lane = threadIdx.x;
   const int j0 = blockIdx.x;
@@ -700,8 +611,9 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
     // start vector: for a wanted value j < kp, e_j (the kept Ritz vector j, which the new
     // eigenvector j is close to once the order settles) plus a small random part so no
     // component is zero; otherwise random.  From e_j one solve usually meets the
-    // single-solve test below (N2V2R_INV_START=rand: random starts, A/B)
-    const bool warm = start_warm && j < kp;
+    // single-solve test below (random starts, round 2's form: 77-79 of 80 vectors per cfg2 cycle
+    // took the second solve; its A/B switch N2V2R_INV_START was retired in round 6)
+    const bool warm = j < kp;
     for (int i = lane; i < c; i += 64) {
       const uint64_t hsh = splitmix64(0x9E3779B97F4A7C15ull ^ ((uint64_t)j << 32) ^ (uint64_t)i);
       const double u = (double)(hsh >> 11) * (1.0 / 9007199254740992.0) - 0.5;
@@ -748,7 +660,7 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
     else if (j == j0 && j == 0 && pw > 1) gap = lam - w[1];
     bool ok = true, done = false;
     for (int it = 0; it < 2 && ok; ++it) {
-      rs_solve(c, kp, Xg, dX, F, fe, f, y, inv_par);
+      rs_solve(c, kp, Xg, dX, F, fe, f, y);
       // classical Gram-Schmidt against the cluster's earlier members (Y columns j0 .. j-1)
       for (int q = j0; q < j; ++q) {
         double dq = 0.0;
@@ -881,12 +793,7 @@ extern "C" hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp,
   }
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  // N2V2R_INV_SOLVE=lane: lane 0 runs the band solves (A/B; read per launch)
-  const char* inv_env = getenv("N2V2R_INV_SOLVE");
-  const bool inv_par = !(inv_env && inv_env[0] == 'l');
-  const char* start_env = getenv("N2V2R_INV_START");  // "rand": random start vectors (A/B)
-  const bool start_warm = !(start_env && start_env[0] == 'r');
   hipLaunchKernelGGL(rr_sturm_inviter_kernel, dim3((unsigned)p), dim3(64), linv, stream, scr, c,
-                     kp, p, pm, wbis, 1e-9, theta, Y, S, ldS, err, inv_par, start_warm);
+                     kp, p, pm, wbis, 1e-9, theta, Y, S, ldS, err);
   return hipGetLastError();
 }

@@ -27,8 +27,8 @@
 using namespace n2v2r_int;
 
 namespace n2v2r_int {
-// The column-block SpMM (the flat-window tiled form): b = 8 CSR panels beyond N2V2R_CB_MIN_MB
-// (default 8 MB: beyond one XCD's L2); N2V2R_SPMM_CB=1 / 0 forces it on / off (tests, A/B runs).
+// The column-block SpMM (the flat-window tiled form): b = 8 CSR panels beyond 8 MB (beyond one
+// XCD's L2); N2V2R_SPMM_CB=1 / 0 forces it on / off (tests, A/B runs).
 // Read on every call, so a test can switch it between fits.
 bool col_blocks_wanted(const n2v2r_handle* h, int b);
 
@@ -1178,8 +1178,8 @@ struct Eig {
       // capped at 1e-6: a loose residual tolerance must not loosen the basis orthogonality the
       // Rayleigh-Ritz and the lean residual estimates assume
       reorth_tol = e ? (float)std::atof(e) : (float)std::min(0.1 * tol, 1e-6);
-      const char* m = std::getenv("N2V2R_REORTH_MODE");  // "whole": all blocks or none
-      if (m && m[0] == 'w') reorth_tol = -reorth_tol;
+      // (the pass-level form -- all blocks or none -- gained less at the same threshold, 37.8 vs
+      // 36.5 ms per cfg2 fit; its switch N2V2R_REORTH_MODE was retired in round 6)
     }
     {
       const char* e = std::getenv("N2V2R_REORTH_DEFER");  // read per fit (A/B runs)
@@ -1818,10 +1818,8 @@ bool col_blocks_wanted(const n2v2r_handle* h, int b) {
   // gathers from one panel block, which the Infinity Cache holds even when the whole panel does
   // not (cfg5 on one GPU, 320 MB panel: 9.5 vs 11.5 ms per stage launch) -- so the window has no
   // upper end
-  const char* m = std::getenv("N2V2R_CB_MIN_MB");
-  const double min_mb = m ? atof(m) : 8.0;
   const double panel = 4.0 * b * (double)h->n;
-  return panel > min_mb * 1e6;
+  return panel > 8.0e6;
 }
 // layer k's local rows (nloc x d, the embedding's first d of its ldy columns) to Y + k * stride
 void copy_embedding(n2v2r_handle* h, float* Y, int64_t layer_stride) {

@@ -701,11 +701,11 @@ def test_uase_split_stage2(engine, monkeypatch, layers_k):
     assert np.array_equal(engine.embedding(), Y1)
 
 
-@pytest.mark.parametrize("mode", ["lean", "lean_whole", "images_kept"])
+@pytest.mark.parametrize("mode", ["lean", "images_kept"])
 def test_uase_lean_images_selective_reorth(engine, monkeypatch, mode):
     """Lean images (Krylov-Schur residual estimates, the true residuals checked before the fit
-    ends) and selective reorthogonalisation (full passes apply only the blocks above tol/10,
-    per block or the whole pass) vs the fit with every image kept and every block of every full
+    ends) and selective reorthogonalisation (full passes apply only the blocks above tol/10)
+    vs the fit with every image kept and every block of every full
     pass applied: same sigma within fp32 tolerance, true residuals and orthonormal U on the
     host, the engine's reported residual matching the host's, bit-identical reruns."""
     from node2vec2rank_amd import synthetic
@@ -718,8 +718,6 @@ def test_uase_lean_images_selective_reorth(engine, monkeypatch, mode):
     s_ref = engine.singular_values().copy()
     monkeypatch.setenv("N2V2R_LEAN_W", "0" if mode == "images_kept" else "1")
     monkeypatch.delenv("N2V2R_REORTH_TOL")
-    if mode == "lean_whole":
-        monkeypatch.setenv("N2V2R_REORTH_MODE", "whole")
     st = engine.uase(d, seed=11)
     assert st["converged"] == d and st["rr_fallbacks"] == 0, st
     s = engine.singular_values()
@@ -734,31 +732,6 @@ def test_uase_lean_images_selective_reorth(engine, monkeypatch, mode):
     assert abs(st["max_residual"] - res.max()) < 0.5 * res.max() + 2e-7, (st["max_residual"], res.max())
     np.testing.assert_allclose(X.T @ X, np.eye(d), atol=1e-5)
     engine.uase(d, seed=11)
-    assert np.array_equal(engine.embedding(), Y1)
-
-
-def test_uase_inverse_iteration_random_starts(engine, monkeypatch):
-    """Random inverse-iteration starts instead of the kept Ritz vectors (N2V2R_INV_START=rand)
-    vs the default fit: same sigma within fp32 tolerance, true residuals and orthonormal U on
-    the host, bit-identical reruns."""
-    from node2vec2rank_amd import synthetic
-    layers = synthetic.er_layers(20_003, 16, 2)
-    d = 32
-    engine.set_layers(layers)
-    engine.uase(d, seed=13)
-    s_ref = engine.singular_values().copy()
-    monkeypatch.setenv("N2V2R_INV_START", "rand")
-    st = engine.uase(d, seed=13)
-    assert st["converged"] == d and st["rr_fallbacks"] == 0, st
-    s = engine.singular_values()
-    Y1 = engine.embedding().copy()
-    np.testing.assert_allclose(s, s_ref, rtol=1e-5)
-    X = engine.left_embedding().astype(np.float64) / np.sqrt(s)[None, :]
-    A = sp.hstack(layers).tocsr().astype(np.float64)
-    res = np.linalg.norm(A @ (A.T @ X) - X * (s ** 2)[None, :], axis=0) / s[0] ** 2
-    assert res.max() < 1e-5
-    np.testing.assert_allclose(X.T @ X, np.eye(d), atol=1e-5)
-    engine.uase(d, seed=13)
     assert np.array_equal(engine.embedding(), Y1)
 
 
@@ -800,7 +773,7 @@ def test_uase_block_widths(engine, name, block):
 
 
 # ----------------------------------------------------------------------------- Rayleigh-Ritz
-@pytest.mark.parametrize("form", ["multi", "multi-pr4", "one"])
+@pytest.mark.parametrize("form", ["multi", "one"])
 @pytest.mark.parametrize("c,p", [(40, 12), (256, 80), (300, 100), (512, 160), (600, 150),
                                  (737, 64), (768, 200)])
 def test_rayleigh_ritz_stage(engine, monkeypatch, c, p, form):
@@ -810,8 +783,6 @@ def test_rayleigh_ritz_stage(engine, monkeypatch, c, p, form):
     tight cluster (gaps 1e-9 relative) and an exactly repeated eigenvalue."""
     if form == "one":
         monkeypatch.setenv("N2V2R_RR_TRI", "1")
-    elif form == "multi-pr4":
-        monkeypatch.setenv("N2V2R_RR_TRI_PR", "4")
     rng = np.random.default_rng(c)
     ev = np.sort(rng.random(c))[::-1] * 100.0
     ev[3:8] = ev[3] - 1e-7 * np.arange(5)
@@ -872,15 +843,13 @@ def _band_problem(c, kp, seed, cluster=False, decoupled=0):
     (40, 0, 12, False, 0), (256, 0, 80, False, 0), (256, 80, 80, False, 0),
     (256, 80, 80, True, 30), (384, 160, 160, False, 0), (512, 184, 184, True, 100),
     (96, 80, 80, False, 0)])
-@pytest.mark.parametrize("method", ["sturm", "sturm_lane0", "band"])
+@pytest.mark.parametrize("method", ["sturm", "band"])
 def test_rayleigh_ritz_band_stage(engine, monkeypatch, c, kp, p, cluster, decoupled, method):
     """Banded Rayleigh-Ritz vs numpy eigh of the same structured matrix, both forms: "sturm"
     (Sturm-count multisection + inverse iteration on the unreduced arrow + band matrix, the
     default) and "band" (arrow reduction, bulge chasing, bisection, tridiagonal inverse
     iteration, back-transform)."""
-    # sturm_lane0: the inverse iteration's band solves by lane 0 instead of 8 lanes
-    monkeypatch.setenv("N2V2R_INV_SOLVE", "lane" if method == "sturm_lane0" else "par")
-    monkeypatch.setenv("N2V2R_RR", "sturm" if method == "sturm_lane0" else method)
+    monkeypatch.setenv("N2V2R_RR", method)
     H, hband, theta = _band_problem(c, kp, seed=c + kp, cluster=cluster, decoupled=decoupled)
     w, S = engine.rr_band_top(hband, c, kp, theta, p)
     ref = np.sort(np.linalg.eigvalsh(H))[::-1][:p]
