@@ -645,6 +645,9 @@ struct n2v2r_handle {
   // rank handle per device and runs every call on all of them, one host thread per rank.
   std::vector<n2v2r_handle*> ranks;
   std::unique_ptr<n2v2r_simgroup> own_group;  // the thread communicator's group (devices repeat)
+  // one persistent host thread per rank, started by the first C-ABI call (multi.cpp), stopped and
+  // joined by multi_destroy
+  struct n2v2r_int_rank_pool* pool = nullptr;
   bool broken = false;  // a rank failed alone and the communicator was aborted
   bool multi() const { return !ranks.empty(); }
 };

@@ -146,6 +146,28 @@ int host_threads() {
   return (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
 }
 
+// every value exactly 1.0f (an unweighted layer: its value array need not cross PCIe -- the
+// device copy is filled with 1.0f instead); large layers in up to 16 host threads
+bool host_all_ones(int64_t nnz, const float* dv) {
+  auto ok = [&](int64_t p0, int64_t p1) {
+    bool good = true;
+    for (int64_t p = p0; p < p1; ++p) good &= dv[p] == 1.0f;
+    return good;
+  };
+  int nt = host_threads();
+  if (nnz < (int64_t)1 << 22) nt = 1;
+  if (nt == 1) return ok(0, nnz);
+  std::vector<char> res(nt, 1);
+  const int64_t per = (nnz + nt - 1) / nt;
+  parallel_chunks(nt, [&](int t) {
+    const int64_t p0 = std::min<int64_t>(nnz, t * per);
+    res[t] = ok(p0, std::min<int64_t>(nnz, p0 + per)) ? 1 : 0;
+  });
+  for (char c : res)
+    if (!c) return false;
+  return true;
+}
+
 // every column index in [0, n); large layers are checked in up to 16 host threads
 bool host_indices_in_range(int64_t nnz, const int32_t* ix, int64_t n) {
   auto ok = [&](int64_t p0, int64_t p1) {
@@ -173,8 +195,7 @@ bool upload_rows(hipStream_t st, int64_t r0, int64_t nr, const int64_t* ip, cons
                  const float* dv, DevBuf& dip, DevBuf& dix, DevBuf& ddv, int64_t& nnz_out) {
   const int64_t p0 = ip[r0], p1 = ip[r0 + nr];
   nnz_out = p1 - p0;
-  bool unit = true;
-  for (int64_t p = p0; p < p1 && unit; ++p) unit = dv[p] == 1.0f;
+  const bool unit = host_all_ones(nnz_out, dv + p0);
   std::vector<int64_t> lip(nr + 1);
   for (int64_t r = 0; r <= nr; ++r) lip[r] = ip[r0 + r] - p0;
   dip.ensure(sizeof(int64_t) * (nr + 1));
@@ -183,7 +204,10 @@ bool upload_rows(hipStream_t st, int64_t r0, int64_t nr, const int64_t* ip, cons
   HIPCHK(hipMemcpyAsync(dip.p, lip.data(), sizeof(int64_t) * (nr + 1), hipMemcpyHostToDevice, st));
   if (nnz_out) {
     HIPCHK(hipMemcpyAsync(dix.p, ix + p0, sizeof(int32_t) * nnz_out, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(ddv.p, dv + p0, sizeof(float) * nnz_out, hipMemcpyHostToDevice, st));
+    if (unit)  // (0x3F800000 = 1.0f)
+      HIPCHK(hipMemsetD32Async((hipDeviceptr_t)ddv.p, 0x3F800000, (size_t)nnz_out, st));
+    else
+      HIPCHK(hipMemcpyAsync(ddv.p, dv + p0, sizeof(float) * nnz_out, hipMemcpyHostToDevice, st));
   }
   HIPCHK(hipStreamSynchronize(st));  // lip dies here
   return unit;
@@ -284,7 +308,7 @@ int set_layer_rows_directed(n2v2r_handle* h, int k, const int64_t* aip, const in
     L.unit = upload_rows(h->stream, 0, nr, aip, aix, adv, L.indptr, L.indices, L.data, L.nnz);
     L.t_unit = upload_rows(h->stream, 0, nr, tip, tix, tdv, L.t_indptr, L.t_indices, L.t_data,
                            L.t_nnz);
-    h->h2d_layer_bytes += 16 * (nr + 1) + 8 * (L.nnz + L.t_nnz);
+    h->h2d_layer_bytes += 16 * (nr + 1) + (L.unit ? 4 : 8) * L.nnz + (L.t_unit ? 4 : 8) * L.t_nnz;
     L.symmetric = false;
     L.loaded = true;
     h->have_embedding = false;
@@ -362,11 +386,15 @@ int n2v2r_set_layer_csr(n2v2r_handle* h, int k, int64_t n, int64_t nnz, const in
     dix.ensure(sizeof(int32_t) * std::max<int64_t>(nnz, 1));
     ddv.ensure(sizeof(float) * std::max<int64_t>(nnz, 1));
     HIPCHK(hipMemcpyAsync(dip.p, indptr, sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, st));
+    const bool ones = nnz > 0 && host_all_ones(nnz, data);  // unweighted: no value upload
     if (nnz) {
       HIPCHK(hipMemcpyAsync(dix.p, indices, sizeof(int32_t) * nnz, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(ddv.p, data, sizeof(float) * nnz, hipMemcpyHostToDevice, st));
+      if (ones)
+        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)ddv.p, 0x3F800000, (size_t)nnz, st));
+      else
+        HIPCHK(hipMemcpyAsync(ddv.p, data, sizeof(float) * nnz, hipMemcpyHostToDevice, st));
     }
-    h->h2d_layer_bytes += 8 * (n + 1) + 8 * nnz;
+    h->h2d_layer_bytes += 8 * (n + 1) + (ones ? 4 : 8) * nnz;
     const bool need_t = symmetric != N2V2R_SYM_YES;
     DevBuf* keys = h->ing_keys;
     DevBuf* pay = h->ing_pay;
@@ -592,7 +620,7 @@ int n2v2r_set_layer_csr_rows(n2v2r_handle* h, int k, int64_t n, int64_t row0, in
     L.n_rows = h->nloc;
     L.unit = upload_rows(h->stream, 0, n_rows, indptr, indices, data, L.indptr, L.indices, L.data,
                          L.nnz);
-    h->h2d_layer_bytes += 8 * (n_rows + 1) + 8 * L.nnz;
+    h->h2d_layer_bytes += 8 * (n_rows + 1) + (L.unit ? 4 : 8) * L.nnz;
     L.symmetric = true;
     L.loaded = true;
     h->have_embedding = false;

@@ -17,14 +17,89 @@
 // broken -- later calls fail until it is destroyed.
 #include "engine.h"
 
+#include <functional>
+
 using namespace n2v2r_int;
 
-namespace n2v2r_int {
+// One persistent host thread per rank of a multi handle (round 5 started W new threads per C-ABI
+// call): fanout() posts fn(rank_handle, rank) as a new job generation, every worker runs it once
+// and reports its status.  The ranks start together (a rank running alone would wait in its first
+// collective for ever), or not at all.
+struct n2v2r_int_rank_pool {
+  std::vector<std::thread> th;
+  std::mutex m;
+  std::condition_variable cv_job, cv_done;
+  uint64_t gen = 0;  // job generation: a worker runs each generation once
+  bool stop = false;
+  std::function<int(n2v2r_handle*, int)> job;
+  std::vector<int> st;
+  int done = 0, failed = 0;
+};
 
+namespace n2v2r_int {
 namespace {
 
-// fn(rank_handle, rank) on every rank, one host thread each.  The threads start together (a
-// rank running alone would wait in its first collective for ever), or not at all.
+void pool_worker(n2v2r_handle* h, n2v2r_int_rank_pool* p, int i) {
+  uint64_t seen = 0;
+  for (;;) {
+    std::function<int(n2v2r_handle*, int)> fn;
+    {
+      std::unique_lock<std::mutex> lk(p->m);
+      p->cv_job.wait(lk, [&] { return p->stop || p->gen != seen; });
+      if (p->stop) return;
+      seen = p->gen;
+      fn = p->job;
+    }
+    int s;
+    try {
+      s = fn(h->ranks[i], i);
+    } catch (...) {  // (the C-ABI entry points are guarded; this keeps the pool alive regardless)
+      s = N2V2R_ERR_INTERNAL;
+    }
+    std::lock_guard<std::mutex> lk(p->m);
+    p->st[i] = s;
+    ++p->done;
+    if (s != N2V2R_OK) ++p->failed;
+    p->cv_done.notify_all();
+  }
+}
+
+// start the pool (once per handle); false when the threads cannot be created
+bool pool_start(n2v2r_handle* h) {
+  if (h->pool) return true;
+  auto* p = new (std::nothrow) n2v2r_int_rank_pool();
+  if (!p) return false;
+  const int W = (int)h->ranks.size();
+  p->st.assign(W, N2V2R_OK);
+  try {
+    for (int i = 0; i < W; ++i) p->th.emplace_back(pool_worker, h, p, i);
+  } catch (const std::system_error&) {
+    {
+      std::lock_guard<std::mutex> lk(p->m);
+      p->stop = true;
+    }
+    p->cv_job.notify_all();
+    for (auto& t : p->th) t.join();
+    delete p;
+    return false;
+  }
+  h->pool = p;
+  return true;
+}
+
+void pool_stop(n2v2r_handle* h) {
+  n2v2r_int_rank_pool* p = h->pool;
+  if (!p) return;
+  {
+    std::lock_guard<std::mutex> lk(p->m);
+    p->stop = true;
+  }
+  p->cv_job.notify_all();
+  for (auto& t : p->th) t.join();
+  delete p;
+  h->pool = nullptr;
+}
+
 template <class F>
 int fanout(n2v2r_handle* h, F&& fn) {
   if (h->broken) {
@@ -32,64 +107,43 @@ int fanout(n2v2r_handle* h, F&& fn) {
              "aborted: destroy the handle";
     return N2V2R_ERR_INTERNAL;
   }
-  const int W = (int)h->ranks.size();
-  std::vector<int> st(W, N2V2R_OK);
-  std::mutex m;
-  std::condition_variable cv;
-  int go = 0;  // 1: run, -1: do not
-  int done = 0, failed = 0;
-  std::vector<std::thread> th;
-  th.reserve(W);
-  auto body = [&](int i) {
-    {
-      std::unique_lock<std::mutex> lk(m);
-      cv.wait(lk, [&] { return go != 0; });
-      if (go < 0) return;
-    }
-    const int s = fn(h->ranks[i], i);
-    std::lock_guard<std::mutex> lk(m);
-    st[i] = s;
-    ++done;
-    if (s != N2V2R_OK) ++failed;
-    cv.notify_all();
-  };
-  try {
-    for (int i = 0; i < W; ++i) th.emplace_back(body, i);
-  } catch (const std::system_error&) {
-    {
-      std::lock_guard<std::mutex> lk(m);
-      go = -1;
-    }
-    cv.notify_all();
-    for (auto& t : th) t.join();
+  if (!pool_start(h)) {
     h->err = "could not start one host thread per GPU";
     return N2V2R_ERR_INTERNAL;
   }
+  n2v2r_int_rank_pool* p = h->pool;
+  const int W = (int)h->ranks.size();
   {
-    std::lock_guard<std::mutex> lk(m);
-    go = 1;
+    std::lock_guard<std::mutex> lk(p->m);
+    p->job = [&fn](n2v2r_handle* r, int i) { return fn(r, i); };
+    std::fill(p->st.begin(), p->st.end(), N2V2R_OK);
+    p->done = p->failed = 0;
+    ++p->gen;
   }
-  cv.notify_all();
+  p->cv_job.notify_all();
   {
     // a failure on some ranks while others are still running: give them 10 s to fail alike
     // (the symmetric case: a bad argument, a non-converged fit), then abort the communicator
-    std::unique_lock<std::mutex> lk(m);
-    cv.wait(lk, [&] { return done == W || failed > 0; });
-    if (done < W &&
-        !cv.wait_for(lk, std::chrono::seconds(10), [&] { return done == W; })) {
+    std::unique_lock<std::mutex> lk(p->m);
+    p->cv_done.wait(lk, [&] { return p->done == W || p->failed > 0; });
+    if (p->done < W &&
+        !p->cv_done.wait_for(lk, std::chrono::seconds(10), [&] { return p->done == W; })) {
       lk.unlock();
       if (h->own_group) h->own_group->abort();
       for (n2v2r_handle* r : h->ranks)
         if (r->comm) r->comm->abort();
       h->broken = true;
+      lk.lock();
     }
+    // every rank's call has returned before fn (this frame's) goes out of scope
+    p->cv_done.wait(lk, [&] { return p->done == W; });
+    p->job = nullptr;
   }
-  for (auto& t : th) t.join();
   for (int i = 0; i < W; ++i)
-    if (st[i] != N2V2R_OK) {
+    if (p->st[i] != N2V2R_OK) {
       h->err = "rank " + std::to_string(i) + " (device " + std::to_string(h->ranks[i]->device) +
                "): " + h->ranks[i]->err;
-      return st[i];
+      return p->st[i];
     }
   return N2V2R_OK;
 }
@@ -97,6 +151,7 @@ int fanout(n2v2r_handle* h, F&& fn) {
 }  // namespace
 
 int multi_destroy(n2v2r_handle* h) {
+  pool_stop(h);
   // every rank at once: tearing down an RCCL communicator finalises it with its peers
   std::vector<std::thread> th;
   for (n2v2r_handle* r : h->ranks) {
