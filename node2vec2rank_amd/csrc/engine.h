@@ -556,10 +556,11 @@ struct n2v2r_handle {
       dense_work_elems = need;
     }
     // a symmetric layer on an unpartitioned handle (the operator and its transpose are the same
-    // stored matrix): its upper triangle streamed once for both products (dense_sym_kernel);
-    // N2V2R_DENSE_SYM=0 takes the full-matrix dense_tn form (A/B, tests; read per call)
+    // stored matrix): N2V2R_DENSE_SYM=1 streams its upper triangle once for both products
+    // (dense_sym_kernel; off by default: measured slower than the full-matrix dense_tn form,
+    // DESIGN section 0 round 6); read per call
     const char* sy = std::getenv("N2V2R_DENSE_SYM");
-    if (Bt && Bt == Aloc && nloc == n && !(sy && sy[0] == '0')) {
+    if (Bt && Bt == Aloc && nloc == n && sy && sy[0] == '1') {
       const hipError_t e = n2v2r_launch_dense_sym(Aloc, lda, n, X, ldx, b, Y, ldy, beta, colscale,
                                                   dense_work.as<float>(), dense_work_elems,
                                                   stream);
