@@ -42,9 +42,6 @@ hipError_t n2v2r_launch_spmm(const SpmmArgs& args, int B, hipStream_t stream);
 int n2v2r_spmm_rpw(const SpmmArgs& args, int B);
 hipError_t n2v2r_launch_row_sums(const CsrDev& A, float* out, hipStream_t stream);
 hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, hipStream_t stream);
-hipError_t n2v2r_launch_dense_sym(const float* A, int64_t lda, int64_t n, const float* X, int ldx,
-                                  int b, float* Y, int64_t ldy, float beta, const float* colscale,
-                                  float* work, size_t work_elems, hipStream_t stream);
 hipError_t n2v2r_launch_chunk_major_keys(uint64_t* keys, int64_t nnz, int64_t npad, int W,
                                          int64_t rc, hipStream_t stream);
 // paired-panel mode (pair.hip)
@@ -548,24 +545,10 @@ struct n2v2r_handle {
   // from HBM into the MFMA operands (N2V2R_DENSE_TN=0, read per call: the LDS-staged kernel)
   void dense_apply(const float* Aloc, int64_t lda, const float* X, int ldx, int b, float* Y,
                    int64_t ldy, float beta, const float* colscale, const float* Bt = nullptr) {
-    // split-K slabs (dense_tn / dense_gemm: <= 16) or the symmetric form's tile-row partials
-    const int64_t slabs = std::max<int64_t>(16, (nloc + 511) / 512);
-    const size_t need = (size_t)std::max<int64_t>(nloc, 1) * b * slabs;
+    const size_t need = (size_t)std::max<int64_t>(nloc, 1) * b * 16;
     if (dense_work_elems < need) {
       dense_work.ensure(sizeof(float) * need);
       dense_work_elems = need;
-    }
-    // a symmetric layer on an unpartitioned handle (the operator and its transpose are the same
-    // stored matrix): N2V2R_DENSE_SYM=1 streams its upper triangle once for both products
-    // (dense_sym_kernel; off by default: measured slower than the full-matrix dense_tn form,
-    // DESIGN section 0 round 6); read per call
-    const char* sy = std::getenv("N2V2R_DENSE_SYM");
-    if (Bt && Bt == Aloc && nloc == n && sy && sy[0] == '1') {
-      const hipError_t e = n2v2r_launch_dense_sym(Aloc, lda, n, X, ldx, b, Y, ldy, beta, colscale,
-                                                  dense_work.as<float>(), dense_work_elems,
-                                                  stream);
-      if (e == hipSuccess) return;
-      if (e != hipErrorNotSupported) throw HipFail{e, "n2v2r_launch_dense_sym"};
     }
     const char* tn = std::getenv("N2V2R_DENSE_TN");
     if (Bt && nloc == n && !(tn && tn[0] == '0')) {

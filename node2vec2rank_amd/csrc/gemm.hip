@@ -371,185 +371,6 @@ extern "C" hipError_t n2v2r_launch_dense_tn(const float* B, int64_t ldb, int64_t
   return hipGetLastError();
 }
 
-// ---- Y = A X for a symmetric A (round 6): the upper triangle streamed once ------------------
-// dense_tn_kernel streams all of A (1.6 GB per cfg3 layer, 0.32 ms at ~5 TB/s); a symmetric
-// layer holds the same information in its upper triangle.  Tiles T x T (T = 512) of the upper
-// triangle (I <= J), one 256-thread workgroup each; wave w owns the tile's columns
-// n in [J T + 128 w, + 128).  The tile's rows k are walked in 32-row chunks, the next chunk's
-// loads in flight across the current one's MFMAs (v_mfma_f32_32x32x2_f32 throughout):
-//   P1, Y[J] += A[I,J]^T X[I] (every tile): as dense_tn_kernel -- a chunk row pair streams from
-//       HBM straight into the B operand (lane l: row k0 + 2p + l/32, columns n_w + 4 (l%32) ..
-//       + 3, element q to accumulator q), X[k] the A operand; 4 accumulators over the wave's
-//       128 columns, summed over all 16 chunks;
-//   P2, Y[I] += A[I,J] X[J] (off-diagonal tiles): the same chunk, written to the wave's LDS
-//       slab (columns past N as zeros) and read back transposed as the B operand (lane l: row
-//       k0 + l%32, columns 2 np + l/32), X[n] the A operand (the wave's 64 column pairs of X
-//       in registers for the whole tile); 4 interleaved accumulators, their sum per chunk folded
-//       over the 4 waves through LDS in wave order.
-// Partials: block J's P1 sum from tile (I, J) goes to slot I, block I's P2 sum from tile (I, J)
-// to slot J, so every output block receives exactly one partial per slot 0 .. nb - 1; the fold
-// sums them in slot order (dense_fold_kernel): deterministic, and each A element is read once
-// for both of its products.
-#define DSY_T 512
-#define DSY_LDW 129             // chunk slab row stride (odd: the transposed reads hit 32 banks)
-#define DSY_SLAB 4224           // floats per wave slab: 32 x 129 chunk, then 128 x 33 for P1's output
-__device__ __forceinline__ void dsy_wave_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-}
-
-__global__ __launch_bounds__(256, 1) void dense_sym_kernel(const float* __restrict__ A,
-                                                           int64_t lda, int64_t n, int nbt,
-                                                           const float* __restrict__ X, int ldx,
-                                                           int b, float* __restrict__ part,
-                                                           int64_t slab) {
-  extern __shared__ float dsl[];  // [4][DSY_SLAB] wave slabs | [4][32][33] P2 fold
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int c = lane & 31, h = lane >> 5;
-  // tile (I, J) of the upper triangle, row-major
-  int t = blockIdx.x, I = 0;
-  while (t >= nbt - I) {
-    t -= nbt - I;
-    ++I;
-  }
-  const int J = I + t;
-  const bool diag = I == J;
-  const int64_t kb = (int64_t)I * DSY_T;
-  const int64_t nw = (int64_t)J * DSY_T + 128 * wave;  // (wave-uniform)
-  const int krel_max = (int)((n - kb < DSY_T ? n - kb : DSY_T) - 1);
-  // (a wave whose columns start past the row -- the last block's -- reads clamped columns; the
-  // offsets stay relative to the tile's first row, not to nw, which can lie beyond lda)
-  int64_t nc = nw + 4 * c;
-  if (nc > lda - 4) nc = lda - 4;
-  const uint32_t ncl = (uint32_t)nc;
-  const float* Aw = A + kb * lda;
-  const uint32_t la = (uint32_t)lda;
-  const int jc = c < b ? c : b - 1;
-  float* slabw = dsl + wave * DSY_SLAB;
-  float* fold = dsl + 4 * DSY_SLAB;
-  // P2's A operand: X[nw + 2 np + h][c] for the wave's 64 column pairs (zero past n and b)
-  float xj[64];
-  if (!diag) {
-#pragma unroll
-    for (int np = 0; np < 64; ++np) {
-      const int64_t nn = nw + 2 * np + h;
-      const float v = X[(nn < n ? nn : n - 1) * ldx + jc];
-      xj[np] = (nn < n && c < b) ? v : 0.f;
-    }
-  }
-  f32x16 acc1[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) acc1[q] = f32x16{0.f};
-  f32x4 bb0[16], bb1[16];
-  float xa0[16], xa1[16];
-  auto load = [&](f32x4 (&bb)[16], float (&xa)[16], int ch) {
-#pragma unroll
-    for (int p = 0; p < 16; ++p) {
-      const int kr = 32 * ch + 2 * p + h;
-      const uint32_t krc = (uint32_t)(kr < krel_max ? kr : krel_max);
-      bb[p] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(Aw + (krc * la + ncl)));
-      xa[p] = X[(kb + krc) * ldx + jc];
-    }
-  };
-  auto process = [&](const f32x4 (&bb)[16], const float (&xa)[16], int ch) {
-#pragma unroll
-    for (int p = 0; p < 16; ++p) {
-      const float xm = xa[p] * ((32 * ch + 2 * p + h <= krel_max && c < b) ? 1.f : 0.f);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        acc1[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(xm, bb[p][q], acc1[q], 0, 0, 0);
-    }
-    if (diag) return;
-    // the chunk into the wave's slab (row 2p + h, columns 4c .. 4c + 3; past n: zeros)
-#pragma unroll
-    for (int p = 0; p < 16; ++p)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        slabw[(2 * p + h) * DSY_LDW + 4 * c + q] = (nw + 4 * c + q < n) ? bb[p][q] : 0.f;
-    dsy_wave_sync();
-    f32x16 acc2[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc2[q] = f32x16{0.f};
-#pragma unroll
-    for (int np = 0; np < 64; ++np)
-      acc2[np & 3] = __builtin_amdgcn_mfma_f32_32x32x2f32(xj[np], slabw[c * DSY_LDW + 2 * np + h],
-                                                          acc2[np & 3], 0, 0, 0);
-    // acc2 at lane l: D2[j][k] with j = (r & 3) + 8 (r >> 2) + 4 h, k = k0 + c; the 4 waves'
-    // sums folded in wave order
-    __syncthreads();  // (the previous chunk's fold has been read)
-    float* fw = fold + wave * (32 * 33);
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-      fw[((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + c] = (acc2[0][r] + acc2[1][r]) + (acc2[2][r] + acc2[3][r]);
-    __syncthreads();
-    float* po = part + (int64_t)J * slab;
-    for (int e = threadIdx.x; e < 32 * 32; e += 256) {
-      const int kk = e >> 5, j = e & 31;
-      const int64_t row = kb + 32 * ch + kk;
-      const float s = ((fold[j * 33 + kk] + fold[32 * 33 + j * 33 + kk]) + fold[2 * 32 * 33 + j * 33 + kk]) +
-                      fold[3 * 32 * 33 + j * 33 + kk];
-      if (row < n && j < b) po[row * b + j] = s;
-    }
-  };
-  // (the loads of chunk ch + 1 issued before chunk ch's MFMAs; sched_barrier keeps them there)
-  load(bb0, xa0, 0);
-  __builtin_amdgcn_sched_barrier(0);
-  for (int ch = 0; ch < DSY_T / 32; ch += 2) {
-    load(bb1, xa1, ch + 1);
-    __builtin_amdgcn_sched_barrier(0);
-    process(bb0, xa0, ch);
-    if (ch + 2 < DSY_T / 32) load(bb0, xa0, ch + 2);
-    __builtin_amdgcn_sched_barrier(0);
-    process(bb1, xa1, ch + 1);
-  }
-  // P1: acc1[q][r] = Y^T[j][nw + 4c + q], j = (r & 3) + 8 (r >> 2) + 4 h -> slot I, through the
-  // wave's slab as [128 n][33]
-  dsy_wave_sync();
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) slabw[(4 * c + q) * 33 + (r & 3) + 8 * (r >> 2) + 4 * h] = acc1[q][r];
-  dsy_wave_sync();
-  float* po = part + (int64_t)I * slab;
-  for (int e = lane; e < 128 * 32; e += 64) {
-    const int nl = e >> 5, j = e & 31;
-    const int64_t col = nw + nl;
-    if (col < n && j < b) po[col * b + j] = slabw[nl * 33 + j];
-  }
-}
-
-// Y (n x b, ld ldy) = beta * Y + colscale .* (A X) for a symmetric n x n A (row-major, lda);
-// `work` holds the partials (ceil(n / 512) * n * b floats).  hipErrorNotSupported when the form
-// does not apply (the caller then takes dense_tn / dense_gemm).
-extern "C" hipError_t n2v2r_launch_dense_sym(const float* A, int64_t lda, int64_t n, const float* X,
-                                            int ldx, int b, float* Y, int64_t ldy, float beta,
-                                            const float* colscale, float* work,
-                                            size_t work_elems, hipStream_t stream) {
-  if (n < 2 * DSY_T || b < 1 || b > 32 || !work || lda % 4 != 0 || lda < n ||
-      ((uintptr_t)A & 15) != 0 || (double)(DSY_T + 1) * (double)lda >= 4294967296.0)
-    return hipErrorNotSupported;
-  const int nbt = (int)((n + DSY_T - 1) / DSY_T);
-  if ((size_t)nbt * (size_t)n * (size_t)b > work_elems) return hipErrorNotSupported;
-  const size_t lds = sizeof(float) * (4 * DSY_SLAB + 4 * 32 * 33);
-  static const bool attr = [lds] {
-    (void)hipFuncSetAttribute((const void*)dense_sym_kernel,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    (void)hipGetLastError();
-    return true;
-  }();
-  (void)attr;
-  const unsigned tiles = (unsigned)((int64_t)nbt * (nbt + 1) / 2);
-  hipLaunchKernelGGL(dense_sym_kernel, dim3(tiles), dim3(256), lds, stream, A, lda, n, nbt, X, ldx,
-                     b, work, n * b);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  const int64_t elems = n * b;
-  hipLaunchKernelGGL(dense_fold_kernel, dim3((unsigned)((elems + 255) / 256)), dim3(256), 0, stream,
-                     work, nbt, n * b, n, b, Y, ldy, beta, colscale);
-  return hipGetLastError();
-}
-
 // out[c][r] = in[r][c] for an (rows x cols) block, leading dimensions ldi / ldo
 __global__ void transpose_kernel(const float* __restrict__ in, int64_t ldi, int64_t rows,
                                  int64_t cols, float* __restrict__ out, int64_t ldo) {

@@ -31,31 +31,6 @@ def test_dense_gemm_matches_numpy(engine, n, b, form, monkeypatch):
             assert ms > 0 and by == pytest.approx(4.0 * n * n + 4.0 * 2 * n * b)
 
 
-@pytest.mark.parametrize("b", [8, 16, 32])
-@pytest.mark.parametrize("n", [1024, 1037, 2501, 4100])
-def test_dense_sym_matches_numpy(engine, n, b, monkeypatch):
-    """The symmetric dense form (dense_sym_kernel: the upper triangle's 512 x 512 tiles read once
-    for both of their products, tile-row partials folded in fixed order) against an fp64 product
-    and against the full-matrix dense_tn form (N2V2R_DENSE_SYM=0), on sizes that are not a
-    multiple of the tile (edge rows and columns masked, uninitialised lda padding ignored);
-    deterministic reruns."""
-    rng = np.random.default_rng(n * 7 + b)
-    S = rng.standard_normal((n, n)).astype(np.float32)
-    S = np.triu(S) + np.triu(S, 1).T          # exactly symmetric
-    engine.set_layers([S, S.copy()], storage="dense", symmetric=-1)
-    X = rng.standard_normal((n, b)).astype(np.float32)
-    monkeypatch.setenv("N2V2R_DENSE_SYM", "1")
-    Y, _, _ = engine.bench_spmm(0, X, transpose=False, reps=2)
-    Y2, _, _ = engine.bench_spmm(0, X, transpose=False, reps=1)
-    np.testing.assert_array_equal(Y, Y2)
-    ref = S.astype(np.float64) @ X.astype(np.float64)
-    scale = np.abs(S).astype(np.float64) @ np.abs(X).astype(np.float64)
-    assert np.all(np.abs(Y - ref) <= 2e-6 * scale + 1e-6), np.abs(Y - ref).max()
-    monkeypatch.setenv("N2V2R_DENSE_SYM", "0")
-    Yt, _, _ = engine.bench_spmm(0, X, transpose=False, reps=1)
-    assert np.all(np.abs(Y - Yt) <= 4e-6 * scale + 1e-6)
-
-
 def test_dense_symmetry_detection(engine):
     rng = np.random.default_rng(5)
     S = rng.random((300, 300)).astype(np.float32)
