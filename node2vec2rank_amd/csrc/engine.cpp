@@ -187,7 +187,7 @@ static int time_tiled(n2v2r_handle* h, int k, int transpose, int nb, const float
     nb = 4;
     while (nb < 64 && (double)h->n * 32.0 / nb > 2.0 * 1024 * 1024) nb *= 2;
   }
-  if (nb != 4 && nb != 8 && nb != 16 && nb != 32 && nb != 64) return N2V2R_ERR_BAD_ARG;
+  if (nb != 4 && nb != 8 && nb != 16 && nb != 32 && nb != 64 && nb != 128) return N2V2R_ERR_BAD_ARG;
   LayerDev& L = *h->layers[k];
   const int wb = tile_wbits(h->layers, nb);
   if (!ensure_col_blocks(L, h->n, h->stream, nb, wb)) return N2V2R_ERR_BAD_ARG;

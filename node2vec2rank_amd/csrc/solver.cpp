@@ -1061,7 +1061,8 @@ struct Eig {
       }
       const char* tn_ = std::getenv("N2V2R_SPMM_TILE_NB");
       tile_nb = tn_ ? std::atoi(tn_) : nb_auto;
-      if (tile_nb != 4 && tile_nb != 8 && tile_nb != 16 && tile_nb != 32 && tile_nb != 64)
+      if (tile_nb != 4 && tile_nb != 8 && tile_nb != 16 && tile_nb != 32 && tile_nb != 64 &&
+          tile_nb != 128)
         tile_nb = nb_auto;
       // packed entries need the in-block column bits to fit beside the row-in-window bits
       // (always, for N < 2^26 per block); otherwise the row kernel runs

@@ -888,6 +888,7 @@ extern "C" hipError_t n2v2r_launch_cb_count(const CsrDev& A, int64_t cw, int nb,
   else if (nb == 16) hipLaunchKernelGGL(cb_count_kernel<16>, g, dim3(256), 0, stream, A, cw, cnt);
   else if (nb == 32) hipLaunchKernelGGL(cb_count_kernel<32>, g, dim3(256), 0, stream, A, cw, cnt);
   else if (nb == 64) hipLaunchKernelGGL(cb_count_kernel<64>, g, dim3(256), 0, stream, A, cw, cnt);
+  else if (nb == 128) hipLaunchKernelGGL(cb_count_kernel<128>, g, dim3(256), 0, stream, A, cw, cnt);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
@@ -903,6 +904,7 @@ extern "C" hipError_t n2v2r_launch_cb_fill(const CsrDev& A, int64_t cw, int nb, 
   else if (nb == 16) FILL(16);
   else if (nb == 32) FILL(32);
   else if (nb == 64) FILL(64);
+  else if (nb == 128) FILL(128);
   else return hipErrorInvalidValue;
 #undef FILL
   return hipGetLastError();

@@ -27,7 +27,7 @@ struct SpmmArgs {
 
 // ---- column blocks (b = 8 panels beyond 8 MB: the flat-window tiled SpMM) --------------------
 #define CB_NB 8      // default column blocks when a caller names none (the fit picks 4-32)
-#define CB_MAX 64    // column blocks per layer at most (N2V2R_SPMM_TILE_NB)
+#define CB_MAX 128   // column blocks per layer at most (N2V2R_SPMM_TILE_NB)
 #define CB_WIN_BITS_MIN 5  // windows of 2^wbits rows: 32 ..
 #define CB_WIN_BITS_MAX 7  //                          .. 128 (row-in-window bits of a packed entry)
 // b = 16 flat tiles: workgroups per CU (2: 1024-row tiles; 1: 2048-row tiles, spmm16_flat_kernel)

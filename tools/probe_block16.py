@@ -16,7 +16,9 @@ d = int(sys.argv[3]) if len(sys.argv) > 3 else 128
 combos = [(8, 0, 0), (16, 0, 0), (16, 0, 640), (16, 0, 768), (16, 192, 640), (16, 224, 768)]
 if len(sys.argv) > 4:  # "b:keep:basis,..."
     combos = [tuple(int(v) for v in c.split(":")) for c in sys.argv[4].split(",")]
-layers = synthetic.er_layers(n, deg, 2, seed_base=int(os.environ.get("PROBE_SEED", "2000")))
+seed_base = int(os.environ.get("PROBE_SEED", "2000"))
+layers = (synthetic.er_layers(n, deg, 2, seed_base=seed_base) if n <= 2_000_000 else
+          [synthetic.er_layer_rows(n, deg, seed_base + k) for k in range(2)])
 eng = _lib.Engine(0)
 eng.set_layers(layers)
 for b, keep, basis in combos:
