@@ -26,10 +26,10 @@ struct CsrDev {
 };
 
 // Up to this many basis blocks are addressed through a by-value pointer table.
-#define N2V2R_MAX_BLOCKS 96
+#define N2V2R_MAX_BLOCKS 112
 // the largest b = 8 basis the fused PIP pass (its (c + 8) x 8 Gram and c x 8 coefficients in
-// 64 KB of LDS), the paired passes and the banded Rayleigh-Ritz take
-#define N2V2R_BAND_MAXC 640
+// LDS: 77 KB at 768), the paired passes and the banded Rayleigh-Ritz take
+#define N2V2R_BAND_MAXC 768
 
 struct BlockList {
   const float* blk[N2V2R_MAX_BLOCKS];

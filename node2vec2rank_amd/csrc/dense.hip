@@ -2215,7 +2215,20 @@ extern "C" hipError_t n2v2r_launch_pip_fused(const BlockList& Q, const float* Zi
   if (skip_tol != 0.f && (Zin != Zout || save)) return hipErrorInvalidValue;
   const size_t lds = sizeof(double) * ((size_t)(c + 8) * 8 + 256) + sizeof(float) * ((size_t)c * 8 + 64) + 16 +
                      4 * (size_t)(c / 8 > 64 ? c / 8 : 64);
-  if (lds > 64 * 1024 || c > N2V2R_BAND_MAXC) return hipErrorInvalidValue;
+  if (lds > 80 * 1024 || c > N2V2R_BAND_MAXC) return hipErrorInvalidValue;
+  if (lds > 64 * 1024) {  // bases past 640 columns (two workgroups per CU still fit)
+    static const hipError_t attr = [] {
+      hipError_t e = hipSuccess;
+      for (const void* f : {(const void*)pip_fused_kernel<4, 2, true>, (const void*)pip_fused_kernel<4, 2, false>,
+                            (const void*)pip_fused_kernel<2, 4, true>, (const void*)pip_fused_kernel<2, 4, false>}) {
+        const hipError_t a = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+        if (e == hipSuccess) e = a;
+      }
+      (void)hipGetLastError();
+      return e;
+    }();
+    if (attr != hipSuccess) return attr;
+  }
   // rows per workgroup (64 or 128 per wave); 128 rows: cfg2 flat, cfg4 +20 % (every workgroup
   // stages the (c + 8) x 8 fp64 Gram, 33 KB at c = 512)
   // 512 rows per workgroup from N = 512k rows on (the per-workgroup prologue -- Gram staging,

@@ -167,6 +167,8 @@ hipError_t n2v2r_launch_rr_sturm(const double* hband, int c, int kp, double* the
                                  size_t scr_elems, double* Y, float* S, int ldS, int p, int* err,
                                  hipStream_t stream);
 size_t n2v2r_rr_sturm_scratch(int c, int p);
+hipError_t n2v2r_launch_rr_band_expand(const double* hband, int c, int kp, const double* theta,
+                                       double* H, hipStream_t stream);
 hipError_t n2v2r_launch_csr_scan(const int64_t* ip, const int32_t* ix, const float* dv,
                                  int64_t n_rows, int64_t n_cols, uint64_t* keys, int32_t* idx,
                                  unsigned* flags, hipStream_t stream);

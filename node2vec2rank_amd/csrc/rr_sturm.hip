@@ -705,6 +705,37 @@ __global__ __launch_bounds__(64) void rr_sturm_inviter_kernel(const double* __re
   }
 }
 
+// Dense H (c x c, fp64, row-major, ld c) from the same arrow + band structure: the dense
+// Rayleigh-Ritz's input when a Sturm vector fails its check and the kept set is past the
+// reducing path's arrow (kp + 8 > 192, rr_band.hip's LDS-resident arrow).  theta: the kept
+// Ritz values (the copy the prep kernel made).
+__global__ __launch_bounds__(256) void rr_band_expand_kernel(const double* __restrict__ hband,
+                                                             int c, int kp,
+                                                             const double* __restrict__ theta,
+                                                             double* __restrict__ H) {
+  constexpr int W = RS_W;
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)c * c) return;
+  const int i = (int)(idx / c), j = (int)(idx % c);
+  const int lo = i < j ? i : j, hi = i < j ? j : i;
+  double v;
+  if (hi < kp) v = (i == j) ? theta[i] : 0.0;                          // diag(Theta)
+  else if (lo < kp) v = (hi < kp + W) ? hband[lo * W + (hi - kp)] : 0.0;  // X rows -> E
+  else v = rs_band_entry(hband, c, kp, hi, lo);                        // the band
+  H[idx] = v;
+}
+
+extern "C" hipError_t n2v2r_launch_rr_band_expand(const double* hband, int c, int kp,
+                                                 const double* theta, double* H,
+                                                 hipStream_t stream) {
+  if (c < 9 || c > RS_MAXC || c % RS_W || kp % RS_W || kp + RS_W > c || (kp > 0 && !theta))
+    return hipErrorInvalidValue;
+  const int64_t total = (int64_t)c * c;
+  hipLaunchKernelGGL(rr_band_expand_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     stream, hband, c, kp, theta, H);
+  return hipGetLastError();
+}
+
 static size_t rs_asm_elems(int c, int kp) {  // header + Xd + Xg + padded band rows
   return (size_t)RS_HDR + (size_t)kp * (1 + RS_W) + (size_t)(c - kp + RS_PADR) * RS_LD;
 }

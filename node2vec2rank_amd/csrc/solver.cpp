@@ -57,6 +57,17 @@ bool pair_default(const n2v2r_handle* h, int d) {
   return false;
 }
 
+// The default basis cap of the b = 8 banded fits: 640 columns, N2V2R_BAND_MAXC = 768 for graphs
+// from 4M nodes (round 6: the fused PIP pass past 64 KB of LDS; at cfg4's 1M nodes 768 columns
+// are no better -- 771 block applications against 788 on one graph, 846 against 788 on the
+// bench's --, at cfg5's 10M they are, see the kept-set rule below; profiles/r06_keep_basis.jsonl).
+// The paired-panel mode keeps 640 (its measured configuration), and so does the reducing banded
+// Rayleigh-Ritz (its arrow, chase and back-transform were never run past 640 columns: the Sturm
+// form's fallback beyond is the dense one on H expanded from the band).
+constexpr int kAutoMaxc = 640;
+constexpr int kPairMaxc = 640;
+constexpr int kReduceMaxc = 640;
+
 // ---- the eigensolver ----------------------------------------------------------------------
 struct Eig {
   n2v2r_handle* h;
@@ -79,7 +90,8 @@ struct Eig {
   uint64_t fill_counter = 0;
   int kry0 = 0;             // index of the first Krylov block of the current cycle
   bool full_first = false;  // N2V2R_EIG_FULL_FIRST_PASS
-  bool band_rr = false;     // banded Rayleigh-Ritz (b = 8, c <= 512), else dense
+  bool band_rr = false;     // banded Rayleigh-Ritz (b = 8, c <= 640), else dense
+  bool band_reduce = false; // the reducing banded path takes the cycle (keep + 8 <= 192, c <= 640)
   // the flat-window tiled column-block SpMM (b = 8, panels beyond 8 MB): row tiles with LDS
   // accumulators walking tile_nb column-block phases, one launch per stage
   bool col_blocks = false;
@@ -948,12 +960,18 @@ struct Eig {
     // applications and 215-218 ms per fit against 66 and 236-240 ms with the general rule's
     // keep 5d/4 = 320 and basis 768 (profiles/r04_cfg3_sweep*.jsonl)
     const bool dense_rule = h->dense_layers() && !o.block;
+    // graphs from 4M nodes (d <= 160, CSR layers): keep 7d/4 and bases up to 768 columns (round
+    // 6, d = 128: cfg5's N = 10M 1,728 block applications and 41.9 s per fit against 1,909 and
+    // 44.7 s at keep 168 / basis 640; at N = 3M keep 224 and 168 tie, at cfg4's 1M keep 168 and
+    // basis 640 win; profiles/r06_keep_basis.jsonl)
+    const bool big_graph = !dense_rule && nglob >= ((int64_t)1 << 22) && d <= 160;
     for (;; b /= 2) {
       keep = o.keep ? o.keep : (dense_rule ? d + b : std::max(d + 16, (d * 21) / 16));
       keep = ((keep + b - 1) / b) * b;
       // (not past the banded Rayleigh-Ritz's 184 kept vectors where the former rule fit them)
       if (!o.keep && !dense_rule && b == 8 && keep > 184 && std::max(d + 16, (d * 5) / 4) <= 184)
         keep = 184;
+      if (!o.keep && big_graph && b == 8) keep = std::max(keep, ((d * 7) / 4 + 7) / 8 * 8);
       // default basis: 3.2 keep for the dense Rayleigh-Ritz (its cost grows as c^3); 4.8 keep
       // (<= 512) for the banded one (b = 8), where fewer, longer cycles win (cfg2: 14 cycles
       // at c = 256, 7 at c = 384, 13 % fewer block applications)
@@ -968,7 +986,7 @@ struct Eig {
       // 1.41-1.42 s per fit at c = 576-640 against 838 and 1.51 s at 512,
       // profiles/r05_basis_b8.jsonl)
       maxc = o.max_basis ? o.max_basis
-                         : (band_ok ? std::min(N2V2R_BAND_MAXC,
+                         : (band_ok ? std::min(big_graph ? N2V2R_BAND_MAXC : kAutoMaxc,
                                                std::max(keep + 3 * b, (24 * keep_basis) / 5))
                                     : std::max(keep + 3 * b, (16 * keep_basis) / 5));
       maxc = ((maxc + b - 1) / b) * b;
@@ -1000,12 +1018,12 @@ struct Eig {
         ((o.solver_flags & N2V2R_EIG_PANEL16) || pair_default(h, d))) {
       int pk = (keep + 15) / 16 * 16;
       int pc = o.max_basis ? o.max_basis / 16 * 16
-                           : std::min(N2V2R_BAND_MAXC,
+                           : std::min(kPairMaxc,
                                       std::max(pk + 48, (24 * ((std::max(d + 16, (d * 5) / 4) + 7) / 8 * 8)) / 5));
       pc = pc / 16 * 16;
-      const int cap16 = (int)std::min<int64_t>((nglob / 2) / 16 * 16, (int64_t)N2V2R_BAND_MAXC);
+      const int cap16 = (int)std::min<int64_t>((nglob / 2) / 16 * 16, (int64_t)kPairMaxc);
       if (pc > cap16) pc = cap16;
-      if (pk + 32 <= pc && pc <= N2V2R_BAND_MAXC) {
+      if (pk + 32 <= pc && pc <= kPairMaxc) {
         pair = true;
         keep = pk;
         maxc = pc;
@@ -1148,8 +1166,12 @@ struct Eig {
     h->ews.anyflag.ensure(sizeof(int) * 4);
     h->theta.ensure(sizeof(double) * c_max);
     h->resid.ensure(sizeof(double) * c_max);
+    // (kept sets past the reducing path's 192-row arrow, and bases past its 640 columns, take
+    // the banded form only with the Sturm one, whose failure falls back to the dense
+    // Rayleigh-Ritz on H expanded from the band)
+    band_reduce = keep + 8 <= 192 && c_max <= kReduceMaxc;
     band_rr = !pair && b == 8 && !(o.solver_flags & N2V2R_EIG_DENSE_RR) &&
-              c_max <= N2V2R_BAND_MAXC && keep + 8 <= 192;
+              c_max <= N2V2R_BAND_MAXC && (band_reduce || rr_sturm_enabled());
     if (band_rr) {
       h->ews.hband.ensure(sizeof(double) * ((size_t)(keep + b) * b + (size_t)nb_max * 2 * b * b));
       h->ews.band.ensure(sizeof(double) * (size_t)c_max * (b + 1));
@@ -1292,6 +1314,7 @@ struct Eig {
       }
       float* E_lean = nullptr;  // lean: the restart block, built before the convergence test
       bool dense_rr = !band_rr;
+      bool band_expand = false;  // dense Rayleigh-Ritz on H expanded from the band (fallback)
       bool sturm_now = sturm;  // this cycle's banded form (the reducing one after a failure)
       int rr_err = 0;
       bool th_saved = false;  // pair: the kept Ritz values copied for this cycle's assembly
@@ -1353,6 +1376,9 @@ struct Eig {
           HIPCHK(n2v2r_launch_pair_h_assemble(h->ews.hcol.as<double>(), hc_ld, hc_lo.data() + kry0,
                                               hc_nr.data() + kry0, kry0, nq - kry0, kry0 * b,
                                               h->ews.pth.as<double>(), Hd, c, st));
+        } else if (band_expand) {
+          HIPCHK(n2v2r_launch_rr_band_expand(h->ews.hband.as<double>(), c, kry0 * b,
+                                             h->theta.as<double>(), h->ews.gsmall.as<double>(), st));
         } else {
           tn(blocks(Q, 0, nq), blocks(W, 0, nq), h->ews.gsmall.as<double>(), nullptr);
         }
@@ -1573,6 +1599,10 @@ struct Eig {
           HIPCHK(hipMemcpyAsync(h->theta.as<double>(), h->ews.sturm.as<double>() + 4,
                                 sizeof(double) * kry0 * b, hipMemcpyDeviceToDevice, st));
         sturm_now = false;
+        if (!band_reduce) {  // past the reducing path's arrow: dense, from the band
+          dense_rr = true;
+          band_expand = true;
+        }
         rr_err = 0;
         ++stats_rr_fallbacks;
         goto rayleigh_ritz;

@@ -954,15 +954,66 @@ def test_uase_sturm_failure_reducing_path_no_pool_growth(engine):
     d = 32
     engine.set_layers(layers)
     st0 = engine.uase(d, seed=21)
+    s0 = engine.singular_values()
     st = engine.uase(d, seed=21, solver_flags=32)
     assert st["converged"] == d and st["rr_fallbacks"] == st["restarts"], st
     assert st["pool_blocks"] <= st0["pool_blocks"], (st["pool_blocks"], st0["pool_blocks"])
-    np.testing.assert_allclose(engine.singular_values()[:d], engine.singular_values()[:d])
     s = engine.singular_values()
+    np.testing.assert_allclose(s[:d], s0[:d], rtol=1e-5)
     X = engine.left_embedding().astype(np.float64) / np.sqrt(s)[None, :]
     A = sp.hstack(layers).tocsr().astype(np.float64)
     res = np.linalg.norm(A @ (A.T @ X) - X * (s ** 2)[None, :], axis=0) / s[0] ** 2
     assert res.max() < 1e-5
+
+
+def test_uase_large_kept_set_sturm_failure_dense_from_band(engine):
+    """A kept set past the reducing band path's 192-row arrow (keep 224) still takes the lean,
+    Sturm Rayleigh-Ritz; forced to fail there (test flag 32), each cycle's fallback is the dense
+    Rayleigh-Ritz on H expanded from the saved band (rr_band_expand_kernel), not a refit without
+    lean images.  Both fits: every pair converged, the same singular values, host fp64
+    residuals."""
+    from node2vec2rank_amd import synthetic
+    layers = synthetic.er_layers(60_001, 20, 2, seed_base=77)
+    d = 128
+    engine.set_layers(layers)
+    st0 = engine.uase(d, seed=5, keep=224)
+    s0 = engine.singular_values()
+    st = engine.uase(d, seed=5, keep=224, solver_flags=32)
+    s = engine.singular_values()
+    assert st0["converged"] == d and st0["rr_fallbacks"] == 0, st0
+    assert st["converged"] == d and st["rr_fallbacks"] == st["restarts"], st
+    assert st["lean_checks"] > 0 and st0["lean_checks"] > 0, (st0, st)
+    np.testing.assert_allclose(s[:d], s0[:d], rtol=1e-5)
+    X = engine.left_embedding().astype(np.float64)[:, [0, d // 2, d - 1]]
+    X /= np.sqrt(s[[0, d // 2, d - 1]])[None, :]
+    A = sp.hstack(layers).tocsr().astype(np.float64)
+    res = np.linalg.norm(A @ (A.T @ X) - X * (s[[0, d // 2, d - 1]] ** 2)[None, :], axis=0) / s[0] ** 2
+    assert res.max() < 1e-5, res
+
+
+@pytest.mark.parametrize("keep,flags", [(168, 0), (168, 32), (256, 0)])
+def test_uase_basis_768_fused_lean(engine, keep, flags):
+    """Bases up to N2V2R_BAND_MAXC = 768 columns on the lean, fused, banded path (the fused PIP
+    pass past 64 KB of LDS, block lists past 96 entries): converged, the singular values of a
+    640-column fit, host fp64 residuals; flag 32 fails every cycle's Sturm stage: past
+    640 columns the fallback is the dense Rayleigh-Ritz on H expanded from the band (the
+    reducing band path stays at <= 640 columns)."""
+    from node2vec2rank_amd import synthetic
+    layers = synthetic.er_layers(60_001, 20, 2, seed_base=78)
+    d = 128
+    engine.set_layers(layers)
+    engine.uase(d, seed=5, max_basis=640)
+    s0 = engine.singular_values()
+    st = engine.uase(d, seed=5, keep=keep, max_basis=768, solver_flags=flags)
+    s = engine.singular_values()
+    assert st["converged"] == d and st["basis"] == 768 and st["lean_checks"] > 0, st
+    assert st["rr_fallbacks"] == (st["restarts"] if flags else 0), st
+    np.testing.assert_allclose(s[:d], s0[:d], rtol=1e-5)
+    cols = [0, d // 2, d - 1]
+    X = engine.left_embedding().astype(np.float64)[:, cols] / np.sqrt(s[cols])[None, :]
+    A = sp.hstack(layers).tocsr().astype(np.float64)
+    res = np.linalg.norm(A @ (A.T @ X) - X * (s[cols] ** 2)[None, :], axis=0) / s[0] ** 2
+    assert res.max() < 1e-5, res
 
 
 def test_uase_loose_tolerance_keeps_orthogonality(engine):
