@@ -1146,10 +1146,12 @@ struct Eig {
     pending = nullptr;
     if (split2) h->ews.s2part.ensure(sizeof(float) * (size_t)K * npad * 8);
     // chunk partials: also the streaming Gram form at b = 8 (chunks of <= 8192 rows, rounded to
-    // a multiple of 8, (c + b) x b fp64 each)
+    // a multiple of 8, (c + b) x b fp64 each) and the paired full passes' two-block Gram
+    // (2 (c + 2b) x b per chunk; round 6: sized for one block's, the pair fell back to two
+    // separate full passes past ~48 basis blocks at N = 10M -- 2 x 3.7 ms instead of one read)
     h->partial_elems = std::max<size_t>(4096ull * 1024ull, (size_t)c_max * c_max * 8);
     h->partial_elems = std::max<size_t>(h->partial_elems,
-                                        (size_t)((n + 8191) / 8192 + 16) * (c_max + b) * b);
+                                        (size_t)((n + 8191) / 8192 + 24) * 2 * (c_max + 2 * b) * b);
     h->partial.ensure(sizeof(double) * h->partial_elems);
     h->ews.gsmall.ensure(sizeof(double) * (size_t)c_max * c_max);
     h->ews.csmall.ensure(sizeof(float) * (size_t)c_max * c_max);
