@@ -129,6 +129,32 @@ def test_multi_engine_matches_hand_run_ranks_and_ingest_forms():
             np.testing.assert_array_equal(o["cs"][k], res[0]["cs"][k])
 
 
+def test_multi_big_graph_rule_matches_single():
+    """Graphs from 4M nodes take the large-graph kept set (7d/4) on the row-partitioned path as
+    on one GPU: a two-rank thread group over one device and a one-GPU engine converge to the
+    same singular values (rtol 1e-5) on a 4,194,305-node ER pair."""
+    from node2vec2rank_amd import _lib, synthetic
+    n = (1 << 22) + 1
+    layers = [synthetic.er_layer_rows(n, 4, 700 + k) for k in range(2)]
+    d = 32
+    eng = _lib.Engine(0)
+    try:
+        eng.set_layers(layers)
+        st1 = eng.uase(d, seed=4)
+        s1 = eng.singular_values()
+    finally:
+        eng.close()
+    eng = _lib.Engine.multi([0, 0])
+    try:
+        eng.set_layers(layers)
+        st2 = eng.uase(d, seed=4)
+        s2 = eng.singular_values()
+    finally:
+        eng.close()
+    assert st1["converged"] == d and st2["converged"] == d, (st1, st2)
+    np.testing.assert_allclose(s2[:d], s1[:d], rtol=1e-5)
+
+
 def test_multi_engine_errors_leave_it_usable():
     """Arguments fail on every rank alike (no rank is left waiting in a collective): a bad
     dimension raises ValueError, an unknown metric NotImplementedError, and the handle then fits
