@@ -17,6 +17,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <mutex>
 
 #include "spmm_args.h"
 
@@ -416,7 +417,70 @@ __device__ __forceinline__ void flat_steps(const __attribute__((address_space(1)
   }
 }
 
+// flat_steps for a register-resident window of 64 rows (spmm8_flat_kernel<true>): lane pair pr
+// keeps rows pr (a0) and pr + 32 (a1), its half `sub`.  The segment sums are formed exactly as
+// in flat_steps (same entries, same order); each then reaches its row's owner through the
+// wave's staging slot, whose products are consumed by then: per half of the window, every lane
+// pair zeroes its slot, the segment heads of that half write their sums into their rows' slots,
+// and every owner adds its slot (0 for rows without entries in the step) -- no atomics, and
+// each row's sum keeps its order, so the result is bit-identical to the LDS-resident form.
+template <int NS, bool UNIT, bool NT>
+__device__ __forceinline__ void flat_steps_v(const __attribute__((address_space(1))) int32_t* ind,
+                                             const __attribute__((address_space(1))) float* dat,
+                                             int64_t beg, int off, int left,
+                                             const __attribute__((address_space(1))) float* Xb,
+                                             uint32_t ldx, int32_t cmask, int cbits, int lane,
+                                             f32x4* stage_, f32x4& a0, f32x4& a1) {
+  const int pr = lane >> 1, sub = lane & 1;
+  // every access to the slot volatile: lanes hand values to each other through it, so the
+  // compiler may neither reorder these accesses nor forward a lane's own store to its load
+  volatile f32x4* stage = stage_;
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  int wd[NS];
+  float v[NS];
+  f32x4 x[NS];
+#pragma unroll
+  for (int u = 0; u < NS; ++u) {
+    const int q = u * 32 + pr;
+    const int64_t e = beg + off + (q < left ? q : 0);
+    wd[u] = NT ? __builtin_nontemporal_load(ind + e) : ind[e];
+    v[u] = UNIT ? 1.f : (NT ? __builtin_nontemporal_load(dat + e) : dat[e]);
+  }
+#pragma unroll
+  for (int u = 0; u < NS; ++u)
+    x[u] = *reinterpret_cast<const __attribute__((address_space(1))) f32x4*>(
+        Xb + ((uint32_t)(wd[u] & cmask) * ldx + sub * 4));
+#pragma unroll
+  for (int u = 0; u < NS; ++u) {
+    stage[pr * 2 + sub] = v[u] * x[u];
+    const int nval = left - u * 32;
+    const int ri = wd[u] >> cbits;
+    const int rprev = __shfl(ri, lane - 2, 64);
+    const bool start = pr < nval && (pr == 0 || rprev != ri);
+    const unsigned long long m = __ballot(start);
+    f32x4 acc = zero;
+    if (start) {
+      const unsigned long long rest = pr == 31 ? 0ull : (m >> (2 * pr + 2));
+      const int end = rest ? pr + 1 + (__builtin_ctzll(rest) >> 1) : (nval < 32 ? nval : 32);
+      acc = stage[pr * 2 + sub];
+      for (int j = pr + 1; j < end; ++j) acc += stage[j * 2 + sub];
+    }
+    stage[pr * 2 + sub] = zero;
+    if (start && ri < 32) stage[ri * 2 + sub] = acc;
+    a0 += stage[pr * 2 + sub];
+    stage[pr * 2 + sub] = zero;
+    if (start && ri >= 32) stage[(ri - 32) * 2 + sub] = acc;
+    a1 += stage[pr * 2 + sub];
+  }
+}
+
 // NT: index / value words loaded non-temporally (read once; the panel gathers keep L2)
+// VW (launches of more than one round of resident tiles, 64-row windows): every wave also owns
+// one 64-row window whose accumulators stay in its registers (8 VGPRs), behind the tile's
+// LDS-resident rows -- a tile of tile_rows + 16 x 64 rows, so fewer rounds.  At cfg5 an L2 line
+// serves 4 deg r / N gathers per round (r: rows in flight per XCD; profiles/r06_tile_nb128_pmc.md),
+// so more rows in flight are fewer misses.
+template <bool VW>
 __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
   constexpr bool NT = true;
   // [tile_rows][8] row accumulators, then a 1-KB staging slot per wave
@@ -427,11 +491,19 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
   const int pr = lane >> 1, sub = lane & 1;
   const int wbits = __builtin_amdgcn_readfirstlane(a.wbits);
   const int W = 1 << wbits;
-  const int64_t r0 = (int64_t)blockIdx.x * a.tile_rows;
+  const int tile_all = a.tile_rows + (VW ? nwave * 64 : 0);  // (VW: wbits = 6)
+  const int64_t r0 = (int64_t)blockIdx.x * tile_all;
   const int64_t gw0 = r0 >> wbits;  // the tile's first window (tile_rows is a multiple of W)
   const int64_t rem = a.n - r0;
-  const int nrows = (int)(rem < a.tile_rows ? rem : a.tile_rows);
-  const int nwin = (nrows + W - 1) >> wbits;
+  const int nrows = (int)(rem < tile_all ? rem : tile_all);
+  const int nwin_all = (nrows + W - 1) >> wbits;
+  const int nwin_l = a.tile_rows >> wbits;  // LDS-resident windows of a full tile
+  const int nwin = nwin_all < nwin_l ? nwin_all : nwin_l;
+  // VW: this wave's register window (local rows vr0 .. vr0 + 63)
+  const int vwin = nwin_l + wave;
+  const bool vown = VW && vwin < nwin_all;
+  const int vr0 = vwin << wbits;
+  f32x4 va0 = {0.f, 0.f, 0.f, 0.f}, va1 = {0.f, 0.f, 0.f, 0.f};
   const uint32_t ldx = (uint32_t)a.ldx;
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
   f32x4* tacc = reinterpret_cast<f32x4*>(tacf);
@@ -466,13 +538,15 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
         const int len = wo[gw0 + w + 1] - e0;
         const int64_t beg = base + e0;
         f32x4* tw = tacc + ((size_t)w << wbits) * 2;
+// (VW: at most 2 steps per batch -- the register window's 8 VGPRs within the 64 of 8 waves per
+// SIMD; cfg5's runs are ~30 entries per window and block, one step)
 #define FLAT_STEPS(U)                                                                          \
-  for (int off = 0; off < len; off += 128) {                                                   \
+  for (int off = 0; off < len; off += (VW ? 64 : 128)) {                                       \
     const int left = len - off;                                                                \
-    if (left > 96)                                                                             \
-      flat_steps<4, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, cbits, lane, stage, tw);  \
-    else if (left > 64)                                                                        \
-      flat_steps<3, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, cbits, lane, stage, tw);  \
+    if (!VW && left > 96)                                                                      \
+      flat_steps<VW ? 1 : 4, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, cbits, lane, stage, tw); \
+    else if (!VW && left > 64)                                                                 \
+      flat_steps<VW ? 1 : 3, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, cbits, lane, stage, tw); \
     else if (left > 32)                                                                        \
       flat_steps<2, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, cbits, lane, stage, tw);  \
     else                                                                                       \
@@ -484,6 +558,25 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
           FLAT_STEPS(false)
         }
 #undef FLAT_STEPS
+      }
+      if (VW && vown) {
+        const int32_t e0 = wo[gw0 + vwin];
+        const int len = wo[gw0 + vwin + 1] - e0;
+        const int64_t beg = base + e0;
+#define FLAT_STEPS_V(U)                                                                        \
+  for (int off = 0; off < len; off += 64) {                                                    \
+    const int left = len - off;                                                                \
+    if (left > 32)                                                                             \
+      flat_steps_v<2, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, cbits, lane, stage, va0, va1); \
+    else                                                                                       \
+      flat_steps_v<1, U, NT>(ind, dat, beg, off, left, Xb, ldx, cmask, cbits, lane, stage, va0, va1); \
+  }
+        if (unit) {
+          FLAT_STEPS_V(true)
+        } else {
+          FLAT_STEPS_V(false)
+        }
+#undef FLAT_STEPS_V
       }
       // the workgroup's waves move to the next panel block together.  (No barrier: 0.57 vs
       // 0.36 ms per cfg4 layer launch; a bounded skew -- a wave starts phase g once all have
@@ -504,6 +597,14 @@ __global__ __launch_bounds__(1024, 8) void spmm8_flat_kernel(SpmmTileArgs a) {
             tacc[lr * 2 + sub] = zero;
           }
         }
+      if (VW && vown) {
+        if (vr0 + pr < nrows)
+          *reinterpret_cast<f32x4*>(Y + (r0 + vr0 + pr) * a.ldy + sub * 4) = va0;
+        if (vr0 + pr + 32 < nrows)
+          *reinterpret_cast<f32x4*>(Y + (r0 + vr0 + pr + 32) * a.ldy + sub * 4) = va1;
+        va0 = zero;
+        va1 = zero;
+      }
     }
   }
 }
@@ -669,6 +770,34 @@ extern "C" int n2v2r_spmm_tile_rows_b(int64_t n, int ncu, int wpc, int wbits, in
   return (int)t;
 }
 
+// The register-window form when the LDS-only tiles take more than one round of resident
+// workgroups (occupancy x CUs of the current device, queried once per LDS size).
+// N2V2R_SPMM_VW (read per launch): 0 off; 2 (tests) on at any size.
+static bool flat_vw_wanted(unsigned grid, size_t flds, int* resident) {
+  const char* env = std::getenv("N2V2R_SPMM_VW");
+  if (env && env[0] == '0') return false;
+  const bool force = env && env[0] == '2';
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+  static std::mutex mu;
+  static size_t occ_flds[64] = {};
+  static int slots[64] = {};
+  std::lock_guard<std::mutex> lk(mu);
+  if (occ_flds[dev] != flds) {
+    int per_cu = 0, ncu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)spmm8_flat_kernel<false>,
+                                                     1024, flds) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+      (void)hipGetLastError();
+      per_cu = 0;
+    }
+    slots[dev] = per_cu * ncu;
+    occ_flds[dev] = flds;
+  }
+  *resident = slots[dev];
+  return slots[dev] > 0 && (force || grid > (unsigned)slots[dev]);
+}
+
 extern "C" hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, hipStream_t stream) {
   if (a.K < 1 || a.K > 8 || a.n <= 0 || a.wbits < CB_WIN_BITS_MIN || a.wbits > CB_WIN_BITS_MAX ||
       a.tile_rows < (1 << a.wbits) || a.tile_rows % (1 << a.wbits) != 0)
@@ -682,7 +811,9 @@ extern "C" hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, hipStream_t 
   const bool wide16 = width == 16 && a.tile_rows > 1024;
   if (flds > (wide16 ? 144 : 80) * 1024) return hipErrorInvalidValue;
   static const bool fattr = [] {
-    (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel,
+    (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel<false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    (void)hipFuncSetAttribute((const void*)spmm8_flat_kernel<true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
     (void)hipFuncSetAttribute((const void*)spmm16_flat_kernel<2>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
@@ -702,7 +833,31 @@ extern "C" hipError_t n2v2r_launch_spmm_tile(const SpmmTileArgs& a, hipStream_t 
   // (Non-temporal index / value loads: cfg4 layer launch 0.354 vs 0.363 ms, fit 1,599 vs
   // 1,609 ms, profiles/r04_flat_nt.jsonl; no phase barrier: 0.57 vs 0.36 ms,
   // profiles/r04_flat_bar.jsonl -- the A/B switches of those runs are gone.)
-  hipLaunchKernelGGL(spmm8_flat_kernel, dim3(grid), dim3(1024), flds, stream, a);
+  // more tiles than one round of resident workgroups (cfg5): tiles with register windows
+  // Tiles: the caller's LDS rows + 1,024 register rows per workgroup (cfg5: 1,984 + 1,024, 4.14-
+  // 4.16 vs 4.38-4.39 ms per layer launch; 2,048 + 1,024: 4.21-4.22; tiles that fill each of 7
+  // rounds, 1,792 + 1,024: 4.21 -- rows in flight win; profiles/r06_register_windows.jsonl), or,
+  // when one round of resident workgroups holds every row, tiles that fill exactly one round (the
+  // 8-GPU row partition's 1.25M rows per rank).
+  int resident = 0;
+  if (a.wbits == 6 && flat_vw_wanted(grid, flds, &resident)) {
+    const int64_t vrows = 16 * 64, cap_all = 2048 + vrows, per = resident;
+    int64_t lds = a.tile_rows;
+    if (a.n <= per * cap_all) {
+      int64_t t_all = (a.n + per - 1) / per;
+      t_all = (t_all + 63) / 64 * 64;
+      lds = t_all - vrows;
+      lds = lds < 64 ? 64 : (lds + 63) / 64 * 64;
+      if (lds > 2048) lds = 2048;
+    }
+    SpmmTileArgs av = a;
+    av.tile_rows = (int)lds;
+    const size_t fv = sizeof(float) * 8 * (size_t)lds + 16 * 1024;
+    const unsigned gv = (unsigned)((a.n + lds + vrows - 1) / (lds + vrows));
+    hipLaunchKernelGGL(spmm8_flat_kernel<true>, dim3(gv), dim3(1024), fv, stream, av);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(spmm8_flat_kernel<false>, dim3(grid), dim3(1024), flds, stream, a);
   return hipGetLastError();
 }
 

@@ -549,6 +549,43 @@ def test_spmm_tiled_flat_blocks(engine, monkeypatch, tiled_layer, nb, wbits):
         assert np.all(np.abs(Y - ref) <= bound), (nb, wbits, tr)
 
 
+@pytest.mark.parametrize("nb", [4, 64])
+def test_spmm_tiled_register_windows_bit_identical(engine, monkeypatch, tiled_layer, nb):
+    """The flat kernel's register-window form (each wave also keeps one 64-row window's
+    accumulators in VGPRs; the default for launches of more than one round of resident tiles,
+    N2V2R_SPMM_VW=2 forces it at this size) is bit-identical to the LDS-only form: the same
+    segment sums in the same order, handed to the rows' owners through the staging slot; both
+    orientations, hub rows, empty rows, the partial last tile."""
+    monkeypatch.setenv("N2V2R_SPMM_WBITS", "6")
+    A, X, refs = tiled_layer
+    engine.set_layers([A])
+    for tr in (False, True):
+        monkeypatch.setenv("N2V2R_SPMM_VW", "0")
+        Y0, _ = engine.bench_spmm_tiled(0, X, transpose=tr, nb=nb, reps=1)
+        monkeypatch.setenv("N2V2R_SPMM_VW", "2")
+        Y1, _ = engine.bench_spmm_tiled(0, X, transpose=tr, nb=nb, reps=2)
+        assert np.array_equal(Y0, Y1), (nb, tr)
+        ref, bound = refs[tr]
+        assert np.all(np.abs(Y1 - ref) <= bound), (nb, tr)
+
+
+def test_fit_register_windows_bit_identical(engine, monkeypatch):
+    """A whole fit on the tiled SpMM (both stages, the sum mode included) with every launch in
+    the register-window form is bit-identical to the LDS-only form."""
+    from node2vec2rank_amd import synthetic
+    engine.set_layers(synthetic.er_layers(300_007, 16, 2, seed_base=31))
+    monkeypatch.setenv("N2V2R_SPMM_CB", "1")
+    monkeypatch.setenv("N2V2R_SPMM_WBITS", "6")
+    monkeypatch.setenv("N2V2R_SPMM_VW", "0")
+    st0 = engine.uase(32, seed=8)
+    s0, U0 = engine.singular_values(), engine.left_embedding()
+    monkeypatch.setenv("N2V2R_SPMM_VW", "2")
+    st1 = engine.uase(32, seed=8)
+    assert st0["block_applications"] == st1["block_applications"] and st1["converged"] == 32
+    assert np.array_equal(engine.singular_values(), s0)
+    assert np.array_equal(engine.left_embedding(), U0)
+
+
 @pytest.mark.parametrize("wbits", ["5", "7"])
 @pytest.mark.parametrize("nb", [4, 32])
 def test_spmm16_tiled_flat_blocks(engine, monkeypatch, tiled_layer, nb, wbits):

@@ -13,7 +13,8 @@ n, deg, var = int(sys.argv[1]), float(sys.argv[2]), sys.argv[3]
 vals = sys.argv[4].split(",")
 reps = int(sys.argv[5]) if len(sys.argv) > 5 else 2
 d = int(os.environ.get("PROBE_D", "128"))
-layers = synthetic.er_layers(n, deg, 2, seed_base=1000)
+layers = (synthetic.er_layers(n, deg, 2, seed_base=1000) if n <= 2_000_000 else
+          [synthetic.er_layer_rows(n, deg, 1000 + k) for k in range(2)])
 eng = _lib.Engine(0)
 eng.set_layers(layers)
 eng.uase(d, seed=42)  # warm-up (workspace, column blocks)
